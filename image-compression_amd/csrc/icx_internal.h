@@ -1,0 +1,84 @@
+// icx_internal.h — device-visible data structures of the MI355X JPEG path.
+//
+// HBM layout per image (DESIGN.md §Data layout):
+//   px          u8 BGR/RGB/grey rows (caller's buffer, or the resize buffer)
+//   coefs       int16 raw jpeg_fdct_islow output, one 64-entry zig-zag block
+//               per scan block, MCU order (Y0 Y1 Y2 Y3 Cb Cr): 3 B per pixel
+//               for 4:2:0.  Written once per visited scale, re-read by every
+//               quality trial (quantisation happens in the trial kernel).
+//   scratch[2]  per-chunk packed Huffman bitstreams (chunk = CHUNK_BLOCKS
+//               scan blocks, MSB-first 32-bit words, chunk-local bit 0),
+//               double-buffered: [best] holds the best fitting trial so the
+//               final file is stuffed from it without a re-encode.
+//   chunk_bits/off/ff [2]  per-chunk bit counts, exclusive bit offsets and
+//               0xFF-byte counts of the owned words (for byte stuffing).
+#pragma once
+#include <stdint.h>
+
+namespace icx {
+
+constexpr int CHUNK_BLOCKS = 128;        // scan blocks per Huffman chunk (one workgroup)
+constexpr int MAX_BLOCK_BITS = 1664;     // >= 22 (DC) + 63 * 26 (AC) bits, multiple of 32
+constexpr int CHUNK_WORDS = CHUNK_BLOCKS * MAX_BLOCK_BITS / 32;  // 6656 words = 26 KiB
+constexpr int FD_TILE_PX = 128;          // FDCT tile width in pixels (8 colour MCUs)
+constexpr int MAX_TRIALS = 8;            // findBestQualityByBinarySearch loop bound (:167)
+constexpr int HDR_COLOR = 623;           // SOI+APP0+2 DQT+SOF0+4 DHT+SOS
+constexpr int HDR_GRAY = 328;            // SOI+APP0+DQT+SOF0+2 DHT+SOS
+
+// One trial quality: a node of the binary-search tree of
+// findBestQualityByBinarySearch (ImageCompressionJpg.java:158-200), or a fixed
+// quality (compressJpgToStream / tryCachedParams).  Everything float-dependent
+// is evaluated on the host with Java's float32 semantics.
+struct QNode {
+    float mid;             // quality of this trial
+    int32_t child_fit;     // next node when size <= target (lo = mid), -1 = stop
+    int32_t child_nofit;   // next node when size >  target (hi = mid), -1 = stop
+    int32_t pad;
+    uint32_t rcp[2][64];   // floor(2^32 / (q<<3)) + 1, zig-zag order, [0]=lum [1]=chroma
+    uint16_t half[2][64];  // (q<<3)>>1 rounding addend, zig-zag order
+    uint16_t qt[2][64];    // quantisation tables, natural order (DQT payload)
+};
+
+struct ImgDesc {
+    const uint8_t* px;     // pixels for the current stage (original or resized)
+    int32_t w, h, stride, fmt;
+    int32_t ncomp, mcux, mcuy, ywb, yhb;
+    int32_t nchunks, hdr_len, pad0;
+    int64_t nblocks;
+    int64_t target;
+    int16_t* coefs;
+    uint32_t* scratch[2];
+    uint32_t* chunk_bits[2];
+    uint64_t* chunk_off[2];   // nchunks + 1 entries
+    uint32_t* chunk_ff[2];
+    uint64_t* chunk_ffoff;    // nchunks entries (final stuffing pass)
+    uint8_t* out;
+    uint64_t cap;
+};
+
+struct ImgState {
+    int32_t node;          // node of the pending trial, -1 = none
+    int32_t best_node;     // node of the best fitting trial, -1 = none
+    int32_t cur;           // scratch buffer the next trial writes
+    int32_t best_buf;      // scratch buffer holding the best trial
+    int32_t active;        // a trial is pending
+    int32_t ntrials;
+    int32_t force;         // single encode: accept regardless of size
+    int32_t status;        // 0 ok, 4 = output buffer too small
+    int64_t best_size;
+    int64_t out_len;
+    uint64_t total_bits[2];
+    uint32_t ff_total[2];
+    float trial_q[MAX_TRIALS + 1];
+    int64_t trial_size[MAX_TRIALS + 1];
+};
+
+// A launch plan: the images taking part (ids into desc/state arrays) and
+// the exclusive prefix of work items (tiles or chunks) per image.
+struct Plan {
+    const int32_t* ids;
+    const int64_t* prefix;  // m + 1 entries
+    int32_t m;
+};
+
+}  // namespace icx

@@ -1,0 +1,840 @@
+// icx_kernels.hip — CDNA4 (gfx950) kernels for the JPEG target-size path.
+//
+// Kernel map (reference rows from SURVEY.md §8a; arithmetic restates IJG 6b
+// as reached through the JDK writer, see oracle/icx_oracle.c for the CPU
+// statement of the same algorithm):
+//   k_fdct_color / k_fdct_gray  A7+A8+A9: rgb_ycc_convert, edge expansion,
+//                               h2v2_downsample, jpeg_fdct_islow (raw, x8)
+//   k_huff                      A9 quantise + A10 Huffman: per-chunk packed
+//                               bitstream, 16 lanes per 8x8 block
+//   k_scan                      exclusive scan of chunk bit counts
+//   k_ffcount                   0xFF bytes of the globally aligned stream
+//                               (exact stuffed size without writing it)
+//   k_decide                    A3 binary-search step (tree walk)
+//   k_ffscan + k_stuff          final file: header, stuffed bytes, EOI
+//   k_resize                    A12 Java2D bilinear (TransformHelper)
+// No MFMA: integer, byte-oriented work bound by HBM.
+#include <hip/hip_runtime.h>
+
+#include "icx_internal.h"
+#include "icx_kernels.h"
+
+namespace icx {
+
+__constant__ uint8_t c_nat_to_zz[64];
+__constant__ uint8_t c_zz_to_nat[64];
+__constant__ uint32_t c_dc[2][16];    // (code << 8) | length, by category
+__constant__ uint32_t c_ac[2][256];   // (code << 8) | length, by run/size symbol
+__constant__ uint8_t c_hdr[2][HDR_COLOR];  // [0] grey template, [1] colour template
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ int find_slot(const int64_t* prefix, int m, int64_t item)
+{
+    int lo = 0, hi = m;  // prefix[lo] <= item < prefix[hi]
+    while (hi - lo > 1) {
+        int mid = (lo + hi) >> 1;
+        if (prefix[mid] <= item) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+#define CONST_BITS 13
+#define PASS1_BITS 2
+#define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
+
+// One 1-D pass of jpeg_fdct_islow (jfdctint.c, IJG 6b).  pass 0 = rows
+// (outputs scaled up by PASS1_BITS), pass 1 = columns.
+template <int PASS>
+__device__ __forceinline__ void fdct8(int32_t& d0, int32_t& d1, int32_t& d2, int32_t& d3,
+                                      int32_t& d4, int32_t& d5, int32_t& d6, int32_t& d7)
+{
+    int32_t t0 = d0 + d7, t7 = d0 - d7, t1 = d1 + d6, t6 = d1 - d6;
+    int32_t t2 = d2 + d5, t5 = d2 - d5, t3 = d3 + d4, t4 = d3 - d4;
+    int32_t t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+    constexpr int SH = PASS == 0 ? CONST_BITS - PASS1_BITS : CONST_BITS + PASS1_BITS;
+    if (PASS == 0) {
+        d0 = (t10 + t11) << PASS1_BITS;
+        d4 = (t10 - t11) << PASS1_BITS;
+    } else {
+        d0 = DESCALE(t10 + t11, PASS1_BITS);
+        d4 = DESCALE(t10 - t11, PASS1_BITS);
+    }
+    int32_t z1 = (t12 + t13) * 4433;                  // FIX_0_541196100
+    d2 = DESCALE(z1 + t13 * 6270, SH);                // FIX_0_765366865
+    d6 = DESCALE(z1 - t12 * 15137, SH);               // FIX_1_847759065
+    z1 = t4 + t7;
+    int32_t z2 = t5 + t6, z3 = t4 + t6, z4 = t5 + t7;
+    int32_t z5 = (z3 + z4) * 9633;                    // FIX_1_175875602
+    t4 *= 2446; t5 *= 16819; t6 *= 25172; t7 *= 12299;
+    z1 *= -7373; z2 *= -20995; z3 *= -16069; z4 *= -3196;
+    z3 += z5; z4 += z5;
+    d7 = DESCALE(t4 + z1 + z3, SH);
+    d5 = DESCALE(t5 + z2 + z4, SH);
+    d3 = DESCALE(t6 + z2 + z3, SH);
+    d1 = DESCALE(t7 + z1 + z4, SH);
+}
+
+// rgb_ycc_convert (jccolor.c): 16-bit fixed point, FIX(x) = (int)(x*65536+0.5)
+__device__ __forceinline__ void rgb_ycc(int r, int g, int b, int& y, int& cb, int& cr)
+{
+    y = (19595 * r + 38470 * g + 7471 * b + 32768) >> 16;
+    cb = (-11059 * r - 21709 * g + 32768 * b + (128 << 16) + 32767) >> 16;
+    cr = (32768 * r - 27439 * g - 5329 * b + (128 << 16) + 32767) >> 16;
+}
+
+// =================================================================== FDCT
+// Colour: one workgroup = 16 rows x 128 px = 8 MCUs of one MCU row.
+//   A. coalesced row loads (16-B when aligned and inside) -> LDS raw tile,
+//      edge expansion by clamping x to W-1 and y to H-1
+//   B. per thread 8 px of one row: YCbCr, Y row-DCT in registers
+//   C. h2v2_downsample (bias 1,2,..) + chroma row-DCT
+//   D. column DCT, zig-zag scatter into LDS
+//   E. dummy blocks (jccoefct.c) + coalesced 16-B stores of 48 blocks
+template <bool BGR>
+__global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ descs,
+                                                    const int32_t* __restrict__ ids,
+                                                    const int64_t* __restrict__ prefix, int m)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t raw[16 * 384];
+    __shared__ __attribute__((aligned(16))) uint8_t cful[2][16][128];
+    __shared__ __attribute__((aligned(16))) int32_t ws[48][64];
+    __shared__ __attribute__((aligned(16))) int16_t oz[48][64];
+
+    const int64_t item = blockIdx.x;
+    const int slot = find_slot(prefix, m, item);
+    const ImgDesc& D = descs[ids[slot]];
+    const int tile = (int)(item - prefix[slot]);
+    const int tiles_x = (D.mcux + 7) >> 3;
+    const int my = tile / tiles_x, tx = tile - my * tiles_x;
+    const int W = D.w, H = D.h, x0 = tx * 128, y0 = my * 16;
+    const int t = threadIdx.x;
+    const uint8_t* px = D.px;
+
+    // ---- A: load 16 x 384 bytes
+    const bool fast = (x0 + 128 <= W) && (((uintptr_t)px & 15) == 0) && ((D.stride & 15) == 0);
+    if (fast) {
+        for (int i = t; i < 16 * 24; i += 256) {
+            int r = i / 24, c = i - r * 24;
+            int y = min(y0 + r, H - 1);
+            const uint4* src = (const uint4*)(px + (size_t)y * D.stride + (size_t)x0 * 3) + c;
+            *(uint4*)(raw + r * 384 + c * 16) = *src;
+        }
+    } else {
+        for (int i = t; i < 16 * 128; i += 256) {
+            int r = i >> 7, x = i & 127;
+            int y = min(y0 + r, H - 1), sx = min(x0 + x, W - 1);
+            const uint8_t* s = px + (size_t)y * D.stride + (size_t)sx * 3;
+            raw[r * 384 + x * 3 + 0] = s[0];
+            raw[r * 384 + x * 3 + 1] = s[1];
+            raw[r * 384 + x * 3 + 2] = s[2];
+        }
+    }
+    __syncthreads();
+
+    // ---- B: colour convert 8 px per thread, Y row DCT
+    {
+        const int r = t >> 4, s = t & 15;
+        const uint8_t* p = raw + r * 384 + s * 24;
+        uint2 a = *(const uint2*)(p), b = *(const uint2*)(p + 8), c = *(const uint2*)(p + 16);
+        uint32_t wv[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+        int yv[8];
+        uint32_t cbw[2] = {0, 0}, crw[2] = {0, 0};
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            int o0 = 3 * k, o1 = 3 * k + 1, o2 = 3 * k + 2;
+            int c0 = (wv[o0 >> 2] >> ((o0 & 3) * 8)) & 255;
+            int c1 = (wv[o1 >> 2] >> ((o1 & 3) * 8)) & 255;
+            int c2 = (wv[o2 >> 2] >> ((o2 & 3) * 8)) & 255;
+            int R = BGR ? c2 : c0, G = c1, B = BGR ? c0 : c2;
+            int yy, cb, cr;
+            rgb_ycc(R, G, B, yy, cb, cr);
+            yv[k] = yy - 128;
+            cbw[k >> 2] |= (uint32_t)cb << ((k & 3) * 8);
+            crw[k >> 2] |= (uint32_t)cr << ((k & 3) * 8);
+        }
+        *(uint2*)&cful[0][r][s * 8] = make_uint2(cbw[0], cbw[1]);
+        *(uint2*)&cful[1][r][s * 8] = make_uint2(crw[0], crw[1]);
+        fdct8<0>(yv[0], yv[1], yv[2], yv[3], yv[4], yv[5], yv[6], yv[7]);
+        const int blk = (s >> 1) * 6 + (r >> 3) * 2 + (s & 1);
+        int32_t* dst = &ws[blk][(r & 7) * 8];
+        *(int4*)dst = make_int4(yv[0], yv[1], yv[2], yv[3]);
+        *(int4*)(dst + 4) = make_int4(yv[4], yv[5], yv[6], yv[7]);
+    }
+    __syncthreads();
+
+    // ---- C: h2v2_downsample + chroma row DCT (128 row tasks)
+    if (t < 128) {
+        const int comp = t >> 6, cr = (t >> 3) & 7, cb = t & 7;
+        const int crows = (H + 1) >> 1;             // chroma rows with image data
+        int re = cr;
+        if (my * 8 + cr >= crows) re = crows - 1 - my * 8;  // replicate last chroma row
+        const uint8_t* r0 = &cful[comp][2 * re][cb * 16];
+        const uint8_t* r1 = &cful[comp][2 * re + 1][cb * 16];
+        uint4 u0 = *(const uint4*)r0, u1 = *(const uint4*)r1;
+        uint32_t a[4] = {u0.x, u0.y, u0.z, u0.w}, bb[4] = {u1.x, u1.y, u1.z, u1.w};
+        int v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            int wd = j >> 1, sh = (j & 1) * 16;
+            int s0 = ((a[wd] >> sh) & 255) + ((a[wd] >> (sh + 8)) & 255) + ((bb[wd] >> sh) & 255) +
+                     ((bb[wd] >> (sh + 8)) & 255);
+            v[j] = ((s0 + 1 + (j & 1)) >> 2) - 128;
+        }
+        fdct8<0>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+        int32_t* dst = &ws[cb * 6 + 4 + comp][cr * 8];
+        *(int4*)dst = make_int4(v[0], v[1], v[2], v[3]);
+        *(int4*)(dst + 4) = make_int4(v[4], v[5], v[6], v[7]);
+    }
+    __syncthreads();
+
+    // ---- D: column DCT (384 column tasks)
+    for (int task = t; task < 48 * 8; task += 256) {
+        const int blk = task >> 3, col = task & 7;
+        int32_t d[8];
+#pragma unroll
+        for (int v = 0; v < 8; v++) d[v] = ws[blk][v * 8 + col];
+        fdct8<1>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+#pragma unroll
+        for (int v = 0; v < 8; v++) oz[blk][c_nat_to_zz[v * 8 + col]] = (int16_t)d[v];
+    }
+    __syncthreads();
+
+    // ---- E: dummy blocks + store.  jccoefct.c compress_data: a Y block right
+    // of ceil(W/8) or below ceil(H/8) gets AC = 0 and the DC of MCU_buffer[blkn-1]
+    // (right edge) or of the last block of the MCU's previous block row (bottom).
+    const int nmcu = min(8, D.mcux - tx * 8);
+    const bool bottom = (2 * my + 1) >= D.yhb;
+    int16_t* gdst = D.coefs + ((int64_t)my * D.mcux + tx * 8) * 384;
+    for (int e = t; e < nmcu * 48; e += 256) {  // 16-B pieces: 8 per block
+        const int blk = e >> 3, part = e & 7, mcu = blk / 6, yb = blk - mcu * 6;
+        int4 val = *(const int4*)&oz[blk][part * 8];
+        if (yb < 4) {
+            const bool right = (2 * (tx * 8 + mcu) + 1) >= D.ywb;
+            const bool dum = (yb >= 2 && bottom) || ((yb & 1) && right);
+            if (dum) {
+                // effective source: right dummy in row 0 -> block 0; bottom row -> eff(block 1);
+                // right dummy in row 1 (not bottom) -> block 2
+                int src;
+                if (yb == 1) src = 0;
+                else if (bottom) src = right ? 0 : 1;
+                else src = 2;
+                int16_t dc = oz[mcu * 6 + src][0];
+                val = make_int4(part == 0 ? (int)(uint16_t)dc : 0, 0, 0, 0);
+            }
+        }
+        *((int4*)gdst + e) = val;
+    }
+}
+
+// Grey (1 component, non-interleaved): one workgroup = 8 rows x 128 px = 16 blocks.
+__global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ descs,
+                                                   const int32_t* __restrict__ ids,
+                                                   const int64_t* __restrict__ prefix, int m)
+{
+    __shared__ __attribute__((aligned(16))) int32_t ws[16][64];
+    __shared__ __attribute__((aligned(16))) int16_t oz[16][64];
+    const int64_t item = blockIdx.x;
+    const int slot = find_slot(prefix, m, item);
+    const ImgDesc& D = descs[ids[slot]];
+    const int tile = (int)(item - prefix[slot]);
+    const int tiles_x = (D.mcux + 15) >> 4;
+    const int by = tile / tiles_x, tx = tile - by * tiles_x;
+    const int W = D.w, H = D.h, x0 = tx * 128;
+    const int t = threadIdx.x;
+    if (t < 128) {
+        const int r = t >> 4, s = t & 15;
+        const int y = min(by * 8 + r, H - 1);
+        const uint8_t* row = D.px + (size_t)y * D.stride;
+        int v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = (int)row[min(x0 + s * 8 + k, W - 1)] - 128;
+        fdct8<0>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+        int32_t* dst = &ws[s][r * 8];
+        *(int4*)dst = make_int4(v[0], v[1], v[2], v[3]);
+        *(int4*)(dst + 4) = make_int4(v[4], v[5], v[6], v[7]);
+    }
+    __syncthreads();
+    if (t < 128) {
+        const int blk = t >> 3, col = t & 7;
+        int32_t d[8];
+#pragma unroll
+        for (int v = 0; v < 8; v++) d[v] = ws[blk][v * 8 + col];
+        fdct8<1>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+#pragma unroll
+        for (int v = 0; v < 8; v++) oz[blk][c_nat_to_zz[v * 8 + col]] = (int16_t)d[v];
+    }
+    __syncthreads();
+    const int nblk = min(16, D.mcux - tx * 16);
+    int16_t* gdst = D.coefs + ((int64_t)by * D.mcux + tx * 16) * 64;
+    for (int e = t; e < nblk * 8; e += 256) *((int4*)gdst + e) = *((const int4*)&oz[0][0] + e);
+}
+
+// =================================================================== Huffman
+__device__ __forceinline__ void put_bits(uint32_t* buf, uint32_t pos, uint32_t val, int len)
+{
+    const uint32_t w = pos >> 5;
+    const int o = pos & 31;
+    if (o + len <= 32) {
+        atomicOr(&buf[w], val << (32 - o - len));
+    } else {
+        atomicOr(&buf[w], val >> (o + len - 32));
+        atomicOr(&buf[w + 1], val << (64 - o - len));
+    }
+}
+
+__device__ __forceinline__ int quant(int c, uint32_t rcp, uint32_t half)
+{
+    // jcdctmgr.c: sign(c) * ((|c| + (q<<3)/2) / (q<<3)); exact for |c|+half < 2^16
+    uint32_t a = (uint32_t)(c < 0 ? -c : c) + half;
+    int q = (int)__umulhi(a, rcp);
+    return c < 0 ? -q : q;
+}
+
+__device__ __forceinline__ int nbits(int a) { return a ? 32 - __clz(a) : 0; }
+
+// One workgroup = one chunk of CHUNK_BLOCKS scan blocks of one image.  Per
+// pass, each 16-lane group owns one block (4 zig-zag coefficients per lane):
+// quantise, run lengths from a segmented max-scan of nonzero positions, code
+// lengths from LDS tables, exclusive bit offsets, then every code is OR-ed
+// into an LDS bit buffer.  The chunk's packed words go to scratch[cur].
+__global__ __launch_bounds__(256) void k_huff(const ImgDesc* __restrict__ descs,
+                                              const ImgState* __restrict__ states,
+                                              const QNode* __restrict__ nodes,
+                                              const int32_t* __restrict__ ids,
+                                              const int64_t* __restrict__ prefix, int m)
+{
+    __shared__ uint32_t bitbuf[CHUNK_WORDS + 1];
+    __shared__ uint32_t s_rcp[2][64];
+    __shared__ uint32_t s_half[2][64];
+    __shared__ uint32_t s_ac[2][256];
+    __shared__ uint32_t s_dc[2][16];
+    __shared__ uint32_t s_blk[16];
+
+    const int64_t item = blockIdx.x;
+    const int slot = find_slot(prefix, m, item);
+    const int img = ids[slot];
+    const ImgState& S = states[img];
+    if (!S.active) return;
+    const ImgDesc& D = descs[img];
+    const int chunk = (int)(item - prefix[slot]);
+    const QNode& N = nodes[S.node];
+    const int cur = S.cur;
+    const int t = threadIdx.x;
+
+    if (t < 128) {
+        s_rcp[t >> 6][t & 63] = N.rcp[t >> 6][t & 63];
+        s_half[t >> 6][t & 63] = N.half[t >> 6][t & 63];
+    }
+    s_ac[0][t] = c_ac[0][t];
+    s_ac[1][t] = c_ac[1][t];
+    if (t < 32) s_dc[t >> 4][t & 15] = c_dc[t >> 4][t & 15];
+    for (int i = t; i < CHUNK_WORDS + 1; i += 256) bitbuf[i] = 0;
+    __syncthreads();
+
+    const int64_t b0 = (int64_t)chunk * CHUNK_BLOCKS;
+    const int nb = (int)min((int64_t)CHUNK_BLOCKS, D.nblocks - b0);
+    const int lane = t & 63, grp = lane >> 4, l = lane & 15, wv = t >> 6;
+    const bool color = D.ncomp == 3;
+    uint32_t running = 0;
+
+    for (int pass = 0; pass < CHUNK_BLOCKS / 16; pass++) {
+        const int bl = pass * 16 + wv * 4 + grp;
+        const bool valid = bl < nb;
+        const int64_t b = b0 + bl;
+        int tb = 0;
+        int64_t pb = -1;
+        if (color) {
+            const int k6 = (int)(b % 6);
+            tb = k6 >= 4;
+            if (k6 >= 1 && k6 <= 3) pb = b - 1;
+            else if (k6 == 0) pb = b >= 6 ? b - 3 : -1;
+            else pb = b >= 6 ? b - 6 : -1;
+        } else {
+            pb = b - 1;
+        }
+        int q[4] = {0, 0, 0, 0};
+        int qprev = 0;
+        if (valid) {
+            const int2 raw = *(const int2*)(D.coefs + b * 64 + 4 * l);
+            const int c[4] = {(int)(int16_t)(raw.x & 0xFFFF), (int)(int16_t)(raw.x >> 16),
+                              (int)(int16_t)(raw.y & 0xFFFF), (int)(int16_t)(raw.y >> 16)};
+#pragma unroll
+            for (int j = 0; j < 4; j++) q[j] = quant(c[j], s_rcp[tb][4 * l + j], s_half[tb][4 * l + j]);
+            if (l == 0 && pb >= 0) qprev = quant(D.coefs[pb * 64], s_rcp[tb][0], s_half[tb][0]);
+        }
+        // last "nonzero" position in this lane (DC counts as the run start)
+        int last = -1;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (q[j] != 0 || (l == 0 && j == 0)) last = 4 * l + j;
+        int incl = last;
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            int y = __shfl_up(incl, d, 16);
+            if (l >= d) incl = max(incl, y);
+        }
+        int excl = __shfl_up(incl, 1, 16);
+        if (l == 0) excl = -1;
+        const int glast = __shfl(incl, 15, 16);
+
+        // code words of this lane, in emission order (DC, AC k..., EOB)
+        uint32_t cv[4], zrl[4];
+        int cl[4];
+        int lane_bits = 0;
+        uint32_t dcv = 0;
+        int dcl = 0;
+        const uint32_t zrlc = s_ac[tb][0xF0];
+        const int zrll = zrlc & 255;
+        if (l == 0) {
+            int diff = q[0] - qprev;
+            int a = diff < 0 ? -diff : diff;
+            int s = nbits(a);
+            uint32_t mag = (uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << s) - 1);
+            uint32_t hc = s_dc[tb][s];
+            dcv = ((hc >> 8) << s) | mag;
+            dcl = (int)(hc & 255) + s;
+            lane_bits += dcl;
+        }
+        int prev = excl;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int k = 4 * l + j;
+            cv[j] = 0; cl[j] = 0; zrl[j] = 0;
+            if (k >= 1 && q[j] != 0) {
+                int r = k - prev - 1;
+                zrl[j] = r >> 4;
+                r &= 15;
+                int a = q[j] < 0 ? -q[j] : q[j];
+                int s = nbits(a);
+                uint32_t mag = (uint32_t)(q[j] < 0 ? q[j] - 1 : q[j]) & ((1u << s) - 1);
+                uint32_t hc = s_ac[tb][(r << 4) | s];
+                cv[j] = ((hc >> 8) << s) | mag;
+                cl[j] = (int)(hc & 255) + s;
+                lane_bits += cl[j] + (int)zrl[j] * zrll;
+            }
+            if (k == 0 || q[j] != 0) prev = k;
+        }
+        const uint32_t eobc = s_ac[tb][0];
+        const bool eob = (l == 15) && glast < 63;
+        if (eob) lane_bits += eobc & 255;
+        if (!valid) lane_bits = 0;
+
+        int off = lane_bits;  // inclusive add-scan over the 16-lane group
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            int y = __shfl_up(off, d, 16);
+            if (l >= d) off += y;
+        }
+        const int block_bits = __shfl(off, 15, 16);
+        off -= lane_bits;
+        if (l == 0) s_blk[wv * 4 + grp] = block_bits;
+        __syncthreads();
+        uint32_t boff = running;
+        const int me = wv * 4 + grp;
+        uint32_t pass_total = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            uint32_t v = s_blk[i];
+            if (i < me) boff += v;
+            pass_total += v;
+        }
+        if (valid) {
+            uint32_t pos = boff + off;
+            if (l == 0) { put_bits(bitbuf, pos, dcv, dcl); pos += dcl; }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (cl[j]) {
+                    for (uint32_t z = 0; z < zrl[j]; z++) { put_bits(bitbuf, pos, zrlc >> 8, zrll); pos += zrll; }
+                    put_bits(bitbuf, pos, cv[j], cl[j]);
+                    pos += cl[j];
+                }
+            }
+            if (eob) put_bits(bitbuf, pos, eobc >> 8, eobc & 255);
+        }
+        running += pass_total;
+        __syncthreads();
+    }
+    const uint32_t nwords = (running + 31) >> 5;
+    uint32_t* dst = D.scratch[cur] + (size_t)chunk * CHUNK_WORDS;
+    for (uint32_t i = t; i < nwords; i += 256) dst[i] = bitbuf[i];
+    if (t == 0) D.chunk_bits[cur][chunk] = running;
+}
+
+// Exclusive scan of the chunk bit counts of one image (one workgroup per image).
+__global__ __launch_bounds__(1024) void k_scan(const ImgDesc* __restrict__ descs, ImgState* states,
+                                               const int32_t* __restrict__ ids, int m)
+{
+    __shared__ uint64_t s_w[16];
+    __shared__ uint64_t s_base;
+    const int img = ids[blockIdx.x];
+    ImgState& S = states[img];
+    if (!S.active) return;
+    const ImgDesc& D = descs[img];
+    const int cur = S.cur;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t == 0) s_base = 0;
+    __syncthreads();
+    for (int base = 0; base < D.nchunks; base += 1024) {
+        const int i = base + t;
+        uint64_t v = i < D.nchunks ? D.chunk_bits[cur][i] : 0;
+        uint64_t x = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            uint64_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) s_w[wv] = x;
+        __syncthreads();
+        uint64_t wbase = s_base;
+        for (int k = 0; k < wv; k++) wbase += s_w[k];
+        if (i < D.nchunks) D.chunk_off[cur][i] = wbase + x - v;
+        __syncthreads();
+        if (t == 1023) s_base = wbase + x;
+        __syncthreads();
+    }
+    if (t == 0) {
+        D.chunk_off[cur][D.nchunks] = s_base;
+        S.total_bits[cur] = s_base;
+        S.ff_total[cur] = 0;
+    }
+}
+
+// 32 bits of the globally aligned stream starting at global bit 32*w, from
+// chunk c (whose bits start at `start`), the next chunk, then 1-bit padding.
+__device__ __forceinline__ uint32_t stream_word(const uint32_t* __restrict__ scratch,
+                                                const uint64_t* __restrict__ off, int nchunks, int c,
+                                                uint64_t w)
+{
+    const uint64_t gbit = w * 32;
+    const uint64_t start = off[c], end = off[c + 1];
+    const uint32_t* cs = scratch + (size_t)c * CHUNK_WORDS;
+    const uint64_t s = gbit - start;
+    const uint32_t lw = (uint32_t)(s >> 5), sh = (uint32_t)(s & 31);
+    uint32_t v = cs[lw] << sh;
+    if (sh) v |= cs[lw + 1] >> (32 - sh);
+    uint64_t avail = end - gbit;
+    if (avail >= 32) return v;
+    v &= ~0u << (32 - avail);
+    int have = (int)avail;
+    if (c + 1 < nchunks) {
+        const uint64_t nlen = off[c + 2] - end;
+        const uint32_t* ns = scratch + (size_t)(c + 1) * CHUNK_WORDS;
+        uint32_t nv = ns[0];
+        int take = (int)min((uint64_t)(32 - have), nlen);
+        if (take > 0) {
+            uint32_t piece = nv & (take == 32 ? ~0u : ~0u << (32 - take));
+            v |= piece >> have;
+            have += take;
+        }
+        // Every chunk but the last holds >= CHUNK_BLOCKS * 4 bits, so a word
+        // left short here ends in the last chunk: the rest is padding.
+    }
+    if (have < 32) v |= ~0u >> have;  // flush_bits: pad with 1-bits
+    return v;
+}
+
+// One wave per chunk: count 0xFF bytes in the words this chunk owns (words
+// whose first bit lies in the chunk), bytes beyond ceil(total/8) excluded.
+__global__ __launch_bounds__(256) void k_ffcount(const ImgDesc* __restrict__ descs, ImgState* states,
+                                                 const int32_t* __restrict__ ids,
+                                                 const int64_t* __restrict__ prefix, int m, int use_best)
+{
+    const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (item >= prefix[m]) return;
+    const int slot = find_slot(prefix, m, item);
+    const int img = ids[slot];
+    ImgState& S = states[img];
+    if (!use_best && !S.active) return;
+    const ImgDesc& D = descs[img];
+    const int c = (int)(item - prefix[slot]);
+    const int buf = use_best ? S.best_buf : S.cur;
+    const uint64_t* off = D.chunk_off[buf];
+    const uint64_t total = off[D.nchunks];
+    const uint64_t nbytes = (total + 7) >> 3;
+    const uint64_t wlim = (nbytes + 3) >> 2;
+    const uint64_t wb = (off[c] + 31) >> 5;
+    const uint64_t we = min((off[c + 1] + 31) >> 5, wlim);
+    const int lane = threadIdx.x & 63;
+    uint32_t cnt = 0;
+    for (uint64_t w = wb + lane; w < we; w += 64) {
+        uint32_t v = stream_word(D.scratch[buf], off, D.nchunks, c, w);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (w * 4 + j < nbytes && ((v >> (24 - 8 * j)) & 255) == 255) cnt++;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+    if (lane == 0) {
+        D.chunk_ff[buf][c] = cnt;
+        if (cnt) atomicAdd(&S.ff_total[buf], cnt);
+    }
+}
+
+// One thread per image: exact file size of the pending trial, then one step
+// of findBestQualityByBinarySearch (ImageCompressionJpg.java:176-189).
+__global__ void k_decide(const ImgDesc* __restrict__ descs, ImgState* states, const QNode* __restrict__ nodes,
+                         const int32_t* __restrict__ ids, int m)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int img = ids[i];
+    ImgState& S = states[img];
+    if (!S.active) return;
+    const ImgDesc& D = descs[img];
+    const int cur = S.cur;
+    const int64_t size = (int64_t)D.hdr_len + (int64_t)((S.total_bits[cur] + 7) >> 3) +
+                         (int64_t)S.ff_total[cur] + 2;
+    const QNode& N = nodes[S.node];
+    if (S.ntrials <= MAX_TRIALS) {
+        S.trial_q[S.ntrials] = N.mid;
+        S.trial_size[S.ntrials] = size;
+    }
+    S.ntrials++;
+    const bool fits = S.force || size <= D.target;  // currentSize <= targetMaxSizeBytes
+    int next;
+    if (fits) {
+        S.best_node = S.node;
+        S.best_buf = cur;
+        S.best_size = size;
+        S.cur = cur ^ 1;
+        next = N.child_fit;
+    } else {
+        next = N.child_nofit;
+    }
+    if (S.force) next = -1;
+    S.node = next;
+    S.active = next >= 0;
+}
+
+// Final pass 1 (one workgroup per image): exclusive scan of the best trial's
+// per-chunk 0xFF counts -> stuffed byte offsets; file length and capacity check.
+__global__ __launch_bounds__(1024) void k_ffscan(const ImgDesc* __restrict__ descs, ImgState* states,
+                                                 const int32_t* __restrict__ ids, int m)
+{
+    __shared__ uint64_t s_w[16];
+    __shared__ uint64_t s_base;
+    const int img = ids[blockIdx.x];
+    ImgState& S = states[img];
+    if (S.best_node < 0) return;
+    const ImgDesc& D = descs[img];
+    const int buf = S.best_buf;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t == 0) s_base = 0;
+    __syncthreads();
+    for (int base = 0; base < D.nchunks; base += 1024) {
+        const int i = base + t;
+        uint64_t v = i < D.nchunks ? D.chunk_ff[buf][i] : 0;
+        uint64_t x = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            uint64_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) s_w[wv] = x;
+        __syncthreads();
+        uint64_t wbase = s_base;
+        for (int k = 0; k < wv; k++) wbase += s_w[k];
+        if (i < D.nchunks) D.chunk_ffoff[i] = wbase + x - v;
+        __syncthreads();
+        if (t == 1023) s_base = wbase + x;
+        __syncthreads();
+    }
+    if (t == 0) {
+        const uint64_t nbytes = (D.chunk_off[buf][D.nchunks] + 7) >> 3;
+        const int64_t len = (int64_t)D.hdr_len + (int64_t)nbytes + (int64_t)s_base + 2;
+        S.out_len = len;
+        S.status = (uint64_t)len > D.cap ? 4 : 0;
+    }
+}
+
+// Final pass 2 (one wave per chunk): header (chunk 0), stuffed entropy bytes,
+// EOI (last chunk), written straight into the caller's output buffer.
+__global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs, const ImgState* __restrict__ states,
+                                               const QNode* __restrict__ nodes, const int32_t* __restrict__ ids,
+                                               const int64_t* __restrict__ prefix, int m)
+{
+    const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (item >= prefix[m]) return;
+    const int slot = find_slot(prefix, m, item);
+    const int img = ids[slot];
+    const ImgState& S = states[img];
+    if (S.best_node < 0 || S.status != 0) return;
+    const ImgDesc& D = descs[img];
+    const int c = (int)(item - prefix[slot]);
+    const int buf = S.best_buf;
+    const int lane = threadIdx.x & 63;
+    uint8_t* out = D.out;
+    const uint64_t* off = D.chunk_off[buf];
+    const uint64_t total = off[D.nchunks];
+    const uint64_t nbytes = (total + 7) >> 3;
+    const int hdr = D.hdr_len;
+
+    if (c == 0) {  // marker segments: template + DQT payload + SOF dimensions
+        const QNode& N = nodes[S.best_node];
+        const uint8_t* tpl = c_hdr[D.ncomp == 3 ? 1 : 0];
+        for (int i = lane; i < hdr; i += 64) {
+            uint8_t v = tpl[i];
+            if (i >= 25 && i < 89) v = (uint8_t)N.qt[0][c_zz_to_nat[i - 25]];
+            else if (D.ncomp == 3 && i >= 94 && i < 158) v = (uint8_t)N.qt[1][c_zz_to_nat[i - 94]];
+            const int sof = D.ncomp == 3 ? 158 : 89;
+            if (i == sof + 5) v = (uint8_t)(D.h >> 8);
+            if (i == sof + 6) v = (uint8_t)D.h;
+            if (i == sof + 7) v = (uint8_t)(D.w >> 8);
+            if (i == sof + 8) v = (uint8_t)D.w;
+            out[i] = v;
+        }
+    }
+    const uint64_t wlim = (nbytes + 3) >> 2;
+    const uint64_t wb = (off[c] + 31) >> 5;
+    const uint64_t we = min((off[c + 1] + 31) >> 5, wlim);
+    uint64_t run = D.chunk_ffoff[c];
+    for (uint64_t w0 = wb; w0 < we; w0 += 64) {
+        const uint64_t w = w0 + lane;
+        uint32_t v = 0;
+        int cnt = 0;
+        if (w < we) {
+            v = stream_word(D.scratch[buf], off, D.nchunks, c, w);
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (w * 4 + j < nbytes && ((v >> (24 - 8 * j)) & 255) == 255) cnt++;
+        }
+        int incl = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            int y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        uint64_t pos = (uint64_t)hdr + w * 4 + run + (uint64_t)(incl - cnt);
+        if (w < we) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (w * 4 + j < nbytes) {
+                    uint8_t byte = (uint8_t)(v >> (24 - 8 * j));
+                    out[pos++] = byte;
+                    if (byte == 0xFF) out[pos++] = 0;
+                }
+            }
+        }
+        run += (uint64_t)__shfl(incl, 63, 64);
+    }
+    if (c == D.nchunks - 1 && lane == 0) {
+        out[S.out_len - 2] = 0xFF;
+        out[S.out_len - 1] = 0xD9;
+    }
+}
+
+// =================================================================== resize
+// ImageTools.resizeImage -> Graphics2D.drawImage(BILINEAR) -> Java2D
+// TransformHelper: inverse scale in 32.32 fixed point, source sample at the
+// pixel centre minus 0.5, edges clamped, 8-bit fraction weights, rounding at
+// bit 16 (BilinearInterp).  One thread per destination pixel.
+struct ResizeArgs {
+    const uint8_t* src;
+    uint8_t* dst;
+    int32_t sw, sh, sstride, nch;
+    int32_t dw, dh, dstride, pad;
+    int64_t x0l, dxl, y0l, dyl;
+};
+
+__global__ __launch_bounds__(256) void k_resize(ResizeArgs a)
+{
+    const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (dx >= a.dw || dy >= a.dh) return;
+    const int64_t half = (int64_t)1 << 31;
+    const int64_t yl = a.y0l + (int64_t)dy * a.dyl - half;
+    const int64_t xl = a.x0l + (int64_t)dx * a.dxl - half;
+    const int yw = (int)(yl >> 32), xw = (int)(xl >> 32);
+    const int yf = (int)((uint32_t)yl >> 24), xf = (int)((uint32_t)xl >> 24);
+    int ya, yb, xa, xb;
+    if (yw < 0) ya = yb = 0; else if (yw + 1 >= a.sh) ya = yb = yw; else { ya = yw; yb = yw + 1; }
+    if (xw < 0) xa = xb = 0; else if (xw + 1 >= a.sw) xa = xb = xw; else { xa = xw; xb = xw + 1; }
+    const uint8_t* ra = a.src + (size_t)ya * a.sstride;
+    const uint8_t* rb = a.src + (size_t)yb * a.sstride;
+    uint8_t* o = a.dst + (size_t)dy * a.dstride + (size_t)dx * a.nch;
+    for (int c = 0; c < a.nch; c++) {
+        int p00 = ra[a.nch * xa + c], p01 = ra[a.nch * xb + c];
+        int p10 = rb[a.nch * xa + c], p11 = rb[a.nch * xb + c];
+        int top = (p00 << 8) + (p01 - p00) * xf;
+        int bot = (p10 << 8) + (p11 - p10) * xf;
+        int v = (top << 8) + (bot - top) * yf;
+        o[c] = (uint8_t)((v + (1 << 15)) >> 16);
+    }
+}
+
+// =================================================================== host side
+hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat[64],
+                            const uint32_t dc[2][16], const uint32_t ac[2][256],
+                            const uint8_t hdr[2][HDR_COLOR])
+{
+    hipError_t e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_nat_to_zz), nat_to_zz, 64))) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_zz_to_nat), zz_to_nat, 64))) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_dc), dc, sizeof(uint32_t) * 2 * 16))) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_ac), ac, sizeof(uint32_t) * 2 * 256))) return e;
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_hdr), hdr, 2 * HDR_COLOR);
+}
+
+static inline unsigned grid_of(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+void launch_fdct(const ImgDesc* d, const Plan& p, int64_t tiles, int kind, hipStream_t st)
+{
+    if (tiles <= 0) return;
+    if (kind == 2)
+        hipLaunchKernelGGL(k_fdct_gray, dim3((unsigned)tiles), dim3(256), 0, st, d, p.ids, p.prefix, p.m);
+    else if (kind == 0)
+        hipLaunchKernelGGL(k_fdct_color<true>, dim3((unsigned)tiles), dim3(256), 0, st, d, p.ids, p.prefix, p.m);
+    else
+        hipLaunchKernelGGL(k_fdct_color<false>, dim3((unsigned)tiles), dim3(256), 0, st, d, p.ids, p.prefix, p.m);
+}
+
+void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, hipStream_t st)
+{
+    if (chunks <= 0) return;
+    hipLaunchKernelGGL(k_huff, dim3((unsigned)chunks), dim3(256), 0, st, d, s, n, p.ids, p.prefix, p.m);
+}
+
+void launch_scan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_scan, dim3(p.m), dim3(1024), 0, st, d, s, p.ids, p.m);
+}
+
+void launch_ffcount(const ImgDesc* d, ImgState* s, const Plan& p, int64_t chunks, int use_best, hipStream_t st)
+{
+    if (chunks <= 0) return;
+    hipLaunchKernelGGL(k_ffcount, dim3(grid_of(chunks, 4)), dim3(256), 0, st, d, s, p.ids, p.prefix, p.m, use_best);
+}
+
+void launch_decide(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_decide, dim3(grid_of(p.m, 64)), dim3(64), 0, st, d, s, n, p.ids, p.m);
+}
+
+void launch_ffscan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_ffscan, dim3(p.m), dim3(1024), 0, st, d, s, p.ids, p.m);
+}
+
+void launch_stuff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, hipStream_t st)
+{
+    if (chunks <= 0) return;
+    hipLaunchKernelGGL(k_stuff, dim3(grid_of(chunks, 4)), dim3(256), 0, st, d, s, n, p.ids, p.prefix, p.m);
+}
+
+void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int nch, uint8_t* dst, int dw, int dh,
+                   int dstride, hipStream_t st)
+{
+    ResizeArgs a;
+    a.src = src; a.dst = dst;
+    a.sw = sw; a.sh = sh; a.sstride = sstride; a.nch = nch;
+    a.dw = dw; a.dh = dh; a.dstride = dstride; a.pad = 0;
+    // AffineTransform.scale(dw/sw, dh/sh).createInverse(): m00 = 1.0 / (dw/sw)
+    const double ix = 1.0 / ((double)dw / sw), iy = 1.0 / ((double)dh / sh);
+    a.dxl = (int64_t)(ix * 4294967296.0);
+    a.dyl = (int64_t)(iy * 4294967296.0);
+    a.x0l = (int64_t)(0.5 * ix * 4294967296.0);  // transform of the first pixel centre (0.5)
+    a.y0l = (int64_t)(0.5 * iy * 4294967296.0);
+    hipLaunchKernelGGL(k_resize, dim3(grid_of(dw, 64), grid_of(dh, 4)), dim3(256), 0, st, a);
+}
+
+}  // namespace icx

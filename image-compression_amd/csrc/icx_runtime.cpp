@@ -1,0 +1,1172 @@
+// icx_runtime.cpp — host runtime behind include/icx.h.
+//
+// Owns one HIP stream, a device workspace arena and a pinned staging arena
+// per context, builds the binary-search trees (all float32 decisions of
+// ImageCompressionJpg.java:158-200 are evaluated here, in Java's order of
+// operations), and drives the batched stage loop of compressJpgWithTargetSize
+// (ImageCompressionJpg.java:77-122) on the device: per stage one FDCT launch,
+// then the quality trials as a fixed sequence of launches with the search
+// state kept in HBM (no host round trip between trials), then one host
+// synchronisation to decide which images move on to the next 0.85x scale.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/icx.h"
+#include "icx_internal.h"
+#include "icx_kernels.h"
+
+using namespace icx;
+
+namespace {
+
+// ------------------------------------------------------------ constants
+// JPEGQTable.K1Luminance / K2Chrominance (ITU-T T.81 Annex K.1/K.2), natural order.
+const int kK1[64] = {16, 11, 10, 16, 24, 40, 51, 61, 12, 12, 14, 19, 26, 58, 60, 55,
+                     14, 13, 16, 24, 40, 57, 69, 56, 14, 17, 22, 29, 51, 87, 80, 62,
+                     18, 22, 37, 56, 68, 109, 103, 77, 24, 35, 55, 64, 81, 104, 113, 92,
+                     49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99};
+const int kK2[64] = {17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99,
+                     24, 26, 56, 99, 99, 99, 99, 99, 47, 66, 99, 99, 99, 99, 99, 99,
+                     99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99,
+                     99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99};
+// zig-zag position -> natural index (jpeg_natural_order)
+const uint8_t kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                             12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                             35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                             58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+// Annex K.3 standard Huffman tables (JPEGHuffmanTable.Std*): counts per length 1..16, symbols.
+const uint8_t kDcLumBits[16] = {0, 1, 5, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0};
+const uint8_t kDcChrBits[16] = {0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0};
+const uint8_t kDcVals[12] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
+const uint8_t kAcLumBits[16] = {0, 2, 1, 3, 3, 2, 4, 3, 5, 5, 4, 4, 0, 0, 1, 0x7d};
+const uint8_t kAcLumVals[162] = {
+    0x01, 0x02, 0x03, 0x00, 0x04, 0x11, 0x05, 0x12, 0x21, 0x31, 0x41, 0x06, 0x13, 0x51, 0x61, 0x07, 0x22, 0x71,
+    0x14, 0x32, 0x81, 0x91, 0xa1, 0x08, 0x23, 0x42, 0xb1, 0xc1, 0x15, 0x52, 0xd1, 0xf0, 0x24, 0x33, 0x62, 0x72,
+    0x82, 0x09, 0x0a, 0x16, 0x17, 0x18, 0x19, 0x1a, 0x25, 0x26, 0x27, 0x28, 0x29, 0x2a, 0x34, 0x35, 0x36, 0x37,
+    0x38, 0x39, 0x3a, 0x43, 0x44, 0x45, 0x46, 0x47, 0x48, 0x49, 0x4a, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58, 0x59,
+    0x5a, 0x63, 0x64, 0x65, 0x66, 0x67, 0x68, 0x69, 0x6a, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7a, 0x83,
+    0x84, 0x85, 0x86, 0x87, 0x88, 0x89, 0x8a, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97, 0x98, 0x99, 0x9a, 0xa2, 0xa3,
+    0xa4, 0xa5, 0xa6, 0xa7, 0xa8, 0xa9, 0xaa, 0xb2, 0xb3, 0xb4, 0xb5, 0xb6, 0xb7, 0xb8, 0xb9, 0xba, 0xc2, 0xc3,
+    0xc4, 0xc5, 0xc6, 0xc7, 0xc8, 0xc9, 0xca, 0xd2, 0xd3, 0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda, 0xe1, 0xe2,
+    0xe3, 0xe4, 0xe5, 0xe6, 0xe7, 0xe8, 0xe9, 0xea, 0xf1, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8, 0xf9, 0xfa};
+const uint8_t kAcChrBits[16] = {0, 2, 1, 2, 4, 4, 3, 4, 7, 5, 4, 4, 0, 1, 2, 0x77};
+const uint8_t kAcChrVals[162] = {
+    0x00, 0x01, 0x02, 0x03, 0x11, 0x04, 0x05, 0x21, 0x31, 0x06, 0x12, 0x41, 0x51, 0x07, 0x61, 0x71, 0x13, 0x22,
+    0x32, 0x81, 0x08, 0x14, 0x42, 0x91, 0xa1, 0xb1, 0xc1, 0x09, 0x23, 0x33, 0x52, 0xf0, 0x15, 0x62, 0x72, 0xd1,
+    0x0a, 0x16, 0x24, 0x34, 0xe1, 0x25, 0xf1, 0x17, 0x18, 0x19, 0x1a, 0x26, 0x27, 0x28, 0x29, 0x2a, 0x35, 0x36,
+    0x37, 0x38, 0x39, 0x3a, 0x43, 0x44, 0x45, 0x46, 0x47, 0x48, 0x49, 0x4a, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58,
+    0x59, 0x5a, 0x63, 0x64, 0x65, 0x66, 0x67, 0x68, 0x69, 0x6a, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7a,
+    0x82, 0x83, 0x84, 0x85, 0x86, 0x87, 0x88, 0x89, 0x8a, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97, 0x98, 0x99, 0x9a,
+    0xa2, 0xa3, 0xa4, 0xa5, 0xa6, 0xa7, 0xa8, 0xa9, 0xaa, 0xb2, 0xb3, 0xb4, 0xb5, 0xb6, 0xb7, 0xb8, 0xb9, 0xba,
+    0xc2, 0xc3, 0xc4, 0xc5, 0xc6, 0xc7, 0xc8, 0xc9, 0xca, 0xd2, 0xd3, 0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda,
+    0xe2, 0xe3, 0xe4, 0xe5, 0xe6, 0xe7, 0xe8, 0xe9, 0xea, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8, 0xf9, 0xfa};
+
+// ------------------------------------------------------- float32 quality math
+// Java float arithmetic; volatile locals keep every product/sum rounded to
+// float32 (no contraction, no extended precision).
+float linear_quality(float q)  // JPEG.convertToLinearQuality
+{
+    if (q <= 0.0f) q = 0.01f;
+    if (q > 1.0f) q = 1.0f;
+    if (q < 0.5f) {
+        volatile float r = 0.5f / q;
+        return r;
+    }
+    volatile float t = q * 2.0f;
+    volatile float r = 2.0f - t;
+    return r;
+}
+
+void scaled_table(const int* base, float lin, uint16_t* out)  // JPEGQTable.getScaledInstance(lin, true)
+{
+    for (int i = 0; i < 64; i++) {
+        volatile float p = (float)base[i] * lin;
+        volatile float s = p + 0.5f;
+        int sv = (int)s;
+        out[i] = (uint16_t)std::min(255, std::max(1, sv));
+    }
+}
+
+void make_node(float q, QNode& n)
+{
+    uint16_t t[2][64];
+    const float lin = linear_quality(q);
+    scaled_table(kK1, lin, t[0]);
+    scaled_table(kK2, lin, t[1]);
+    n.mid = q;
+    n.child_fit = n.child_nofit = -1;
+    n.pad = 0;
+    for (int c = 0; c < 2; c++) {
+        for (int k = 0; k < 64; k++) {
+            const uint32_t div = (uint32_t)t[c][kZigzag[k]] << 3;
+            n.rcp[c][k] = (uint32_t)((1ull << 32) / div + 1);
+            n.half[c][k] = (uint16_t)(div >> 1);
+        }
+        for (int i = 0; i < 64; i++) n.qt[c][i] = t[c][i];
+    }
+}
+
+// Tree of findBestQualityByBinarySearch: a node is the loop state (lo, hi, i)
+// at the top of an iteration that performs an encode.
+int build_tree(float lo, float hi, int iter, std::vector<QNode>& nodes, int& depth)
+{
+    if (iter >= MAX_TRIALS) return -1;
+    volatile float sum = lo + hi;
+    volatile float mid = sum / 2.0f;  // (lowQuality + highQuality) / 2.0f
+    if (mid < 0.01f) return -1;       // midQuality < 0.01f -> break
+    const int idx = (int)nodes.size();
+    nodes.emplace_back();
+    make_node(mid, nodes[idx]);
+    depth = std::max(depth, iter + 1);
+    volatile float dfit = hi - mid;   // fits: lowQuality = mid
+    volatile float dno = mid - lo;    // too big: highQuality = mid
+    const int cf = dfit < 0.01f ? -1 : build_tree(mid, hi, iter + 1, nodes, depth);
+    const int cn = dno < 0.01f ? -1 : build_tree(lo, mid, iter + 1, nodes, depth);
+    nodes[idx].child_fit = cf;
+    nodes[idx].child_nofit = cn;
+    return idx;
+}
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// ------------------------------------------------------------ arenas
+struct DevArena {
+    uint8_t* base = nullptr;
+    size_t cap = 0, used = 0;
+    hipError_t reserve(size_t bytes)
+    {
+        if (bytes <= cap) return hipSuccess;
+        if (base) hipFree(base);
+        base = nullptr;
+        cap = 0;
+        size_t want = std::max(bytes, cap * 3 / 2);
+        hipError_t e = hipMalloc(&base, want);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            e = hipMalloc(&base, bytes);
+            if (e != hipSuccess) return e;
+            want = bytes;
+        }
+        cap = want;
+        return hipSuccess;
+    }
+    void* take(size_t n)
+    {
+        used = align_up(used, 256);
+        void* p = base + used;
+        used += n;
+        return p;
+    }
+    ~DevArena() { if (base) hipFree(base); }
+};
+
+struct HostArena {
+    uint8_t* base = nullptr;
+    size_t cap = 0, used = 0;
+    hipError_t reserve(size_t bytes)
+    {
+        if (bytes <= cap) return hipSuccess;
+        if (base) hipHostFree(base);
+        base = nullptr;
+        size_t want = std::max(bytes, cap * 2);
+        hipError_t e = hipHostMalloc((void**)&base, want, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        cap = want;
+        return hipSuccess;
+    }
+    void* take(size_t n)
+    {
+        used = align_up(used, 64);
+        if (used + n > cap) return nullptr;
+        void* p = base + used;
+        used += n;
+        return p;
+    }
+    ~HostArena() { if (base) hipHostFree(base); }
+};
+
+struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+    int64_t units;
+};
+
+struct KStat {
+    int64_t launches = 0, units = 0;
+    double ms = 0;
+};
+
+int channels(int fmt) { return fmt == ICX_GRAY8 ? 1 : 3; }
+
+void geometry(ImgDesc& d, int w, int h, int fmt)
+{
+    d.w = w;
+    d.h = h;
+    d.fmt = fmt;
+    d.ncomp = fmt == ICX_GRAY8 ? 1 : 3;
+    d.ywb = (w + 7) / 8;
+    d.yhb = (h + 7) / 8;
+    if (d.ncomp == 1) {
+        d.mcux = d.ywb;
+        d.mcuy = d.yhb;
+        d.nblocks = (int64_t)d.mcux * d.mcuy;
+        d.hdr_len = HDR_GRAY;
+    } else {
+        d.mcux = (w + 15) / 16;
+        d.mcuy = (h + 15) / 16;
+        d.nblocks = (int64_t)d.mcux * d.mcuy * 6;
+        d.hdr_len = HDR_COLOR;
+    }
+    d.nchunks = (int)((d.nblocks + CHUNK_BLOCKS - 1) / CHUNK_BLOCKS);
+}
+
+int64_t fdct_tiles(const ImgDesc& d)
+{
+    return d.ncomp == 1 ? (int64_t)((d.mcux + 15) / 16) * d.mcuy : (int64_t)((d.mcux + 7) / 8) * d.mcuy;
+}
+
+// worst-case entropy bytes after stuffing
+uint64_t worst_file(const ImgDesc& d) { return (uint64_t)d.hdr_len + (uint64_t)d.nblocks * (MAX_BLOCK_BITS / 8) * 2 + 16; }
+
+bool is_device_ptr(const void* p)
+{
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+}  // namespace
+
+// ============================================================ context
+struct icx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::recursive_mutex mu;
+    std::string err;
+    DevArena dev;
+    HostArena host;
+    bool prof = false;
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> evpool;
+    std::map<std::string, KStat> stats;
+    size_t budget = 0;  // device workspace budget per sub-batch
+};
+
+namespace {
+
+icx_status fail(icx_ctx* c, icx_status s, const char* msg)
+{
+    if (c) c->err = msg;
+    return s;
+}
+
+icx_status hip_fail(icx_ctx* c, hipError_t e, const char* where)
+{
+    if (c) c->err = std::string(where) + ": " + hipGetErrorString(e);
+    (void)hipGetLastError();
+    return e == hipErrorOutOfMemory ? ICX_E_NOMEM : ICX_E_DEVICE;
+}
+
+hipEvent_t get_event(icx_ctx* c)
+{
+    if (!c->evpool.empty()) {
+        hipEvent_t e = c->evpool.back();
+        c->evpool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+}
+
+struct Timed {  // brackets one launch with events when profiling is on
+    icx_ctx* c;
+    Pending p;
+    bool on;
+    Timed(icx_ctx* ctx, const char* name, int64_t units) : c(ctx), on(ctx->prof)
+    {
+        if (!on) return;
+        p.name = name;
+        p.units = units;
+        p.a = get_event(c);
+        p.b = get_event(c);
+        hipEventRecord(p.a, c->stream);
+    }
+    ~Timed()
+    {
+        if (!on) return;
+        hipEventRecord(p.b, c->stream);
+        c->pending.push_back(p);
+    }
+};
+
+void resolve_profile(icx_ctx* c)  // call after a stream synchronisation
+{
+    for (auto& p : c->pending) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, p.a, p.b);
+        KStat& s = c->stats[p.name];
+        s.launches++;
+        s.ms += ms;
+        s.units += p.units;
+        c->evpool.push_back(p.a);
+        c->evpool.push_back(p.b);
+    }
+    c->pending.clear();
+}
+
+// ---------------------------------------------------------------- batch driver
+struct Item {
+    icx_fit_job* job;
+    int kind;              // 0 BGR, 1 RGB, 2 GRAY
+    int nch;
+    ImgDesc orig;          // geometry of the original image
+    const uint8_t* dpx;    // original pixels on device
+    uint8_t* dresize;
+    uint8_t* dout;
+    bool host_out;
+    int root;              // search tree root for this job's quality bound
+    int depth;
+    int cached_node;
+    double coef_scale;     // scale whose coefficients are resident, NaN = none
+    bool done, found, hit;
+    float best_q;
+    double best_scale;
+    int encodes;
+};
+
+enum class Mode { Fit, Encode, Search, Fdct };
+
+struct Batch {
+    icx_ctx* c;
+    std::vector<Item> it;
+    std::vector<QNode> nodes;
+    ImgDesc* d_desc = nullptr;
+    ImgState* d_state = nullptr;
+    QNode* d_nodes = nullptr;
+    std::vector<ImgDesc> desc;
+    std::vector<ImgState> state;
+    ImgState* h_state = nullptr;  // pinned mirror for downloads
+};
+
+struct DPlan {
+    Plan p;
+    int64_t total;
+};
+
+icx_status upload(icx_ctx* c, void* dst, const void* src, size_t n)
+{
+    void* h = c->host.take(n);
+    if (!h) return fail(c, ICX_E_NOMEM, "pinned staging exhausted");
+    memcpy(h, src, n);
+    hipError_t e = hipMemcpyAsync(dst, h, n, hipMemcpyHostToDevice, c->stream);
+    return e == hipSuccess ? ICX_OK : hip_fail(c, e, "hipMemcpyAsync(H2D)");
+}
+
+// Build a launch plan over `ids` with per-image work counts.
+icx_status make_plan(Batch& B, const std::vector<int>& ids, const std::vector<int64_t>& counts, DPlan& out)
+{
+    icx_ctx* c = B.c;
+    std::vector<int64_t> pre(ids.size() + 1, 0);
+    for (size_t i = 0; i < ids.size(); i++) pre[i + 1] = pre[i] + counts[i];
+    int32_t* d_ids = (int32_t*)c->dev.take(ids.size() * sizeof(int32_t) + 4);
+    int64_t* d_pre = (int64_t*)c->dev.take(pre.size() * sizeof(int64_t));
+    std::vector<int32_t> ids32(ids.begin(), ids.end());
+    icx_status s;
+    if (!ids32.empty() && (s = upload(c, d_ids, ids32.data(), ids32.size() * 4))) return s;
+    if ((s = upload(c, d_pre, pre.data(), pre.size() * 8))) return s;
+    out.p.ids = d_ids;
+    out.p.prefix = d_pre;
+    out.p.m = (int32_t)ids.size();
+    out.total = pre.back();
+    return ICX_OK;
+}
+
+icx_status sync_states(Batch& B)
+{
+    icx_ctx* c = B.c;
+    hipError_t e = hipMemcpyAsync(B.h_state, B.d_state, sizeof(ImgState) * B.state.size(), hipMemcpyDeviceToHost,
+                                  c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "state download");
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
+    memcpy(B.state.data(), B.h_state, sizeof(ImgState) * B.state.size());
+    resolve_profile(c);
+    return ICX_OK;
+}
+
+icx_status push_desc_state(Batch& B)
+{
+    icx_status s = upload(B.c, B.d_desc, B.desc.data(), sizeof(ImgDesc) * B.desc.size());
+    if (s) return s;
+    return upload(B.c, B.d_state, B.state.data(), sizeof(ImgState) * B.state.size());
+}
+
+// Point image i's descriptor at its pixels for `scale` (resizing on device).
+void stage_pixels(Batch& B, int i, double scale)
+{
+    icx_ctx* c = B.c;
+    Item& I = B.it[i];
+    ImgDesc& d = B.desc[i];
+    const ImgDesc keep = d;
+    if (scale < 1.0) {
+        int32_t dw, dh;
+        icx_scaled_dims(I.orig.w, I.orig.h, scale, &dw, &dh);
+        {
+            Timed tm(c, "resize", (int64_t)dw * dh);
+            launch_resize(I.dpx, I.orig.w, I.orig.h, I.orig.stride, I.nch, I.dresize, dw, dh, dw * I.nch, c->stream);
+        }
+        geometry(d, dw, dh, I.orig.fmt);
+        d.px = I.dresize;
+        d.stride = dw * I.nch;
+    } else {
+        geometry(d, I.orig.w, I.orig.h, I.orig.fmt);
+        d.px = I.dpx;
+        d.stride = I.orig.stride;
+    }
+    // buffers and limits stay those sized for the original image
+    d.coefs = keep.coefs;
+    for (int k = 0; k < 2; k++) {
+        d.scratch[k] = keep.scratch[k];
+        d.chunk_bits[k] = keep.chunk_bits[k];
+        d.chunk_off[k] = keep.chunk_off[k];
+        d.chunk_ff[k] = keep.chunk_ff[k];
+    }
+    d.chunk_ffoff = keep.chunk_ffoff;
+    d.out = keep.out;
+    d.cap = keep.cap;
+    d.target = keep.target;
+}
+
+icx_status run_fdct(Batch& B, const std::vector<int>& ids)
+{
+    for (int kind = 0; kind < 3; kind++) {
+        std::vector<int> sel;
+        std::vector<int64_t> cnt;
+        for (int i : ids)
+            if (B.it[i].kind == kind) {
+                sel.push_back(i);
+                cnt.push_back(fdct_tiles(B.desc[i]));
+            }
+        if (sel.empty()) continue;
+        DPlan P;
+        icx_status s = make_plan(B, sel, cnt, P);
+        if (s) return s;
+        int64_t px = 0;
+        for (int i : sel) px += (int64_t)B.desc[i].w * B.desc[i].h;
+        Timed tm(B.c, "fdct", px);
+        launch_fdct(B.d_desc, P.p, P.total, kind, B.c->stream);
+    }
+    return ICX_OK;
+}
+
+icx_status run_trials(Batch& B, const std::vector<int>& ids, int depth)
+{
+    std::vector<int64_t> cnt;
+    int64_t blocks = 0;
+    for (int i : ids) {
+        cnt.push_back(B.desc[i].nchunks);
+        blocks += B.desc[i].nblocks;
+    }
+    DPlan P;
+    icx_status s = make_plan(B, ids, cnt, P);
+    if (s) return s;
+    icx_ctx* c = B.c;
+    for (int t = 0; t < depth; t++) {
+        { Timed tm(c, "huff", blocks); launch_huff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
+        { Timed tm(c, "scan", (int64_t)ids.size()); launch_scan(B.d_desc, B.d_state, P.p, c->stream); }
+        { Timed tm(c, "ffcount", P.total); launch_ffcount(B.d_desc, B.d_state, P.p, P.total, 0, c->stream); }
+        { Timed tm(c, "decide", (int64_t)ids.size()); launch_decide(B.d_desc, B.d_state, B.d_nodes, P.p, c->stream); }
+    }
+    return ICX_OK;
+}
+
+icx_status run_final(Batch& B, const std::vector<int>& ids)
+{
+    std::vector<int64_t> cnt;
+    for (int i : ids) cnt.push_back(B.desc[i].nchunks);
+    DPlan P;
+    icx_status s = make_plan(B, ids, cnt, P);
+    if (s) return s;
+    icx_ctx* c = B.c;
+    { Timed tm(c, "ffscan", (int64_t)ids.size()); launch_ffscan(B.d_desc, B.d_state, P.p, c->stream); }
+    { Timed tm(c, "stuff", P.total); launch_stuff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
+    return ICX_OK;
+}
+
+void init_state(ImgState& s, int node, bool force)
+{
+    memset(&s, 0, sizeof(s));
+    s.node = node;
+    s.best_node = -1;
+    s.cur = 0;
+    s.best_buf = 1;
+    s.active = node >= 0;
+    s.force = force;
+}
+
+int kind_of(int fmt) { return fmt == ICX_BGR24 ? 0 : fmt == ICX_RGB24 ? 1 : 2; }
+
+icx_status validate(const icx_image* img)
+{
+    if (!img || !img->px) return ICX_E_NULL;
+    if (img->width <= 0 || img->height <= 0 || img->width > 65535 || img->height > 65535) return ICX_E_INVALID;
+    if (img->fmt < ICX_BGR24 || img->fmt > ICX_GRAY8) return ICX_E_INVALID;
+    if (img->stride < img->width * channels(img->fmt)) return ICX_E_INVALID;
+    return ICX_OK;
+}
+
+// Core driver.  mode Fit: A2 per job; Encode: A4 (job.quality, forced);
+// Search: A3 only (no output); Fdct: coefficients only (debug).
+icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* fdct_out = nullptr,
+                     ImgState* search_out = nullptr)
+{
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    hipError_t he = hipSetDevice(c->device);
+    if (he != hipSuccess) return hip_fail(c, he, "hipSetDevice");
+    std::vector<int> order;
+    for (int i = 0; i < n; i++) {
+        icx_fit_job& j = jobs[i];
+        j.success = 0;
+        j.cache_hit = 0;
+        j.out_len = 0;
+        j.learned.quality = -1.0f;
+        j.learned.scale = 0.0;
+        j.encodes = 0;
+        j.status = validate(&j.img);
+        if (j.status == ICX_OK && mode != Mode::Search && mode != Mode::Fdct && !j.out) j.status = ICX_E_NULL;
+        if (j.status == ICX_OK) order.push_back(i);
+    }
+    size_t pos = 0;
+    while (pos < order.size()) {
+        // ---- size a sub-batch against the workspace budget
+        std::vector<int> sub;
+        size_t need = 1 << 20;
+        while (pos < order.size()) {
+            icx_fit_job& j = jobs[order[pos]];
+            ImgDesc g{};
+            geometry(g, j.img.width, j.img.height, j.img.fmt);
+            const int nch = channels(j.img.fmt);
+            size_t per = (size_t)g.nblocks * 128 + 2 * ((size_t)g.nchunks * CHUNK_WORDS + 1) * 4 +
+                         (size_t)g.nchunks * (2 * 4 + 2 * 8 + 2 * 4 + 8) + 64 + 8 * 256;
+            per += (size_t)j.img.width * j.img.height * nch * 2;  // input staging + resize buffer
+            per += std::min<uint64_t>(worst_file(g), j.cap);
+            if (!sub.empty() && need + per > c->budget) break;
+            need += per;
+            sub.push_back(order[pos++]);
+        }
+        hipError_t e = c->dev.reserve(need + ((size_t)sub.size() + 8) * 4096 + (16 << 20));
+        if (e != hipSuccess) {
+            for (int i : sub) jobs[i].status = ICX_E_NOMEM;
+            (void)hipGetLastError();
+            c->err = "device workspace allocation failed";
+            continue;
+        }
+        c->dev.used = 0;
+        e = c->host.reserve(64 << 20);
+        if (e != hipSuccess) return hip_fail(c, e, "hipHostMalloc");
+        c->host.used = 0;
+
+        Batch B;
+        B.c = c;
+        const int m = (int)sub.size();
+        B.it.resize(m);
+        B.desc.assign(m, ImgDesc{});
+        B.state.assign(m, ImgState{});
+        int max_depth = 0;
+        std::map<uint32_t, int> tree_of_q;   // bit pattern of q0 -> root
+        std::map<uint32_t, int> depth_of_q;
+        std::map<uint32_t, int> single_of_q; // fixed-quality node
+        auto single = [&](float q) {
+            uint32_t key;
+            memcpy(&key, &q, 4);
+            auto f = single_of_q.find(key);
+            if (f != single_of_q.end()) return f->second;
+            int idx = (int)B.nodes.size();
+            B.nodes.emplace_back();
+            make_node(q, B.nodes[idx]);
+            single_of_q[key] = idx;
+            return idx;
+        };
+        for (int k = 0; k < m; k++) {
+            icx_fit_job& j = jobs[sub[k]];
+            Item& I = B.it[k];
+            I.job = &j;
+            I.kind = kind_of(j.img.fmt);
+            I.nch = channels(j.img.fmt);
+            I.done = I.found = I.hit = false;
+            I.best_q = -1.0f;
+            I.best_scale = 0;
+            I.encodes = 0;
+            I.coef_scale = NAN;
+            I.root = I.cached_node = -1;
+            I.depth = 0;
+            ImgDesc& d = B.desc[k];
+            geometry(d, j.img.width, j.img.height, j.img.fmt);
+            d.stride = j.img.stride;
+            d.target = j.target_max_size;
+            d.coefs = (int16_t*)c->dev.take((size_t)d.nblocks * 128);
+            for (int b = 0; b < 2; b++) {
+                d.scratch[b] = (uint32_t*)c->dev.take(((size_t)d.nchunks * CHUNK_WORDS + 1) * 4);
+                d.chunk_bits[b] = (uint32_t*)c->dev.take((size_t)d.nchunks * 4);
+                d.chunk_off[b] = (uint64_t*)c->dev.take(((size_t)d.nchunks + 1) * 8);
+                d.chunk_ff[b] = (uint32_t*)c->dev.take((size_t)d.nchunks * 4);
+            }
+            d.chunk_ffoff = (uint64_t*)c->dev.take((size_t)d.nchunks * 8);
+            // input pixels
+            if (is_device_ptr(j.img.px)) {
+                I.dpx = j.img.px;
+            } else {
+                const size_t row = (size_t)j.img.width * I.nch;
+                uint8_t* st = (uint8_t*)c->dev.take(row * j.img.height);
+                e = hipMemcpy2DAsync(st, row, j.img.px, j.img.stride, row, j.img.height, hipMemcpyHostToDevice,
+                                     c->stream);
+                if (e != hipSuccess) return hip_fail(c, e, "input upload");
+                I.dpx = st;
+                d.stride = (int32_t)row;
+            }
+            d.px = I.dpx;
+            I.orig = d;
+            I.dresize = (mode == Mode::Fit) ? (uint8_t*)c->dev.take((size_t)j.img.width * j.img.height * I.nch)
+                                            : nullptr;
+            // output
+            I.host_out = false;
+            I.dout = nullptr;
+            if (mode == Mode::Fit || mode == Mode::Encode) {
+                if (is_device_ptr(j.out)) {
+                    I.dout = j.out;
+                    d.cap = j.cap;
+                } else {
+                    const uint64_t cap = std::min<uint64_t>(worst_file(d), j.cap);
+                    I.dout = (uint8_t*)c->dev.take(cap);
+                    I.host_out = true;
+                    d.cap = cap;
+                    if (cap < j.cap) d.cap = cap;  // staging bound >= any file we can produce
+                }
+            }
+            d.out = I.dout;
+            I.orig = d;
+            // quality nodes
+            if (mode == Mode::Fit || mode == Mode::Search) {
+                uint32_t key;
+                memcpy(&key, &j.quality, 4);
+                auto f = tree_of_q.find(key);
+                if (f == tree_of_q.end()) {
+                    int depth = 0;
+                    int root = build_tree(0.0f, j.quality, 0, B.nodes, depth);
+                    tree_of_q[key] = root;
+                    depth_of_q[key] = depth;
+                    f = tree_of_q.find(key);
+                }
+                I.root = f->second;
+                I.depth = depth_of_q[key];
+                max_depth = std::max(max_depth, I.depth);
+                if (mode == Mode::Fit && j.has_cached) I.cached_node = single(j.cached.quality);
+            } else if (mode == Mode::Encode) {
+                I.cached_node = single(j.quality);
+            }
+        }
+        if (B.nodes.empty()) B.nodes.emplace_back();
+        B.d_desc = (ImgDesc*)c->dev.take(sizeof(ImgDesc) * m);
+        B.d_state = (ImgState*)c->dev.take(sizeof(ImgState) * m);
+        B.d_nodes = (QNode*)c->dev.take(sizeof(QNode) * B.nodes.size());
+        B.h_state = (ImgState*)c->host.take(sizeof(ImgState) * m);
+        if (!B.h_state) return fail(c, ICX_E_NOMEM, "pinned staging exhausted");
+        icx_status s = upload(c, B.d_nodes, B.nodes.data(), sizeof(QNode) * B.nodes.size());
+        if (s) return s;
+
+        std::vector<int> all(m);
+        for (int k = 0; k < m; k++) all[k] = k;
+
+        if (mode == Mode::Fdct) {
+            for (int k = 0; k < m; k++) init_state(B.state[k], -1, false);
+            if ((s = push_desc_state(B)) || (s = run_fdct(B, all)) || (s = sync_states(B))) return s;
+            e = hipMemcpy(fdct_out, B.desc[0].coefs, (size_t)B.desc[0].nblocks * 128, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return hip_fail(c, e, "coef download");
+            continue;
+        }
+
+        auto finish_found = [&](const std::vector<int>& ids) -> icx_status {
+            if (ids.empty()) return ICX_OK;
+            icx_status st = run_final(B, ids);
+            if (st) return st;
+            return sync_states(B);
+        };
+
+        if (mode == Mode::Encode) {  // A4: one forced encode
+            for (int k = 0; k < m; k++) init_state(B.state[k], B.it[k].cached_node, true);
+            if ((s = push_desc_state(B)) || (s = run_fdct(B, all)) || (s = run_trials(B, all, 1)) ||
+                (s = sync_states(B)) || (s = finish_found(all)))
+                return s;
+            for (int k = 0; k < m; k++) {
+                B.it[k].found = B.state[k].best_node >= 0;
+                B.it[k].best_q = jobs[sub[k]].quality;
+                B.it[k].best_scale = 1.0;
+                B.it[k].encodes = B.state[k].ntrials;
+            }
+        } else {
+            // ---- stage 0: tryCachedParams (ImageCompressionJpg.java:82-89, :216-238)
+            std::vector<int> probe;
+            if (mode == Mode::Fit)
+                for (int k = 0; k < m; k++)
+                    if (B.it[k].cached_node >= 0) probe.push_back(k);
+            for (int k = 0; k < m; k++) init_state(B.state[k], -1, false);
+            if (!probe.empty()) {
+                for (int k : probe) {
+                    const double sc = jobs[sub[k]].cached.scale;
+                    stage_pixels(B, k, sc < 1.0 ? sc : 1.0);
+                    init_state(B.state[k], B.it[k].cached_node, false);
+                    B.it[k].coef_scale = sc < 1.0 ? sc : 1.0;
+                }
+                if ((s = push_desc_state(B)) || (s = run_fdct(B, probe)) || (s = run_trials(B, probe, 1)) ||
+                    (s = sync_states(B)))
+                    return s;
+                std::vector<int> hits;
+                for (int k : probe) {
+                    B.it[k].encodes += B.state[k].ntrials;
+                    if (B.state[k].best_node >= 0) {
+                        Item& I = B.it[k];
+                        I.found = I.hit = I.done = true;
+                        I.best_q = jobs[sub[k]].cached.quality;
+                        I.best_scale = jobs[sub[k]].cached.scale;
+                        hits.push_back(k);
+                    }
+                }
+                if ((s = finish_found(hits))) return s;
+            }
+            // ---- scale loop (ImageCompressionJpg.java:91-115)
+            std::vector<int> pend;
+            for (int k = 0; k < m; k++)
+                if (!B.it[k].done) pend.push_back(k);
+            const double STEP = 0.85;
+            for (double scale = 1.0; scale > 0.1 && !pend.empty(); scale = (scale == 1.0) ? STEP : scale * STEP) {
+                std::vector<int> need_fdct;
+                int depth = 0;
+                for (int k : pend) {
+                    if (!(B.it[k].coef_scale == scale)) {
+                        stage_pixels(B, k, scale);
+                        need_fdct.push_back(k);
+                        B.it[k].coef_scale = scale;
+                    }
+                    init_state(B.state[k], B.it[k].root, false);
+                    depth = std::max(depth, B.it[k].depth);
+                }
+                if ((s = push_desc_state(B)) || (s = run_fdct(B, need_fdct)) || (s = run_trials(B, pend, depth)) ||
+                    (s = sync_states(B)))
+                    return s;
+                std::vector<int> found, rest;
+                for (int k : pend) {
+                    Item& I = B.it[k];
+                    I.encodes += B.state[k].ntrials;
+                    if (mode == Mode::Search) {  // A3 only: report the first scale's search
+                        I.done = true;
+                        I.found = B.state[k].best_node >= 0;
+                        I.best_q = I.found ? B.nodes[B.state[k].best_node].mid : -1.0f;
+                        continue;
+                    }
+                    if (B.state[k].best_node >= 0) {
+                        I.found = I.done = true;
+                        I.best_q = B.nodes[B.state[k].best_node].mid;
+                        I.best_scale = scale;
+                        found.push_back(k);
+                    } else {
+                        rest.push_back(k);
+                    }
+                }
+                if (mode == Mode::Search) break;
+                if ((s = finish_found(found))) return s;
+                pend.swap(rest);
+            }
+        }
+        // ---- results + host outputs
+        for (int k = 0; k < m; k++) {
+            Item& I = B.it[k];
+            icx_fit_job& j = *I.job;
+            j.encodes = I.encodes;
+            if (mode == Mode::Search) {
+                j.learned.quality = I.best_q;
+                j.success = I.found;
+                j.status = ICX_OK;
+                continue;
+            }
+            if (!I.found) {
+                j.success = 0;
+                j.status = ICX_OK;
+                continue;
+            }
+            j.success = 1;
+            j.cache_hit = I.hit;
+            j.learned.quality = I.best_q;
+            j.learned.scale = I.best_scale;
+            j.out_len = (size_t)B.state[k].out_len;
+            if (B.state[k].status == 4 || j.out_len > j.cap) {
+                j.status = ICX_E_BUFFER;
+                continue;
+            }
+            j.status = ICX_OK;
+            if (I.host_out) {
+                e = hipMemcpyAsync(j.out, I.dout, j.out_len, hipMemcpyDeviceToHost, c->stream);
+                if (e != hipSuccess) return hip_fail(c, e, "output download");
+            }
+        }
+        e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "hipStreamSynchronize");
+        resolve_profile(c);
+        if (search_out && m > 0 && sub[0] == 0) *search_out = B.state[0];  // trial record of job 0
+    }
+    return ICX_OK;
+}
+
+}  // namespace
+
+// ============================================================ C ABI
+extern "C" {
+
+int icx_abi_version(void) { return ICX_ABI_VERSION; }
+
+const char* icx_status_string(icx_status s)
+{
+    switch (s) {
+    case ICX_OK: return "ok";
+    case ICX_E_INVALID: return "invalid argument";
+    case ICX_E_NOMEM: return "out of memory";
+    case ICX_E_DEVICE: return "device error";
+    case ICX_E_BUFFER: return "output buffer too small";
+    case ICX_E_UNSUPPORTED: return "unsupported input";
+    case ICX_E_CORRUPT: return "corrupt input";
+    case ICX_E_NULL: return "null argument";
+    }
+    return "unknown";
+}
+
+const char* icx_last_error(const icx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+icx_status icx_create(int device, icx_ctx** out)
+{
+    if (!out) return ICX_E_NULL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        (void)hipGetLastError();
+        return ICX_E_DEVICE;
+    }
+    if (device < 0 || device >= n) return ICX_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return ICX_E_DEVICE;
+    icx_ctx* c = new icx_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return ICX_E_DEVICE;
+    }
+    // constant tables: zig-zag, Huffman codes, marker templates
+    static std::once_flag once;
+    static hipError_t up = hipSuccess;
+    std::call_once(once, [] {
+        uint8_t nat2zz[64], zz2nat[64];
+        for (int k = 0; k < 64; k++) {
+            zz2nat[k] = kZigzag[k];
+            nat2zz[kZigzag[k]] = (uint8_t)k;
+        }
+        uint32_t dc[2][16] = {}, ac[2][256] = {};
+        auto derive = [](const uint8_t* bits, const uint8_t* vals, uint32_t* tbl) {
+            unsigned code = 0;
+            int k = 0;
+            for (int l = 1; l <= 16; l++) {
+                for (int i = 0; i < bits[l - 1]; i++, k++) tbl[vals[k]] = (code++ << 8) | (uint32_t)l;
+                code <<= 1;
+            }
+        };
+        derive(kDcLumBits, kDcVals, dc[0]);
+        derive(kDcChrBits, kDcVals, dc[1]);
+        derive(kAcLumBits, kAcLumVals, ac[0]);
+        derive(kAcChrBits, kAcChrVals, ac[1]);
+        uint8_t hdr[2][HDR_COLOR] = {};
+        for (int g = 0; g < 2; g++) {
+            const int nc = g ? 3 : 1;
+            std::vector<uint8_t> h;
+            auto put = [&](std::initializer_list<int> v) { for (int x : v) h.push_back((uint8_t)x); };
+            put({0xFF, 0xD8});
+            // APP0 as the JDK's JFIFMarkerSegment writes it: JFIF 1.02, aspect-ratio units, 1x1
+            put({0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0x00, 0x01, 0x02, 0x00, 0x00, 0x01, 0x00, 0x01, 0x00, 0x00});
+            for (int t = 0; t < (nc == 3 ? 2 : 1); t++) {
+                put({0xFF, 0xDB, 0x00, 0x43, t});
+                for (int i = 0; i < 64; i++) h.push_back(0);  // DQT payload patched on device
+            }
+            put({0xFF, 0xC0, 0x00, 8 + 3 * nc, 8, 0, 0, 0, 0, nc});
+            if (nc == 1) put({1, 0x11, 0});
+            else put({1, 0x22, 0, 2, 0x11, 1, 3, 0x11, 1});
+            auto dht = [&](int idx, const uint8_t* bits, const uint8_t* vals) {
+                int cnt = 0;
+                for (int i = 0; i < 16; i++) cnt += bits[i];
+                put({0xFF, 0xC4, (19 + cnt) >> 8, (19 + cnt) & 255, idx});
+                for (int i = 0; i < 16; i++) h.push_back(bits[i]);
+                for (int i = 0; i < cnt; i++) h.push_back(vals[i]);
+            };
+            dht(0x00, kDcLumBits, kDcVals);
+            dht(0x10, kAcLumBits, kAcLumVals);
+            if (nc == 3) {
+                dht(0x01, kDcChrBits, kDcVals);
+                dht(0x11, kAcChrBits, kAcChrVals);
+            }
+            if (nc == 1) put({0xFF, 0xDA, 0x00, 0x08, 1, 1, 0x00, 0, 63, 0});
+            else put({0xFF, 0xDA, 0x00, 0x0C, 3, 1, 0x00, 2, 0x11, 3, 0x11, 0, 63, 0});
+            memcpy(hdr[g], h.data(), h.size());
+        }
+        up = upload_constants(nat2zz, zz2nat, dc, ac, hdr);
+    });
+    if (up != hipSuccess) {
+        hipStreamDestroy(c->stream);
+        delete c;
+        return ICX_E_DEVICE;
+    }
+    size_t budget_mb = 16384;
+    if (const char* env = getenv("ICX_WORKSPACE_MB")) budget_mb = (size_t)atoll(env);
+    c->budget = budget_mb << 20;
+    *out = c;
+    return ICX_OK;
+}
+
+void icx_destroy(icx_ctx* ctx)
+{
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    for (auto& p : ctx->pending) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
+    for (auto e : ctx->evpool) hipEventDestroy(e);
+    hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+void icx_quality_tables(float quality, uint16_t lum[64], uint16_t chrom[64])
+{
+    const float lin = linear_quality(quality);
+    if (lum) scaled_table(kK1, lin, lum);
+    if (chrom) scaled_table(kK2, lin, chrom);
+}
+
+void icx_create_key(int32_t width, int32_t height, int64_t file_size, icx_similarity_key* key)
+{
+    if (!key) return;
+    key->width_bucket = width / 100;
+    key->height_bucket = height / 100;
+    key->size_bucket = file_size / 102400;
+}
+
+int32_t icx_subsampling_factor(int32_t width, int32_t height)
+{
+    const int maxd = std::max(width, height);
+    int s = 1;
+    if (maxd > 4096) s = (int)std::floor((double)maxd / 4096);
+    if (s > 1) {  // Integer.highestOneBit
+        int hb = 1;
+        while (hb <= s / 2) hb <<= 1;
+        s = hb;
+    }
+    return s;
+}
+
+void icx_scaled_dims(int32_t width, int32_t height, double scale, int32_t* out_w, int32_t* out_h)
+{
+    const int nw = (int)(width * scale), nh = (int)(height * scale);
+    if (out_w) *out_w = std::max(1, nw);
+    if (out_h) *out_h = std::max(1, nh);
+}
+
+int32_t icx_jpeg_header_size(int32_t fmt) { return fmt == ICX_GRAY8 ? HDR_GRAY : HDR_COLOR; }
+
+int64_t icx_num_blocks(int32_t width, int32_t height, int32_t fmt)
+{
+    if (width <= 0 || height <= 0) return 0;
+    ImgDesc d{};
+    geometry(d, width, height, fmt);
+    return d.nblocks;
+}
+
+icx_status icx_compress_jpg_to_stream(icx_ctx* ctx, const icx_image* img, float quality, uint8_t* out, size_t cap,
+                                      size_t* out_len)
+{
+    if (!ctx || !img || !out || !out_len) return ICX_E_NULL;
+    icx_fit_job j{};
+    j.img = *img;
+    j.quality = quality;
+    j.out = out;
+    j.cap = cap;
+    j.target_max_size = INT64_MAX;
+    icx_status s = run_batch(ctx, &j, 1, Mode::Encode);
+    if (s) return s;
+    *out_len = j.out_len;
+    return j.status;
+}
+
+icx_status icx_find_best_quality(icx_ctx* ctx, const icx_image* img, int64_t target_max_size, float initial_quality,
+                                 float* best_quality, float* trial_q, int64_t* trial_size, int32_t* ntrials)
+{
+    if (!ctx || !img || !best_quality) return ICX_E_NULL;
+    icx_fit_job j{};
+    j.img = *img;
+    j.quality = initial_quality;
+    j.target_max_size = target_max_size;
+    ImgState st{};
+    icx_status s = run_batch(ctx, &j, 1, Mode::Search, nullptr, &st);
+    if (s) return s;
+    if (j.status) return j.status;
+    *best_quality = j.learned.quality;
+    const int nt = std::min<int>(st.ntrials, MAX_TRIALS);
+    for (int i = 0; i < nt; i++) {
+        if (trial_q) trial_q[i] = st.trial_q[i];
+        if (trial_size) trial_size[i] = st.trial_size[i];
+    }
+    if (ntrials) *ntrials = nt;
+    return ICX_OK;
+}
+
+icx_status icx_compress_jpg_with_target_size(icx_ctx* ctx, icx_fit_job* job)
+{
+    if (!ctx || !job) return ICX_E_NULL;
+    icx_status s = run_batch(ctx, job, 1, Mode::Fit);
+    return s ? s : job->status;
+}
+
+icx_status icx_compress_jpg_batch(icx_ctx* ctx, icx_fit_job* jobs, int32_t n)
+{
+    if (!ctx || (!jobs && n > 0)) return ICX_E_NULL;
+    if (n < 0) return ICX_E_INVALID;
+    return run_batch(ctx, jobs, n, Mode::Fit);
+}
+
+icx_status icx_debug_fdct(icx_ctx* ctx, const icx_image* img, int16_t* coefs, size_t ncoefs)
+{
+    if (!ctx || !img || !coefs) return ICX_E_NULL;
+    icx_status v = validate(img);
+    if (v) return v;
+    if ((int64_t)ncoefs < icx_num_blocks(img->width, img->height, img->fmt) * 64) return ICX_E_BUFFER;
+    icx_fit_job j{};
+    j.img = *img;
+    icx_status s = run_batch(ctx, &j, 1, Mode::Fdct, coefs);
+    return s ? s : j.status;
+}
+
+icx_status icx_resize_bilinear(icx_ctx* ctx, const icx_image* src, uint8_t* dst, int32_t dst_w, int32_t dst_h,
+                               int32_t dst_stride)
+{
+    if (!ctx || !src || !dst) return ICX_E_NULL;
+    icx_status v = validate(src);
+    if (v) return v;
+    const int nch = channels(src->fmt);
+    if (dst_w <= 0 || dst_h <= 0 || dst_stride < dst_w * nch) return ICX_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    hipSetDevice(ctx->device);
+    const bool din = is_device_ptr(src->px), dout = is_device_ptr(dst);
+    size_t need = 1 << 20;
+    if (!din) need += (size_t)src->width * nch * src->height + 256;
+    if (!dout) need += (size_t)dst_stride * dst_h + 256;
+    hipError_t e = ctx->dev.reserve(need);
+    if (e != hipSuccess) return hip_fail(ctx, e, "resize workspace");
+    ctx->dev.used = 0;
+    const uint8_t* s = src->px;
+    int sstride = src->stride;
+    if (!din) {
+        const size_t row = (size_t)src->width * nch;
+        uint8_t* st = (uint8_t*)ctx->dev.take(row * src->height);
+        e = hipMemcpy2DAsync(st, row, src->px, src->stride, row, src->height, hipMemcpyHostToDevice, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "resize upload");
+        s = st;
+        sstride = (int)row;
+    }
+    uint8_t* d = dout ? dst : (uint8_t*)ctx->dev.take((size_t)dst_stride * dst_h);
+    {
+        Timed tm(ctx, "resize", (int64_t)dst_w * dst_h);
+        launch_resize(s, src->width, src->height, sstride, nch, d, dst_w, dst_h, dst_stride, ctx->stream);
+    }
+    if (!dout) {
+        e = hipMemcpyAsync(dst, d, (size_t)dst_stride * dst_h, hipMemcpyDeviceToHost, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "resize download");
+    }
+    e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(ctx, e, "resize");
+    resolve_profile(ctx);
+    return ICX_OK;
+}
+
+icx_status icx_resize_image(icx_ctx* ctx, const icx_image* src, double scale, uint8_t* dst, size_t cap,
+                            int32_t* out_w, int32_t* out_h)
+{
+    if (!ctx || !src || !dst) return ICX_E_NULL;
+    icx_status v = validate(src);
+    if (v) return v;
+    if (!(scale > 0.0)) return ICX_E_INVALID;
+    int32_t dw, dh;
+    icx_scaled_dims(src->width, src->height, scale, &dw, &dh);
+    if (out_w) *out_w = dw;
+    if (out_h) *out_h = dh;
+    const size_t need = (size_t)dw * dh * channels(src->fmt);
+    if (cap < need) return ICX_E_BUFFER;
+    return icx_resize_bilinear(ctx, src, dst, dw, dh, dw * channels(src->fmt));
+}
+
+icx_status icx_png_fit(icx_ctx* ctx, const icx_image* src, int32_t min_width, int32_t min_height, uint8_t* dst,
+                       size_t cap, int32_t* out_w, int32_t* out_h, int32_t* resized)
+{
+    if (!ctx || !src || !src->px || !dst || !resized) return ICX_E_NULL;
+    icx_status v = validate(src);
+    if (v) return v;
+    *resized = 0;
+    if (src->width <= min_width && src->height <= min_height) {  // ImageCompressionPng.java:49-53
+        if (out_w) *out_w = src->width;
+        if (out_h) *out_h = src->height;
+        return ICX_OK;
+    }
+    const double wr = (double)min_width / src->width, hr = (double)min_height / src->height;
+    const double scale = std::min(wr, hr);  // ImageCompressionPng.java:57-61
+    icx_status s = icx_resize_image(ctx, src, scale, dst, cap, out_w, out_h);
+    if (s == ICX_OK) *resized = 1;
+    return s;
+}
+
+icx_status icx_profile_enable(icx_ctx* ctx, int32_t on)
+{
+    if (!ctx) return ICX_E_NULL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    ctx->prof = on != 0;
+    return ICX_OK;
+}
+
+icx_status icx_profile_reset(icx_ctx* ctx)
+{
+    if (!ctx) return ICX_E_NULL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    ctx->stats.clear();
+    return ICX_OK;
+}
+
+icx_status icx_profile_query(icx_ctx* ctx, const char* kernel, int64_t* launches, double* total_ms, int64_t* units)
+{
+    if (!ctx || !kernel) return ICX_E_NULL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    auto f = ctx->stats.find(kernel);
+    const KStat z;
+    const KStat& s = f == ctx->stats.end() ? z : f->second;
+    if (launches) *launches = s.launches;
+    if (total_ms) *total_ms = s.ms;
+    if (units) *units = s.units;
+    return ICX_OK;
+}
+
+}  // extern "C"

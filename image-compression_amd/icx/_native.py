@@ -1,0 +1,112 @@
+"""ctypes binding of libicx.so (the C ABI declared in include/icx.h).
+
+The product path: every compute call goes through this library's HIP
+kernels.  There is no CPU fallback; a missing or unloadable library raises
+immediately (NativeLibraryError).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ICX_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libicx.so")
+
+# icx_status
+OK, E_INVALID, E_NOMEM, E_DEVICE, E_BUFFER, E_UNSUPPORTED, E_CORRUPT, E_NULL = range(8)
+# icx_fmt
+BGR24, RGB24, GRAY8 = 0, 1, 2
+
+EXPORTS = [
+    "icx_abi_version", "icx_create", "icx_destroy", "icx_status_string", "icx_last_error",
+    "icx_quality_tables", "icx_create_key", "icx_subsampling_factor", "icx_scaled_dims",
+    "icx_jpeg_header_size", "icx_compress_jpg_to_stream", "icx_find_best_quality",
+    "icx_compress_jpg_with_target_size", "icx_compress_jpg_batch", "icx_resize_image",
+    "icx_resize_bilinear", "icx_png_fit", "icx_num_blocks", "icx_debug_fdct",
+    "icx_profile_enable", "icx_profile_reset", "icx_profile_query",
+]
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class IcxError(RuntimeError):
+    def __init__(self, status, msg=""):
+        self.status = status
+        super().__init__(f"icx status {status}: {msg}")
+
+
+class Image(ctypes.Structure):
+    _fields_ = [("px", ctypes.c_void_p), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("stride", ctypes.c_int32), ("fmt", ctypes.c_int32)]
+
+
+class LearnedParams(ctypes.Structure):
+    _fields_ = [("quality", ctypes.c_float), ("scale", ctypes.c_double)]
+
+
+class SimilarityKey(ctypes.Structure):
+    _fields_ = [("width_bucket", ctypes.c_int32), ("height_bucket", ctypes.c_int32),
+                ("size_bucket", ctypes.c_int64)]
+
+
+class FitJob(ctypes.Structure):
+    _fields_ = [("img", Image), ("target_max_size", ctypes.c_int64), ("quality", ctypes.c_float),
+                ("has_cached", ctypes.c_int32), ("cached", LearnedParams),
+                ("out", ctypes.c_void_p), ("cap", ctypes.c_size_t),
+                ("success", ctypes.c_int32), ("cache_hit", ctypes.c_int32),
+                ("out_len", ctypes.c_size_t), ("learned", LearnedParams),
+                ("encodes", ctypes.c_int32), ("status", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def load():
+    """Load libicx.so once; raise NativeLibraryError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(f"libicx.so not built at {LIB_PATH}; run __graft_entry__.build()")
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:
+        raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    c = ctypes
+    P = c.POINTER
+    sig = {
+        "icx_abi_version": (c.c_int, []),
+        "icx_create": (c.c_int, [c.c_int, P(c.c_void_p)]),
+        "icx_destroy": (None, [c.c_void_p]),
+        "icx_status_string": (c.c_char_p, [c.c_int]),
+        "icx_last_error": (c.c_char_p, [c.c_void_p]),
+        "icx_quality_tables": (None, [c.c_float, P(c.c_uint16), P(c.c_uint16)]),
+        "icx_create_key": (None, [c.c_int32, c.c_int32, c.c_int64, P(SimilarityKey)]),
+        "icx_subsampling_factor": (c.c_int32, [c.c_int32, c.c_int32]),
+        "icx_scaled_dims": (None, [c.c_int32, c.c_int32, c.c_double, P(c.c_int32), P(c.c_int32)]),
+        "icx_jpeg_header_size": (c.c_int32, [c.c_int32]),
+        "icx_compress_jpg_to_stream": (c.c_int, [c.c_void_p, P(Image), c.c_float, c.c_void_p, c.c_size_t,
+                                                 P(c.c_size_t)]),
+        "icx_find_best_quality": (c.c_int, [c.c_void_p, P(Image), c.c_int64, c.c_float, P(c.c_float),
+                                            P(c.c_float), P(c.c_int64), P(c.c_int32)]),
+        "icx_compress_jpg_with_target_size": (c.c_int, [c.c_void_p, P(FitJob)]),
+        "icx_compress_jpg_batch": (c.c_int, [c.c_void_p, P(FitJob), c.c_int32]),
+        "icx_resize_image": (c.c_int, [c.c_void_p, P(Image), c.c_double, c.c_void_p, c.c_size_t,
+                                       P(c.c_int32), P(c.c_int32)]),
+        "icx_resize_bilinear": (c.c_int, [c.c_void_p, P(Image), c.c_void_p, c.c_int32, c.c_int32, c.c_int32]),
+        "icx_png_fit": (c.c_int, [c.c_void_p, P(Image), c.c_int32, c.c_int32, c.c_void_p, c.c_size_t,
+                                  P(c.c_int32), P(c.c_int32), P(c.c_int32)]),
+        "icx_num_blocks": (c.c_int64, [c.c_int32, c.c_int32, c.c_int32]),
+        "icx_debug_fdct": (c.c_int, [c.c_void_p, P(Image), P(c.c_int16), c.c_size_t]),
+        "icx_profile_enable": (c.c_int, [c.c_void_p, c.c_int32]),
+        "icx_profile_reset": (c.c_int, [c.c_void_p]),
+        "icx_profile_query": (c.c_int, [c.c_void_p, c.c_char_p, P(c.c_int64), P(c.c_double), P(c.c_int64)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if lib.icx_abi_version() != 1:
+        raise NativeLibraryError("libicx ABI version mismatch")
+    _lib = lib
+    return lib

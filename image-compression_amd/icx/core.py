@@ -1,0 +1,374 @@
+"""Host-side mirror of the reference's hot-path interface, backed by libicx.
+
+Reference (PolloChang/image-compression @ 2025-07-25) -> here:
+
+  report/CompressionParams.java:3        CompressionParams
+  report/CompressionReport.java:5        CompressionReport
+  core/CompressionResult.java:3-11       CompressionResult
+  learn/LearnedParams.java:8             LearnedParams
+  learn/jpg/SimilarityKey.java:9         SimilarityKey
+  tools/CacheTools.java:14-21            create_key
+  tools/ImageTools.java:7-26             Codec.resize_image
+  core/ImageCompressionJpg.java:136-147  Codec.compress_jpg_to_stream
+  core/ImageCompressionJpg.java:158-200  Codec.find_best_quality_by_binary_search
+  core/ImageCompressionJpg.java:77-122   Codec.compress_jpg_with_target_size
+  core/ImageCompressionPng.java:37-75    Codec.compress_png_with_target_size
+
+Images are numpy arrays (H, W, 3) uint8 in BGR order (BufferedImage
+TYPE_3BYTE_BGR) or (H, W) uint8 grey (TYPE_BYTE_GRAY), or CUDA tensors of the
+same shape (then no host<->device copy of the pixels happens).
+"""
+import ctypes
+import enum
+import logging
+import threading
+from dataclasses import dataclass
+from typing import Dict, MutableMapping, Optional
+
+import numpy as np
+
+from . import _native as N
+
+log = logging.getLogger("icx")
+
+
+class CompressionResult(enum.Enum):
+    COMPRESSED_SUCCESS = "成功壓縮"
+    SKIPPED_CONDITION_NOT_MET = "不符條件跳過"
+    SKIPPED_NOT_FOUND = "來源檔案不存在"
+    FAILED_COMPRESSION = "壓縮失敗(無法達標)"
+    FAILED_UNSUPPORTED_FORMAT = "格式不支援"
+    FAILED_IO_ERROR = "IO錯誤"
+    FAILED_OUT_OF_MEMORY = "記憶體溢位"
+    FAILED_UNKNOWN = "未知錯誤"
+
+    @property
+    def description(self):
+        return self.value
+
+
+@dataclass(frozen=True)
+class CompressionParams:
+    quality: float
+    min_size_bytes: int
+    min_width: int
+    min_height: int
+    target_max_size_bytes: int
+
+
+@dataclass(frozen=True)
+class CompressionReport:
+    result: CompressionResult
+    original_size: int
+    compressed_size: int
+
+
+@dataclass(frozen=True)
+class LearnedParams:
+    quality: float  # Java float: always a float32-representable value here
+    scale: float
+
+
+@dataclass(frozen=True)
+class SimilarityKey:
+    width_bucket: int
+    height_bucket: int
+    size_bucket: int
+
+
+def _f32(x):
+    return float(np.float32(x))
+
+
+def image_dims(img):
+    shape = tuple(img.shape)
+    return shape[1], shape[0]
+
+
+def create_key(image, file_size) -> SimilarityKey:
+    """CacheTools.createKey: (w/100, h/100, fileSize/102400), decoded dims."""
+    w, h = image_dims(image)
+    return SimilarityKey(w // 100, h // 100, int(file_size) // 102400)
+
+
+def _fmt_of(img):
+    if img.ndim == 2 or (img.ndim == 3 and img.shape[2] == 1):
+        return N.GRAY8
+    if img.ndim == 3 and img.shape[2] == 3:
+        return N.BGR24
+    raise ValueError(f"unsupported image shape {tuple(img.shape)}")
+
+
+def _image_struct(img, fmt=None):
+    """Describe a numpy array or CUDA tensor as an icx_image (no copy)."""
+    if img is None:
+        raise TypeError("image must not be null")
+    if fmt is None:
+        fmt = _fmt_of(img)
+    h, w = int(img.shape[0]), int(img.shape[1])
+    if isinstance(img, np.ndarray):
+        if img.dtype != np.uint8:
+            raise ValueError("image must be uint8")
+        if not (img.flags["C_CONTIGUOUS"] or (img.strides[-1] == 1 and (img.ndim == 2 or img.strides[1] == 3))):
+            img = np.ascontiguousarray(img)
+        ptr, stride = img.ctypes.data, img.strides[0]
+    else:  # torch tensor (CUDA or CPU)
+        if str(img.dtype) != "torch.uint8":
+            raise ValueError("image must be uint8")
+        if not img.is_contiguous():
+            raise ValueError("tensor image must be contiguous")
+        ptr, stride = img.data_ptr(), img.stride(0)
+    return N.Image(ptr, w, h, stride, fmt), img
+
+
+class Codec:
+    """One libicx context (one GPU).  Thread-safe."""
+
+    def __init__(self, device: int = 0):
+        self._lib = N.load()
+        self._ctx = ctypes.c_void_p()
+        st = self._lib.icx_create(device, ctypes.byref(self._ctx))
+        if st != N.OK:
+            raise N.IcxError(st, f"icx_create(device={device}) failed: "
+                                 f"{self._lib.icx_status_string(st).decode()}")
+        self.device = device
+        self._lock = threading.Lock()
+
+    def close(self):
+        if self._ctx:
+            self._lib.icx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st, what):
+        if st != N.OK:
+            raise N.IcxError(st, f"{what}: {self._lib.icx_status_string(st).decode()} "
+                                 f"({self._lib.icx_last_error(self._ctx).decode()})")
+
+    # -------------------------------------------------------------- A12
+    def resize_image(self, original_image, scale: float) -> np.ndarray:
+        """ImageTools.resizeImage(BufferedImage, double): Java2D bilinear."""
+        img, keep = _image_struct(original_image)
+        w = ctypes.c_int32()
+        h = ctypes.c_int32()
+        self._lib.icx_scaled_dims(img.width, img.height, float(scale), ctypes.byref(w), ctypes.byref(h))
+        nch = 1 if img.fmt == N.GRAY8 else 3
+        out = np.empty((h.value, w.value, nch) if nch == 3 else (h.value, w.value), np.uint8)
+        st = self._lib.icx_resize_image(self._ctx, ctypes.byref(img), float(scale), out.ctypes.data, out.nbytes,
+                                        ctypes.byref(w), ctypes.byref(h))
+        self._check(st, "icx_resize_image")
+        return out
+
+    def resize_to(self, original_image, width: int, height: int) -> np.ndarray:
+        img, keep = _image_struct(original_image)
+        nch = 1 if img.fmt == N.GRAY8 else 3
+        out = np.empty((height, width, nch) if nch == 3 else (height, width), np.uint8)
+        st = self._lib.icx_resize_bilinear(self._ctx, ctypes.byref(img), out.ctypes.data, width, height,
+                                           width * nch)
+        self._check(st, "icx_resize_bilinear")
+        return out
+
+    # -------------------------------------------------------------- A4
+    def compress_jpg_to_stream(self, image, quality: float) -> bytes:
+        """compressJpgToStream: one JPEG encode at `quality` (float32)."""
+        img, keep = _image_struct(image)
+        cap = max(1 << 16, img.width * img.height * 3 + 4096)
+        for _ in range(2):
+            out = np.empty(cap, np.uint8)
+            n = ctypes.c_size_t()
+            st = self._lib.icx_compress_jpg_to_stream(self._ctx, ctypes.byref(img), _f32(quality),
+                                                      out.ctypes.data, cap, ctypes.byref(n))
+            if st == N.E_BUFFER:
+                cap = n.value
+                continue
+            self._check(st, "icx_compress_jpg_to_stream")
+            return out[:n.value].tobytes()
+        raise N.IcxError(N.E_BUFFER, "output buffer")
+
+    # -------------------------------------------------------------- A3
+    def find_best_quality_by_binary_search(self, image, target_max_size_bytes: int, initial_quality: float,
+                                           trace: Optional[list] = None) -> float:
+        img, keep = _image_struct(image)
+        best = ctypes.c_float()
+        tq = (ctypes.c_float * 8)()
+        ts = (ctypes.c_int64 * 8)()
+        nt = ctypes.c_int32()
+        st = self._lib.icx_find_best_quality(self._ctx, ctypes.byref(img), int(target_max_size_bytes),
+                                             _f32(initial_quality), ctypes.byref(best), tq, ts, ctypes.byref(nt))
+        self._check(st, "icx_find_best_quality")
+        if trace is not None:
+            trace.extend((tq[i], ts[i], ts[i] <= target_max_size_bytes) for i in range(nt.value))
+        return best.value
+
+    # -------------------------------------------------------------- A2
+    def fit(self, images, target_max_size_bytes, quality, cached=None, outputs=None):
+        """Batched compressJpgWithTargetSize core: returns one dict per image.
+        cached: list of LearnedParams|None; outputs: optional preallocated buffers."""
+        n = len(images)
+        jobs = (N.FitJob * n)()
+        keep, bufs = [], []
+        for i, im in enumerate(images):
+            img, k = _image_struct(im)
+            keep.append(k)
+            j = jobs[i]
+            j.img = img
+            j.target_max_size = int(target_max_size_bytes)
+            j.quality = _f32(quality)
+            c = cached[i] if cached else None
+            if c is not None:
+                j.has_cached = 1
+                j.cached = N.LearnedParams(_f32(c.quality), float(c.scale))
+            if outputs is not None:
+                buf = outputs[i]
+                j.out = buf.data_ptr() if hasattr(buf, "data_ptr") else buf.ctypes.data
+                j.cap = buf.numel() if hasattr(buf, "numel") else buf.nbytes
+            else:
+                buf = np.empty(int(target_max_size_bytes) + 1, np.uint8)
+                j.out = buf.ctypes.data
+                j.cap = buf.nbytes
+            bufs.append(buf)
+        with self._lock:
+            st = self._lib.icx_compress_jpg_batch(self._ctx, jobs, n)
+        self._check(st, "icx_compress_jpg_batch")
+        res = []
+        for i in range(n):
+            j = jobs[i]
+            r = {"status": j.status, "success": bool(j.success), "cache_hit": bool(j.cache_hit),
+                 "out_len": j.out_len, "encodes": j.encodes,
+                 "learned": LearnedParams(j.learned.quality, j.learned.scale) if j.success else None}
+            if outputs is None and j.success and j.status == N.OK:
+                r["data"] = bufs[i][:j.out_len].tobytes()
+            res.append(r)
+        return res
+
+    def prepare(self, images, target_max_size_bytes, quality, cached=None, outputs=None):
+        """A reusable job array over device- or host-resident images (bench)."""
+        return PreparedBatch(self, images, target_max_size_bytes, quality, cached, outputs)
+
+    def compress_jpg_with_target_size(self, original_image, original_size: int, output_file,
+                                      params: CompressionParams,
+                                      cache: MutableMapping[SimilarityKey, LearnedParams]) -> bool:
+        """ImageCompressionJpg.compressJpgWithTargetSize (cache probe, scale loop,
+        binary search, save, learn)."""
+        key = create_key(original_image, original_size)
+        cached = cache.get(key)
+        r = self.fit([original_image], params.target_max_size_bytes, params.quality, cached=[cached])[0]
+        if r["status"] == N.E_NOMEM:
+            raise MemoryError("device out of memory")
+        if r["status"] != N.OK:
+            raise OSError(f"icx encode failed with status {r['status']}")
+        if cached is not None and r["cache_hit"]:
+            log.info("快取成功: %s 使用學習參數直接達成目標。", output_file)
+        elif cached is not None:
+            log.warning("快取失效: %s 使用學習參數後檔案仍超標，退回標準流程。", output_file)
+        if not r["success"]:
+            log.warning("無法在目標大小限制下完成壓縮: %s", output_file)
+            return False
+        with open(output_file, "wb") as f:
+            f.write(r["data"])
+        if not r["cache_hit"]:
+            cache[key] = r["learned"]
+        return True
+
+    # -------------------------------------------------------------- PNG
+    def compress_png_with_target_size(self, original_image, output_file, params: CompressionParams) -> bool:
+        """ImageCompressionPng.compressPngWithTargetSize: fit into the
+        (minWidth x minHeight) box with the bilinear scaler, write PNG."""
+        if original_image is None:
+            raise TypeError("originalImage must not be null")
+        if output_file is None:
+            raise TypeError("outputFile must not be null")
+        if params is None:
+            raise TypeError("params must not be null")
+        w, h = image_dims(original_image)
+        if w <= params.min_width and h <= params.min_height:
+            log.info("PNG 圖片尺寸 %dx%d 未超過目標 %dx%d，不處理。", w, h, params.min_width, params.min_height)
+            return False
+        scale = min(params.min_width / w, params.min_height / h)
+        resized = self.resize_image(original_image, scale)
+        from .pngio import write_png
+        write_png(output_file, resized)
+        return True
+
+    # -------------------------------------------------------------- parity / metrics
+    def debug_fdct(self, image) -> np.ndarray:
+        img, keep = _image_struct(image)
+        nb = self._lib.icx_num_blocks(img.width, img.height, img.fmt)
+        out = np.empty((nb, 64), np.int16)
+        st = self._lib.icx_debug_fdct(self._ctx, ctypes.byref(img),
+                                      out.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)), out.size)
+        self._check(st, "icx_debug_fdct")
+        return out
+
+    def profile(self, on=True):
+        self._check(self._lib.icx_profile_enable(self._ctx, 1 if on else 0), "icx_profile_enable")
+
+    def profile_reset(self):
+        self._check(self._lib.icx_profile_reset(self._ctx), "icx_profile_reset")
+
+    def profile_query(self, kernel: str) -> Dict[str, float]:
+        n = ctypes.c_int64()
+        ms = ctypes.c_double()
+        u = ctypes.c_int64()
+        self._check(self._lib.icx_profile_query(self._ctx, kernel.encode(), ctypes.byref(n), ctypes.byref(ms),
+                                                ctypes.byref(u)), "icx_profile_query")
+        return {"launches": n.value, "ms": ms.value, "units": u.value}
+
+
+def quality_tables(quality: float):
+    lib = N.load()
+    lum = (ctypes.c_uint16 * 64)()
+    chrom = (ctypes.c_uint16 * 64)()
+    lib.icx_quality_tables(_f32(quality), lum, chrom)
+    return list(lum), list(chrom)
+
+
+def subsampling_factor(width: int, height: int) -> int:
+    return N.load().icx_subsampling_factor(width, height)
+
+
+def scaled_dims(width: int, height: int, scale: float):
+    w = ctypes.c_int32()
+    h = ctypes.c_int32()
+    N.load().icx_scaled_dims(width, height, float(scale), ctypes.byref(w), ctypes.byref(h))
+    return w.value, h.value
+
+
+class PreparedBatch:
+    """icx_fit_job array built once and re-run (outputs overwritten each run)."""
+
+    def __init__(self, codec, images, target, quality, cached=None, outputs=None):
+        self.codec = codec
+        self.n = len(images)
+        self.jobs = (N.FitJob * self.n)()
+        self._keep = []
+        for i, im in enumerate(images):
+            img, k = _image_struct(im)
+            self._keep.append(k)
+            j = self.jobs[i]
+            j.img = img
+            j.target_max_size = int(target)
+            j.quality = _f32(quality)
+            c = cached[i] if cached else None
+            if c is not None:
+                j.has_cached = 1
+                j.cached = N.LearnedParams(_f32(c.quality), float(c.scale))
+            buf = outputs[i] if outputs is not None else np.empty(int(target) + 1, np.uint8)
+            self._keep.append(buf)
+            j.out = buf.data_ptr() if hasattr(buf, "data_ptr") else buf.ctypes.data
+            j.cap = buf.numel() if hasattr(buf, "numel") else buf.nbytes
+
+    def run(self):
+        st = self.codec._lib.icx_compress_jpg_batch(self.codec._ctx, self.jobs, self.n)
+        self.codec._check(st, "icx_compress_jpg_batch")
+        return self
+
+    def results(self):
+        return [{"status": j.status, "success": bool(j.success), "cache_hit": bool(j.cache_hit),
+                 "out_len": j.out_len, "encodes": j.encodes,
+                 "learned": LearnedParams(j.learned.quality, j.learned.scale)} for j in self.jobs]

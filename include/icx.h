@@ -1,0 +1,189 @@
+/*
+ * icx.h — C-ABI of the MI355X-native JPEG target-size compression path.
+ *
+ * Drop-in boundary for PolloChang/image-compression's per-image encode hot
+ * path.  The reference has no FFI: the hot path is reached through static
+ * Java functions and the javax.imageio SPI.  Each entry point
+ * below replaces one of those functions; the JNI/ctypes bindings a maintainer
+ * would add are in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Pixel/output pointers may be host memory
+ *    or device (HBM) memory of the context's GPU; the library detects which.
+ *    The caller owns every buffer; nothing is retained past return.
+ *  - Errors are status codes (no exceptions cross the ABI).  The mapping to the
+ *    reference's CompressionResult (CompressionResult.java:3-11) is:
+ *      ICX_E_NOMEM  -> FAILED_OUT_OF_MEMORY   (ImageCompression.java:97-100)
+ *      ICX_E_DEVICE -> FAILED_IO_ERROR        (ImageCompression.java:94-96)
+ *      other errors -> FAILED_UNKNOWN         (ImageCompression.java:101-104)
+ *    A NULL required argument returns ICX_E_NULL, the analogue of the
+ *    NullPointerException contract tested in ImageCompressionPngTest.java:76-88.
+ *  - Every function is thread-safe; calls on one context are serialised on
+ *    its device stream (one context per GPU per process).
+ *  - Floating-point parameters keep Java's types: quality is float32, scale
+ *    is float64, so results match the reference's arithmetic bit for bit.
+ */
+#ifndef ICX_H
+#define ICX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ICX_ABI_VERSION 1
+
+typedef struct icx_ctx icx_ctx;
+
+typedef enum icx_status {
+    ICX_OK = 0,
+    ICX_E_INVALID = 1,     /* bad dimensions / format / argument value            */
+    ICX_E_NOMEM = 2,       /* host or device allocation failed                    */
+    ICX_E_DEVICE = 3,      /* HIP runtime error                                   */
+    ICX_E_BUFFER = 4,      /* output capacity too small; *out_len = needed bytes  */
+    ICX_E_UNSUPPORTED = 5, /* valid but unsupported input (e.g. progressive JPEG) */
+    ICX_E_CORRUPT = 6,     /* malformed compressed input                          */
+    ICX_E_NULL = 7         /* required pointer argument is NULL                   */
+} icx_status;
+
+/* Pixel layouts.  ICX_BGR24 is java.awt.image.BufferedImage.TYPE_3BYTE_BGR,
+ * the type the JDK JPEG reader returns for YCbCr JPEGs; ICX_GRAY8 is
+ * TYPE_BYTE_GRAY (1-component JPEG). */
+typedef enum icx_fmt { ICX_BGR24 = 0, ICX_RGB24 = 1, ICX_GRAY8 = 2 } icx_fmt;
+
+/* A decoded image (BufferedImage).  stride in bytes. */
+typedef struct icx_image {
+    const uint8_t* px;
+    int32_t width;
+    int32_t height;
+    int32_t stride;
+    int32_t fmt; /* icx_fmt */
+} icx_image;
+
+/* learn/LearnedParams.java:8  record LearnedParams(float quality, double scale) */
+typedef struct icx_learned_params {
+    float quality;
+    double scale;
+} icx_learned_params;
+
+/* learn/jpg/SimilarityKey.java:9  record SimilarityKey(int, int, long) */
+typedef struct icx_similarity_key {
+    int32_t width_bucket;
+    int32_t height_bucket;
+    int64_t size_bucket;
+} icx_similarity_key;
+
+/* ---------------------------------------------------------------- context */
+/* One context per GPU per process: owns the HIP stream, workspace pool and
+ * staging buffers.  device = HIP ordinal. */
+icx_status icx_create(int device, icx_ctx** out);
+void icx_destroy(icx_ctx* ctx);
+const char* icx_status_string(icx_status s);
+/* Last error text recorded on this context (never NULL). */
+const char* icx_last_error(const icx_ctx* ctx);
+int icx_abi_version(void);
+
+/* ------------------------------------------------------- pure host helpers */
+/* A6: JPEG.convertToLinearQuality + JPEGQTable.K1Luminance/K2Chrominance
+ * .getScaledInstance(lin, true), natural order; the tables the JDK writer
+ * uses for setCompressionQuality(q) (ImageCompressionJpg.java:140-143). */
+void icx_quality_tables(float quality, uint16_t lum[64], uint16_t chrom[64]);
+
+/* A13: CacheTools.createKey (CacheTools.java:14-21). */
+void icx_create_key(int32_t width, int32_t height, int64_t file_size, icx_similarity_key* key);
+
+/* A11: ImageCompression.decodeImageWithSubsampling's factor
+ * (ImageCompression.java:140-153): maxDim > 4096 ? highestOneBit(floor(maxDim/4096)) : 1. */
+int32_t icx_subsampling_factor(int32_t width, int32_t height);
+
+/* A12 dims: ImageTools.java:8-9, max(1, (int)(w*scale)). */
+void icx_scaled_dims(int32_t width, int32_t height, double scale, int32_t* out_w, int32_t* out_h);
+
+/* Exact JPEG file size this library writes for a given entropy-segment size
+ * (headers + EOI).  Header layout: SOI, JFIF APP0, DQT per table, SOF0, DHT per
+ * table, SOS (623 B for 3 components, 328 B for grey). */
+int32_t icx_jpeg_header_size(int32_t fmt);
+
+/* ------------------------------------------------------------- hot path */
+/* A4  ImageCompressionJpg.compressJpgToStream (ImageCompressionJpg.java:136-147):
+ * one baseline JPEG encode at float quality q.  Writes the complete file to
+ * out (host or device).  ICX_E_BUFFER if cap < size (then *out_len = size). */
+icx_status icx_compress_jpg_to_stream(icx_ctx* ctx, const icx_image* img, float quality,
+                                      uint8_t* out, size_t cap, size_t* out_len);
+
+/* A3  ImageCompressionJpg.findBestQualityByBinarySearch (:158-200).
+ * Returns the best quality (or -1.0f) in *best_quality.  trial_q/trial_size
+ * (each >= 8 entries, may be NULL) receive the trial sequence. */
+icx_status icx_find_best_quality(icx_ctx* ctx, const icx_image* img, int64_t target_max_size,
+                                 float initial_quality, float* best_quality, float* trial_q,
+                                 int64_t* trial_size, int32_t* ntrials);
+
+/* A2  ImageCompressionJpg.compressJpgWithTargetSize (:77-122), including the
+ * cache-hit branch tryCachedParams (:216-238).  The Map<SimilarityKey,
+ * LearnedParams> stays on the caller's side: pass cache.get(key) in `cached`
+ * (has_cached = 1 on a hit); on return `learned` is what the reference would
+ * cache.put (valid when success && !cache_hit). */
+typedef struct icx_fit_job {
+    /* inputs */
+    icx_image img;
+    int64_t target_max_size; /* CompressionParams.targetMaxSizeBytes */
+    float quality;           /* CompressionParams.quality (search upper bound) */
+    int32_t has_cached;
+    icx_learned_params cached;
+    uint8_t* out; /* host or device */
+    size_t cap;
+    /* outputs */
+    int32_t success;   /* compressJpgWithTargetSize's return value */
+    int32_t cache_hit; /* tryCachedParams wrote the file */
+    size_t out_len;
+    icx_learned_params learned;
+    int32_t encodes;   /* trial encodes performed (cache probe + search trials) */
+    icx_status status;
+} icx_fit_job;
+
+icx_status icx_compress_jpg_with_target_size(icx_ctx* ctx, icx_fit_job* job);
+
+/* Batched A2 for throughput: the images are processed together, sharing
+ * kernel launches.  Per-job results/status are filled in; the return value is
+ * ICX_OK unless a context-level failure occurred. */
+icx_status icx_compress_jpg_batch(icx_ctx* ctx, icx_fit_job* jobs, int32_t n);
+
+/* A12  ImageTools.resizeImage (ImageTools.java:7-26): Java2D bilinear resize
+ * to (max(1,(int)(w*scale)), max(1,(int)(h*scale))).  dst gets the same fmt,
+ * tightly packed (stride = w*channels). */
+icx_status icx_resize_image(icx_ctx* ctx, const icx_image* src, double scale, uint8_t* dst,
+                            size_t cap, int32_t* out_w, int32_t* out_h);
+
+/* Bilinear resize to explicit dims (dstride in bytes). */
+icx_status icx_resize_bilinear(icx_ctx* ctx, const icx_image* src, uint8_t* dst, int32_t dst_w,
+                               int32_t dst_h, int32_t dst_stride);
+
+/* The resize step of ImageCompressionPng.compressPngWithTargetSize
+ * (ImageCompressionPng.java:37-75): if w <= min_w && h <= min_h sets
+ * *resized = 0 (the reference returns false); else scales by
+ * min(min_w/w, min_h/h) into dst and sets *resized = 1. */
+icx_status icx_png_fit(icx_ctx* ctx, const icx_image* src, int32_t min_width, int32_t min_height,
+                       uint8_t* dst, size_t cap, int32_t* out_w, int32_t* out_h,
+                       int32_t* resized);
+
+/* ------------------------------------------------------- parity / metrics */
+/* Raw jpeg_fdct_islow coefficients (x8 scale, before quantisation) in scan
+ * block order (MCU: Y0 Y1 Y2 Y3 Cb Cr), zig-zag within each block: the
+ * device-resident layout the search re-quantises every trial. */
+int64_t icx_num_blocks(int32_t width, int32_t height, int32_t fmt);
+icx_status icx_debug_fdct(icx_ctx* ctx, const icx_image* img, int16_t* coefs, size_t ncoefs);
+
+/* Per-kernel timing with HIP events recorded on the context's stream around
+ * every launch of the named kernel ("fdct", "huff", "scan", "ffcount",
+ * "decide", "stuff", "resize").  Enabling adds one event pair per launch. */
+icx_status icx_profile_enable(icx_ctx* ctx, int32_t on);
+icx_status icx_profile_reset(icx_ctx* ctx);
+icx_status icx_profile_query(icx_ctx* ctx, const char* kernel, int64_t* launches, double* total_ms,
+                             int64_t* units);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ICX_H */

@@ -1,0 +1,177 @@
+"""ctypes access to oracle/liboracle.so — the CPU restatement used as the
+checker (test infrastructure only; never imported by the product package)."""
+import ctypes
+import json
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
+FMT = {"bgr": 0, "rgb": 1, "gray": 2}
+
+
+def build_oracle():
+    lib = os.path.join(ORACLE_DIR, "liboracle.so")
+    src = os.path.join(ORACLE_DIR, "icx_oracle.c")
+    if not os.path.exists(lib) or os.path.getmtime(lib) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+    return lib
+
+
+def fmt_of(img):
+    return 2 if img.ndim == 2 else 0
+
+
+class Oracle:
+    def __init__(self):
+        L = ctypes.CDLL(build_oracle())
+        c, P = ctypes, ctypes.POINTER
+        L.oracle_encode.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int, c.c_float, c.c_void_p,
+                                    c.c_size_t, P(c.c_size_t)]
+        L.oracle_num_blocks.restype = c.c_long
+        L.oracle_num_blocks.argtypes = [c.c_int, c.c_int, c.c_int]
+        L.oracle_fdct.restype = c.c_long
+        L.oracle_fdct.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int, c.c_void_p]
+        L.oracle_qtables.argtypes = [c.c_float, P(c.c_uint16), P(c.c_uint16)]
+        L.oracle_find_best_quality.restype = c.c_float
+        L.oracle_find_best_quality.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int64,
+                                               c.c_float, P(c.c_float), P(c.c_int64), P(c.c_int)]
+        L.oracle_resize.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int, c.c_void_p, c.c_int,
+                                    c.c_int, c.c_int]
+        L.oracle_scaled_dims.argtypes = [c.c_int, c.c_int, c.c_double, P(c.c_int), P(c.c_int)]
+        L.oracle_compress_jpg_with_target_size.argtypes = [
+            c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int64, c.c_float, c.c_int, c.c_float,
+            c.c_double, c.c_void_p, c.c_size_t, P(c.c_size_t), P(c.c_float), P(c.c_double), P(c.c_int),
+            P(c.c_int)]
+        L.oracle_subsampling.argtypes = [c.c_int, c.c_int]
+        L.oracle_create_key.argtypes = [c.c_int, c.c_int, c.c_int64, P(c.c_int), P(c.c_int), P(c.c_int64)]
+        L.oracle_fit_batch.restype = c.c_long
+        L.oracle_fit_batch.argtypes = [c.c_int, P(c.c_void_p), P(c.c_int), P(c.c_int), P(c.c_int), c.c_int,
+                                       c.c_int64, c.c_float, c.c_int, c.c_float, c.c_double, c.c_int,
+                                       P(c.c_int64), P(c.c_float), P(c.c_double)]
+        self.L = L
+
+    def encode(self, img, q):
+        img = np.ascontiguousarray(img)
+        h, w = img.shape[:2]
+        cap = w * h * 4 + 8192
+        out = np.empty(cap, np.uint8)
+        n = ctypes.c_size_t()
+        rc = self.L.oracle_encode(img.ctypes.data, w, h, img.strides[0], fmt_of(img), float(np.float32(q)),
+                                  out.ctypes.data, cap, ctypes.byref(n))
+        assert rc == 0, rc
+        return out[:n.value].tobytes()
+
+    def fdct(self, img):
+        img = np.ascontiguousarray(img)
+        h, w = img.shape[:2]
+        nb = self.L.oracle_num_blocks(w, h, fmt_of(img))
+        out = np.empty((nb, 64), np.int16)
+        self.L.oracle_fdct(img.ctypes.data, w, h, img.strides[0], fmt_of(img), out.ctypes.data)
+        return out
+
+    def qtables(self, q):
+        a = (ctypes.c_uint16 * 64)()
+        b = (ctypes.c_uint16 * 64)()
+        self.L.oracle_qtables(float(np.float32(q)), a, b)
+        return list(a), list(b)
+
+    def find_best_quality(self, img, target, q0):
+        img = np.ascontiguousarray(img)
+        h, w = img.shape[:2]
+        tq = (ctypes.c_float * 8)()
+        ts = (ctypes.c_int64 * 8)()
+        nt = ctypes.c_int()
+        best = self.L.oracle_find_best_quality(img.ctypes.data, w, h, img.strides[0], fmt_of(img), int(target),
+                                               float(np.float32(q0)), tq, ts, ctypes.byref(nt))
+        return best, [(tq[i], ts[i]) for i in range(nt.value)]
+
+    def scaled_dims(self, w, h, s):
+        a, b = ctypes.c_int(), ctypes.c_int()
+        self.L.oracle_scaled_dims(w, h, float(s), ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
+
+    def resize(self, img, dw, dh):
+        img = np.ascontiguousarray(img)
+        h, w = img.shape[:2]
+        nch = 1 if img.ndim == 2 else 3
+        out = np.empty((dh, dw, nch) if nch == 3 else (dh, dw), np.uint8)
+        self.L.oracle_resize(img.ctypes.data, w, h, img.strides[0], fmt_of(img), out.ctypes.data, dw, dh,
+                             dw * nch)
+        return out
+
+    def fit(self, img, target, q0, cached=None):
+        img = np.ascontiguousarray(img)
+        h, w = img.shape[:2]
+        cap = w * h * 4 + 8192
+        out = np.empty(cap, np.uint8)
+        n = ctypes.c_size_t()
+        bq, bs = ctypes.c_float(), ctypes.c_double()
+        enc, hit = ctypes.c_int(), ctypes.c_int()
+        has = cached is not None
+        cq, cs = (cached if has else (0.0, 1.0))
+        rc = self.L.oracle_compress_jpg_with_target_size(
+            img.ctypes.data, w, h, img.strides[0], fmt_of(img), int(target), float(np.float32(q0)), int(has),
+            float(np.float32(cq)), float(cs), out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(bq),
+            ctypes.byref(bs), ctypes.byref(enc), ctypes.byref(hit))
+        assert rc >= 0
+        return {"success": rc == 1, "data": out[:n.value].tobytes() if rc == 1 else None,
+                "quality": bq.value if rc == 1 else None, "scale": bs.value if rc == 1 else None,
+                "encodes": enc.value, "cache_hit": bool(hit.value)}
+
+    def subsampling(self, w, h):
+        return self.L.oracle_subsampling(w, h)
+
+    def create_key(self, w, h, size):
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+        self.L.oracle_create_key(w, h, size, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return a.value, b.value, c.value
+
+    def fit_batch(self, imgs, target, q0, cached=None, threads=1):
+        n = len(imgs)
+        imgs = [np.ascontiguousarray(i) for i in imgs]
+        ptrs = (ctypes.c_void_p * n)(*[i.ctypes.data for i in imgs])
+        ws = (ctypes.c_int * n)(*[i.shape[1] for i in imgs])
+        hs = (ctypes.c_int * n)(*[i.shape[0] for i in imgs])
+        ss = (ctypes.c_int * n)(*[i.strides[0] for i in imgs])
+        sizes = (ctypes.c_int64 * n)()
+        qs = (ctypes.c_float * n)()
+        sc = (ctypes.c_double * n)()
+        has = cached is not None
+        cq, cs = cached if has else (0.0, 1.0)
+        enc = self.L.oracle_fit_batch(n, ptrs, ws, hs, ss, fmt_of(imgs[0]), int(target), float(np.float32(q0)),
+                                      int(has), float(np.float32(cq)), float(cs), threads, sizes, qs, sc)
+        return enc, list(sizes), list(qs), list(sc)
+
+
+def load_golden():
+    meta = json.load(open(os.path.join(GOLDEN_DIR, "golden.json")))
+    inputs = dict(np.load(os.path.join(GOLDEN_DIR, "inputs.npz")))
+    jpegs = dict(np.load(os.path.join(GOLDEN_DIR, "jpeg_golden.npz")))
+    return meta, inputs, jpegs
+
+
+def jdk_bytes(turbo_bytes, meta):
+    """The golden file with the JFIF minor version the JDK writes (1.02)."""
+    b = bytearray(turbo_bytes)
+    b[meta["jfif_version_offset"]] = 2
+    return bytes(b)
+
+
+def smooth(h, w, seed):
+    rng = np.random.default_rng(seed)
+    fx, fy, ph = rng.uniform(0.002, 0.02, 3)
+    y = np.arange(h, dtype=np.float32)[:, None]
+    x = np.arange(w, dtype=np.float32)[None, :]
+    r = 127 + 100 * np.sin(x * fx * 10 + ph) + 0 * y
+    g = 127 + 100 * np.sin(y * fy * 10 + 2 * ph) + 0 * x
+    b = 127 + 100 * np.sin((x + y) * fx * 5)
+    rgb = np.stack([r, g, b], -1) + rng.normal(0, 16, (h, w, 3)).astype(np.float32)
+    return np.clip(np.rint(rgb), 0, 255).astype(np.uint8)[:, :, ::-1].copy()
+
+
+def noise(h, w, seed):
+    return np.random.default_rng(seed).integers(0, 256, (h, w, 3), dtype=np.uint8)

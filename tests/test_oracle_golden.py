@@ -1,0 +1,108 @@
+"""Pins the CPU oracle against the committed golden vectors (libjpeg-turbo
+3.1.4 driven with the JDK writer's tables; tests/golden/gen_golden.py)."""
+import numpy as np
+import pytest
+
+from tests.oracle_ffi import jdk_bytes
+
+
+def test_quality_tables_match_golden(oracle, golden):
+    meta, _, _ = golden
+    for q, t in meta["tables"].items():
+        lum, chrom = oracle.qtables(float(q))
+        assert lum == t["lum"] and chrom == t["chrom"], q
+
+
+def test_encode_bytes_match_golden(oracle, golden):
+    meta, inputs, jpegs = golden
+    n = 0
+    for name, img in inputs.items():
+        for q in meta["images"][name]["encodes"]:
+            ref = jdk_bytes(jpegs[f"{name}@{q}"].tobytes(), meta)
+            got = oracle.encode(img, float(q))
+            assert got == ref, (name, q)
+            n += 1
+    assert n == 121
+
+
+def test_header_layout(oracle, golden):
+    _, inputs, _ = golden
+    d = oracle.encode(inputs["smooth_64x48"], 0.25)
+    # SOI, APP0 JFIF 1.02, DQT, DQT, SOF0, DHT x4, SOS: 623 bytes before the scan
+    assert d[:2] == b"\xff\xd8" and d[2:4] == b"\xff\xe0" and d[6:11] == b"JFIF\x00"
+    assert d[11:13] == b"\x01\x02"
+    markers, i = [], 2
+    while True:
+        m, ln = d[i + 1], d[i + 2] * 256 + d[i + 3]
+        markers.append(m)
+        i += 2 + ln
+        if m == 0xDA:
+            break
+    assert markers == [0xE0, 0xDB, 0xDB, 0xC0, 0xC4, 0xC4, 0xC4, 0xC4, 0xDA]
+    assert i == 623 and d[-2:] == b"\xff\xd9"
+    g = oracle.encode(inputs["grey_37x29"], 0.25)
+    i, markers = 2, []
+    while True:
+        m, ln = g[i + 1], g[i + 2] * 256 + g[i + 3]
+        markers.append(m)
+        i += 2 + ln
+        if m == 0xDA:
+            break
+    assert markers == [0xE0, 0xDB, 0xC0, 0xC4, 0xC4, 0xDA] and i == 328
+
+
+def test_search_traces_match_golden(oracle, golden):
+    meta, inputs, _ = golden
+    for name, img in inputs.items():
+        for s in meta["images"][name]["searches"]:
+            best, trace = oracle.find_best_quality(img, s["target"], s["q0"])
+            assert [(round(q, 9), sz) for q, sz in trace] == [(round(q, 9), sz) for q, sz, _ in s["trace"]], name
+            assert best == pytest.approx(s["best"], abs=0)
+
+
+def test_fdct_dummy_blocks(oracle, golden):
+    _, inputs, _ = golden
+    co = oracle.fdct(inputs["smooth_200x136"])   # 13x9 MCUs, Y 25x17 blocks
+    mcux, mcuy = 13, 9
+    blk = co.reshape(mcuy, mcux, 6, 64)
+    # right column: Y1/Y3 dummy -> AC 0, DC of the left neighbour
+    assert np.all(blk[:-1, -1, 1, 1:] == 0) and np.all(blk[:-1, -1, 1, 0] == blk[:-1, -1, 0, 0])
+    # bottom row: Y2/Y3 dummy -> DC of Y1
+    assert np.all(blk[-1, :, 2:4, 1:] == 0)
+    assert np.all(blk[-1, :, 2, 0] == blk[-1, :, 1, 0]) and np.all(blk[-1, :, 3, 0] == blk[-1, :, 1, 0])
+
+
+def test_subsampling_and_keys(oracle):
+    for w, h, s in [(3840, 2160, 1), (7680, 4320, 1), (8192, 4608, 2), (4096, 10, 1), (4097, 1, 1),
+                    (12288, 10, 2), (16384, 1, 4), (20000, 5, 4)]:
+        assert oracle.subsampling(w, h) == s, (w, h)
+    assert oracle.create_key(3840, 2160, 5 * 1024 * 1024 + 7) == (38, 21, 51)
+
+
+def test_scale_sequence_and_dims(oracle):
+    scales, s = [], 1.0
+    while s > 0.1:
+        scales.append(s)
+        s = 0.85 if s == 1.0 else s * 0.85
+    assert len(scales) == 15 and scales[-1] == pytest.approx(0.10276966953088429, abs=1e-15)
+    assert oracle.scaled_dims(3840, 2160, 0.85) == (3264, 1836)
+    assert oracle.scaled_dims(7680, 4320, 0.85 * 0.85) == (5548, 3121)
+    assert oracle.scaled_dims(3, 3, 0.1) == (1, 1)
+
+
+def test_resize_identity_and_constant(oracle):
+    img = np.full((50, 80, 3), 77, np.uint8)
+    out = oracle.resize(img, 33, 21)
+    assert out.shape == (21, 33, 3) and np.all(out == 77)
+    g = np.random.default_rng(0).integers(0, 256, (40, 40, 3), dtype=np.uint8)
+    assert np.array_equal(oracle.resize(g, 40, 40), g)  # scale 1: exact sample positions
+
+
+def test_fit_scale_loop(oracle, golden):
+    _, inputs, _ = golden
+    img = inputs["noise_120x90"]
+    target = len(oracle.encode(img, 0.015625)) - 1   # smallest trial at scale 1 does not fit
+    r = oracle.fit(img, target, 0.25)
+    assert r["success"] and r["scale"] < 1.0 and len(r["data"]) <= target
+    r2 = oracle.fit(img, target, 0.25, cached=(r["quality"], r["scale"]))
+    assert r2["cache_hit"] and r2["data"] == r["data"] and r2["encodes"] == 1
