@@ -2,9 +2,12 @@
 //
 // HBM layout per image (DESIGN.md §Data layout):
 //   px          u8 BGR/RGB/grey rows (caller's buffer, or the resize buffer)
-//   coefs       int16 raw jpeg_fdct_islow output, one 64-entry zig-zag block
-//               per scan block, MCU order (Y0 Y1 Y2 Y3 Cb Cr): 3 B per pixel
-//               for 4:2:0.  Written once per visited scale, re-read by every
+//   coefs       int16 raw jpeg_fdct_islow output (3 B per pixel for 4:2:0),
+//               scan blocks in MCU order (Y0 Y1 Y2 Y3 Cb Cr), chunk-interleaved:
+//               inside a chunk of CHUNK_BLOCKS blocks, zig-zag coefficients
+//               4k..4k+3 of block j sit at quad k, lane j (8 B), so the
+//               thread-per-block Huffman kernel reads 512 contiguous bytes per
+//               wave-load.  Written once per visited scale, re-read by every
 //               quality trial (quantisation happens in the trial kernel).
 //   scratch[2]  per-chunk packed Huffman bitstreams (chunk = CHUNK_BLOCKS
 //               scan blocks, MSB-first 32-bit words, chunk-local bit 0),
@@ -13,13 +16,22 @@
 //   chunk_bits/off/ff [2]  per-chunk bit counts, exclusive bit offsets and
 //               0xFF-byte counts of the owned words (for byte stuffing).
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace icx {
 
-constexpr int CHUNK_BLOCKS = 128;        // scan blocks per Huffman chunk (one workgroup)
+constexpr int CHUNK_BLOCKS = 256;        // scan blocks per Huffman chunk (one workgroup)
 constexpr int MAX_BLOCK_BITS = 1664;     // >= 22 (DC) + 63 * 26 (AC) bits, multiple of 32
-constexpr int CHUNK_WORDS = CHUNK_BLOCKS * MAX_BLOCK_BITS / 32;  // 6656 words = 26 KiB
+constexpr int BLOCK_WORDS = MAX_BLOCK_BITS / 32;               // 52
+constexpr int CHUNK_WORDS = CHUNK_BLOCKS * BLOCK_WORDS;        // 13312 words = 52 KiB
+
+// int16 index of zig-zag coefficient k of scan block b (chunk-interleaved)
+__host__ __device__ inline int64_t coef_index(int64_t b, int k)
+{
+    return (b / CHUNK_BLOCKS) * (CHUNK_BLOCKS * 64) + (k >> 2) * (CHUNK_BLOCKS * 4) +
+           (b % CHUNK_BLOCKS) * 4 + (k & 3);
+}
 constexpr int FD_TILE_PX = 128;          // FDCT tile width in pixels (8 colour MCUs)
 constexpr int MAX_TRIALS = 8;            // findBestQualityByBinarySearch loop bound (:167)
 constexpr int HDR_COLOR = 623;           // SOI+APP0+2 DQT+SOF0+4 DHT+SOS
@@ -52,6 +64,7 @@ struct ImgDesc {
     uint64_t* chunk_off[2];   // nchunks + 1 entries
     uint32_t* chunk_ff[2];
     uint64_t* chunk_ffoff;    // nchunks entries (final stuffing pass)
+    uint32_t* ovf;            // per-block spill of Huffman words beyond the LDS slot
     uint8_t* out;
     uint64_t cap;
 };

@@ -203,11 +203,12 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
     // of ceil(W/8) or below ceil(H/8) gets AC = 0 and the DC of MCU_buffer[blkn-1]
     // (right edge) or of the last block of the MCU's previous block row (bottom).
     const int nmcu = min(8, D.mcux - tx * 8);
+    const int nblk = nmcu * 6;
     const bool bottom = (2 * my + 1) >= D.yhb;
-    int16_t* gdst = D.coefs + ((int64_t)my * D.mcux + tx * 8) * 384;
-    for (int e = t; e < nmcu * 48; e += 256) {  // 16-B pieces: 8 per block
-        const int blk = e >> 3, part = e & 7, mcu = blk / 6, yb = blk - mcu * 6;
-        int4 val = *(const int4*)&oz[blk][part * 8];
+    const int64_t bbase = ((int64_t)my * D.mcux + tx * 8) * 6;
+    for (int e = t; e < nblk * 16; e += 256) {  // (quad, block) pieces of 8 B, block fastest
+        const int quad = e / nblk, blk = e - quad * nblk, mcu = blk / 6, yb = blk - mcu * 6;
+        int2 val = *(const int2*)&oz[blk][quad * 4];
         if (yb < 4) {
             const bool right = (2 * (tx * 8 + mcu) + 1) >= D.ywb;
             const bool dum = (yb >= 2 && bottom) || ((yb & 1) && right);
@@ -218,11 +219,11 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
                 if (yb == 1) src = 0;
                 else if (bottom) src = right ? 0 : 1;
                 else src = 2;
-                int16_t dc = oz[mcu * 6 + src][0];
-                val = make_int4(part == 0 ? (int)(uint16_t)dc : 0, 0, 0, 0);
+                const int16_t dc = oz[mcu * 6 + src][0];
+                val = make_int2(quad == 0 ? (int)(uint16_t)dc : 0, 0);
             }
         }
-        *((int4*)gdst + e) = val;
+        *(int2*)(D.coefs + coef_index(bbase + blk, quad * 4)) = val;
     }
 }
 
@@ -265,23 +266,14 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
     }
     __syncthreads();
     const int nblk = min(16, D.mcux - tx * 16);
-    int16_t* gdst = D.coefs + ((int64_t)by * D.mcux + tx * 16) * 64;
-    for (int e = t; e < nblk * 8; e += 256) *((int4*)gdst + e) = *((const int4*)&oz[0][0] + e);
-}
-
-// =================================================================== Huffman
-__device__ __forceinline__ void put_bits(uint32_t* buf, uint32_t pos, uint32_t val, int len)
-{
-    const uint32_t w = pos >> 5;
-    const int o = pos & 31;
-    if (o + len <= 32) {
-        atomicOr(&buf[w], val << (32 - o - len));
-    } else {
-        atomicOr(&buf[w], val >> (o + len - 32));
-        atomicOr(&buf[w + 1], val << (64 - o - len));
+    const int64_t bbase = (int64_t)by * D.mcux + tx * 16;
+    for (int e = t; e < nblk * 16; e += 256) {
+        const int quad = e / nblk, blk = e - quad * nblk;
+        *(int2*)(D.coefs + coef_index(bbase + blk, quad * 4)) = *(const int2*)&oz[blk][quad * 4];
     }
 }
 
+// =================================================================== Huffman
 __device__ __forceinline__ int quant(int c, uint32_t rcp, uint32_t half)
 {
     // jcdctmgr.c: sign(c) * ((|c| + (q<<3)/2) / (q<<3)); exact for |c|+half < 2^16
@@ -292,23 +284,57 @@ __device__ __forceinline__ int quant(int c, uint32_t rcp, uint32_t half)
 
 __device__ __forceinline__ int nbits(int a) { return a ? 32 - __clz(a) : 0; }
 
-// One workgroup = one chunk of CHUNK_BLOCKS scan blocks of one image.  Per
-// pass, each 16-lane group owns one block (4 zig-zag coefficients per lane):
-// quantise, run lengths from a segmented max-scan of nonzero positions, code
-// lengths from LDS tables, exclusive bit offsets, then every code is OR-ed
-// into an LDS bit buffer.  The chunk's packed words go to scratch[cur].
-__global__ __launch_bounds__(256) void k_huff(const ImgDesc* __restrict__ descs,
-                                              const ImgState* __restrict__ states,
-                                              const QNode* __restrict__ nodes,
-                                              const int32_t* __restrict__ ids,
-                                              const int64_t* __restrict__ prefix, int m)
+constexpr int SLOT_WORDS = 17;  // per-block LDS slot (544 bits, odd stride); longer blocks spill to D.ovf
+
+// Per-thread bit sink: a 64-bit accumulator flushing whole 32-bit words into
+// the thread's LDS slot (or its HBM spill region past SLOT_WORDS).
+struct BlockSink {
+    uint64_t acc;
+    int n, widx;
+    uint32_t* lds;
+    uint32_t* spill;
+    __device__ __forceinline__ void store(uint32_t w)
+    {
+        if (widx < SLOT_WORDS) lds[widx] = w; else spill[widx] = w;
+        widx++;
+    }
+    __device__ __forceinline__ void put(uint32_t v, int len)  // len <= 32
+    {
+        acc = (acc << len) | v;
+        n += len;
+        if (n >= 32) {
+            n -= 32;
+            store((uint32_t)(acc >> n));
+        }
+    }
+    __device__ __forceinline__ void finish()
+    {
+        if (n) store((uint32_t)(acc << (32 - n)));
+    }
+};
+
+// One workgroup = one chunk of CHUNK_BLOCKS scan blocks; one thread = one
+// 8x8 block (encode_one_block, jchuff.c), run once per trial:
+//   1. quantise + Huffman-code the thread's block straight into its LDS slot
+//      (coefficient quads read 512 B-coalesced from the interleaved layout)
+//   2. workgroup scan of the block bit counts -> offsets inside the chunk
+//   3. gather: every 32-bit word of the chunk stream is assembled by the
+//      thread whose block holds the word's first bit (reading the following
+//      blocks' slots as needed) and stored once to scratch[cur] - no atomics.
+__global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict__ descs,
+                                                       const ImgState* __restrict__ states,
+                                                       const QNode* __restrict__ nodes,
+                                                       const int32_t* __restrict__ ids,
+                                                       const int64_t* __restrict__ prefix, int m)
 {
-    __shared__ uint32_t bitbuf[CHUNK_WORDS + 1];
-    __shared__ uint32_t s_rcp[2][64];
-    __shared__ uint32_t s_half[2][64];
+    __shared__ uint32_t slots[CHUNK_BLOCKS * SLOT_WORDS];
     __shared__ uint32_t s_ac[2][256];
     __shared__ uint32_t s_dc[2][16];
-    __shared__ uint32_t s_blk[16];
+    __shared__ uint2 s_q[2][64];
+    __shared__ int32_t s_dcq[CHUNK_BLOCKS];
+    __shared__ uint32_t s_off[CHUNK_BLOCKS + 1];
+    __shared__ uint32_t s_bits[CHUNK_BLOCKS];
+    __shared__ uint32_t s_wsum[CHUNK_BLOCKS / 64];
 
     const int64_t item = blockIdx.x;
     const int slot = find_slot(prefix, m, item);
@@ -319,145 +345,123 @@ __global__ __launch_bounds__(256) void k_huff(const ImgDesc* __restrict__ descs,
     const int chunk = (int)(item - prefix[slot]);
     const QNode& N = nodes[S.node];
     const int cur = S.cur;
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
 
-    if (t < 128) {
-        s_rcp[t >> 6][t & 63] = N.rcp[t >> 6][t & 63];
-        s_half[t >> 6][t & 63] = N.half[t >> 6][t & 63];
-    }
-    s_ac[0][t] = c_ac[0][t];
-    s_ac[1][t] = c_ac[1][t];
+    if (t < 128) s_q[t >> 6][t & 63] = make_uint2(N.rcp[t >> 6][t & 63], N.half[t >> 6][t & 63]);
+    for (int i = t; i < 512; i += CHUNK_BLOCKS) s_ac[i >> 8][i & 255] = c_ac[i >> 8][i & 255];
     if (t < 32) s_dc[t >> 4][t & 15] = c_dc[t >> 4][t & 15];
-    for (int i = t; i < CHUNK_WORDS + 1; i += 256) bitbuf[i] = 0;
-    __syncthreads();
 
     const int64_t b0 = (int64_t)chunk * CHUNK_BLOCKS;
     const int nb = (int)min((int64_t)CHUNK_BLOCKS, D.nblocks - b0);
-    const int lane = t & 63, grp = lane >> 4, l = lane & 15, wv = t >> 6;
-    const bool color = D.ncomp == 3;
-    uint32_t running = 0;
-
-    for (int pass = 0; pass < CHUNK_BLOCKS / 16; pass++) {
-        const int bl = pass * 16 + wv * 4 + grp;
-        const bool valid = bl < nb;
-        const int64_t b = b0 + bl;
-        int tb = 0;
-        int64_t pb = -1;
-        if (color) {
-            const int k6 = (int)(b % 6);
-            tb = k6 >= 4;
-            if (k6 >= 1 && k6 <= 3) pb = b - 1;
-            else if (k6 == 0) pb = b >= 6 ? b - 3 : -1;
-            else pb = b >= 6 ? b - 6 : -1;
-        } else {
-            pb = b - 1;
-        }
-        int q[4] = {0, 0, 0, 0};
-        int qprev = 0;
-        if (valid) {
-            const int2 raw = *(const int2*)(D.coefs + b * 64 + 4 * l);
-            const int c[4] = {(int)(int16_t)(raw.x & 0xFFFF), (int)(int16_t)(raw.x >> 16),
-                              (int)(int16_t)(raw.y & 0xFFFF), (int)(int16_t)(raw.y >> 16)};
-#pragma unroll
-            for (int j = 0; j < 4; j++) q[j] = quant(c[j], s_rcp[tb][4 * l + j], s_half[tb][4 * l + j]);
-            if (l == 0 && pb >= 0) qprev = quant(D.coefs[pb * 64], s_rcp[tb][0], s_half[tb][0]);
-        }
-        // last "nonzero" position in this lane (DC counts as the run start)
-        int last = -1;
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (q[j] != 0 || (l == 0 && j == 0)) last = 4 * l + j;
-        int incl = last;
-#pragma unroll
-        for (int d = 1; d < 16; d <<= 1) {
-            int y = __shfl_up(incl, d, 16);
-            if (l >= d) incl = max(incl, y);
-        }
-        int excl = __shfl_up(incl, 1, 16);
-        if (l == 0) excl = -1;
-        const int glast = __shfl(incl, 15, 16);
-
-        // code words of this lane, in emission order (DC, AC k..., EOB)
-        uint32_t cv[4], zrl[4];
-        int cl[4];
-        int lane_bits = 0;
-        uint32_t dcv = 0;
-        int dcl = 0;
-        const uint32_t zrlc = s_ac[tb][0xF0];
-        const int zrll = zrlc & 255;
-        if (l == 0) {
-            int diff = q[0] - qprev;
-            int a = diff < 0 ? -diff : diff;
-            int s = nbits(a);
-            uint32_t mag = (uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << s) - 1);
-            uint32_t hc = s_dc[tb][s];
-            dcv = ((hc >> 8) << s) | mag;
-            dcl = (int)(hc & 255) + s;
-            lane_bits += dcl;
-        }
-        int prev = excl;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int k = 4 * l + j;
-            cv[j] = 0; cl[j] = 0; zrl[j] = 0;
-            if (k >= 1 && q[j] != 0) {
-                int r = k - prev - 1;
-                zrl[j] = r >> 4;
-                r &= 15;
-                int a = q[j] < 0 ? -q[j] : q[j];
-                int s = nbits(a);
-                uint32_t mag = (uint32_t)(q[j] < 0 ? q[j] - 1 : q[j]) & ((1u << s) - 1);
-                uint32_t hc = s_ac[tb][(r << 4) | s];
-                cv[j] = ((hc >> 8) << s) | mag;
-                cl[j] = (int)(hc & 255) + s;
-                lane_bits += cl[j] + (int)zrl[j] * zrll;
-            }
-            if (k == 0 || q[j] != 0) prev = k;
-        }
-        const uint32_t eobc = s_ac[tb][0];
-        const bool eob = (l == 15) && glast < 63;
-        if (eob) lane_bits += eobc & 255;
-        if (!valid) lane_bits = 0;
-
-        int off = lane_bits;  // inclusive add-scan over the 16-lane group
-#pragma unroll
-        for (int d = 1; d < 16; d <<= 1) {
-            int y = __shfl_up(off, d, 16);
-            if (l >= d) off += y;
-        }
-        const int block_bits = __shfl(off, 15, 16);
-        off -= lane_bits;
-        if (l == 0) s_blk[wv * 4 + grp] = block_bits;
-        __syncthreads();
-        uint32_t boff = running;
-        const int me = wv * 4 + grp;
-        uint32_t pass_total = 0;
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            uint32_t v = s_blk[i];
-            if (i < me) boff += v;
-            pass_total += v;
-        }
-        if (valid) {
-            uint32_t pos = boff + off;
-            if (l == 0) { put_bits(bitbuf, pos, dcv, dcl); pos += dcl; }
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                if (cl[j]) {
-                    for (uint32_t z = 0; z < zrl[j]; z++) { put_bits(bitbuf, pos, zrlc >> 8, zrll); pos += zrll; }
-                    put_bits(bitbuf, pos, cv[j], cl[j]);
-                    pos += cl[j];
-                }
-            }
-            if (eob) put_bits(bitbuf, pos, eobc >> 8, eobc & 255);
-        }
-        running += pass_total;
-        __syncthreads();
+    const bool valid = t < nb;
+    const int64_t b = b0 + t;
+    int tb = 0;
+    int64_t pb;
+    if (D.ncomp == 3) {
+        const uint32_t k6 = (uint32_t)(b % 6);
+        tb = k6 >= 4;
+        if (k6 >= 1 && k6 <= 3) pb = b - 1;
+        else if (k6 == 0) pb = b >= 6 ? b - 3 : -1;
+        else pb = b >= 6 ? b - 6 : -1;
+    } else {
+        pb = b - 1;
     }
-    const uint32_t nwords = (running + 31) >> 5;
+    const int16_t* cbase = D.coefs + (b0 * 64) + t * 4;  // quad k of this block at cbase + k*CHUNK_BLOCKS*4
+    int2 quad[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) quad[k] = valid ? *(const int2*)(cbase + k * (CHUNK_BLOCKS * 4)) : make_int2(0, 0);
+    __syncthreads();  // tables ready
+
+    const uint2 q0t = s_q[tb][0];
+    const int dq = quant((int)(int16_t)(quad[0].x & 0xFFFF), q0t.x, q0t.y);
+    s_dcq[t] = dq;
+    __syncthreads();
+    int qprev = 0;
+    if (pb >= b0) qprev = s_dcq[pb - b0];
+    else if (pb >= 0) qprev = quant(D.coefs[coef_index(pb, 0)], q0t.x, q0t.y);
+
+    // ---- 1. encode_one_block into the slot
+    BlockSink sink{0, 0, 0, &slots[t * SLOT_WORDS], D.ovf + b * BLOCK_WORDS};
+    int bits = 0;
+    if (valid) {
+        const int diff = dq - qprev;
+        const int ds = nbits(diff < 0 ? -diff : diff);
+        const uint32_t hc = s_dc[tb][ds];
+        const uint32_t mag = (uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << ds) - 1);
+        sink.put(((hc >> 8) << ds) | mag, (int)(hc & 255) + ds);
+        const uint32_t zrlc = s_ac[tb][0xF0];
+        int run = 0;
+#pragma unroll
+        for (int k = 1; k < 64; k++) {
+            const uint32_t w = (k & 2) ? (uint32_t)quad[k >> 2].y : (uint32_t)quad[k >> 2].x;
+            const int c = (int)(int16_t)(w >> ((k & 1) * 16));
+            const uint2 qq = s_q[tb][k];
+            const int q = quant(c, qq.x, qq.y);
+            if (q != 0) {
+                while (run > 15) {
+                    sink.put(zrlc >> 8, (int)(zrlc & 255));
+                    run -= 16;
+                }
+                const int s = nbits(q < 0 ? -q : q);
+                const uint32_t ac = s_ac[tb][(run << 4) | s];
+                const uint32_t mg = (uint32_t)(q < 0 ? q - 1 : q) & ((1u << s) - 1);
+                sink.put(((ac >> 8) << s) | mg, (int)(ac & 255) + s);
+                run = 0;
+            } else {
+                run++;
+            }
+        }
+        if (run > 0) {
+            const uint32_t eob = s_ac[tb][0];
+            sink.put(eob >> 8, (int)(eob & 255));
+        }
+        bits = sink.widx * 32 + sink.n;
+        sink.finish();
+    }
+
+    // ---- 2. exclusive scan of block bits
+    int incl = bits;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) s_wsum[wv] = incl;
+    __syncthreads();
+    uint32_t off = incl - bits, total = 0;
+#pragma unroll
+    for (int i = 0; i < CHUNK_BLOCKS / 64; i++) {
+        if (i < wv) off += s_wsum[i];
+        total += s_wsum[i];
+    }
+    s_off[t] = off;
+    s_bits[t] = bits;
+    __syncthreads();
+
+    // ---- 3. gather the chunk's words
     uint32_t* dst = D.scratch[cur] + (size_t)chunk * CHUNK_WORDS;
-    for (uint32_t i = t; i < nwords; i += 256) dst[i] = bitbuf[i];
-    if (t == 0) D.chunk_bits[cur][chunk] = running;
+    const uint32_t* spill0 = D.ovf + b0 * BLOCK_WORDS;
+    for (uint32_t j = (off + 31) >> 5; j * 32 < off + bits; j++) {
+        uint32_t outw = 0;
+        int have = 0, u = t;
+        uint32_t p = j * 32 - off;
+        while (have < 32 && u < nb) {
+            const int avail = (int)s_bits[u] - (int)p;
+            const int take = min(32 - have, avail);
+            const uint32_t wi = p >> 5, sh = p & 31;
+            const uint32_t* ls = &slots[u * SLOT_WORDS];
+            const uint32_t* gs = spill0 + (size_t)u * BLOCK_WORDS;
+            uint32_t v = (wi < SLOT_WORDS ? ls[wi] : gs[wi]) << sh;
+            if (sh + take > 32) v |= (wi + 1 < SLOT_WORDS ? ls[wi + 1] : gs[wi + 1]) >> (32 - sh);
+            v &= take == 32 ? ~0u : ~(~0u >> take);
+            outw |= v >> have;
+            have += take;
+            u++;
+            p = 0;
+        }
+        dst[j] = outw;
+    }
+    if (t == 0) D.chunk_bits[cur][chunk] = total;
 }
 
 // Exclusive scan of the chunk bit counts of one image (one workgroup per image).
@@ -791,7 +795,7 @@ void launch_fdct(const ImgDesc* d, const Plan& p, int64_t tiles, int kind, hipSt
 void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, hipStream_t st)
 {
     if (chunks <= 0) return;
-    hipLaunchKernelGGL(k_huff, dim3((unsigned)chunks), dim3(256), 0, st, d, s, n, p.ids, p.prefix, p.m);
+    hipLaunchKernelGGL(k_huff, dim3((unsigned)chunks), dim3(CHUNK_BLOCKS), 0, st, d, s, n, p.ids, p.prefix, p.m);
 }
 
 void launch_scan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st)

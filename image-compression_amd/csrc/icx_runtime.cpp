@@ -449,6 +449,7 @@ void stage_pixels(Batch& B, int i, double scale)
         d.chunk_ff[k] = keep.chunk_ff[k];
     }
     d.chunk_ffoff = keep.chunk_ffoff;
+    d.ovf = keep.ovf;
     d.out = keep.out;
     d.cap = keep.cap;
     d.target = keep.target;
@@ -476,20 +477,27 @@ icx_status run_fdct(Batch& B, const std::vector<int>& ids)
     return ICX_OK;
 }
 
+// Blocks actually quantised+coded by the trials of `ids` since their state
+// was initialised (inactive images exit k_huff at once): the huff kernel's
+// algorithmic work, credited after the stage's synchronisation.
+void credit_huff(Batch& B, const std::vector<int>& ids)
+{
+    if (!B.c->prof) return;
+    int64_t blocks = 0;
+    for (int i : ids) blocks += (int64_t)B.state[i].ntrials * B.desc[i].nblocks;
+    B.c->stats["huff"].units += blocks;
+}
+
 icx_status run_trials(Batch& B, const std::vector<int>& ids, int depth)
 {
     std::vector<int64_t> cnt;
-    int64_t blocks = 0;
-    for (int i : ids) {
-        cnt.push_back(B.desc[i].nchunks);
-        blocks += B.desc[i].nblocks;
-    }
+    for (int i : ids) cnt.push_back(B.desc[i].nchunks);
     DPlan P;
     icx_status s = make_plan(B, ids, cnt, P);
     if (s) return s;
     icx_ctx* c = B.c;
     for (int t = 0; t < depth; t++) {
-        { Timed tm(c, "huff", blocks); launch_huff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
+        { Timed tm(c, "huff", 0); launch_huff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
         { Timed tm(c, "scan", (int64_t)ids.size()); launch_scan(B.d_desc, B.d_state, P.p, c->stream); }
         { Timed tm(c, "ffcount", P.total); launch_ffcount(B.d_desc, B.d_state, P.p, P.total, 0, c->stream); }
         { Timed tm(c, "decide", (int64_t)ids.size()); launch_decide(B.d_desc, B.d_state, B.d_nodes, P.p, c->stream); }
@@ -563,7 +571,8 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             ImgDesc g{};
             geometry(g, j.img.width, j.img.height, j.img.fmt);
             const int nch = channels(j.img.fmt);
-            size_t per = (size_t)g.nblocks * 128 + 2 * ((size_t)g.nchunks * CHUNK_WORDS + 1) * 4 +
+            size_t per = (size_t)g.nchunks * CHUNK_BLOCKS * 128 + (size_t)g.nblocks * BLOCK_WORDS * 4 + 1024 +
+                         2 * ((size_t)g.nchunks * CHUNK_WORDS + 1) * 4 +
                          (size_t)g.nchunks * (2 * 4 + 2 * 8 + 2 * 4 + 8) + 64 + 8 * 256;
             per += (size_t)j.img.width * j.img.height * nch * 2;  // input staging + resize buffer
             per += std::min<uint64_t>(worst_file(g), j.cap);
@@ -621,7 +630,8 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             geometry(d, j.img.width, j.img.height, j.img.fmt);
             d.stride = j.img.stride;
             d.target = j.target_max_size;
-            d.coefs = (int16_t*)c->dev.take((size_t)d.nblocks * 128);
+            d.coefs = (int16_t*)c->dev.take((size_t)d.nchunks * CHUNK_BLOCKS * 128);
+            d.ovf = (uint32_t*)c->dev.take((size_t)d.nblocks * BLOCK_WORDS * 4 + 1024);
             for (int b = 0; b < 2; b++) {
                 d.scratch[b] = (uint32_t*)c->dev.take(((size_t)d.nchunks * CHUNK_WORDS + 1) * 4);
                 d.chunk_bits[b] = (uint32_t*)c->dev.take((size_t)d.nchunks * 4);
@@ -697,8 +707,12 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
         if (mode == Mode::Fdct) {
             for (int k = 0; k < m; k++) init_state(B.state[k], -1, false);
             if ((s = push_desc_state(B)) || (s = run_fdct(B, all)) || (s = sync_states(B))) return s;
-            e = hipMemcpy(fdct_out, B.desc[0].coefs, (size_t)B.desc[0].nblocks * 128, hipMemcpyDeviceToHost);
+            const ImgDesc& d0 = B.desc[0];
+            std::vector<int16_t> raw((size_t)d0.nchunks * CHUNK_BLOCKS * 64);
+            e = hipMemcpy(raw.data(), d0.coefs, raw.size() * 2, hipMemcpyDeviceToHost);
             if (e != hipSuccess) return hip_fail(c, e, "coef download");
+            for (int64_t blk = 0; blk < d0.nblocks; blk++)  // chunk-interleaved -> block-major
+                for (int k = 0; k < 64; k++) fdct_out[blk * 64 + k] = raw[coef_index(blk, k)];
             continue;
         }
 
@@ -712,8 +726,10 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
         if (mode == Mode::Encode) {  // A4: one forced encode
             for (int k = 0; k < m; k++) init_state(B.state[k], B.it[k].cached_node, true);
             if ((s = push_desc_state(B)) || (s = run_fdct(B, all)) || (s = run_trials(B, all, 1)) ||
-                (s = sync_states(B)) || (s = finish_found(all)))
+                (s = sync_states(B)))
                 return s;
+            credit_huff(B, all);
+            if ((s = finish_found(all))) return s;
             for (int k = 0; k < m; k++) {
                 B.it[k].found = B.state[k].best_node >= 0;
                 B.it[k].best_q = jobs[sub[k]].quality;
@@ -737,6 +753,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                 if ((s = push_desc_state(B)) || (s = run_fdct(B, probe)) || (s = run_trials(B, probe, 1)) ||
                     (s = sync_states(B)))
                     return s;
+                credit_huff(B, probe);
                 std::vector<int> hits;
                 for (int k : probe) {
                     B.it[k].encodes += B.state[k].ntrials;
@@ -770,6 +787,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                 if ((s = push_desc_state(B)) || (s = run_fdct(B, need_fdct)) || (s = run_trials(B, pend, depth)) ||
                     (s = sync_states(B)))
                     return s;
+                credit_huff(B, pend);
                 std::vector<int> found, rest;
                 for (int k : pend) {
                     Item& I = B.it[k];
