@@ -60,6 +60,20 @@ def make_frames(n, seed0, device):
     return frames
 
 
+def pmc_traffic(kernel, units_per_launch):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_summary.json, scripts/gpu_pmc.sh): measured bytes per unit
+    of work x this run's units per launch.  None when no summary exists."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        per_unit = json.load(open(path))["bytes_per_unit"][kernel]
+    except (KeyError, ValueError):
+        return None
+    return int(per_unit * units_per_launch)
+
+
 def cpu_baseline(frames, n_sample, threads):
     """Oracle (scalar C restatement, test infrastructure) on host cores."""
     from tests.oracle_ffi import Oracle
@@ -84,6 +98,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
+    ap.add_argument("--target", type=int, default=TARGET, help="-t bytes (default 1 MiB)")
+    ap.add_argument("--no-cache", action="store_true", help="no cached LearnedParams: full binary search")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -97,17 +113,24 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     frames = make_frames(args.images, 1000003 * rank, dev)
-    outs = torch.empty((args.images, TARGET + 1), dtype=torch.uint8, device=dev)
+    outs = torch.empty((args.images, min(args.target, 1 << 24) + 1), dtype=torch.uint8, device=dev)
     codec = icx.Codec(local)
-    batch = codec.prepare(frames, TARGET, Q0, cached=[icx.LearnedParams(Q0, 1.0)] * args.images,
-                          outputs=[outs[i] for i in range(args.images)])
+    cached = None if args.no_cache else [icx.LearnedParams(Q0, 1.0)] * args.images
+    batch = codec.prepare(frames, args.target, Q0, cached=cached, outputs=[outs[i] for i in range(args.images)])
     torch.cuda.synchronize()
+
+    def validate():
+        res = batch.results()
+        ok = sum(r["success"] and r["status"] == 0 for r in res)
+        if ok != args.images:
+            from collections import Counter
+            raise SystemExit(f"{args.images - ok} frames failed: "
+                             f"{Counter((r['success'], r['status']) for r in res)} err={codec.last_error()}")
 
     for _ in range(args.warmup):
         batch.run()
-    res = batch.results()
-    ok = sum(r["success"] and r["status"] == 0 for r in res)
-    assert ok == args.images, f"{args.images - ok} frames failed"
+    if args.warmup:
+        validate()
 
     codec.profile(bool(args.profile))
     codec.profile_reset()
@@ -122,6 +145,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     codec.profile(False)
+    validate()
     if dist:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -132,9 +156,17 @@ def main():
     kstats = {k: codec.profile_query(k) for k in ("fdct", "huff", "scan", "ffcount", "decide", "ffscan",
                                                   "stuff", "resize")}
     kstats = {k: v for k, v in kstats.items() if v["launches"]}
-    dom = max((k for k in kstats if k in ALGO_BYTES), key=lambda k: kstats[k]["ms"])
-    ks = kstats[dom]
-    achieved = ALGO_BYTES[dom] * ks["units"] / (ks["ms"] / 1e3) / 1e9
+    roof = None
+    cands = [k for k in kstats if k in ALGO_BYTES]
+    if cands:
+        dom = max(cands, key=lambda k: kstats[k]["ms"])
+        ks = kstats[dom]
+        achieved = ALGO_BYTES[dom] * ks["units"] / (ks["ms"] / 1e3) / 1e9
+        algo_launch = ALGO_BYTES[dom] * ks["units"] / ks["launches"]
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": pmc_traffic(dom, ks["units"] / ks["launches"]),
+                "avg_launch_ms": round(ks["ms"] / ks["launches"], 4), "algo_bytes_per_launch": int(algo_launch)}
     res = batch.results()
     line = {
         "metric": "megapixels/sec JPEG encode (4K, -t 1MiB, q=0.25 cached)",
@@ -148,10 +180,7 @@ def main():
                    "target_bytes": TARGET, "quality": Q0, "parallelism": f"file-list shard x{world}",
                    "encodes_per_image": round(sum(r["encodes"] for r in res) / len(res), 3),
                    "mean_out_bytes": int(np.mean([r["out_len"] for r in res]))},
-        "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "avg_launch_ms": round(ks["ms"] / ks["launches"], 4),
-                     "algo_bytes_per_launch": int(ALGO_BYTES[dom] * ks["units"] / ks["launches"])},
+        "roofline": roof,
         "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k, v in kstats.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -16,6 +16,8 @@
 // No MFMA: integer, byte-oriented work bound by HBM.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "icx_internal.h"
 #include "icx_kernels.h"
 
@@ -28,6 +30,31 @@ __constant__ uint32_t c_ac[2][256];   // (code << 8) | length, by run/size symbo
 __constant__ uint8_t c_hdr[2][HDR_COLOR];  // [0] grey template, [1] colour template
 
 // ------------------------------------------------------------------ helpers
+// Pointers read from descriptors are generic; casting them to the global
+// address space makes hipcc emit global_load/store instead of flat_* (which
+// need a private segment and are waited for on both vmcnt and lgkmcnt).
+#define GAS __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ GAS T* gp(T* p) { return (GAS T*)p; }
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 ld16(const void* p)
+{
+    const u32x4_t v = *(const GAS u32x4_t*)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ int2 ld8(const void* p)
+{
+    const i32x2_t v = *(const GAS i32x2_t*)p;
+    return make_int2(v.x, v.y);
+}
+__device__ __forceinline__ void st8(void* p, int2 v)
+{
+    i32x2_t w;
+    w.x = v.x;
+    w.y = v.y;
+    *(GAS i32x2_t*)p = w;
+}
 __device__ __forceinline__ int find_slot(const int64_t* prefix, int m, int64_t item)
 {
     int lo = 0, hi = m;  // prefix[lo] <= item < prefix[hi]
@@ -83,134 +110,156 @@ __device__ __forceinline__ void rgb_ycc(int r, int g, int b, int& y, int& cb, in
 }
 
 // =================================================================== FDCT
-// Colour: one workgroup = 16 rows x 128 px = 8 MCUs of one MCU row.
-//   A. coalesced row loads (16-B when aligned and inside) -> LDS raw tile,
-//      edge expansion by clamping x to W-1 and y to H-1
-//   B. per thread 8 px of one row: YCbCr, Y row-DCT in registers
-//   C. h2v2_downsample (bias 1,2,..) + chroma row-DCT
-//   D. column DCT, zig-zag scatter into LDS
-//   E. dummy blocks (jccoefct.c) + coalesced 16-B stores of 48 blocks
+// natural (v, u) -> zig-zag position, byte u of kZZRow[v] (v is always a
+// compile-time constant at the call sites, so the table is immediate)
+__device__ __forceinline__ int zz_of(int v, int u)
+{
+    constexpr uint64_t kZZRow[8] = {0x1C1B0F0E06050100ull, 0x2A1D1A100D070402ull, 0x2B291E19110C0803ull, 0x352C281F18120B09ull,
+                                    0x36342D272017130Aull, 0x3C37332E26211614ull, 0x3D3B38322F252215ull, 0x3F3E3A3931302423ull};
+    return (int)((kZZRow[v] >> (8 * u)) & 0xFF);
+}
+
+// Colour: one workgroup = 16 rows x 256 px = 16 MCUs of one MCU row (96 blocks);
+// every phase has 1-3 equal tasks per thread.
+//   A. 16-B coalesced row loads -> LDS raw tile (edge expansion by clamping)
+//   B. 2 x 8 px per thread: YCbCr, Y row-DCT in registers (int16 workspace)
+//   C. h2v2_downsample (bias 1,2,..) + chroma row-DCT, one row task per thread
+//   D. column DCT, 3 column tasks per thread, zig-zag scatter (aliases raw)
+//   E. dummy blocks (jccoefct.c) + 8-B stores into the interleaved layout
+constexpr int FDC_MCU = 16;           // MCUs per colour tile
+constexpr int FDC_PX = FDC_MCU * 16;  // 256 px
+constexpr int FDC_BLK = FDC_MCU * 6;  // 96 blocks
+
 template <bool BGR>
 __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ descs,
                                                     const int32_t* __restrict__ ids,
                                                     const int64_t* __restrict__ prefix, int m)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t raw[16 * 384];
-    __shared__ __attribute__((aligned(16))) uint8_t cful[2][16][128];
-    __shared__ __attribute__((aligned(16))) int32_t ws[48][64];
-    __shared__ __attribute__((aligned(16))) int16_t oz[48][64];
+    __shared__ __attribute__((aligned(16))) uint8_t rawz[16 * FDC_PX * 3];  // 12 KB; later zig-zag output
+    __shared__ __attribute__((aligned(16))) uint8_t cful[2][16][FDC_PX];    // 8 KB full-res Cb, Cr
+    __shared__ __attribute__((aligned(16))) int16_t ws[FDC_BLK][64];        // 12 KB row-pass output
+    uint8_t* raw = rawz;
+    int16_t (*oz)[64] = (int16_t (*)[64])rawz;
 
     const int64_t item = blockIdx.x;
     const int slot = find_slot(prefix, m, item);
     const ImgDesc& D = descs[ids[slot]];
     const int tile = (int)(item - prefix[slot]);
-    const int tiles_x = (D.mcux + 7) >> 3;
+    const int tiles_x = (D.mcux + FDC_MCU - 1) / FDC_MCU;
     const int my = tile / tiles_x, tx = tile - my * tiles_x;
-    const int W = D.w, H = D.h, x0 = tx * 128, y0 = my * 16;
+    const int W = D.w, H = D.h, x0 = tx * FDC_PX, y0 = my * 16;
     const int t = threadIdx.x;
     const uint8_t* px = D.px;
+    constexpr int ROWB = FDC_PX * 3;  // 768 bytes per tile row
 
-    // ---- A: load 16 x 384 bytes
-    const bool fast = (x0 + 128 <= W) && (((uintptr_t)px & 15) == 0) && ((D.stride & 15) == 0);
+    // ---- A
+    const bool fast = (x0 + FDC_PX <= W) && (((uintptr_t)px & 15) == 0) && ((D.stride & 15) == 0);
     if (fast) {
-        for (int i = t; i < 16 * 24; i += 256) {
-            int r = i / 24, c = i - r * 24;
-            int y = min(y0 + r, H - 1);
-            const uint4* src = (const uint4*)(px + (size_t)y * D.stride + (size_t)x0 * 3) + c;
-            *(uint4*)(raw + r * 384 + c * 16) = *src;
+        uint4 v[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {  // piece i: row i/48, 16-B column i%48, LDS offset 16*i
+            const int i = t + 256 * k, r = i / 48, c = i - r * 48;
+            const int y = min(y0 + r, H - 1);
+            v[k] = ld16(px + (size_t)y * D.stride + (size_t)x0 * 3 + 16 * c);
         }
+#pragma unroll
+        for (int k = 0; k < 3; k++) *(uint4*)(raw + (t + 256 * k) * 16) = v[k];
     } else {
-        for (int i = t; i < 16 * 128; i += 256) {
-            int r = i >> 7, x = i & 127;
-            int y = min(y0 + r, H - 1), sx = min(x0 + x, W - 1);
-            const uint8_t* s = px + (size_t)y * D.stride + (size_t)sx * 3;
-            raw[r * 384 + x * 3 + 0] = s[0];
-            raw[r * 384 + x * 3 + 1] = s[1];
-            raw[r * 384 + x * 3 + 2] = s[2];
+        for (int i = t; i < 16 * FDC_PX; i += 256) {
+            const int r = i / FDC_PX, x = i - r * FDC_PX;
+            const int y = min(y0 + r, H - 1), sx = min(x0 + x, W - 1);
+            const GAS uint8_t* sp = gp(px + (size_t)y * D.stride + (size_t)sx * 3);
+            raw[r * ROWB + x * 3 + 0] = sp[0];
+            raw[r * ROWB + x * 3 + 1] = sp[1];
+            raw[r * ROWB + x * 3 + 2] = sp[2];
         }
     }
     __syncthreads();
 
-    // ---- B: colour convert 8 px per thread, Y row DCT
-    {
-        const int r = t >> 4, s = t & 15;
-        const uint8_t* p = raw + r * 384 + s * 24;
-        uint2 a = *(const uint2*)(p), b = *(const uint2*)(p + 8), c = *(const uint2*)(p + 16);
-        uint32_t wv[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+    // ---- B: 2 row tasks of 8 px
+#pragma unroll
+    for (int rep = 0; rep < 2; rep++) {
+        const int task = t + 256 * rep, r = task >> 5, sg = task & 31;
+        const uint8_t* p = raw + r * ROWB + sg * 24;
+        const uint2 a = *(const uint2*)(p), b = *(const uint2*)(p + 8), c = *(const uint2*)(p + 16);
+        const uint32_t wv[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
         int yv[8];
         uint32_t cbw[2] = {0, 0}, crw[2] = {0, 0};
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-            int o0 = 3 * k, o1 = 3 * k + 1, o2 = 3 * k + 2;
-            int c0 = (wv[o0 >> 2] >> ((o0 & 3) * 8)) & 255;
-            int c1 = (wv[o1 >> 2] >> ((o1 & 3) * 8)) & 255;
-            int c2 = (wv[o2 >> 2] >> ((o2 & 3) * 8)) & 255;
-            int R = BGR ? c2 : c0, G = c1, B = BGR ? c0 : c2;
+            const int o0 = 3 * k, o1 = 3 * k + 1, o2 = 3 * k + 2;
+            const int c0 = (wv[o0 >> 2] >> ((o0 & 3) * 8)) & 255;
+            const int c1 = (wv[o1 >> 2] >> ((o1 & 3) * 8)) & 255;
+            const int c2 = (wv[o2 >> 2] >> ((o2 & 3) * 8)) & 255;
+            const int R = BGR ? c2 : c0, G = c1, B = BGR ? c0 : c2;
             int yy, cb, cr;
             rgb_ycc(R, G, B, yy, cb, cr);
             yv[k] = yy - 128;
             cbw[k >> 2] |= (uint32_t)cb << ((k & 3) * 8);
             crw[k >> 2] |= (uint32_t)cr << ((k & 3) * 8);
         }
-        *(uint2*)&cful[0][r][s * 8] = make_uint2(cbw[0], cbw[1]);
-        *(uint2*)&cful[1][r][s * 8] = make_uint2(crw[0], crw[1]);
+        *(uint2*)&cful[0][r][sg * 8] = make_uint2(cbw[0], cbw[1]);
+        *(uint2*)&cful[1][r][sg * 8] = make_uint2(crw[0], crw[1]);
         fdct8<0>(yv[0], yv[1], yv[2], yv[3], yv[4], yv[5], yv[6], yv[7]);
-        const int blk = (s >> 1) * 6 + (r >> 3) * 2 + (s & 1);
-        int32_t* dst = &ws[blk][(r & 7) * 8];
-        *(int4*)dst = make_int4(yv[0], yv[1], yv[2], yv[3]);
-        *(int4*)(dst + 4) = make_int4(yv[4], yv[5], yv[6], yv[7]);
+        const int blk = (sg >> 1) * 6 + (r >> 3) * 2 + (sg & 1);
+        *(int4*)&ws[blk][(r & 7) * 8] =
+            make_int4((yv[0] & 0xFFFF) | (yv[1] << 16), (yv[2] & 0xFFFF) | (yv[3] << 16),
+                      (yv[4] & 0xFFFF) | (yv[5] << 16), (yv[6] & 0xFFFF) | (yv[7] << 16));
     }
     __syncthreads();
 
-    // ---- C: h2v2_downsample + chroma row DCT (128 row tasks)
-    if (t < 128) {
-        const int comp = t >> 6, cr = (t >> 3) & 7, cb = t & 7;
-        const int crows = (H + 1) >> 1;             // chroma rows with image data
+    // ---- C: h2v2_downsample + chroma row DCT, 256 row tasks
+    {
+        const int comp = t >> 7, cr = (t >> 4) & 7, cb = t & 15;
+        const int crows = (H + 1) >> 1;  // chroma rows with image data
         int re = cr;
         if (my * 8 + cr >= crows) re = crows - 1 - my * 8;  // replicate last chroma row
-        const uint8_t* r0 = &cful[comp][2 * re][cb * 16];
-        const uint8_t* r1 = &cful[comp][2 * re + 1][cb * 16];
-        uint4 u0 = *(const uint4*)r0, u1 = *(const uint4*)r1;
-        uint32_t a[4] = {u0.x, u0.y, u0.z, u0.w}, bb[4] = {u1.x, u1.y, u1.z, u1.w};
+        const uint4 u0 = *(const uint4*)&cful[comp][2 * re][cb * 16];
+        const uint4 u1 = *(const uint4*)&cful[comp][2 * re + 1][cb * 16];
+        const uint32_t a[4] = {u0.x, u0.y, u0.z, u0.w}, bb[4] = {u1.x, u1.y, u1.z, u1.w};
         int v[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-            int wd = j >> 1, sh = (j & 1) * 16;
-            int s0 = ((a[wd] >> sh) & 255) + ((a[wd] >> (sh + 8)) & 255) + ((bb[wd] >> sh) & 255) +
-                     ((bb[wd] >> (sh + 8)) & 255);
+            const int wd = j >> 1, sh = (j & 1) * 16;
+            const int s0 = ((a[wd] >> sh) & 255) + ((a[wd] >> (sh + 8)) & 255) + ((bb[wd] >> sh) & 255) +
+                           ((bb[wd] >> (sh + 8)) & 255);
             v[j] = ((s0 + 1 + (j & 1)) >> 2) - 128;
         }
         fdct8<0>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
-        int32_t* dst = &ws[cb * 6 + 4 + comp][cr * 8];
-        *(int4*)dst = make_int4(v[0], v[1], v[2], v[3]);
-        *(int4*)(dst + 4) = make_int4(v[4], v[5], v[6], v[7]);
+        *(int4*)&ws[cb * 6 + 4 + comp][cr * 8] =
+            make_int4((v[0] & 0xFFFF) | (v[1] << 16), (v[2] & 0xFFFF) | (v[3] << 16),
+                      (v[4] & 0xFFFF) | (v[5] << 16), (v[6] & 0xFFFF) | (v[7] << 16));
     }
     __syncthreads();
 
-    // ---- D: column DCT (384 column tasks)
-    for (int task = t; task < 48 * 8; task += 256) {
-        const int blk = task >> 3, col = task & 7;
-        int32_t d[8];
+    // ---- D: column DCT, 3 tasks per thread (raw is dead: oz aliases it)
+    {
+        const int col = t & 7;
 #pragma unroll
-        for (int v = 0; v < 8; v++) d[v] = ws[blk][v * 8 + col];
-        fdct8<1>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+        for (int rep = 0; rep < 3; rep++) {
+            const int blk = (t >> 3) + 32 * rep;
+            int32_t d[8];
 #pragma unroll
-        for (int v = 0; v < 8; v++) oz[blk][c_nat_to_zz[v * 8 + col]] = (int16_t)d[v];
+            for (int v = 0; v < 8; v++) d[v] = ws[blk][v * 8 + col];
+            fdct8<1>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+#pragma unroll
+            for (int v = 0; v < 8; v++) oz[blk][zz_of(v, col)] = (int16_t)d[v];
+        }
     }
     __syncthreads();
 
     // ---- E: dummy blocks + store.  jccoefct.c compress_data: a Y block right
     // of ceil(W/8) or below ceil(H/8) gets AC = 0 and the DC of MCU_buffer[blkn-1]
     // (right edge) or of the last block of the MCU's previous block row (bottom).
-    const int nmcu = min(8, D.mcux - tx * 8);
+    const int nmcu = min(FDC_MCU, D.mcux - tx * FDC_MCU);
     const int nblk = nmcu * 6;
     const bool bottom = (2 * my + 1) >= D.yhb;
-    const int64_t bbase = ((int64_t)my * D.mcux + tx * 8) * 6;
+    const int64_t bbase = ((int64_t)my * D.mcux + tx * FDC_MCU) * 6;
     for (int e = t; e < nblk * 16; e += 256) {  // (quad, block) pieces of 8 B, block fastest
         const int quad = e / nblk, blk = e - quad * nblk, mcu = blk / 6, yb = blk - mcu * 6;
         int2 val = *(const int2*)&oz[blk][quad * 4];
         if (yb < 4) {
-            const bool right = (2 * (tx * 8 + mcu) + 1) >= D.ywb;
+            const bool right = (2 * (tx * FDC_MCU + mcu) + 1) >= D.ywb;
             const bool dum = (yb >= 2 && bottom) || ((yb & 1) && right);
             if (dum) {
                 // effective source: right dummy in row 0 -> block 0; bottom row -> eff(block 1);
@@ -223,7 +272,7 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
                 val = make_int2(quad == 0 ? (int)(uint16_t)dc : 0, 0);
             }
         }
-        *(int2*)(D.coefs + coef_index(bbase + blk, quad * 4)) = val;
+        st8(D.coefs + coef_index(bbase + blk, quad * 4), val);
     }
 }
 
@@ -245,7 +294,7 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
     if (t < 128) {
         const int r = t >> 4, s = t & 15;
         const int y = min(by * 8 + r, H - 1);
-        const uint8_t* row = D.px + (size_t)y * D.stride;
+        const GAS uint8_t* row = gp(D.px + (size_t)y * D.stride);
         int v[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) v[k] = (int)row[min(x0 + s * 8 + k, W - 1)] - 128;
@@ -262,14 +311,14 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
         for (int v = 0; v < 8; v++) d[v] = ws[blk][v * 8 + col];
         fdct8<1>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
 #pragma unroll
-        for (int v = 0; v < 8; v++) oz[blk][c_nat_to_zz[v * 8 + col]] = (int16_t)d[v];
+        for (int v = 0; v < 8; v++) oz[blk][zz_of(v, col)] = (int16_t)d[v];
     }
     __syncthreads();
     const int nblk = min(16, D.mcux - tx * 16);
     const int64_t bbase = (int64_t)by * D.mcux + tx * 16;
     for (int e = t; e < nblk * 16; e += 256) {
         const int quad = e / nblk, blk = e - quad * nblk;
-        *(int2*)(D.coefs + coef_index(bbase + blk, quad * 4)) = *(const int2*)&oz[blk][quad * 4];
+        st8(D.coefs + coef_index(bbase + blk, quad * 4), *(const int2*)&oz[blk][quad * 4]);
     }
 }
 
@@ -292,7 +341,7 @@ struct BlockSink {
     uint64_t acc;
     int n, widx;
     uint32_t* lds;
-    uint32_t* spill;
+    GAS uint32_t* spill;
     __device__ __forceinline__ void store(uint32_t w)
     {
         if (widx < SLOT_WORDS) lds[widx] = w; else spill[widx] = w;
@@ -366,10 +415,11 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     } else {
         pb = b - 1;
     }
-    const int16_t* cbase = D.coefs + (b0 * 64) + t * 4;  // quad k of this block at cbase + k*CHUNK_BLOCKS*4
+    const GAS int16_t* cbase = gp(D.coefs + (b0 * 64) + t * 4);  // quad k at cbase + k*CHUNK_BLOCKS*4
     int2 quad[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) quad[k] = valid ? *(const int2*)(cbase + k * (CHUNK_BLOCKS * 4)) : make_int2(0, 0);
+    for (int k = 0; k < 16; k++)
+        quad[k] = valid ? ld8((const int16_t*)cbase + k * (CHUNK_BLOCKS * 4)) : make_int2(0, 0);
     __syncthreads();  // tables ready
 
     const uint2 q0t = s_q[tb][0];
@@ -378,10 +428,10 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     __syncthreads();
     int qprev = 0;
     if (pb >= b0) qprev = s_dcq[pb - b0];
-    else if (pb >= 0) qprev = quant(D.coefs[coef_index(pb, 0)], q0t.x, q0t.y);
+    else if (pb >= 0) qprev = quant(gp(D.coefs)[coef_index(pb, 0)], q0t.x, q0t.y);
 
     // ---- 1. encode_one_block into the slot
-    BlockSink sink{0, 0, 0, &slots[t * SLOT_WORDS], D.ovf + b * BLOCK_WORDS};
+    BlockSink sink{0, 0, 0, &slots[t * SLOT_WORDS], gp(D.ovf + b * BLOCK_WORDS)};
     int bits = 0;
     if (valid) {
         const int diff = dq - qprev;
@@ -439,8 +489,8 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     __syncthreads();
 
     // ---- 3. gather the chunk's words
-    uint32_t* dst = D.scratch[cur] + (size_t)chunk * CHUNK_WORDS;
-    const uint32_t* spill0 = D.ovf + b0 * BLOCK_WORDS;
+    GAS uint32_t* dst = gp(D.scratch[cur] + (size_t)chunk * CHUNK_WORDS);
+    const GAS uint32_t* spill0 = gp(D.ovf + b0 * BLOCK_WORDS);
     for (uint32_t j = (off + 31) >> 5; j * 32 < off + bits; j++) {
         uint32_t outw = 0;
         int have = 0, u = t;
@@ -450,7 +500,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
             const int take = min(32 - have, avail);
             const uint32_t wi = p >> 5, sh = p & 31;
             const uint32_t* ls = &slots[u * SLOT_WORDS];
-            const uint32_t* gs = spill0 + (size_t)u * BLOCK_WORDS;
+            const GAS uint32_t* gs = spill0 + (size_t)u * BLOCK_WORDS;
             uint32_t v = (wi < SLOT_WORDS ? ls[wi] : gs[wi]) << sh;
             if (sh + take > 32) v |= (wi + 1 < SLOT_WORDS ? ls[wi + 1] : gs[wi + 1]) >> (32 - sh);
             v &= take == 32 ? ~0u : ~(~0u >> take);
@@ -505,13 +555,13 @@ __global__ __launch_bounds__(1024) void k_scan(const ImgDesc* __restrict__ descs
 
 // 32 bits of the globally aligned stream starting at global bit 32*w, from
 // chunk c (whose bits start at `start`), the next chunk, then 1-bit padding.
-__device__ __forceinline__ uint32_t stream_word(const uint32_t* __restrict__ scratch,
-                                                const uint64_t* __restrict__ off, int nchunks, int c,
+__device__ __forceinline__ uint32_t stream_word(const GAS uint32_t* __restrict__ scratch,
+                                                const GAS uint64_t* __restrict__ off, int nchunks, int c,
                                                 uint64_t w)
 {
     const uint64_t gbit = w * 32;
     const uint64_t start = off[c], end = off[c + 1];
-    const uint32_t* cs = scratch + (size_t)c * CHUNK_WORDS;
+    const GAS uint32_t* cs = scratch + (size_t)c * CHUNK_WORDS;
     const uint64_t s = gbit - start;
     const uint32_t lw = (uint32_t)(s >> 5), sh = (uint32_t)(s & 31);
     uint32_t v = cs[lw] << sh;
@@ -522,7 +572,7 @@ __device__ __forceinline__ uint32_t stream_word(const uint32_t* __restrict__ scr
     int have = (int)avail;
     if (c + 1 < nchunks) {
         const uint64_t nlen = off[c + 2] - end;
-        const uint32_t* ns = scratch + (size_t)(c + 1) * CHUNK_WORDS;
+        const GAS uint32_t* ns = scratch + (size_t)(c + 1) * CHUNK_WORDS;
         uint32_t nv = ns[0];
         int take = (int)min((uint64_t)(32 - have), nlen);
         if (take > 0) {
@@ -552,7 +602,7 @@ __global__ __launch_bounds__(256) void k_ffcount(const ImgDesc* __restrict__ des
     const ImgDesc& D = descs[img];
     const int c = (int)(item - prefix[slot]);
     const int buf = use_best ? S.best_buf : S.cur;
-    const uint64_t* off = D.chunk_off[buf];
+    const GAS uint64_t* off = gp(D.chunk_off[buf]);
     const uint64_t total = off[D.nchunks];
     const uint64_t nbytes = (total + 7) >> 3;
     const uint64_t wlim = (nbytes + 3) >> 2;
@@ -561,7 +611,7 @@ __global__ __launch_bounds__(256) void k_ffcount(const ImgDesc* __restrict__ des
     const int lane = threadIdx.x & 63;
     uint32_t cnt = 0;
     for (uint64_t w = wb + lane; w < we; w += 64) {
-        uint32_t v = stream_word(D.scratch[buf], off, D.nchunks, c, w);
+        uint32_t v = stream_word(gp(D.scratch[buf]), off, D.nchunks, c, w);
 #pragma unroll
         for (int j = 0; j < 4; j++)
             if (w * 4 + j < nbytes && ((v >> (24 - 8 * j)) & 255) == 255) cnt++;
@@ -667,8 +717,8 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
     const int c = (int)(item - prefix[slot]);
     const int buf = S.best_buf;
     const int lane = threadIdx.x & 63;
-    uint8_t* out = D.out;
-    const uint64_t* off = D.chunk_off[buf];
+    GAS uint8_t* out = gp(D.out);
+    const GAS uint64_t* off = gp(D.chunk_off[buf]);
     const uint64_t total = off[D.nchunks];
     const uint64_t nbytes = (total + 7) >> 3;
     const int hdr = D.hdr_len;
@@ -697,7 +747,7 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
         uint32_t v = 0;
         int cnt = 0;
         if (w < we) {
-            v = stream_word(D.scratch[buf], off, D.nchunks, c, w);
+            v = stream_word(gp(D.scratch[buf]), off, D.nchunks, c, w);
 #pragma unroll
             for (int j = 0; j < 4; j++)
                 if (w * 4 + j < nbytes && ((v >> (24 - 8 * j)) & 255) == 255) cnt++;

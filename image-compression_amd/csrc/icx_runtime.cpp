@@ -232,7 +232,7 @@ void geometry(ImgDesc& d, int w, int h, int fmt)
 
 int64_t fdct_tiles(const ImgDesc& d)
 {
-    return d.ncomp == 1 ? (int64_t)((d.mcux + 15) / 16) * d.mcuy : (int64_t)((d.mcux + 7) / 8) * d.mcuy;
+    return d.ncomp == 1 ? (int64_t)((d.mcux + 15) / 16) * d.mcuy : (int64_t)((d.mcux + 15) / 16) * d.mcuy;
 }
 
 // worst-case entropy bytes after stuffing

@@ -145,6 +145,9 @@ class Codec:
         except Exception:
             pass
 
+    def last_error(self) -> str:
+        return self._lib.icx_last_error(self._ctx).decode()
+
     def _check(self, st, what):
         if st != N.OK:
             raise N.IcxError(st, f"{what}: {self._lib.icx_status_string(st).decode()} "
