@@ -1,0 +1,89 @@
+"""L2 learned-parameter cache: the reference's H2CacheManager surface
+(cache/H2CacheManager.java:23-171) on a file database.
+
+H2 is a Java database engine and cannot be embedded here; SQLite (Python
+stdlib) stands in with the same schema and the same semantics:
+
+  * table LEARNED_PARAMS_CACHE(WIDTH_BUCKET INT, HEIGHT_BUCKET INT,
+    SIZE_BUCKET BIGINT, QUALITY FLOAT, SCALE DOUBLE, PK(w, h, s))  (:48-55)
+  * the configured path has a trailing ".mv.db" stripped (:32); the file is
+    "<path>.icx.sqlite"
+  * load_all_to_map reads every row into the in-memory L1 map (:68-93)
+  * save_all_from_map upserts (MERGE) every entry in batches of 1000 inside
+    one transaction (:100-155)
+  * the L1 map itself is a plain dict guarded by the caller (the reference's
+    ConcurrentHashMap, :69); quality values stay float32-exact.
+"""
+import logging
+import os
+import sqlite3
+import threading
+
+import numpy as np
+
+from .core import LearnedParams, SimilarityKey
+
+log = logging.getLogger("icx.cache")
+
+SCHEMA = """CREATE TABLE IF NOT EXISTS LEARNED_PARAMS_CACHE (
+    WIDTH_BUCKET INT NOT NULL,
+    HEIGHT_BUCKET INT NOT NULL,
+    SIZE_BUCKET BIGINT NOT NULL,
+    QUALITY FLOAT NOT NULL,
+    SCALE DOUBLE NOT NULL,
+    PRIMARY KEY (WIDTH_BUCKET, HEIGHT_BUCKET, SIZE_BUCKET))"""
+
+
+def db_file(path) -> str:
+    p = str(path)
+    if p.endswith(".mv.db"):
+        p = p[: -len(".mv.db")]
+    return p + ".icx.sqlite"
+
+
+class LockedDict(dict):
+    """dict with an explicit lock for compound updates (ConcurrentHashMap role)."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.lock = threading.Lock()
+
+
+class CacheManager:
+    def __init__(self, path):
+        self.path = db_file(path)
+        d = os.path.dirname(os.path.abspath(self.path))
+        os.makedirs(d, exist_ok=True)
+        self.conn = sqlite3.connect(self.path, check_same_thread=False)
+        log.info("成功連接到 L2 快取: %s", self.path)
+
+    def init_schema(self):
+        with self.conn:
+            self.conn.execute(SCHEMA)
+
+    def load_all_to_map(self) -> LockedDict:
+        m = LockedDict()
+        for wb, hb, sb, q, s in self.conn.execute(
+                "SELECT WIDTH_BUCKET, HEIGHT_BUCKET, SIZE_BUCKET, QUALITY, SCALE FROM LEARNED_PARAMS_CACHE"):
+            m[SimilarityKey(int(wb), int(hb), int(sb))] = LearnedParams(float(np.float32(q)), float(s))
+        log.info("從 L2 快取載入 %d 筆學習參數到 L1", len(m))
+        return m
+
+    def save_all_from_map(self, m, batch_size: int = 1000) -> int:
+        rows = [(k.width_bucket, k.height_bucket, k.size_bucket, float(np.float32(v.quality)), float(v.scale))
+                for k, v in list(m.items())]
+        if not rows:
+            return 0
+        with self.conn:  # one transaction
+            for i in range(0, len(rows), batch_size):
+                self.conn.executemany(
+                    "INSERT OR REPLACE INTO LEARNED_PARAMS_CACHE "
+                    "(WIDTH_BUCKET, HEIGHT_BUCKET, SIZE_BUCKET, QUALITY, SCALE) VALUES (?, ?, ?, ?, ?)",
+                    rows[i:i + batch_size])
+        log.info("成功將 %d 筆 L1 快取資料寫回 L2", len(rows))
+        return len(rows)
+
+    def close(self):
+        if self.conn is not None:
+            self.conn.close()
+            self.conn = None

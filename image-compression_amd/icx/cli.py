@@ -1,0 +1,113 @@
+"""Execute.java's picocli command (Execute.java:14-88) with the same flags and
+defaults, plus GPU placement flags.
+
+  python -m icx -f list.txt -o outdir [-q 0.25] [-s 1048576] [-w 1920] [-i 1920]
+                [-t 1048576] [--timeOut 24] [--cache-db image-compression-cache]
+                [--devices 0,1] [--group 16] [--decode-threads N]
+
+Multi-GPU: either one process driving several devices (--devices, one worker
+thread per GPU sharing one L1 cache), or one process per GPU under torchrun
+(RANK/WORLD_SIZE/LOCAL_RANK): the file list is sharded by line index, result
+counters are summed and the learned-cache entries merged on rank 0, which
+writes the L2 cache (H2 AUTO_SERVER's multi-process role,
+H2CacheManager.java:34-35).
+"""
+import argparse
+import logging
+import os
+import sys
+
+from .core import CompressionParams
+
+log = logging.getLogger("icx")
+
+
+def build_parser():
+    p = argparse.ArgumentParser(prog="image-compressor", description="批次圖片壓縮工具")
+    p.add_argument("-f", "--file-list", required=True, help="包含圖片路徑的文字檔案。")
+    p.add_argument("-o", "--output-dir", required=True, help="壓縮後圖片的儲存目錄。")
+    p.add_argument("-q", "--quality", type=float, default=0.25)
+    p.add_argument("-s", "--minSize", type=int, default=1048576)
+    p.add_argument("-w", "--minWidth", type=int, default=1920)
+    p.add_argument("-i", "--minHeight", type=int, default=1920)
+    p.add_argument("-t", "--target-max-size", type=int, default=1048576)
+    p.add_argument("--timeOut", type=float, default=24)
+    p.add_argument("--cache-db", default="image-compression-cache")
+    p.add_argument("--devices", default=None, help="GPU ordinals for this process, e.g. 0,1 (default: LOCAL_RANK or 0)")
+    p.add_argument("--group", type=int, default=16, help="JPEGs per device batch")
+    p.add_argument("--decode-threads", type=int, default=None)
+    p.add_argument("-V", "--version", action="version", version="1.0")
+    return p
+
+
+def params_of(a) -> CompressionParams:
+    return CompressionParams(float(a.quality), int(a.minSize), int(a.minWidth), int(a.minHeight),
+                             int(a.target_max_size))
+
+
+def main(argv=None) -> int:
+    a = build_parser().parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s - %(message)s")
+    from .pipeline import BatchReport, CompressionBatch
+    from . import Codec
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    devices = [int(x) for x in a.devices.split(",")] if a.devices else [local]
+    params = params_of(a)
+    log.info("壓縮任務開始: 來源列表 %s, 輸出目錄 %s, q=%s, 最小尺寸 %dx%d, 最小大小 %d, 目標 %d, 快取 %s",
+             os.path.abspath(a.file_list), os.path.abspath(a.output_dir), a.quality, a.minWidth, a.minHeight,
+             a.minSize, a.target_max_size, os.path.abspath(a.cache_db))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    codecs = [Codec(d) for d in devices]
+    batch = CompressionBatch(a.file_list, a.output_dir, params, a.timeOut, a.cache_db, codecs=codecs,
+                             group_size=a.group, decode_threads=a.decode_threads, rank=rank, world=world)
+    if dist is None:
+        rep = batch.execute()
+    else:
+        rep, _ = run_distributed(batch, dist)
+    if rank == 0:
+        rep.log()
+        log.info("所有任務執行完畢 (%.2f s)", rep.seconds)
+    for c in codecs:
+        c.close()
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+def run_distributed(batch, dist):
+    """Every rank compresses its shard with its own L1 cache (loaded from the
+    same L2 file); counters are summed, cache entries merged and saved on rank 0."""
+    import torch
+    from .cache import CacheManager
+    from .pipeline import BatchReport
+    mgr = CacheManager(batch.h2_cache_path) if dist.get_rank() == 0 else None
+    if mgr is not None:
+        mgr.init_schema()
+    dist.barrier()
+    cache = CacheManager(batch.h2_cache_path).load_all_to_map()
+    rep = batch.execute(cache=cache, save_cache=False)
+    v = torch.tensor(rep.to_vector(), dtype=torch.int64)
+    dist.all_reduce(v)
+    total = BatchReport.from_vector(v.tolist())
+    t = torch.tensor([rep.seconds], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    total.seconds = float(t.item())
+    gathered = [None] * dist.get_world_size()
+    dist.all_gather_object(gathered, dict(cache))
+    merged = {}
+    for g in gathered:  # rank order: later ranks win on equal keys (last-writer-wins, as the reference)
+        merged.update(g)
+    total.cache_size = len(merged)
+    if mgr is not None:
+        mgr.save_all_from_map(merged)
+        mgr.close()
+    return total, merged
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,412 @@
+"""Per-image pipeline and batch driver around the GPU hot path.
+
+Mirrors (reference = src/main/java/work/pollochang/compression/image/):
+  core/ImageCompression.java:47-105    process_image          (gates, dispatch, result mapping)
+  core/ImageCompression.java:107-165   decode_image_with_subsampling
+  core/ImageCompression.java:167-183   compress_image_iteratively (format switch)
+  CompressionBatch.java:41-148         CompressionBatch.execute
+
+Differences that are design, not semantics:
+  * the reference runs processImage on N CPU threads; here decoding runs on
+    host threads while JPEG images are grouped into device batches (one
+    icx_compress_jpg_batch launch sequence per group), one worker per GPU;
+  * the learned-cache lookup for an image happens when its group is formed
+    (the reference's lookups also race with other tasks' puts: results of
+    both depend on completion order).
+Decoding uses libjpeg-turbo through Pillow (6b-lineage ISLOW IDCT + h2v2 fancy
+upsampling, the JDK decoder's arithmetic); device decode is the
+next row of the plan.
+"""
+import concurrent.futures as cf
+import logging
+import os
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+from . import _native as N
+from .core import (CompressionParams, CompressionReport, CompressionResult, create_key,
+                   subsampling_factor)
+
+log = logging.getLogger("icx.pipeline")
+
+# Pillow format -> javax.imageio reader SPI getFormatNames()[0].toLowerCase()
+# (formats the JDK can read; anything else has no reader: readers.hasNext() == false)
+IMAGEIO_FORMATS = {"JPEG": "jpeg", "PNG": "png", "GIF": "gif", "BMP": "bmp", "TIFF": "tif", "WBMP": "wbmp"}
+
+
+@dataclass
+class DecodedImage:
+    """core/DecodedImage.java:7-16: pixels + the reader's format name."""
+    image: np.ndarray
+    format_name: str
+    width: int
+    height: int
+    subsampling: int
+
+
+def format_file_size(size: int) -> str:
+    """FileTools.formatFileSize: 1024-based, '#,##0.#'."""
+    if size <= 0:
+        return "0"
+    units = ["B", "KB", "MB", "GB", "TB"]
+    import math
+    g = min(int(math.log10(size) / math.log10(1024)), len(units) - 1)
+    return f"{size / 1024 ** g:,.1f}".rstrip("0").rstrip(".") + " " + units[g]
+
+
+def _to_array(im):
+    """Decoded raster as the BufferedImage type the JDK reader returns."""
+    mode = im.mode
+    if mode == "L":
+        return np.asarray(im, dtype=np.uint8)
+    if mode in ("I;16", "I;16B", "I", "F", "1"):
+        return np.asarray(im.convert("L"), dtype=np.uint8)
+    if mode != "RGB":
+        im = im.convert("RGB")  # CMYK/P/RGBA/LA: approximate
+    rgb = np.asarray(im, dtype=np.uint8)
+    return np.ascontiguousarray(rgb[:, :, ::-1])  # TYPE_3BYTE_BGR
+
+
+def decode_image_with_subsampling(input_path, params: CompressionParams, file_size: int) -> Optional[DecodedImage]:
+    """ImageCompression.decodeImageWithSubsampling: None when the file is at or
+    below -s, has no reader, or is not larger than (-w, -i) on both axes."""
+    from PIL import Image
+    if file_size <= params.min_size_bytes:
+        log.info("%s - 跳過: 檔案大小 %s 未超過最小壓縮門檻 %s", input_path, format_file_size(file_size),
+                 format_file_size(params.min_size_bytes))
+        return None
+    try:
+        im = Image.open(input_path)
+    except (Image.UnidentifiedImageError, ValueError):
+        log.warning("%s - 找不到對應的圖片讀取器，跳過", input_path)
+        return None
+    with im:
+        fmt = IMAGEIO_FORMATS.get(im.format or "")
+        if fmt is None:
+            log.warning("%s - 找不到對應的圖片讀取器，跳過", input_path)
+            return None
+        width, height = im.size
+        if width <= params.min_width or height <= params.min_height:
+            log.debug("%s - 跳過: 圖片尺寸 %dx%d 未超過最小壓縮門檻 %dx%d", input_path, width, height,
+                      params.min_width, params.min_height)
+            return None
+        s = subsampling_factor(width, height)
+        arr = _to_array(im)
+    if s > 1:  # ImageReadParam.setSourceSubsampling(s, s, 0, 0): keep pixels (x*s, y*s)
+        log.debug("%s - 對圖片應用二次取樣，比率: %d", os.path.basename(str(input_path)), s)
+        arr = np.ascontiguousarray(arr[::s, ::s])
+    return DecodedImage(arr, fmt, width, height, s)
+
+
+@dataclass
+class _Item:
+    index: int
+    path: str
+    original_size: int = 0
+    decoded: Optional[DecodedImage] = None
+    report: Optional[CompressionReport] = None
+    output: Optional[str] = None
+
+
+def _prepare(index, path, output_dir, params) -> _Item:
+    """processImage up to and including the decode (ImageCompression.java:53-76)."""
+    it = _Item(index, path)
+    try:
+        if not os.path.exists(path) or not os.access(path, os.R_OK):
+            log.warning("%s - 檔案不存在或不可讀，跳過", path)
+            it.report = CompressionReport(CompressionResult.SKIPPED_NOT_FOUND, 0, 0)
+            return it
+        it.original_size = os.path.getsize(path)
+    except OSError:
+        it.report = CompressionReport(CompressionResult.FAILED_IO_ERROR, 0, 0)
+        return it
+    try:
+        d = decode_image_with_subsampling(path, params, it.original_size)
+    except MemoryError:
+        it.report = CompressionReport(CompressionResult.FAILED_OUT_OF_MEMORY, it.original_size, 0)
+        return it
+    except OSError:
+        log.warning("%s - 處理圖片時發生 I/O 錯誤 (可能非支援格式或檔案損毀)", path)
+        it.report = CompressionReport(CompressionResult.FAILED_IO_ERROR, it.original_size, 0)
+        return it
+    except Exception:
+        log.exception("%s - 處理檔案時發生未知錯誤", path)
+        it.report = CompressionReport(CompressionResult.FAILED_UNKNOWN, it.original_size, 0)
+        return it
+    if d is None:
+        should = it.original_size > params.min_size_bytes
+        it.report = CompressionReport(
+            CompressionResult.FAILED_UNSUPPORTED_FORMAT if should else CompressionResult.SKIPPED_CONDITION_NOT_MET,
+            it.original_size, it.original_size)
+        return it
+    it.decoded = d
+    it.output = os.path.join(str(output_dir), os.path.basename(str(path)))
+    return it
+
+
+def _finish(it: _Item, success: bool):
+    """Result mapping after compressImageIteratively (ImageCompression.java:79-93)."""
+    if success:
+        comp = os.path.getsize(it.output)
+        ratio = 100.0 * (it.original_size - comp) / it.original_size if it.original_size else 0.0
+        log.info("%s - 處理成功 -> %s (大小: %s -> %s, 節省: %.2f%%)", it.path, it.output,
+                 format_file_size(it.original_size), format_file_size(comp), ratio)
+        it.report = CompressionReport(CompressionResult.COMPRESSED_SUCCESS, it.original_size, comp)
+    else:
+        log.warning("%s - 無法在目標大小限制下完成壓縮", it.path)
+        try:
+            os.remove(it.output)
+        except FileNotFoundError:
+            pass
+        it.report = CompressionReport(CompressionResult.FAILED_COMPRESSION, it.original_size, 0)
+    it.decoded = None
+
+
+def _fail(it: _Item, exc: BaseException):
+    if isinstance(exc, MemoryError) or getattr(exc, "status", None) == N.E_NOMEM:
+        res = CompressionResult.FAILED_OUT_OF_MEMORY
+    elif isinstance(exc, OSError) or getattr(exc, "status", None) == N.E_DEVICE:
+        res = CompressionResult.FAILED_IO_ERROR
+    else:
+        res = CompressionResult.FAILED_UNKNOWN
+    log.error("%s - %s", it.path, exc)
+    it.report = CompressionReport(res, it.original_size, 0)
+    it.decoded = None
+
+
+def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, cache):
+    """compressJpgWithTargetSize for a group of decoded JPEGs in one device batch."""
+    keys = [create_key(it.decoded.image, it.original_size) for it in items]
+    with cache.lock:
+        cached = [cache.get(k) for k in keys]
+    try:
+        res = codec.fit([it.decoded.image for it in items], params.target_max_size_bytes, params.quality,
+                        cached=cached)
+    except Exception as e:  # context-level failure: every image of the group fails alike
+        for it in items:
+            _fail(it, e)
+        return
+    for it, key, c, r in zip(items, keys, cached, res):
+        try:
+            if r["status"] == N.E_NOMEM:
+                raise MemoryError("device out of memory")
+            if r["status"] != N.OK:
+                raise OSError(f"encode failed (icx status {r['status']})")
+            if r["success"]:
+                with open(it.output, "wb") as f:
+                    f.write(r["data"])
+                if not r["cache_hit"]:
+                    with cache.lock:
+                        cache[key] = r["learned"]
+            _finish(it, r["success"])
+        except Exception as e:
+            _fail(it, e)
+
+
+def compress_png_item(codec, it: _Item, params: CompressionParams):
+    try:
+        _finish(it, codec.compress_png_with_target_size(it.decoded.image, it.output, params))
+    except Exception as e:
+        _fail(it, e)
+
+
+def compress_image_iteratively(codec, it: _Item, params, cache):
+    """The format switch (ImageCompression.java:167-183) for one item."""
+    fmt = it.decoded.format_name
+    if fmt in ("jpeg", "jpg"):
+        compress_jpeg_group(codec, [it], params, cache)
+    elif fmt == "png":
+        compress_png_item(codec, it, params)
+    else:
+        log.warning("不支援的檔案格式: %s ...", fmt)
+        _finish(it, False)
+
+
+def process_image(input_path, output_dir, params: CompressionParams, cache, codec) -> CompressionReport:
+    """ImageCompression.processImage for one file (codec used only to compress)."""
+    from .cache import LockedDict
+    if not hasattr(cache, "lock"):
+        cache = LockedDict(cache) if cache is not None else LockedDict()
+    it = _prepare(0, str(input_path), output_dir, params)
+    if it.report is None:
+        compress_image_iteratively(codec, it, params, cache)
+    return it.report
+
+
+@dataclass
+class BatchReport:
+    total: int = 0
+    counts: dict = field(default_factory=lambda: {r: 0 for r in CompressionResult})
+    original_size: int = 0
+    compressed_size: int = 0
+    cache_size: int = 0
+    seconds: float = 0.0
+    megapixels: float = 0.0
+
+    @property
+    def success(self):
+        return self.counts[CompressionResult.COMPRESSED_SUCCESS]
+
+    @property
+    def skipped(self):
+        return self.counts[CompressionResult.SKIPPED_CONDITION_NOT_MET] + self.counts[CompressionResult.SKIPPED_NOT_FOUND]
+
+    @property
+    def failed(self):  # CompressionBatch.java:112-115
+        return self.total - self.success - self.skipped
+
+    def add(self, rep: CompressionReport):
+        self.counts[rep.result] += 1
+        self.original_size += rep.original_size
+        self.compressed_size += rep.compressed_size
+
+    def to_vector(self):
+        return [self.total] + [self.counts[r] for r in CompressionResult] + \
+            [self.original_size, self.compressed_size]
+
+    @classmethod
+    def from_vector(cls, v):
+        b = cls()
+        b.total = int(v[0])
+        for i, r in enumerate(CompressionResult):
+            b.counts[r] = int(v[1 + i])
+        b.original_size, b.compressed_size = int(v[-2]), int(v[-1])
+        return b
+
+    def log(self):
+        log.info("處理結果 -> 總計: %d, 成功壓縮: %d, 跳過不壓縮: %d, 失敗: %d", self.total, self.success,
+                 self.skipped, self.failed)
+        saved = self.original_size - self.compressed_size
+        pct = 0.0 if self.original_size == 0 else saved / self.original_size * 100.0
+        log.info(" 原始檔案總大小: %s", format_file_size(self.original_size))
+        log.info(" 壓縮後檔案總大小: %s", format_file_size(self.compressed_size))
+        log.info(" 共節省硬碟空間: %s", format_file_size(saved))
+        log.info(" 總空間節省百分比: %.2f %%", pct)
+
+
+def read_file_list(path) -> List[str]:
+    with open(path, encoding="utf-8") as f:
+        return [ln.strip() for ln in f if ln.strip()]
+
+
+def shard(lines, rank: int, world: int):
+    """File-list sharding across ranks: line i goes to rank i % world."""
+    return [(i, p) for i, p in enumerate(lines) if i % world == rank]
+
+
+class CompressionBatch:
+    """CompressionBatch.execute: decode on host threads, compress on the GPU(s).
+
+    codecs: one icx.Codec per device this process drives (a worker thread
+    each); they share one L1 learned cache (the reference's ConcurrentHashMap)."""
+
+    def __init__(self, file_list_path, save_dir, params: CompressionParams, time_out_hr: float = 24,
+                 h2_cache_path="image-compression-cache", codecs=None, group_size: int = 16,
+                 decode_threads: Optional[int] = None, rank: int = 0, world: int = 1):
+        self.file_list_path = file_list_path
+        self.save_dir = save_dir
+        self.params = params
+        self.time_out_hr = time_out_hr
+        self.h2_cache_path = h2_cache_path
+        self.codecs = codecs or []
+        self.group_size = max(1, group_size)
+        self.decode_threads = decode_threads or min(16, os.cpu_count() or 1)
+        self.rank, self.world = rank, world
+
+    def execute(self, cache=None, save_cache: bool = True) -> BatchReport:
+        from .cache import CacheManager, LockedDict
+        os.makedirs(self.save_dir, exist_ok=True)
+        mgr = None
+        if cache is None:
+            mgr = CacheManager(self.h2_cache_path)
+            mgr.init_schema()
+            cache = mgr.load_all_to_map()
+            log.info("初始化 H2 二級快取，並載入至記憶體 L1 快取。")
+        elif not hasattr(cache, "lock"):
+            cache = LockedDict(cache)
+        rep = BatchReport()
+        t0 = time.perf_counter()
+        try:
+            lines = read_file_list(self.file_list_path)
+            mine = shard(lines, self.rank, self.world)
+            rep.total = len(mine)
+            deadline = t0 + self.time_out_hr * 3600.0
+            items = self._run(mine, cache, deadline)
+            for it in items:
+                if it.report is not None:
+                    rep.add(it.report)
+            rep.megapixels = sum(getattr(it, "mp", 0.0) for it in items)
+        finally:
+            rep.seconds = time.perf_counter() - t0
+            rep.cache_size = len(cache)
+            if mgr is not None:
+                log.info("記憶體中 L1 快取最終大小: %d", len(cache))
+                if save_cache:
+                    mgr.save_all_from_map(cache)
+                mgr.close()
+        return rep
+
+    def _run(self, mine, cache, deadline):
+        work: "queue.Queue" = queue.Queue()
+        done_items: List[_Item] = []
+        lock = threading.Lock()
+
+        def gpu_worker(codec):
+            while True:
+                grp = work.get()
+                if grp is None:
+                    return
+                kind, its = grp
+                if time.perf_counter() > deadline:  # shutdownNow(): unfinished tasks are dropped
+                    continue
+                if kind == "jpeg":
+                    compress_jpeg_group(codec, its, self.params, cache)
+                elif kind == "png":
+                    for it in its:
+                        compress_png_item(codec, it, self.params)
+                else:
+                    for it in its:
+                        compress_image_iteratively(codec, it, self.params, cache)
+
+        workers = [threading.Thread(target=gpu_worker, args=(c,), daemon=True) for c in self.codecs]
+        for w in workers:
+            w.start()
+        pending_jpeg: List[_Item] = []
+        with cf.ThreadPoolExecutor(self.decode_threads) as pool:
+            futs = [pool.submit(_prepare, i, p, self.save_dir, self.params) for i, p in mine]
+            try:
+                for f in cf.as_completed(futs, timeout=max(0.0, deadline - time.perf_counter())):
+                    it = f.result()
+                    with lock:
+                        done_items.append(it)
+                    if it.report is not None:
+                        continue
+                    it.mp = it.decoded.width * it.decoded.height / 1e6
+                    if not self.codecs:
+                        raise RuntimeError("no GPU codec available to compress decoded images")
+                    fmt = it.decoded.format_name
+                    if fmt in ("jpeg", "jpg"):
+                        pending_jpeg.append(it)
+                        if len(pending_jpeg) >= self.group_size:
+                            work.put(("jpeg", pending_jpeg))
+                            pending_jpeg = []
+                    elif fmt == "png":
+                        work.put(("png", [it]))
+                    else:
+                        work.put(("other", [it]))
+            except cf.TimeoutError:
+                log.warning("執行緒池等待逾時，部分任務可能未完成。")
+                for f in futs:
+                    f.cancel()
+        if pending_jpeg:
+            work.put(("jpeg", pending_jpeg))
+        for _ in workers:
+            work.put(None)
+        for w in workers:
+            w.join(timeout=max(1.0, deadline - time.perf_counter()))
+        return done_items

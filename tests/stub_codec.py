@@ -1,0 +1,35 @@
+"""Test double for icx.Codec backed by the CPU oracle.  Test infrastructure
+only: lets the host-side batch/cache/sharding logic run in CPU-only CI; the
+product package never uses it."""
+import numpy as np
+
+from icx.core import LearnedParams, image_dims
+from tests.oracle_ffi import Oracle
+
+
+class OracleCodec:
+    def __init__(self):
+        self.o = Oracle()
+        self.calls = 0
+
+    def fit(self, images, target, quality, cached=None, outputs=None):
+        self.calls += 1
+        res = []
+        for i, im in enumerate(images):
+            c = cached[i] if cached else None
+            r = self.o.fit(im, target, quality, cached=(c.quality, c.scale) if c else None)
+            res.append({"status": 0, "success": r["success"], "cache_hit": r["cache_hit"],
+                        "out_len": len(r["data"]) if r["success"] else 0, "encodes": r["encodes"],
+                        "learned": LearnedParams(r["quality"], r["scale"]) if r["success"] else None,
+                        "data": r["data"]})
+        return res
+
+    def compress_png_with_target_size(self, img, output_file, params):
+        w, h = image_dims(img)
+        if w <= params.min_width and h <= params.min_height:
+            return False
+        s = min(params.min_width / w, params.min_height / h)
+        dw, dh = self.o.scaled_dims(w, h, s)
+        from icx.pngio import write_png
+        write_png(output_file, self.o.resize(img, dw, dh))
+        return True

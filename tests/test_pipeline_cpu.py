@@ -1,0 +1,166 @@
+"""Host-side logic of processImage / CompressionBatch / cache / CLI, restating
+the reference's rules (ImageCompression.java:47-183, CompressionBatch.java,
+H2CacheManager.java, Execute.java).  No GPU: compression goes to an
+oracle-backed test double."""
+import io
+import os
+
+import numpy as np
+import pytest
+from PIL import Image
+
+import icx
+from icx import pipeline
+from icx.cache import CacheManager, LockedDict, db_file
+from icx.cli import build_parser, params_of
+from icx.core import CompressionParams, CompressionResult, LearnedParams, SimilarityKey
+from tests.oracle_ffi import noise, smooth
+from tests.stub_codec import OracleCodec
+
+
+def write_jpeg(path, bgr, quality=95):
+    Image.fromarray(np.ascontiguousarray(bgr[:, :, ::-1])).save(path, "JPEG", quality=quality)
+
+
+P = CompressionParams(0.25, 1000, 100, 60, 20000)
+
+
+def test_not_found(tmp_path):
+    r = pipeline.process_image(tmp_path / "missing.jpg", tmp_path, P, {}, None)
+    assert r == icx.CompressionReport(CompressionResult.SKIPPED_NOT_FOUND, 0, 0)
+
+
+def test_small_file_skipped(tmp_path):
+    f = tmp_path / "a.jpg"
+    write_jpeg(f, smooth(16, 16, 1))
+    size = os.path.getsize(f)
+    r = pipeline.process_image(f, tmp_path, CompressionParams(0.25, size, 1, 1, 10 ** 6), {}, None)
+    assert r == icx.CompressionReport(CompressionResult.SKIPPED_CONDITION_NOT_MET, size, size)
+
+
+def test_dims_gate_reports_unsupported_format(tmp_path):
+    """Appendix A.1/A.2: w <= minW || h <= minH gives a null decode, which a
+    file above -s reports as FAILED_UNSUPPORTED_FORMAT."""
+    f = tmp_path / "wide.jpg"
+    write_jpeg(f, noise(60, 400, 2))
+    size = os.path.getsize(f)
+    r = pipeline.process_image(f, tmp_path, CompressionParams(0.25, 10, 100, 60, 10 ** 6), {}, None)
+    assert r == icx.CompressionReport(CompressionResult.FAILED_UNSUPPORTED_FORMAT, size, size)
+
+
+def test_no_reader_is_unsupported(tmp_path):
+    f = tmp_path / "text.jpg"
+    f.write_bytes(b"not an image" * 500)
+    r = pipeline.process_image(f, tmp_path, P, {}, None)
+    assert r.result == CompressionResult.FAILED_UNSUPPORTED_FORMAT
+
+
+def test_other_readable_format_fails_compression(tmp_path):
+    f = tmp_path / "x.gif"
+    Image.fromarray(noise(80, 120, 3)[:, :, 0]).save(f, "GIF")
+    out = tmp_path / "out"
+    out.mkdir()
+    r = pipeline.process_image(f, out, CompressionParams(0.25, 10, 100, 60, 10 ** 6), {}, OracleCodec())
+    assert r.result == CompressionResult.FAILED_COMPRESSION and r.compressed_size == 0
+    assert not (out / "x.gif").exists()
+
+
+def test_subsampled_decode(tmp_path):
+    f = tmp_path / "big.jpg"
+    img = smooth(6, 8200, 4)
+    write_jpeg(f, img, 90)
+    d = pipeline.decode_image_with_subsampling(str(f), CompressionParams(0.25, 0, 1, 1, 0), os.path.getsize(f))
+    assert d.subsampling == 2 and d.image.shape == (3, 4100, 3) and d.format_name == "jpeg"
+    full = np.asarray(Image.open(f).convert("RGB"))[:, :, ::-1]
+    assert np.array_equal(d.image, full[::2, ::2])
+
+
+def test_jpeg_pipeline_with_cache(tmp_path):
+    f = tmp_path / "in.jpg"
+    img = noise(90, 120, 5)
+    write_jpeg(f, img)
+    out = tmp_path / "out"
+    out.mkdir()
+    cache = LockedDict()
+    codec = OracleCodec()
+    r = pipeline.process_image(f, out, P, cache, codec)
+    assert r.result == CompressionResult.COMPRESSED_SUCCESS
+    data = (out / "in.jpg").read_bytes()
+    assert len(data) <= P.target_max_size_bytes and r.compressed_size == len(data)
+    decoded = np.asarray(Image.open(f).convert("RGB"))[:, :, ::-1]
+    assert data == codec.o.fit(decoded, P.target_max_size_bytes, P.quality)["data"]
+    key = SimilarityKey(1, 0, os.path.getsize(f) // 102400)
+    assert key in cache
+    # second run: cache hit, same bytes
+    r2 = pipeline.process_image(f, out, P, cache, codec)
+    assert r2.result == CompressionResult.COMPRESSED_SUCCESS and (out / "in.jpg").read_bytes() == data
+
+
+def test_unreachable_target_deletes_output(tmp_path):
+    f = tmp_path / "in.jpg"
+    write_jpeg(f, noise(90, 120, 6))
+    out = tmp_path / "out"
+    out.mkdir()
+    (out / "in.jpg").write_bytes(b"stale")
+    r = pipeline.process_image(f, out, CompressionParams(0.25, 10, 100, 60, 300), LockedDict(), OracleCodec())
+    assert r.result == CompressionResult.FAILED_COMPRESSION and not (out / "in.jpg").exists()
+
+
+def test_png_pipeline(tmp_path):
+    f = tmp_path / "p.png"
+    Image.fromarray(smooth(300, 400, 7)[:, :, ::-1]).save(f)
+    out = tmp_path / "out"
+    out.mkdir()
+    r = pipeline.process_image(f, out, CompressionParams(0.25, 10, 100, 60, 0), LockedDict(), OracleCodec())
+    assert r.result == CompressionResult.COMPRESSED_SUCCESS
+    assert Image.open(out / "p.png").size == (80, 60)  # scale = min(100/400, 60/300)
+
+
+def test_cache_manager_roundtrip(tmp_path):
+    path = tmp_path / "db" / "cache.mv.db"
+    assert db_file(path).endswith("db/cache.icx.sqlite")
+    m = CacheManager(path)
+    m.init_schema()
+    d = {SimilarityKey(38, 21, 9): LearnedParams(0.2421875, 1.0),
+         SimilarityKey(1, 2, 3): LearnedParams(float(np.float32(0.1)), 0.85 * 0.85)}
+    assert m.save_all_from_map(d) == 2
+    m.save_all_from_map({SimilarityKey(1, 2, 3): LearnedParams(0.5, 1.0)})  # MERGE replaces
+    back = m.load_all_to_map()
+    assert back[SimilarityKey(38, 21, 9)] == LearnedParams(0.2421875, 1.0)
+    assert back[SimilarityKey(1, 2, 3)] == LearnedParams(0.5, 1.0)
+    m.close()
+
+
+def test_batch_report_counts(tmp_path):
+    files = []
+    for i in range(4):
+        f = tmp_path / f"n{i}.jpg"
+        write_jpeg(f, noise(70 + i, 110, 10 + i))
+        files.append(str(f))
+    files.append(str(tmp_path / "missing.jpg"))
+    small = tmp_path / "tiny.jpg"
+    write_jpeg(small, smooth(8, 8, 1))
+    files.append(str(small))
+    lst = tmp_path / "list.txt"
+    lst.write_text("\n".join(files) + "\n\n")
+    b = pipeline.CompressionBatch(lst, tmp_path / "out", CompressionParams(0.25, 1000, 100, 60, 20000), 1,
+                                  tmp_path / "cache", codecs=[OracleCodec()], group_size=3)
+    rep = b.execute()
+    assert rep.total == 6 and rep.success == 4
+    assert rep.counts[CompressionResult.SKIPPED_NOT_FOUND] == 1
+    assert rep.counts[CompressionResult.SKIPPED_CONDITION_NOT_MET] == 1
+    assert rep.failed == 0 and rep.cache_size >= 1
+    assert len(CacheManager(tmp_path / "cache").load_all_to_map()) == rep.cache_size
+
+
+def test_cli_defaults():
+    a = build_parser().parse_args(["-f", "l.txt", "-o", "o"])
+    assert params_of(a) == CompressionParams(0.25, 1048576, 1920, 1920, 1048576)
+    assert a.timeOut == 24 and a.cache_db == "image-compression-cache"
+
+
+def test_shard_partition():
+    lines = [f"f{i}" for i in range(11)]
+    parts = [pipeline.shard(lines, r, 3) for r in range(3)]
+    assert sorted(i for p in parts for i, _ in p) == list(range(11))
+    assert [len(p) for p in parts] == [4, 4, 3]
