@@ -14,7 +14,12 @@
 //               double-buffered: [best] holds the best fitting trial so the
 //               final file is stuffed from it without a re-encode.
 //   chunk_bits/off/ff [2]  per-chunk bit counts, exclusive bit offsets and
-//               0xFF-byte counts of the owned words (for byte stuffing).
+//               0xFF-byte counts of the owned bytes (bytes whose first bit
+//               lies in the chunk), for byte stuffing.
+//   chunk_ffa[2] per chunk, 8 counts: byte-long runs of 1-bits lying wholly
+//               inside the chunk, binned by chunk-local start bit mod 8 —
+//               the chunk's 0xFF count for each possible byte alignment,
+//               resolved by k_scan once the chunk's global offset is known.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -63,6 +68,7 @@ struct ImgDesc {
     uint32_t* chunk_bits[2];
     uint64_t* chunk_off[2];   // nchunks + 1 entries
     uint32_t* chunk_ff[2];
+    uint32_t* chunk_ffa[2];   // nchunks * 8 entries
     uint64_t* chunk_ffoff;    // nchunks entries (final stuffing pass)
     uint32_t* ovf;            // per-block spill of Huffman words beyond the LDS slot
     uint8_t* out;

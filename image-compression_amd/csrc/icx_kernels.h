@@ -15,8 +15,6 @@ void launch_fdct(const ImgDesc* d, const Plan& p, int64_t tiles, int kind, hipSt
 void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks,
                  hipStream_t st);
 void launch_scan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st);
-void launch_ffcount(const ImgDesc* d, ImgState* s, const Plan& p, int64_t chunks, int use_best,
-                    hipStream_t st);
 void launch_decide(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, hipStream_t st);
 void launch_ffscan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st);
 void launch_stuff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks,

@@ -7,8 +7,8 @@
 //                               h2v2_downsample, jpeg_fdct_islow (raw, x8)
 //   k_huff                      A9 quantise + A10 Huffman: per-chunk packed
 //                               bitstream, 16 lanes per 8x8 block
-//   k_scan                      exclusive scan of chunk bit counts
-//   k_ffcount                   0xFF bytes of the globally aligned stream
+//   k_scan                      exclusive scan of chunk bit counts; 0xFF bytes
+//                               per chunk from the huff kernel's alignment bins
 //                               (exact stuffed size without writing it)
 //   k_decide                    A3 binary-search step (tree walk)
 //   k_ffscan + k_stuff          final file: header, stuffed bytes, EOI
@@ -369,7 +369,10 @@ struct BlockSink {
 //   2. workgroup scan of the block bit counts -> offsets inside the chunk
 //   3. gather: every 32-bit word of the chunk stream is assembled by the
 //      thread whose block holds the word's first bit (reading the following
-//      blocks' slots as needed) and stored once to scratch[cur] - no atomics.
+//      blocks' slots as needed) and stored once to scratch[cur].
+//   4. every run of eight 1-bits inside the chunk is binned by start position
+//      mod 8 (chunk_ffa): the chunk's 0xFF-byte count for each alignment the
+//      chunk may land on once k_scan places it.
 __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict__ descs,
                                                        const ImgState* __restrict__ states,
                                                        const QNode* __restrict__ nodes,
@@ -384,6 +387,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     __shared__ uint32_t s_off[CHUNK_BLOCKS + 1];
     __shared__ uint32_t s_bits[CHUNK_BLOCKS];
     __shared__ uint32_t s_wsum[CHUNK_BLOCKS / 64];
+    __shared__ uint32_t s_ffa[8];
 
     const int64_t item = blockIdx.x;
     const int slot = find_slot(prefix, m, item);
@@ -399,6 +403,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     if (t < 128) s_q[t >> 6][t & 63] = make_uint2(N.rcp[t >> 6][t & 63], N.half[t >> 6][t & 63]);
     for (int i = t; i < 512; i += CHUNK_BLOCKS) s_ac[i >> 8][i & 255] = c_ac[i >> 8][i & 255];
     if (t < 32) s_dc[t >> 4][t & 15] = c_dc[t >> 4][t & 15];
+    if (t < 8) s_ffa[t] = 0;
 
     const int64_t b0 = (int64_t)chunk * CHUNK_BLOCKS;
     const int nb = (int)min((int64_t)CHUNK_BLOCKS, D.nblocks - b0);
@@ -511,10 +516,67 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         }
         dst[j] = outw;
     }
+    __syncthreads();  // the chunk's words are in dst (same CU: visible through its L1)
+
+    // ---- 4. alignment bins of 0xFF candidates: word pairs read back coalesced.
+    // Bit 31-d of r set <=> eight 1-bits start at chunk bit 32i+d (zero past
+    // the chunk's end, so no run leaves it).
+    const uint32_t nw = (total + 31) >> 5;
+    for (uint32_t i = t; i < nw; i += CHUNK_BLOCKS) {
+        uint64_t x = ((uint64_t)dst[i] << 32) | (i + 1 < nw ? dst[i + 1] : 0u);
+        x &= x << 1;
+        x &= x << 2;
+        x &= x << 4;
+        const uint32_t r = (uint32_t)(x >> 32);
+        if (r) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int n = __popc(r & (0x80808080u >> k));
+                if (n) atomicAdd(&s_ffa[k], (uint32_t)n);
+            }
+        }
+    }
+    __syncthreads();
+    if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = s_ffa[t];
     if (t == 0) D.chunk_bits[cur][chunk] = total;
 }
 
-// Exclusive scan of the chunk bit counts of one image (one workgroup per image).
+// 32 bits of the image's entropy stream starting at global bit gbit (inside
+// chunk c): from chunk c, the next chunk, then the 1-bit padding of flush_bits.
+__device__ __forceinline__ uint32_t stream_bits(const GAS uint32_t* __restrict__ scratch,
+                                                const GAS uint64_t* __restrict__ off, int nchunks, int c,
+                                                uint64_t gbit)
+{
+    const uint64_t start = off[c], end = off[c + 1];
+    const GAS uint32_t* cs = scratch + (size_t)c * CHUNK_WORDS;
+    const uint64_t s = gbit - start;
+    const uint32_t lw = (uint32_t)(s >> 5), sh = (uint32_t)(s & 31);
+    uint32_t v = cs[lw] << sh;
+    if (sh) v |= cs[lw + 1] >> (32 - sh);
+    uint64_t avail = end - gbit;
+    if (avail >= 32) return v;
+    v &= ~0u << (32 - avail);
+    int have = (int)avail;
+    if (c + 1 < nchunks) {
+        const uint64_t nlen = off[c + 2] - end;
+        const GAS uint32_t* ns = scratch + (size_t)(c + 1) * CHUNK_WORDS;
+        uint32_t nv = ns[0];
+        int take = (int)min((uint64_t)(32 - have), nlen);
+        if (take > 0) {
+            uint32_t piece = nv & (take == 32 ? ~0u : ~0u << (32 - take));
+            v |= piece >> have;
+            have += take;
+        }
+        // Every chunk but the last holds >= CHUNK_BLOCKS * 4 bits, so a word
+        // left short here ends in the last chunk: the rest is padding.
+    }
+    if (have < 32) v |= ~0u >> have;  // flush_bits: pad with 1-bits
+    return v;
+}
+
+// One workgroup per image: exclusive scan of the chunk bit counts, then each
+// chunk's 0xFF count: its alignment bin chunk_ffa[(8 - off%8) % 8] plus the
+// byte that starts in the chunk and ends in the next one (or in the padding).
 __global__ __launch_bounds__(1024) void k_scan(const ImgDesc* __restrict__ descs, ImgState* states,
                                                const int32_t* __restrict__ ids, int m)
 {
@@ -546,81 +608,30 @@ __global__ __launch_bounds__(1024) void k_scan(const ImgDesc* __restrict__ descs
         if (t == 1023) s_base = wbase + x;
         __syncthreads();
     }
+    if (t == 0) D.chunk_off[cur][D.nchunks] = s_base;
+    __syncthreads();
+    const GAS uint64_t* off = gp(D.chunk_off[cur]);
+    const GAS uint32_t* ffa = gp(D.chunk_ffa[cur]);
+    uint32_t sum = 0;
+    for (int i = t; i < D.nchunks; i += 1024) {
+        const uint64_t o = off[i], e = off[i + 1];
+        uint32_t n = ffa[i * 8 + ((8 - (o & 7)) & 7)];
+        if ((e & 7) && (e & ~(uint64_t)7) >= o &&
+            (stream_bits(gp(D.scratch[cur]), off, D.nchunks, i, e & ~(uint64_t)7) >> 24) == 0xFF)
+            n++;
+        D.chunk_ff[cur][i] = n;
+        sum += n;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    __syncthreads();
+    if (lane == 0) s_w[wv] = sum;
+    __syncthreads();
     if (t == 0) {
-        D.chunk_off[cur][D.nchunks] = s_base;
+        uint64_t ff = 0;
+        for (int k = 0; k < 16; k++) ff += s_w[k];
         S.total_bits[cur] = s_base;
-        S.ff_total[cur] = 0;
-    }
-}
-
-// 32 bits of the globally aligned stream starting at global bit 32*w, from
-// chunk c (whose bits start at `start`), the next chunk, then 1-bit padding.
-__device__ __forceinline__ uint32_t stream_word(const GAS uint32_t* __restrict__ scratch,
-                                                const GAS uint64_t* __restrict__ off, int nchunks, int c,
-                                                uint64_t w)
-{
-    const uint64_t gbit = w * 32;
-    const uint64_t start = off[c], end = off[c + 1];
-    const GAS uint32_t* cs = scratch + (size_t)c * CHUNK_WORDS;
-    const uint64_t s = gbit - start;
-    const uint32_t lw = (uint32_t)(s >> 5), sh = (uint32_t)(s & 31);
-    uint32_t v = cs[lw] << sh;
-    if (sh) v |= cs[lw + 1] >> (32 - sh);
-    uint64_t avail = end - gbit;
-    if (avail >= 32) return v;
-    v &= ~0u << (32 - avail);
-    int have = (int)avail;
-    if (c + 1 < nchunks) {
-        const uint64_t nlen = off[c + 2] - end;
-        const GAS uint32_t* ns = scratch + (size_t)(c + 1) * CHUNK_WORDS;
-        uint32_t nv = ns[0];
-        int take = (int)min((uint64_t)(32 - have), nlen);
-        if (take > 0) {
-            uint32_t piece = nv & (take == 32 ? ~0u : ~0u << (32 - take));
-            v |= piece >> have;
-            have += take;
-        }
-        // Every chunk but the last holds >= CHUNK_BLOCKS * 4 bits, so a word
-        // left short here ends in the last chunk: the rest is padding.
-    }
-    if (have < 32) v |= ~0u >> have;  // flush_bits: pad with 1-bits
-    return v;
-}
-
-// One wave per chunk: count 0xFF bytes in the words this chunk owns (words
-// whose first bit lies in the chunk), bytes beyond ceil(total/8) excluded.
-__global__ __launch_bounds__(256) void k_ffcount(const ImgDesc* __restrict__ descs, ImgState* states,
-                                                 const int32_t* __restrict__ ids,
-                                                 const int64_t* __restrict__ prefix, int m, int use_best)
-{
-    const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (item >= prefix[m]) return;
-    const int slot = find_slot(prefix, m, item);
-    const int img = ids[slot];
-    ImgState& S = states[img];
-    if (!use_best && !S.active) return;
-    const ImgDesc& D = descs[img];
-    const int c = (int)(item - prefix[slot]);
-    const int buf = use_best ? S.best_buf : S.cur;
-    const GAS uint64_t* off = gp(D.chunk_off[buf]);
-    const uint64_t total = off[D.nchunks];
-    const uint64_t nbytes = (total + 7) >> 3;
-    const uint64_t wlim = (nbytes + 3) >> 2;
-    const uint64_t wb = (off[c] + 31) >> 5;
-    const uint64_t we = min((off[c + 1] + 31) >> 5, wlim);
-    const int lane = threadIdx.x & 63;
-    uint32_t cnt = 0;
-    for (uint64_t w = wb + lane; w < we; w += 64) {
-        uint32_t v = stream_word(gp(D.scratch[buf]), off, D.nchunks, c, w);
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (w * 4 + j < nbytes && ((v >> (24 - 8 * j)) & 255) == 255) cnt++;
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
-    if (lane == 0) {
-        D.chunk_ff[buf][c] = cnt;
-        if (cnt) atomicAdd(&S.ff_total[buf], cnt);
+        S.ff_total[cur] = (uint32_t)ff;
     }
 }
 
@@ -701,8 +712,9 @@ __global__ __launch_bounds__(1024) void k_ffscan(const ImgDesc* __restrict__ des
     }
 }
 
-// Final pass 2 (one wave per chunk): header (chunk 0), stuffed entropy bytes,
-// EOI (last chunk), written straight into the caller's output buffer.
+// Final pass 2 (one wave per chunk): header (chunk 0), stuffed entropy bytes
+// of the bytes the chunk owns (first bit inside it), EOI (last chunk), written
+// straight into the caller's output buffer.
 __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs, const ImgState* __restrict__ states,
                                                const QNode* __restrict__ nodes, const int32_t* __restrict__ ids,
                                                const int64_t* __restrict__ prefix, int m)
@@ -738,19 +750,18 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
             out[i] = v;
         }
     }
-    const uint64_t wlim = (nbytes + 3) >> 2;
-    const uint64_t wb = (off[c] + 31) >> 5;
-    const uint64_t we = min((off[c + 1] + 31) >> 5, wlim);
+    const uint64_t bb = (off[c] + 7) >> 3;                 // owned bytes [bb, be)
+    const uint64_t be = min((off[c + 1] + 7) >> 3, nbytes);
     uint64_t run = D.chunk_ffoff[c];
-    for (uint64_t w0 = wb; w0 < we; w0 += 64) {
-        const uint64_t w = w0 + lane;
+    for (uint64_t q0 = bb; q0 < be; q0 += 256) {
+        const uint64_t q = q0 + 4 * lane;                    // this lane: bytes q..q+3
         uint32_t v = 0;
         int cnt = 0;
-        if (w < we) {
-            v = stream_word(gp(D.scratch[buf]), off, D.nchunks, c, w);
+        if (q < be) {
+            v = stream_bits(gp(D.scratch[buf]), off, D.nchunks, c, q * 8);
 #pragma unroll
             for (int j = 0; j < 4; j++)
-                if (w * 4 + j < nbytes && ((v >> (24 - 8 * j)) & 255) == 255) cnt++;
+                if (q + j < be && ((v >> (24 - 8 * j)) & 255) == 255) cnt++;
         }
         int incl = cnt;
 #pragma unroll
@@ -758,11 +769,11 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
             int y = __shfl_up(incl, d, 64);
             if (lane >= d) incl += y;
         }
-        uint64_t pos = (uint64_t)hdr + w * 4 + run + (uint64_t)(incl - cnt);
-        if (w < we) {
+        uint64_t pos = (uint64_t)hdr + q + run + (uint64_t)(incl - cnt);
+        if (q < be) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                if (w * 4 + j < nbytes) {
+                if (q + j < be) {
                     uint8_t byte = (uint8_t)(v >> (24 - 8 * j));
                     out[pos++] = byte;
                     if (byte == 0xFF) out[pos++] = 0;
@@ -851,12 +862,6 @@ void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan
 void launch_scan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st)
 {
     hipLaunchKernelGGL(k_scan, dim3(p.m), dim3(1024), 0, st, d, s, p.ids, p.m);
-}
-
-void launch_ffcount(const ImgDesc* d, ImgState* s, const Plan& p, int64_t chunks, int use_best, hipStream_t st)
-{
-    if (chunks <= 0) return;
-    hipLaunchKernelGGL(k_ffcount, dim3(grid_of(chunks, 4)), dim3(256), 0, st, d, s, p.ids, p.prefix, p.m, use_best);
 }
 
 void launch_decide(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, hipStream_t st)

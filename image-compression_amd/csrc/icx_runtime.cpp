@@ -447,6 +447,7 @@ void stage_pixels(Batch& B, int i, double scale)
         d.chunk_bits[k] = keep.chunk_bits[k];
         d.chunk_off[k] = keep.chunk_off[k];
         d.chunk_ff[k] = keep.chunk_ff[k];
+        d.chunk_ffa[k] = keep.chunk_ffa[k];
     }
     d.chunk_ffoff = keep.chunk_ffoff;
     d.ovf = keep.ovf;
@@ -499,7 +500,6 @@ icx_status run_trials(Batch& B, const std::vector<int>& ids, int depth)
     for (int t = 0; t < depth; t++) {
         { Timed tm(c, "huff", 0); launch_huff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
         { Timed tm(c, "scan", (int64_t)ids.size()); launch_scan(B.d_desc, B.d_state, P.p, c->stream); }
-        { Timed tm(c, "ffcount", P.total); launch_ffcount(B.d_desc, B.d_state, P.p, P.total, 0, c->stream); }
         { Timed tm(c, "decide", (int64_t)ids.size()); launch_decide(B.d_desc, B.d_state, B.d_nodes, P.p, c->stream); }
     }
     return ICX_OK;
@@ -573,7 +573,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             const int nch = channels(j.img.fmt);
             size_t per = (size_t)g.nchunks * CHUNK_BLOCKS * 128 + (size_t)g.nblocks * BLOCK_WORDS * 4 + 1024 +
                          2 * ((size_t)g.nchunks * CHUNK_WORDS + 1) * 4 +
-                         (size_t)g.nchunks * (2 * 4 + 2 * 8 + 2 * 4 + 8) + 64 + 8 * 256;
+                         (size_t)g.nchunks * (2 * 4 + 2 * 8 + 2 * 4 + 2 * 32 + 8) + 64 + 8 * 256;
             per += (size_t)j.img.width * j.img.height * nch * 2;  // input staging + resize buffer
             per += std::min<uint64_t>(worst_file(g), j.cap);
             if (!sub.empty() && need + per > c->budget) break;
@@ -637,6 +637,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                 d.chunk_bits[b] = (uint32_t*)c->dev.take((size_t)d.nchunks * 4);
                 d.chunk_off[b] = (uint64_t*)c->dev.take(((size_t)d.nchunks + 1) * 8);
                 d.chunk_ff[b] = (uint32_t*)c->dev.take((size_t)d.nchunks * 4);
+                d.chunk_ffa[b] = (uint32_t*)c->dev.take((size_t)d.nchunks * 32);
             }
             d.chunk_ffoff = (uint64_t*)c->dev.take((size_t)d.nchunks * 8);
             // input pixels
