@@ -51,8 +51,12 @@ struct QNode {
     int32_t child_fit;     // next node when size <= target (lo = mid), -1 = stop
     int32_t child_nofit;   // next node when size >  target (hi = mid), -1 = stop
     int32_t pad;
-    uint32_t rcp[2][64];   // floor(2^32 / (q<<3)) + 1, zig-zag order, [0]=lum [1]=chroma
-    uint16_t half[2][64];  // (q<<3)>>1 rounding addend, zig-zag order
+    // Quantiser of zig-zag coefficient k, table c ([0]=lum [1]=chroma), for the
+    // divisor d = q<<3 (jcdctmgr.c: |c| -> (|c| + d/2) / d, truncating):
+    float thr[2][64];      // d - d/2: the quotient is nonzero iff |c| >= thr
+    float frcp[2][64];     // fl(1/d)
+    float fbias[2][64];    // fl((d/2 + 0.5) * frcp): floor(fma(|c|, frcp, fbias)) is
+                           // the quotient exactly for |c| < 2^15 (error << 0.5/d)
     uint16_t qt[2][64];    // quantisation tables, natural order (DQT payload)
 };
 

@@ -323,17 +323,23 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
 }
 
 // =================================================================== Huffman
-__device__ __forceinline__ int quant(int c, uint32_t rcp, uint32_t half)
+// jcdctmgr.c: sign(c) * ((|c| + d/2) / d) for d = q<<3, via the exact float
+// form of QNode (|c| <= 2^15, so y*d < 2^16 and the error stays < 2^-6/d).
+__device__ __forceinline__ int quant(int c, float rcp, float bias)
 {
-    // jcdctmgr.c: sign(c) * ((|c| + (q<<3)/2) / (q<<3)); exact for |c|+half < 2^16
-    uint32_t a = (uint32_t)(c < 0 ? -c : c) + half;
-    int q = (int)__umulhi(a, rcp);
+    const int q = (int)fmaf(fabsf((float)c), rcp, bias);
     return c < 0 ? -q : q;
 }
 
 __device__ __forceinline__ int nbits(int a) { return a ? 32 - __clz(a) : 0; }
 
-constexpr int SLOT_WORDS = 17;  // per-block LDS slot (544 bits, odd stride); longer blocks spill to D.ovf
+// Per-block LDS slot (odd stride: same-index words of a wave hit distinct
+// banks); longer blocks spill to D.ovf.  Sized with the other k_huff LDS so a
+// workgroup stays under 20 KiB (in 512 B allocation granules): 8 per CU.
+#ifndef ICX_SLOT_WORDS
+#define ICX_SLOT_WORDS 13
+#endif
+constexpr int SLOT_WORDS = ICX_SLOT_WORDS;
 
 // Per-thread bit sink: a 64-bit accumulator flushing whole 32-bit words into
 // the thread's LDS slot (or its HBM spill region past SLOT_WORDS).
@@ -382,10 +388,11 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     __shared__ uint32_t slots[CHUNK_BLOCKS * SLOT_WORDS];
     __shared__ uint32_t s_ac[2][256];
     __shared__ uint32_t s_dc[2][16];
-    __shared__ uint2 s_q[2][64];
-    __shared__ int32_t s_dcq[CHUNK_BLOCKS];
+    __shared__ float s_thr[2][64];
+    __shared__ float2 s_rb[2][64];
     __shared__ uint32_t s_off[CHUNK_BLOCKS + 1];
     __shared__ uint32_t s_bits[CHUNK_BLOCKS];
+    int32_t* const s_dcq = (int32_t*)s_bits;  // DC exchange; dead before s_bits is written
     __shared__ uint32_t s_wsum[CHUNK_BLOCKS / 64];
     __shared__ uint32_t s_ffa[8];
 
@@ -400,8 +407,15 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     const int cur = S.cur;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
 
-    if (t < 128) s_q[t >> 6][t & 63] = make_uint2(N.rcp[t >> 6][t & 63], N.half[t >> 6][t & 63]);
-    for (int i = t; i < 512; i += CHUNK_BLOCKS) s_ac[i >> 8][i & 255] = c_ac[i >> 8][i & 255];
+    if (t < 128) {
+        s_thr[t >> 6][t & 63] = N.thr[t >> 6][t & 63];
+        s_rb[t >> 6][t & 63] = make_float2(N.frcp[t >> 6][t & 63], N.fbias[t >> 6][t & 63]);
+    }
+    // AC codes pre-shifted for their (run, size) slot: ((code << size) << 5) | (len + size)
+    for (int i = t; i < 512; i += CHUNK_BLOCKS) {
+        const uint32_t h = c_ac[i >> 8][i & 255], sz = i & 15;
+        s_ac[i >> 8][i & 255] = sz <= 10 ? (((h >> 8) << sz) << 5) | ((h & 255) + sz) : 0u;
+    }
     if (t < 32) s_dc[t >> 4][t & 15] = c_dc[t >> 4][t & 15];
     if (t < 8) s_ffa[t] = 0;
 
@@ -427,7 +441,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         quad[k] = valid ? ld8((const int16_t*)cbase + k * (CHUNK_BLOCKS * 4)) : make_int2(0, 0);
     __syncthreads();  // tables ready
 
-    const uint2 q0t = s_q[tb][0];
+    const float2 q0t = s_rb[tb][0];
     const int dq = quant((int)(int16_t)(quad[0].x & 0xFFFF), q0t.x, q0t.y);
     s_dcq[t] = dq;
     __syncthreads();
@@ -444,31 +458,36 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         const uint32_t hc = s_dc[tb][ds];
         const uint32_t mag = (uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << ds) - 1);
         sink.put(((hc >> 8) << ds) | mag, (int)(hc & 255) + ds);
-        const uint32_t zrlc = s_ac[tb][0xF0];
-        int run = 0;
+        // run kept as the index of s_ac[tb][run << 4] in the flattened table
+        const uint32_t* acf = &s_ac[0][0];
+        const uint32_t abase = (uint32_t)tb * 256;
+        const uint32_t zrl = acf[abase + 0xF0];
+        uint32_t arun = abase;
 #pragma unroll
         for (int k = 1; k < 64; k++) {
             const uint32_t w = (k & 2) ? (uint32_t)quad[k >> 2].y : (uint32_t)quad[k >> 2].x;
-            const int c = (int)(int16_t)(w >> ((k & 1) * 16));
-            const uint2 qq = s_q[tb][k];
-            const int q = quant(c, qq.x, qq.y);
-            if (q != 0) {
-                while (run > 15) {
-                    sink.put(zrlc >> 8, (int)(zrlc & 255));
-                    run -= 16;
+            const float f = (float)(int)(int16_t)(w >> ((k & 1) * 16));
+            if (fabsf(f) >= s_thr[tb][k]) {
+                while (arun >= abase + 256) {
+                    sink.put(zrl >> 5, (int)(zrl & 31));
+                    arun -= 256;
                 }
-                const int s = nbits(q < 0 ? -q : q);
-                const uint32_t ac = s_ac[tb][(run << 4) | s];
-                const uint32_t mg = (uint32_t)(q < 0 ? q - 1 : q) & ((1u << s) - 1);
-                sink.put(((ac >> 8) << s) | mg, (int)(ac & 255) + s);
-                run = 0;
+                const float2 rb = s_rb[tb][k];
+                const float y = fmaf(fabsf(f), rb.x, rb.y);
+                const uint32_t u = (uint32_t)y;                    // |q| >= 1
+                const int sz = __builtin_amdgcn_frexp_expf(y);     // bit length of |q|
+                const uint32_t e = acf[arun + sz];
+                const uint32_t sm = (uint32_t)((int32_t)__float_as_uint(f) >> 31);
+                const uint32_t mk = (1u << sz) - 1;
+                sink.put((e >> 5) | ((u ^ sm) & mk), (int)(e & 31));
+                arun = abase;
             } else {
-                run++;
+                arun += 16;
             }
         }
-        if (run > 0) {
-            const uint32_t eob = s_ac[tb][0];
-            sink.put(eob >> 8, (int)(eob & 255));
+        if (arun != abase) {
+            const uint32_t eob = acf[abase];
+            sink.put(eob >> 5, (int)(eob & 31));
         }
         bits = sink.widx * 32 + sink.n;
         sink.finish();

@@ -109,8 +109,11 @@ void make_node(float q, QNode& n)
     for (int c = 0; c < 2; c++) {
         for (int k = 0; k < 64; k++) {
             const uint32_t div = (uint32_t)t[c][kZigzag[k]] << 3;
-            n.rcp[c][k] = (uint32_t)((1ull << 32) / div + 1);
-            n.half[c][k] = (uint16_t)(div >> 1);
+            volatile float r = 1.0f / (float)div;
+            volatile float b = ((float)(div >> 1) + 0.5f) * r;
+            n.thr[c][k] = (float)(div - (div >> 1));
+            n.frcp[c][k] = r;
+            n.fbias[c][k] = b;
         }
         for (int i = 0; i < 64; i++) n.qt[c][i] = t[c][i];
     }
