@@ -388,8 +388,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     __shared__ uint32_t slots[CHUNK_BLOCKS * SLOT_WORDS];
     __shared__ uint32_t s_ac[2][256];
     __shared__ uint32_t s_dc[2][16];
-    __shared__ float s_thr[2][64];
-    __shared__ float2 s_rb[2][64];
+    __shared__ float4 s_qf[2][64];  // (thr, frcp, fbias, -) per zig-zag index
     __shared__ uint32_t s_off[CHUNK_BLOCKS + 1];
     __shared__ uint32_t s_bits[CHUNK_BLOCKS];
     int32_t* const s_dcq = (int32_t*)s_bits;  // DC exchange; dead before s_bits is written
@@ -408,8 +407,8 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
 
     if (t < 128) {
-        s_thr[t >> 6][t & 63] = N.thr[t >> 6][t & 63];
-        s_rb[t >> 6][t & 63] = make_float2(N.frcp[t >> 6][t & 63], N.fbias[t >> 6][t & 63]);
+        const int c = t >> 6, k = t & 63;
+        s_qf[c][k] = make_float4(N.thr[c][k], N.frcp[c][k], N.fbias[c][k], 0.0f);
     }
     // AC codes pre-shifted for their (run, size) slot: ((code << size) << 5) | (len + size)
     for (int i = t; i < 512; i += CHUNK_BLOCKS) {
@@ -441,13 +440,13 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         quad[k] = valid ? ld8((const int16_t*)cbase + k * (CHUNK_BLOCKS * 4)) : make_int2(0, 0);
     __syncthreads();  // tables ready
 
-    const float2 q0t = s_rb[tb][0];
-    const int dq = quant((int)(int16_t)(quad[0].x & 0xFFFF), q0t.x, q0t.y);
+    const float4 q0t = s_qf[tb][0];
+    const int dq = quant((int)(int16_t)(quad[0].x & 0xFFFF), q0t.y, q0t.z);
     s_dcq[t] = dq;
     __syncthreads();
     int qprev = 0;
     if (pb >= b0) qprev = s_dcq[pb - b0];
-    else if (pb >= 0) qprev = quant(gp(D.coefs)[coef_index(pb, 0)], q0t.x, q0t.y);
+    else if (pb >= 0) qprev = quant(gp(D.coefs)[coef_index(pb, 0)], q0t.y, q0t.z);
 
     // ---- 1. encode_one_block into the slot
     BlockSink sink{0, 0, 0, &slots[t * SLOT_WORDS], gp(D.ovf + b * BLOCK_WORDS)};
@@ -463,17 +462,19 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         const uint32_t abase = (uint32_t)tb * 256;
         const uint32_t zrl = acf[abase + 0xF0];
         uint32_t arun = abase;
+        float4 qn = s_qf[tb][1];
 #pragma unroll
         for (int k = 1; k < 64; k++) {
+            const float4 qk = qn;
+            if (k < 63) qn = s_qf[tb][k + 1];  // in flight while index k is coded
             const uint32_t w = (k & 2) ? (uint32_t)quad[k >> 2].y : (uint32_t)quad[k >> 2].x;
             const float f = (float)(int)(int16_t)(w >> ((k & 1) * 16));
-            if (fabsf(f) >= s_thr[tb][k]) {
+            if (fabsf(f) >= qk.x) {
                 while (arun >= abase + 256) {
                     sink.put(zrl >> 5, (int)(zrl & 31));
                     arun -= 256;
                 }
-                const float2 rb = s_rb[tb][k];
-                const float y = fmaf(fabsf(f), rb.x, rb.y);
+                const float y = fmaf(fabsf(f), qk.y, qk.z);
                 const uint32_t u = (uint32_t)y;                    // |q| >= 1
                 const int sz = __builtin_amdgcn_frexp_expf(y);     // bit length of |q|
                 const uint32_t e = acf[arun + sz];
