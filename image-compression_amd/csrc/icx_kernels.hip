@@ -341,32 +341,95 @@ __device__ __forceinline__ int nbits(int a) { return a ? 32 - __clz(a) : 0; }
 #endif
 constexpr int SLOT_WORDS = ICX_SLOT_WORDS;
 
-// Per-thread bit sink: a 64-bit accumulator flushing whole 32-bit words into
-// the thread's LDS slot (or its HBM spill region past SLOT_WORDS).
-struct BlockSink {
+constexpr int SLOT_BITS = SLOT_WORDS * 32;
+constexpr int AC_SIZES = 11;                // AC magnitude categories 0..10 (8-bit JPEG)
+constexpr int AC_ENTRIES = 16 * AC_SIZES;   // (run, size) slots per table
+
+// Per-thread bit sinks: a 64-bit accumulator flushing whole 32-bit words.
+// LdsSink writes the thread's LDS slot, clamped to its last word; a block that
+// outgrows the slot (bits > SLOT_BITS) is coded again into a GlobalSink.
+struct LdsSink {
     uint64_t acc;
-    int n, widx;
-    uint32_t* lds;
-    GAS uint32_t* spill;
-    __device__ __forceinline__ void store(uint32_t w)
-    {
-        if (widx < SLOT_WORDS) lds[widx] = w; else spill[widx] = w;
-        widx++;
-    }
+    int n;
+    uint32_t wb, wlast;  // byte offsets into `slots` of the next and the last slot word
+    uint32_t* slots;
     __device__ __forceinline__ void put(uint32_t v, int len)  // len <= 32
     {
         acc = (acc << len) | v;
         n += len;
         if (n >= 32) {
             n -= 32;
-            store((uint32_t)(acc >> n));
+            *(uint32_t*)((char*)slots + min(wb, wlast)) = (uint32_t)(acc >> n);
+            wb += 4;
         }
     }
     __device__ __forceinline__ void finish()
     {
-        if (n) store((uint32_t)(acc << (32 - n)));
+        if (n) *(uint32_t*)((char*)slots + min(wb, wlast)) = (uint32_t)(acc << (32 - n));
     }
 };
+
+struct GlobalSink {
+    uint64_t acc;
+    int n, widx;
+    GAS uint32_t* w;
+    __device__ __forceinline__ void put(uint32_t v, int len)
+    {
+        acc = (acc << len) | v;
+        n += len;
+        if (n >= 32) {
+            n -= 32;
+            w[widx++] = (uint32_t)(acc >> n);
+        }
+    }
+    __device__ __forceinline__ void finish()
+    {
+        if (n) w[widx] = (uint32_t)(acc << (32 - n));
+    }
+};
+
+// encode_one_block (jchuff.c) of one 8x8 block: DC difference, then the AC
+// run/size codes.  quad[] holds the raw zig-zag FDCT coefficients; qf/ac/dc
+// are the LDS tables of the block's component (ac entries: (code << size,
+// len + size) at [run * AC_SIZES + size]).  The quantiser constants of index
+// k+1 are read while index k is coded.
+template <class Sink>
+__device__ __forceinline__ void encode_block(Sink& sink, const int2 (&quad)[16], int diff, const float4* qf,
+                                             const uint2* ac, const uint32_t* dc)
+{
+    {
+        const int ds = nbits(diff < 0 ? -diff : diff);
+        const uint32_t hc = dc[ds];
+        const uint32_t mag = (uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << ds) - 1);
+        sink.put(((hc >> 8) << ds) | mag, (int)(hc & 255) + ds);
+    }
+    const uint2 zrl = ac[15 * AC_SIZES];
+    const char* acb = (const char*)ac;
+    uint32_t run = 0;  // byte offset of ac[run * AC_SIZES]
+    float4 qn = qf[1];
+#pragma unroll
+    for (int k = 1; k < 64; k++) {
+        const float4 qk = qn;
+        if (k < 63) qn = qf[k + 1];
+        const uint32_t w = (k & 2) ? (uint32_t)quad[k >> 2].y : (uint32_t)quad[k >> 2].x;
+        const float f = (float)(int)(int16_t)(w >> ((k & 1) * 16));
+        const bool nz = fabsf(f) >= qk.x;  // quotient != 0
+        if (nz) {
+            while (run >= 16 * AC_SIZES * 8) {
+                sink.put(zrl.x, (int)zrl.y);
+                run -= 16 * AC_SIZES * 8;
+            }
+            const float y = fmaf(fabsf(f), qk.y, qk.z);
+            const uint32_t u = (uint32_t)y;                    // |q| >= 1
+            const int sz = __builtin_amdgcn_frexp_expf(y);     // bit length of |q|
+            const uint2 e = *(const uint2*)(acb + run + (sz << 3));
+            const uint32_t sm = (uint32_t)((int32_t)__float_as_uint(f) >> 31);
+            sink.put(e.x | ((u ^ sm) & ((1u << sz) - 1)), (int)e.y);
+        }
+        run = nz ? 0u : run + AC_SIZES * 8;
+    }
+    if (run) sink.put(ac[0].x, (int)ac[0].y);  // EOB
+}
 
 // One workgroup = one chunk of CHUNK_BLOCKS scan blocks; one thread = one
 // 8x8 block (encode_one_block, jchuff.c), run once per trial:
@@ -386,7 +449,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
                                                        const int64_t* __restrict__ prefix, int m)
 {
     __shared__ uint32_t slots[CHUNK_BLOCKS * SLOT_WORDS];
-    __shared__ uint32_t s_ac[2][256];
+    __shared__ uint2 s_ac[2][AC_ENTRIES];
     __shared__ uint32_t s_dc[2][16];
     __shared__ float4 s_qf[2][64];  // (thr, frcp, fbias, -) per zig-zag index
     __shared__ uint32_t s_off[CHUNK_BLOCKS + 1];
@@ -410,10 +473,11 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         const int c = t >> 6, k = t & 63;
         s_qf[c][k] = make_float4(N.thr[c][k], N.frcp[c][k], N.fbias[c][k], 0.0f);
     }
-    // AC codes pre-shifted for their (run, size) slot: ((code << size) << 5) | (len + size)
-    for (int i = t; i < 512; i += CHUNK_BLOCKS) {
-        const uint32_t h = c_ac[i >> 8][i & 255], sz = i & 15;
-        s_ac[i >> 8][i & 255] = sz <= 10 ? (((h >> 8) << sz) << 5) | ((h & 255) + sz) : 0u;
+    // AC codes pre-shifted for their (run, size) slot: (code << size, len + size)
+    for (int i = t; i < 2 * AC_ENTRIES; i += CHUNK_BLOCKS) {
+        const int c = i / AC_ENTRIES, r = i - c * AC_ENTRIES, run = r / AC_SIZES, sz = r - run * AC_SIZES;
+        const uint32_t h = c_ac[c][(run << 4) | sz];
+        s_ac[c][r] = make_uint2((h >> 8) << sz, (h & 255) + sz);
     }
     if (t < 32) s_dc[t >> 4][t & 15] = c_dc[t >> 4][t & 15];
     if (t < 8) s_ffa[t] = 0;
@@ -448,50 +512,22 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     if (pb >= b0) qprev = s_dcq[pb - b0];
     else if (pb >= 0) qprev = quant(gp(D.coefs)[coef_index(pb, 0)], q0t.y, q0t.z);
 
-    // ---- 1. encode_one_block into the slot
-    BlockSink sink{0, 0, 0, &slots[t * SLOT_WORDS], gp(D.ovf + b * BLOCK_WORDS)};
+    // ---- 1. encode_one_block into the slot (rarely: into the block's HBM spill)
     int bits = 0;
     if (valid) {
-        const int diff = dq - qprev;
-        const int ds = nbits(diff < 0 ? -diff : diff);
-        const uint32_t hc = s_dc[tb][ds];
-        const uint32_t mag = (uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << ds) - 1);
-        sink.put(((hc >> 8) << ds) | mag, (int)(hc & 255) + ds);
-        // run kept as the index of s_ac[tb][run << 4] in the flattened table
-        const uint32_t* acf = &s_ac[0][0];
-        const uint32_t abase = (uint32_t)tb * 256;
-        const uint32_t zrl = acf[abase + 0xF0];
-        uint32_t arun = abase;
-        float4 qn = s_qf[tb][1];
-#pragma unroll
-        for (int k = 1; k < 64; k++) {
-            const float4 qk = qn;
-            if (k < 63) qn = s_qf[tb][k + 1];  // in flight while index k is coded
-            const uint32_t w = (k & 2) ? (uint32_t)quad[k >> 2].y : (uint32_t)quad[k >> 2].x;
-            const float f = (float)(int)(int16_t)(w >> ((k & 1) * 16));
-            if (fabsf(f) >= qk.x) {
-                while (arun >= abase + 256) {
-                    sink.put(zrl >> 5, (int)(zrl & 31));
-                    arun -= 256;
-                }
-                const float y = fmaf(fabsf(f), qk.y, qk.z);
-                const uint32_t u = (uint32_t)y;                    // |q| >= 1
-                const int sz = __builtin_amdgcn_frexp_expf(y);     // bit length of |q|
-                const uint32_t e = acf[arun + sz];
-                const uint32_t sm = (uint32_t)((int32_t)__float_as_uint(f) >> 31);
-                const uint32_t mk = (1u << sz) - 1;
-                sink.put((e >> 5) | ((u ^ sm) & mk), (int)(e & 31));
-                arun = abase;
-            } else {
-                arun += 16;
-            }
-        }
-        if (arun != abase) {
-            const uint32_t eob = acf[abase];
-            sink.put(eob >> 5, (int)(eob & 31));
-        }
-        bits = sink.widx * 32 + sink.n;
+        const uint32_t sb = (uint32_t)(t * SLOT_WORDS * 4);
+        LdsSink sink{0, 0, sb, sb + (SLOT_WORDS - 1) * 4, slots};
+        encode_block(sink, quad, dq - qprev, s_qf[tb], s_ac[tb], s_dc[tb]);
+        bits = (int)(sink.wb - sb) * 8 + sink.n;
         sink.finish();
+        if (bits > SLOT_BITS) {  // rare: reload the coefficients (quad[] is dead by now)
+            int2 q2[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) q2[k] = ld8((const int16_t*)cbase + k * (CHUNK_BLOCKS * 4));
+            GlobalSink g{0, 0, 0, gp(D.ovf + b * BLOCK_WORDS)};
+            encode_block(g, q2, dq - qprev, s_qf[tb], s_ac[tb], s_dc[tb]);
+            g.finish();
+        }
     }
 
     // ---- 2. exclusive scan of block bits
@@ -524,10 +560,18 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
             const int avail = (int)s_bits[u] - (int)p;
             const int take = min(32 - have, avail);
             const uint32_t wi = p >> 5, sh = p & 31;
-            const uint32_t* ls = &slots[u * SLOT_WORDS];
-            const GAS uint32_t* gs = spill0 + (size_t)u * BLOCK_WORDS;
-            uint32_t v = (wi < SLOT_WORDS ? ls[wi] : gs[wi]) << sh;
-            if (sh + take > 32) v |= (wi + 1 < SLOT_WORDS ? ls[wi + 1] : gs[wi + 1]) >> (32 - sh);
+            uint32_t v0, v1 = 0;
+            if (s_bits[u] <= SLOT_BITS) {
+                const uint32_t* ls = &slots[u * SLOT_WORDS];
+                v0 = ls[wi];
+                if (sh + take > 32) v1 = ls[wi + 1];
+            } else {
+                const GAS uint32_t* gs = spill0 + (size_t)u * BLOCK_WORDS;
+                v0 = gs[wi];
+                if (sh + take > 32) v1 = gs[wi + 1];
+            }
+            uint32_t v = v0 << sh;
+            if (sh + take > 32) v |= v1 >> (32 - sh);
             v &= take == 32 ? ~0u : ~(~0u >> take);
             outw |= v >> have;
             have += take;

@@ -37,7 +37,7 @@ def test_encode_matches_golden_bytes(codec, golden):
 @pytest.mark.parametrize("kind", ["smooth", "noise"])
 def test_encode_4k_matches_oracle(codec, oracle, kind):
     img = (smooth if kind == "smooth" else noise)(2160, 3840, 11)
-    for q in (0.25, 0.125, 0.0625, 0.9):
+    for q in (0.25, 0.125, 0.0625, 0.9, 1.0):  # 0.9/1.0 noise: most blocks outgrow the LDS slot
         assert codec.compress_jpg_to_stream(img, q) == oracle.encode(img, q), q
 
 
