@@ -120,11 +120,13 @@ __device__ __forceinline__ int zz_of(int v, int u)
 }
 
 // Colour: one workgroup = 16 rows x 256 px = 16 MCUs of one MCU row (96 blocks);
-// every phase has 1-3 equal tasks per thread.
-//   A. 16-B coalesced row loads -> LDS raw tile (edge expansion by clamping)
-//   B. 2 x 8 px per thread: YCbCr, Y row-DCT in registers (int16 workspace)
+// every phase has 1-3 equal tasks per thread.  LDS 20 KiB -> 8 workgroups/CU.
+//   B. 2 x 8 px per thread straight from HBM (24 B runs, a wave reads two
+//      contiguous 768 B row pieces; edges clamped): YCbCr, Y row-DCT in
+//      registers -> int16 workspace, full-res Cb/Cr bytes -> LDS
 //   C. h2v2_downsample (bias 1,2,..) + chroma row-DCT, one row task per thread
-//   D. column DCT, 3 column tasks per thread, zig-zag scatter (aliases raw)
+//   D. column DCT, 3 column tasks per thread into registers; barrier; zig-zag
+//      scatter over the (now dead) workspace
 //   E. dummy blocks (jccoefct.c) + 8-B stores into the interleaved layout
 constexpr int FDC_MCU = 16;           // MCUs per colour tile
 constexpr int FDC_PX = FDC_MCU * 16;  // 256 px
@@ -135,11 +137,9 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
                                                     const int32_t* __restrict__ ids,
                                                     const int64_t* __restrict__ prefix, int m)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t rawz[16 * FDC_PX * 3];  // 12 KB; later zig-zag output
     __shared__ __attribute__((aligned(16))) uint8_t cful[2][16][FDC_PX];    // 8 KB full-res Cb, Cr
     __shared__ __attribute__((aligned(16))) int16_t ws[FDC_BLK][64];        // 12 KB row-pass output
-    uint8_t* raw = rawz;
-    int16_t (*oz)[64] = (int16_t (*)[64])rawz;
+    int16_t (*oz)[64] = ws;                                                 // zig-zag output (phase D)
 
     const int64_t item = blockIdx.x;
     const int slot = find_slot(prefix, m, item);
@@ -150,47 +150,46 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
     const int W = D.w, H = D.h, x0 = tx * FDC_PX, y0 = my * 16;
     const int t = threadIdx.x;
     const uint8_t* px = D.px;
-    constexpr int ROWB = FDC_PX * 3;  // 768 bytes per tile row
 
-    // ---- A
-    const bool fast = (x0 + FDC_PX <= W) && (((uintptr_t)px & 15) == 0) && ((D.stride & 15) == 0);
-    if (fast) {
-        uint4 v[3];
-#pragma unroll
-        for (int k = 0; k < 3; k++) {  // piece i: row i/48, 16-B column i%48, LDS offset 16*i
-            const int i = t + 256 * k, r = i / 48, c = i - r * 48;
-            const int y = min(y0 + r, H - 1);
-            v[k] = ld16(px + (size_t)y * D.stride + (size_t)x0 * 3 + 16 * c);
-        }
-#pragma unroll
-        for (int k = 0; k < 3; k++) *(uint4*)(raw + (t + 256 * k) * 16) = v[k];
-    } else {
-        for (int i = t; i < 16 * FDC_PX; i += 256) {
-            const int r = i / FDC_PX, x = i - r * FDC_PX;
-            const int y = min(y0 + r, H - 1), sx = min(x0 + x, W - 1);
-            const GAS uint8_t* sp = gp(px + (size_t)y * D.stride + (size_t)sx * 3);
-            raw[r * ROWB + x * 3 + 0] = sp[0];
-            raw[r * ROWB + x * 3 + 1] = sp[1];
-            raw[r * ROWB + x * 3 + 2] = sp[2];
-        }
-    }
-    __syncthreads();
-
-    // ---- B: 2 row tasks of 8 px
+    // ---- B: 2 row tasks of 8 px; all six 8-B loads issued before any use
+    const bool fast = (x0 + FDC_PX <= W) && (((uintptr_t)px & 7) == 0) && ((D.stride & 7) == 0);
+    uint32_t wv[2][6];
 #pragma unroll
     for (int rep = 0; rep < 2; rep++) {
         const int task = t + 256 * rep, r = task >> 5, sg = task & 31;
-        const uint8_t* p = raw + r * ROWB + sg * 24;
-        const uint2 a = *(const uint2*)(p), b = *(const uint2*)(p + 8), c = *(const uint2*)(p + 16);
-        const uint32_t wv[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+        const int y = min(y0 + r, H - 1);
+        const uint8_t* row = px + (size_t)y * D.stride;
+        if (fast) {
+            const uint8_t* p = row + (size_t)(x0 + sg * 8) * 3;
+            const int2 a = ld8(p), b = ld8(p + 8), c = ld8(p + 16);
+            wv[rep][0] = a.x; wv[rep][1] = a.y; wv[rep][2] = b.x;
+            wv[rep][3] = b.y; wv[rep][4] = c.x; wv[rep][5] = c.y;
+        } else {
+            const GAS uint8_t* g = gp(row);
+#pragma unroll
+            for (int i = 0; i < 6; i++) wv[rep][i] = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int sx = min(x0 + sg * 8 + k, W - 1);
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const int o = 3 * k + c;
+                    wv[rep][o >> 2] |= (uint32_t)g[(size_t)sx * 3 + c] << ((o & 3) * 8);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int rep = 0; rep < 2; rep++) {
+        const int task = t + 256 * rep, r = task >> 5, sg = task & 31;
         int yv[8];
         uint32_t cbw[2] = {0, 0}, crw[2] = {0, 0};
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             const int o0 = 3 * k, o1 = 3 * k + 1, o2 = 3 * k + 2;
-            const int c0 = (wv[o0 >> 2] >> ((o0 & 3) * 8)) & 255;
-            const int c1 = (wv[o1 >> 2] >> ((o1 & 3) * 8)) & 255;
-            const int c2 = (wv[o2 >> 2] >> ((o2 & 3) * 8)) & 255;
+            const int c0 = (wv[rep][o0 >> 2] >> ((o0 & 3) * 8)) & 255;
+            const int c1 = (wv[rep][o1 >> 2] >> ((o1 & 3) * 8)) & 255;
+            const int c2 = (wv[rep][o2 >> 2] >> ((o2 & 3) * 8)) & 255;
             const int R = BGR ? c2 : c0, G = c1, B = BGR ? c0 : c2;
             int yy, cb, cr;
             rgb_ycc(R, G, B, yy, cb, cr);
@@ -232,9 +231,11 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
     }
     __syncthreads();
 
-    // ---- D: column DCT, 3 tasks per thread (raw is dead: oz aliases it)
+    // ---- D: column DCT, 3 tasks per thread into registers, then the zig-zag
+    // scatter over the workspace once every column has been read
     {
         const int col = t & 7;
+        uint32_t res[3][4];
 #pragma unroll
         for (int rep = 0; rep < 3; rep++) {
             const int blk = (t >> 3) + 32 * rep;
@@ -243,7 +244,15 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
             for (int v = 0; v < 8; v++) d[v] = ws[blk][v * 8 + col];
             fdct8<1>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
 #pragma unroll
-            for (int v = 0; v < 8; v++) oz[blk][zz_of(v, col)] = (int16_t)d[v];
+            for (int v = 0; v < 4; v++) res[rep][v] = (d[2 * v] & 0xFFFF) | ((uint32_t)d[2 * v + 1] << 16);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int rep = 0; rep < 3; rep++) {
+            const int blk = (t >> 3) + 32 * rep;
+#pragma unroll
+            for (int v = 0; v < 8; v++)
+                oz[blk][zz_of(v, col)] = (int16_t)(res[rep][v >> 1] >> ((v & 1) * 16));
         }
     }
     __syncthreads();
@@ -254,7 +263,19 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
     const int nmcu = min(FDC_MCU, D.mcux - tx * FDC_MCU);
     const int nblk = nmcu * 6;
     const bool bottom = (2 * my + 1) >= D.yhb;
-    const int64_t bbase = ((int64_t)my * D.mcux + tx * FDC_MCU) * 6;
+    const uint32_t bbase = (uint32_t)(my * D.mcux + tx * FDC_MCU) * 6;  // < 2^31 blocks per image
+    const bool plain = nmcu == FDC_MCU && !bottom && 2 * (tx * FDC_MCU + FDC_MCU - 1) + 1 < D.ywb;
+    if (plain) {  // full interior tile: no dummy blocks, constant-divisor indexing
+#pragma unroll
+        for (int i = 0; i < FDC_BLK * 16 / 256; i++) {
+            const int e = t + 256 * i, quad = e / FDC_BLK, blk = e - quad * FDC_BLK;
+            const uint32_t b = bbase + blk;
+            st8(D.coefs + ((size_t)(b / CHUNK_BLOCKS) * (CHUNK_BLOCKS * 64) + quad * (CHUNK_BLOCKS * 4) +
+                           (b % CHUNK_BLOCKS) * 4),
+                *(const int2*)&oz[blk][quad * 4]);
+        }
+        return;
+    }
     for (int e = t; e < nblk * 16; e += 256) {  // (quad, block) pieces of 8 B, block fastest
         const int quad = e / nblk, blk = e - quad * nblk, mcu = blk / 6, yb = blk - mcu * 6;
         int2 val = *(const int2*)&oz[blk][quad * 4];
