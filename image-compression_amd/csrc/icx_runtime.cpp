@@ -957,7 +957,13 @@ icx_status icx_create(int device, icx_ctx** out)
         delete c;
         return ICX_E_DEVICE;
     }
+    // Sub-batch workspace: a quarter of the free HBM at creation (a 4K image
+    // needs ~210 MB, so ~80 GB holds a few hundred frames per sub-batch and the
+    // host synchronises a few times per call, not per handful of images).
+    size_t free_b = 0, total_b = 0;
     size_t budget_mb = 16384;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
+        budget_mb = std::max<size_t>(2048, (free_b / 4) >> 20);
     if (const char* env = getenv("ICX_WORKSPACE_MB")) budget_mb = (size_t)atoll(env);
     c->budget = budget_mb << 20;
     *out = c;
