@@ -120,26 +120,37 @@ __device__ __forceinline__ int zz_of(int v, int u)
 }
 
 // Colour: one workgroup = 16 rows x 256 px = 16 MCUs of one MCU row (96 blocks);
-// every phase has 1-3 equal tasks per thread.  LDS 20 KiB -> 8 workgroups/CU.
-//   B. 2 x 8 px per thread straight from HBM (24 B runs, a wave reads two
-//      contiguous 768 B row pieces; edges clamped): YCbCr, Y row-DCT in
-//      registers -> int16 workspace, full-res Cb/Cr bytes -> LDS
-//   C. h2v2_downsample (bias 1,2,..) + chroma row-DCT, one row task per thread
+// every phase has 1-3 equal tasks per thread.  LDS 15 KiB -> 8 workgroups/CU.
+//   B. one row pair x 8 px per thread straight from HBM (24 B runs; a wave
+//      reads four contiguous 768 B row pieces; edges clamped): YCbCr, two Y
+//      row-DCTs in registers -> workspace; h2v2_downsample of its own 2x8
+//      Cb/Cr (bias 1,2,..) -> 4 + 4 bytes of the downsampled chroma tile
+//   C. chroma row-DCT, one row task per thread (bottom rows past the image
+//      replicate the last chroma row, jcprepct.c expand_bottom_edge)
 //   D. column DCT, 3 column tasks per thread into registers; barrier; zig-zag
 //      scatter over the (now dead) workspace
 //   E. dummy blocks (jccoefct.c) + 8-B stores into the interleaved layout
+// The workspace stride of 68 int16 (34 dwords) puts consecutive blocks on
+// distinct LDS banks for every access pattern above.
 constexpr int FDC_MCU = 16;           // MCUs per colour tile
 constexpr int FDC_PX = FDC_MCU * 16;  // 256 px
 constexpr int FDC_BLK = FDC_MCU * 6;  // 96 blocks
+constexpr int WSTR = 68;              // workspace int16 per block
+
+__device__ __forceinline__ void st_row8(int16_t* p, const int (&v)[8])  // 8 int16, 8-B aligned
+{
+    *(uint2*)p = make_uint2((v[0] & 0xFFFF) | (v[1] << 16), (v[2] & 0xFFFF) | (v[3] << 16));
+    *(uint2*)(p + 4) = make_uint2((v[4] & 0xFFFF) | (v[5] << 16), (v[6] & 0xFFFF) | (v[7] << 16));
+}
 
 template <bool BGR>
 __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ descs,
                                                     const int32_t* __restrict__ ids,
                                                     const int64_t* __restrict__ prefix, int m)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t cful[2][16][FDC_PX];    // 8 KB full-res Cb, Cr
-    __shared__ __attribute__((aligned(16))) int16_t ws[FDC_BLK][64];        // 12 KB row-pass output
-    int16_t (*oz)[64] = ws;                                                 // zig-zag output (phase D)
+    __shared__ __attribute__((aligned(16))) uint8_t cds[2][8][FDC_PX / 2];  // 2 KB downsampled Cb, Cr
+    __shared__ __attribute__((aligned(16))) int16_t ws[FDC_BLK][WSTR];     // 12.75 KB row-pass output
+    int16_t (*oz)[WSTR] = ws;                                               // zig-zag output (phase D)
 
     const int64_t item = blockIdx.x;
     const int slot = find_slot(prefix, m, item);
@@ -151,83 +162,78 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
     const int t = threadIdx.x;
     const uint8_t* px = D.px;
 
-    // ---- B: 2 row tasks of 8 px; all six 8-B loads issued before any use
-    const bool fast = (x0 + FDC_PX <= W) && (((uintptr_t)px & 7) == 0) && ((D.stride & 7) == 0);
-    uint32_t wv[2][6];
+    // ---- B: rows 2i, 2i+1 of the tile, pixels 8sg..8sg+7
+    {
+        const int i = t >> 5, sg = t & 31;
+        const bool fast = (x0 + FDC_PX <= W) && (((uintptr_t)px & 7) == 0) && ((D.stride & 7) == 0);
+        uint32_t wv[2][6];
 #pragma unroll
-    for (int rep = 0; rep < 2; rep++) {
-        const int task = t + 256 * rep, r = task >> 5, sg = task & 31;
-        const int y = min(y0 + r, H - 1);
-        const uint8_t* row = px + (size_t)y * D.stride;
-        if (fast) {
-            const uint8_t* p = row + (size_t)(x0 + sg * 8) * 3;
-            const int2 a = ld8(p), b = ld8(p + 8), c = ld8(p + 16);
-            wv[rep][0] = a.x; wv[rep][1] = a.y; wv[rep][2] = b.x;
-            wv[rep][3] = b.y; wv[rep][4] = c.x; wv[rep][5] = c.y;
-        } else {
-            const GAS uint8_t* g = gp(row);
+        for (int h = 0; h < 2; h++) {
+            const int y = min(y0 + 2 * i + h, H - 1);
+            const uint8_t* row = px + (size_t)y * D.stride;
+            if (fast) {
+                const uint8_t* p = row + (size_t)(x0 + sg * 8) * 3;
+                const int2 a = ld8(p), b = ld8(p + 8), c = ld8(p + 16);
+                wv[h][0] = a.x; wv[h][1] = a.y; wv[h][2] = b.x;
+                wv[h][3] = b.y; wv[h][4] = c.x; wv[h][5] = c.y;
+            } else {
+                const GAS uint8_t* g = gp(row);
 #pragma unroll
-            for (int i = 0; i < 6; i++) wv[rep][i] = 0;
+                for (int k = 0; k < 6; k++) wv[h][k] = 0;
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const int sx = min(x0 + sg * 8 + k, W - 1);
+                for (int k = 0; k < 8; k++) {
+                    const int sx = min(x0 + sg * 8 + k, W - 1);
 #pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    const int o = 3 * k + c;
-                    wv[rep][o >> 2] |= (uint32_t)g[(size_t)sx * 3 + c] << ((o & 3) * 8);
+                    for (int c = 0; c < 3; c++) {
+                        const int o = 3 * k + c;
+                        wv[h][o >> 2] |= (uint32_t)g[(size_t)sx * 3 + c] << ((o & 3) * 8);
+                    }
                 }
             }
         }
-    }
+        int csum[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};  // 2x2 sums of Cb, Cr
 #pragma unroll
-    for (int rep = 0; rep < 2; rep++) {
-        const int task = t + 256 * rep, r = task >> 5, sg = task & 31;
-        int yv[8];
-        uint32_t cbw[2] = {0, 0}, crw[2] = {0, 0};
+        for (int h = 0; h < 2; h++) {
+            int yv[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int o0 = 3 * k, o1 = 3 * k + 1, o2 = 3 * k + 2;
-            const int c0 = (wv[rep][o0 >> 2] >> ((o0 & 3) * 8)) & 255;
-            const int c1 = (wv[rep][o1 >> 2] >> ((o1 & 3) * 8)) & 255;
-            const int c2 = (wv[rep][o2 >> 2] >> ((o2 & 3) * 8)) & 255;
-            const int R = BGR ? c2 : c0, G = c1, B = BGR ? c0 : c2;
-            int yy, cb, cr;
-            rgb_ycc(R, G, B, yy, cb, cr);
-            yv[k] = yy - 128;
-            cbw[k >> 2] |= (uint32_t)cb << ((k & 3) * 8);
-            crw[k >> 2] |= (uint32_t)cr << ((k & 3) * 8);
+            for (int k = 0; k < 8; k++) {
+                const int o0 = 3 * k, o1 = 3 * k + 1, o2 = 3 * k + 2;
+                const int c0 = (wv[h][o0 >> 2] >> ((o0 & 3) * 8)) & 255;
+                const int c1 = (wv[h][o1 >> 2] >> ((o1 & 3) * 8)) & 255;
+                const int c2 = (wv[h][o2 >> 2] >> ((o2 & 3) * 8)) & 255;
+                const int R = BGR ? c2 : c0, G = c1, B = BGR ? c0 : c2;
+                int yy, cb, cr;
+                rgb_ycc(R, G, B, yy, cb, cr);
+                yv[k] = yy - 128;
+                csum[0][k >> 1] += cb;
+                csum[1][k >> 1] += cr;
+            }
+            fdct8<0>(yv[0], yv[1], yv[2], yv[3], yv[4], yv[5], yv[6], yv[7]);
+            const int r = 2 * i + h;
+            const int blk = (sg >> 1) * 6 + (r >> 3) * 2 + (sg & 1);
+            st_row8(&ws[blk][(r & 7) * 8], yv);
         }
-        *(uint2*)&cful[0][r][sg * 8] = make_uint2(cbw[0], cbw[1]);
-        *(uint2*)&cful[1][r][sg * 8] = make_uint2(crw[0], crw[1]);
-        fdct8<0>(yv[0], yv[1], yv[2], yv[3], yv[4], yv[5], yv[6], yv[7]);
-        const int blk = (sg >> 1) * 6 + (r >> 3) * 2 + (sg & 1);
-        *(int4*)&ws[blk][(r & 7) * 8] =
-            make_int4((yv[0] & 0xFFFF) | (yv[1] << 16), (yv[2] & 0xFFFF) | (yv[3] << 16),
-                      (yv[4] & 0xFFFF) | (yv[5] << 16), (yv[6] & 0xFFFF) | (yv[7] << 16));
+#pragma unroll
+        for (int c = 0; c < 2; c++) {  // h2v2_downsample: bias 1, 2, 1, 2 by output column
+            uint32_t w = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) w |= (uint32_t)((csum[c][j] + 1 + (j & 1)) >> 2) << (8 * j);
+            *(uint32_t*)&cds[c][i][sg * 4] = w;
+        }
     }
     __syncthreads();
 
-    // ---- C: h2v2_downsample + chroma row DCT, 256 row tasks
+    // ---- C: chroma row DCT, 256 row tasks
     {
         const int comp = t >> 7, cr = (t >> 4) & 7, cb = t & 15;
         const int crows = (H + 1) >> 1;  // chroma rows with image data
-        int re = cr;
-        if (my * 8 + cr >= crows) re = crows - 1 - my * 8;  // replicate last chroma row
-        const uint4 u0 = *(const uint4*)&cful[comp][2 * re][cb * 16];
-        const uint4 u1 = *(const uint4*)&cful[comp][2 * re + 1][cb * 16];
-        const uint32_t a[4] = {u0.x, u0.y, u0.z, u0.w}, bb[4] = {u1.x, u1.y, u1.z, u1.w};
+        const int re = min(cr, crows - 1 - my * 8);
+        const uint2 u = *(const uint2*)&cds[comp][re][cb * 8];
         int v[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int wd = j >> 1, sh = (j & 1) * 16;
-            const int s0 = ((a[wd] >> sh) & 255) + ((a[wd] >> (sh + 8)) & 255) + ((bb[wd] >> sh) & 255) +
-                           ((bb[wd] >> (sh + 8)) & 255);
-            v[j] = ((s0 + 1 + (j & 1)) >> 2) - 128;
-        }
+        for (int j = 0; j < 8; j++) v[j] = (int)(((j < 4 ? u.x : u.y) >> (8 * (j & 3))) & 255) - 128;
         fdct8<0>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
-        *(int4*)&ws[cb * 6 + 4 + comp][cr * 8] =
-            make_int4((v[0] & 0xFFFF) | (v[1] << 16), (v[2] & 0xFFFF) | (v[3] << 16),
-                      (v[4] & 0xFFFF) | (v[5] << 16), (v[6] & 0xFFFF) | (v[7] << 16));
+        st_row8(&ws[cb * 6 + 4 + comp][cr * 8], v);
     }
     __syncthreads();
 
