@@ -367,6 +367,9 @@ __device__ __forceinline__ int nbits(int a) { return a ? 32 - __clz(a) : 0; }
 #define ICX_SLOT_WORDS 13
 #endif
 constexpr int SLOT_WORDS = ICX_SLOT_WORDS;
+#ifndef ICX_HUFF_EXP
+#define ICX_HUFF_EXP 0  // timing-only variants (scripts/huff_phases.sh); 0 = the product
+#endif
 
 constexpr int SLOT_BITS = SLOT_WORDS * 32;
 constexpr int AC_SIZES = 11;                // AC magnitude categories 0..10 (8-bit JPEG)
@@ -463,12 +466,13 @@ __device__ __forceinline__ void encode_block(Sink& sink, const int2 (&quad)[16],
 //   1. quantise + Huffman-code the thread's block straight into its LDS slot
 //      (coefficient quads read 512 B-coalesced from the interleaved layout)
 //   2. workgroup scan of the block bit counts -> offsets inside the chunk
-//   3. gather: every 32-bit word of the chunk stream is assembled by the
+//   3. every run of eight 1-bits inside the chunk is binned by start position
+//      mod 8 (chunk_ffa), by the thread of the block it starts in: the chunk's
+//      0xFF-byte count for each alignment the chunk may land on once k_scan
+//      places it.
+//   4. gather: every 32-bit word of the chunk stream is assembled by the
 //      thread whose block holds the word's first bit (reading the following
 //      blocks' slots as needed) and stored once to scratch[cur].
-//   4. every run of eight 1-bits inside the chunk is binned by start position
-//      mod 8 (chunk_ffa): the chunk's 0xFF-byte count for each alignment the
-//      chunk may land on once k_scan places it.
 __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict__ descs,
                                                        const ImgState* __restrict__ states,
                                                        const QNode* __restrict__ nodes,
@@ -557,6 +561,10 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         }
     }
 
+#if ICX_HUFF_EXP == 1  // timing only: encode, nothing after
+    if (t == 0) D.chunk_bits[cur][chunk] = (uint32_t)bits;
+    return;
+#endif
     // ---- 2. exclusive scan of block bits
     int incl = bits;
 #pragma unroll
@@ -576,9 +584,50 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     s_bits[t] = bits;
     __syncthreads();
 
-    // ---- 3. gather the chunk's words
-    GAS uint32_t* dst = gp(D.scratch[cur] + (size_t)chunk * CHUNK_WORDS);
     const GAS uint32_t* spill0 = gp(D.ovf + b0 * BLOCK_WORDS);
+    auto slot_word = [&](int u, uint32_t wi) -> uint32_t {  // word wi of block u's stream
+        return s_bits[u] <= SLOT_BITS ? slots[u * SLOT_WORDS + wi] : spill0[(size_t)u * BLOCK_WORDS + wi];
+    };
+
+    // ---- 3. 0xFF candidates: every run of eight 1-bits that starts in this
+    // block, binned by chunk-local start position mod 8 (s_ffa) - the chunk's
+    // 0xFF-byte count for each alignment k_scan may place it at.  Runs may
+    // reach into the following blocks (their first <= 8 bits); nothing
+    // follows the chunk's last bit here (k_scan checks the boundary bytes).
+    if (bits > 0) {
+        uint32_t la = 0;  // the <= 8 bits after this block, MSB-aligned
+        int have = 0;
+        for (int u = t + 1; have < 8 && u < nb; u++) {
+            const int take = min(8 - have, (int)s_bits[u]);
+            la |= (slot_word(u, 0) & ~(~0u >> take)) >> have;
+            have += take;
+        }
+        const uint32_t nwb = ((uint32_t)bits + 31) >> 5;
+        uint32_t cw = slot_word(t, 0);
+        for (uint32_t i = 0; i < nwb; i++) {
+            const uint32_t nx = i + 1 < nwb ? slot_word(t, i + 1) : 0u;
+            uint64_t x = ((uint64_t)cw << 32) | nx;
+            const int rem = bits - 32 * (int)i;  // block bits from word i on
+            if (rem <= 32) x |= (uint64_t)la << (32 - rem);
+            else if (rem < 40) x |= (uint64_t)(la >> (rem - 32));
+            x &= x << 1;
+            x &= x << 2;
+            x &= x << 4;
+            uint32_t r = (uint32_t)(x >> 32);  // bit 31-d: a run starts at block bit 32i+d
+            if (rem < 32) r &= ~(~0u >> rem);
+            if (r) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int n = __popc(r & (0x80808080u >> k));
+                    if (n) atomicAdd(&s_ffa[(off + k) & 7], (uint32_t)n);
+                }
+            }
+            cw = nx;
+        }
+    }
+
+    // ---- 4. gather the chunk's words
+    GAS uint32_t* dst = gp(D.scratch[cur] + (size_t)chunk * CHUNK_WORDS);
     for (uint32_t j = (off + 31) >> 5; j * 32 < off + bits; j++) {
         uint32_t outw = 0;
         int have = 0, u = t;
@@ -587,18 +636,8 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
             const int avail = (int)s_bits[u] - (int)p;
             const int take = min(32 - have, avail);
             const uint32_t wi = p >> 5, sh = p & 31;
-            uint32_t v0, v1 = 0;
-            if (s_bits[u] <= SLOT_BITS) {
-                const uint32_t* ls = &slots[u * SLOT_WORDS];
-                v0 = ls[wi];
-                if (sh + take > 32) v1 = ls[wi + 1];
-            } else {
-                const GAS uint32_t* gs = spill0 + (size_t)u * BLOCK_WORDS;
-                v0 = gs[wi];
-                if (sh + take > 32) v1 = gs[wi + 1];
-            }
-            uint32_t v = v0 << sh;
-            if (sh + take > 32) v |= v1 >> (32 - sh);
+            uint32_t v = slot_word(u, wi) << sh;
+            if (sh + take > 32) v |= slot_word(u, wi + 1) >> (32 - sh);
             v &= take == 32 ? ~0u : ~(~0u >> take);
             outw |= v >> have;
             have += take;
@@ -607,27 +646,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         }
         dst[j] = outw;
     }
-    __syncthreads();  // the chunk's words are in dst (same CU: visible through its L1)
-
-    // ---- 4. alignment bins of 0xFF candidates: word pairs read back coalesced.
-    // Bit 31-d of r set <=> eight 1-bits start at chunk bit 32i+d (zero past
-    // the chunk's end, so no run leaves it).
-    const uint32_t nw = (total + 31) >> 5;
-    for (uint32_t i = t; i < nw; i += CHUNK_BLOCKS) {
-        uint64_t x = ((uint64_t)dst[i] << 32) | (i + 1 < nw ? dst[i + 1] : 0u);
-        x &= x << 1;
-        x &= x << 2;
-        x &= x << 4;
-        const uint32_t r = (uint32_t)(x >> 32);
-        if (r) {
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const int n = __popc(r & (0x80808080u >> k));
-                if (n) atomicAdd(&s_ffa[k], (uint32_t)n);
-            }
-        }
-    }
-    __syncthreads();
+    __syncthreads();  // s_ffa complete
     if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = s_ffa[t];
     if (t == 0) D.chunk_bits[cur][chunk] = total;
 }

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Build an experimental libicx variant: build_variant.sh NAME "-DFLAG=..." -> image-compression_amd/lib/libicx_NAME.so
+set -e
+cd "$(dirname "$0")/../image-compression_amd"
+mkdir -p build/var lib
+F="-O3 -std=c++17 -fPIC -ffp-contract=off $2"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 $F -c csrc/icx_kernels.hip -o build/var/k_$1.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 $F -x hip -c csrc/icx_runtime.cpp -o build/var/r_$1.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/libicx_$1.so build/var/k_$1.o build/var/r_$1.o

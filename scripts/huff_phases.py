@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Timing-only driver: per-kernel HIP-event times of codec.fit on the bench
+workload, no output validation (for the ICX_HUFF_EXP builds, whose output is
+deliberately incomplete).  ICX_LIB selects the library build."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "image-compression_amd"))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import icx  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+dev = torch.device("cuda:0")
+frames = bench.make_frames(n, 1000, dev)
+codec = icx.Codec(0)
+outs = [torch.empty(bench.TARGET + 1, dtype=torch.uint8, device=dev) for _ in range(n)]
+cached = [icx.LearnedParams(bench.Q0, 1.0)] * n
+codec.fit(frames, bench.TARGET, bench.Q0, cached=cached, outputs=outs)
+torch.cuda.synchronize()
+codec.profile(True)
+codec.profile_reset()
+for _ in range(2):
+    codec.fit(frames, bench.TARGET, bench.Q0, cached=cached, outputs=outs)
+torch.cuda.synchronize()
+res = {k: codec.profile_query(k) for k in ("fdct", "huff", "scan", "decide", "ffscan", "stuff")}
+print(json.dumps({"lib": os.path.basename(os.environ.get("ICX_LIB", "libicx.so")), "images": n,
+                  "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k, v in res.items()}}))
