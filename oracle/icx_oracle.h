@@ -87,6 +87,18 @@ long oracle_fit_batch(int n, const uint8_t* const* px, const int* w, const int* 
                       int have_cached, float cached_q, double cached_scale,
                       int nthreads, int64_t* out_sizes, float* out_q, double* out_scale);
 
+/* ---- A11 decode (icx_oracle_decode.c): IJG 6b baseline decompression as the
+ * JDK JPEGImageReader runs it (ImageCompression.java:113-155).  Status codes
+ * as include/icx.h: 0 ok, 4 cap too small, 5 unsupported, 6 corrupt. */
+int oracle_jpeg_info(const uint8_t* jpg, size_t len, int* w, int* h, int* ncomp);
+/* blocks in the scan (MCU order, dummy blocks included); -1 if unparsable */
+long oracle_jpeg_num_blocks(const uint8_t* jpg, size_t len);
+/* quantised coefficients after DC prediction, natural order, 64 per block */
+int oracle_jpeg_coefs(const uint8_t* jpg, size_t len, int16_t* coefs, size_t nblocks);
+/* decode + source subsampling s: ceil(W/s) x ceil(H/s), BGR24 or GRAY8, packed */
+int oracle_jpeg_decode(const uint8_t* jpg, size_t len, int s, uint8_t* out, size_t cap, int* w,
+                       int* h, int* fmt);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,546 @@
+/*
+ * icx_oracle_decode.c — scalar CPU restatement of the reference's JPEG decode
+ * (row A11 of SURVEY.md §8a).  TEST INFRASTRUCTURE ONLY (see icx_oracle.h):
+ * the checker for the device decoder; never linked into libicx.so.
+ *
+ * Reference call site: ImageCompression.decodeImageWithSubsampling
+ * (core/ImageCompression.java:107-165) reads a JPEG through javax.imageio's
+ * JPEGImageReader with ImageReadParam.setSourceSubsampling(s, s, 0, 0)
+ * (:150-153) and ignoreMetadata = true (:126).  The arithmetic lives in the
+ * JDK's bundled IJG libjpeg 6b (absent from /root/reference); this file
+ * restates its published baseline decompression algorithm:
+ *   jdmarker.c   SOI/APPn/DQT/DHT/SOF0-1/DRI/SOS parsing
+ *   jdhuff.c     decode_mcu: canonical Huffman decode, HUFF_EXTEND, DC
+ *                prediction per component reset at every restart interval
+ *   jidctint.c   jpeg_idct_islow (CONST_BITS 13, PASS1_BITS 2) with the
+ *                post-IDCT range-limit table of jdmaster.c
+ *   jdcoefct.c   IDCT only for real (non-dummy) blocks
+ *   jdsample.c   h2v2/h2v1 "fancy" (triangle) upsampling when
+ *                downsampled_width > 2, else box replication; context rows
+ *                replicate the first / last real sample row (jdmainct.c)
+ *   jdcolor.c    ycc_rgb_convert (SCALEBITS 16 tables)
+ * then keeps pixels (x*s, y*s) as the JDK reader does for source subsampling
+ * and returns TYPE_3BYTE_BGR (3 components) or TYPE_BYTE_GRAY.
+ *
+ * Pinned against libjpeg-turbo 3.1.4 (6b API level, via Pillow) decodes of
+ * tests/golden/decode/ (gen_decode_golden.py).
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "icx_oracle.h"
+
+typedef struct {
+    uint16_t maxcode_ok[18];
+    int32_t maxcode[18]; /* largest code of length l, -1 if none */
+    int32_t valoff[17];  /* huffval index of the first code of length l minus that code */
+    uint8_t vals[256];
+    int present;
+} dhuff_t;
+
+typedef struct {
+    int w, h, ncomp, ri;
+    int id[3], hs[3], vs[3], tq[3], td[3], ta[3];
+    int hmax, vmax, mcux, mcuy;
+    uint16_t qt[4][64]; /* natural order */
+    int qt_present[4];
+    dhuff_t dc[4], ac[4];
+    const uint8_t* scan; /* first byte of the entropy-coded segment */
+    size_t scan_len;
+} jinfo_t;
+
+static const int ZZ_NAT[64 + 16] = {
+    0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5,
+    12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6, 7, 14, 21, 28,
+    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63,
+    /* jpeg_natural_order's safety tail: corrupt runs past 63 land on 63 */
+    63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+
+static int build_dhuff(const uint8_t* counts, const uint8_t* vals, int nvals, dhuff_t* t)
+{
+    int code = 0, k = 0;
+    memset(t, 0, sizeof(*t));
+    for (int l = 1; l <= 16; l++) {
+        int n = counts[l - 1];
+        t->valoff[l] = k - code;
+        if (n) {
+            code += n;
+            k += n;
+            t->maxcode[l] = code - 1;
+        } else {
+            t->maxcode[l] = -1;
+        }
+        if (code > (1 << l)) return 6; /* over-subscribed */
+        code <<= 1;
+    }
+    t->maxcode[17] = 0x7FFFFFFF;
+    if (k != nvals) return 6;
+    memcpy(t->vals, vals, (size_t)nvals);
+    t->present = 1;
+    return 0;
+}
+
+/* jdmarker.c, baseline subset.  0 ok, 5 unsupported, 6 corrupt. */
+static int parse(const uint8_t* p, size_t len, jinfo_t* J)
+{
+    memset(J, 0, sizeof(*J));
+    if (len < 4 || p[0] != 0xFF || p[1] != 0xD8) return 6;
+    size_t i = 2;
+    int have_sof = 0;
+    for (;;) {
+        while (i < len && p[i] != 0xFF) i++; /* jdmarker next_marker: skip garbage */
+        while (i < len && p[i] == 0xFF) i++; /* fill bytes */
+        if (i >= len) return 6;
+        int m = p[i++];
+        if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+        if (m == 0xD9) return 6; /* EOI before SOS */
+        if (i + 2 > len) return 6;
+        size_t seg = ((size_t)p[i] << 8) | p[i + 1];
+        if (seg < 2 || i + seg > len) return 6;
+        const uint8_t* s = p + i + 2;
+        size_t n = seg - 2;
+        i += seg;
+        if (m == 0xDB) { /* DQT */
+            size_t o = 0;
+            while (o < n) {
+                int pq = s[o] >> 4, tq = s[o] & 15;
+                if (tq > 3 || pq > 1) return 6;
+                size_t need = 1 + (pq ? 128 : 64);
+                if (o + need > n) return 6;
+                for (int k = 0; k < 64; k++)
+                    J->qt[tq][ZZ_NAT[k]] = pq ? (uint16_t)((s[o + 1 + 2 * k] << 8) | s[o + 2 + 2 * k])
+                                              : s[o + 1 + k];
+                J->qt_present[tq] = 1;
+                o += need;
+            }
+        } else if (m == 0xC4) { /* DHT */
+            size_t o = 0;
+            while (o < n) {
+                if (o + 17 > n) return 6;
+                int tc = s[o] >> 4, th = s[o] & 15;
+                if (tc > 1 || th > 3) return 6;
+                int tot = 0;
+                for (int l = 0; l < 16; l++) tot += s[o + 1 + l];
+                if (tot > 256 || o + 17 + (size_t)tot > n) return 6;
+                int rc = build_dhuff(s + o + 1, s + o + 17, tot, tc ? &J->ac[th] : &J->dc[th]);
+                if (rc) return rc;
+                o += 17 + (size_t)tot;
+            }
+        } else if (m == 0xC0 || m == 0xC1) { /* SOF0 / SOF1: sequential Huffman */
+            if (n < 6 || s[0] != 8) return 5;
+            J->h = (s[1] << 8) | s[2];
+            J->w = (s[3] << 8) | s[4];
+            J->ncomp = s[5];
+            if (J->w == 0 || J->h == 0) return 5; /* DNL-defined height */
+            if (J->ncomp != 1 && J->ncomp != 3) return 5;
+            if (n < 6 + 3 * (size_t)J->ncomp) return 6;
+            for (int c = 0; c < J->ncomp; c++) {
+                J->id[c] = s[6 + 3 * c];
+                J->hs[c] = s[7 + 3 * c] >> 4;
+                J->vs[c] = s[7 + 3 * c] & 15;
+                J->tq[c] = s[8 + 3 * c];
+                if (J->tq[c] > 3 || J->hs[c] < 1 || J->vs[c] < 1) return 6;
+            }
+            have_sof = 1;
+        } else if ((m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC)) {
+            if (n >= 6) { /* progressive / lossless / arithmetic: dims only */
+                J->h = (s[1] << 8) | s[2];
+                J->w = (s[3] << 8) | s[4];
+                J->ncomp = s[5];
+            }
+            return 5;
+        } else if (m == 0xDD) { /* DRI */
+            if (n < 2) return 6;
+            J->ri = (s[0] << 8) | s[1];
+        } else if (m == 0xDA) { /* SOS */
+            if (!have_sof) return 6;
+            int ns = s[0];
+            if (ns != J->ncomp || n < 1 + 2 * (size_t)ns + 3) return 5; /* single interleaved scan */
+            for (int k = 0; k < ns; k++) {
+                int cid = s[1 + 2 * k], c;
+                for (c = 0; c < J->ncomp && J->id[c] != cid; c++) {}
+                if (c != k) return 5;
+                J->td[c] = s[2 + 2 * k] >> 4;
+                J->ta[c] = s[2 + 2 * k] & 15;
+                if (J->td[c] > 3 || J->ta[c] > 3) return 6;
+            }
+            if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0) return 5;
+            J->scan = p + i;
+            J->scan_len = len - i;
+            break;
+        }
+        /* APPn, COM, DNL, ...: skipped (ignoreMetadata = true, ImageCompression.java:126) */
+    }
+    /* sampling: colour = Y (1|2 x 1|2) with Cb, Cr at 1x1 except 1x2 (4:4:0,
+     * whose 6b upsampler is not the one libjpeg-turbo uses); grey = any */
+    J->hmax = J->vmax = 1;
+    if (J->ncomp == 3) {
+        if (J->hs[1] != 1 || J->vs[1] != 1 || J->hs[2] != 1 || J->vs[2] != 1) return 5;
+        if (J->hs[0] > 2 || J->vs[0] > 2) return 5;
+        if (J->hs[0] == 1 && J->vs[0] == 2) return 5;
+        J->hmax = J->hs[0];
+        J->vmax = J->vs[0];
+        J->mcux = (J->w + 8 * J->hmax - 1) / (8 * J->hmax);
+        J->mcuy = (J->h + 8 * J->vmax - 1) / (8 * J->vmax);
+    } else { /* non-interleaved single component: one block per MCU */
+        J->hs[0] = J->vs[0] = 1;
+        J->mcux = (J->w + 7) / 8;
+        J->mcuy = (J->h + 7) / 8;
+    }
+    for (int c = 0; c < J->ncomp; c++) {
+        if (!J->qt_present[J->tq[c]] || !J->dc[J->td[c]].present || !J->ac[J->ta[c]].present) return 6;
+    }
+    return 0;
+}
+
+int oracle_jpeg_info(const uint8_t* jpg, size_t len, int* w, int* h, int* ncomp)
+{
+    jinfo_t J;
+    int rc = parse(jpg, len, &J);
+    if (rc == 0 || rc == 5) {
+        if (w) *w = J.w;
+        if (h) *h = J.h;
+        if (ncomp) *ncomp = J.ncomp;
+    }
+    return rc;
+}
+
+/* ----------------------------------------------------- jdhuff.c bit reader */
+typedef struct {
+    const uint8_t* p;
+    size_t len, pos;
+    uint64_t acc;
+    int nbits;
+    int hit_marker;
+} breader_t;
+
+static void fill(breader_t* b)
+{
+    while (b->nbits <= 56) {
+        int v;
+        if (b->hit_marker || b->pos >= b->len) {
+            v = 0; /* jdhuff.c: past a marker / the end, feed zeros (with a warning) */
+            b->hit_marker = 1;
+        } else {
+            v = b->p[b->pos];
+            if (v == 0xFF) {
+                size_t q = b->pos + 1;
+                while (q < b->len && b->p[q] == 0xFF) q++;
+                if (q < b->len && b->p[q] == 0x00) {
+                    b->pos = q + 1;
+                } else {
+                    b->hit_marker = 1;
+                    v = 0;
+                }
+            } else {
+                b->pos++;
+            }
+        }
+        b->acc |= (uint64_t)v << (56 - b->nbits);
+        b->nbits += 8;
+    }
+}
+
+static inline int get_bits(breader_t* b, int n)
+{
+    if (n == 0) return 0;
+    if (b->nbits < n) fill(b);
+    int v = (int)(b->acc >> (64 - n));
+    b->acc <<= n;
+    b->nbits -= n;
+    return v;
+}
+
+static int decode_sym(breader_t* b, const dhuff_t* t)
+{
+    if (b->nbits < 16) fill(b);
+    int code = 0;
+    for (int l = 1; l <= 16; l++) {
+        code = (code << 1) | (int)(b->acc >> 63);
+        b->acc <<= 1;
+        b->nbits--;
+        if (code <= t->maxcode[l]) return t->vals[(t->valoff[l] + code) & 0xFF];
+    }
+    return -1; /* bad Huffman code */
+}
+
+static inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
+
+/* After an interval: skip to the RSTn marker, reset the reader (jdhuff.c process_restart). */
+static int restart(breader_t* b)
+{
+    /* discard buffered bits; find the marker following the bytes consumed */
+    size_t q = b->pos;
+    while (q + 1 < b->len && !(b->p[q] == 0xFF && b->p[q + 1] >= 0xD0 && b->p[q + 1] <= 0xD7)) {
+        if (b->p[q] == 0xFF && b->p[q + 1] != 0x00 && b->p[q + 1] != 0xFF) return 6;
+        q++;
+    }
+    if (q + 1 >= b->len) return 6;
+    b->pos = q + 2;
+    b->acc = 0;
+    b->nbits = 0;
+    b->hit_marker = 0;
+    return 0;
+}
+
+/* Decode the scan into quantised coefficients, natural order, scan (MCU) block
+ * order including dummy blocks.  Returns 0 / 6. */
+static int decode_scan(const jinfo_t* J, int16_t* coefs)
+{
+    breader_t b = {J->scan, J->scan_len, 0, 0, 0, 0};
+    int nb_mcu = J->ncomp == 3 ? J->hs[0] * J->vs[0] + 2 : 1;
+    int comp_of[6];
+    for (int k = 0; k < nb_mcu; k++) comp_of[k] = J->ncomp == 1 ? 0 : (k < nb_mcu - 2 ? 0 : k - (nb_mcu - 3));
+    long nmcu = (long)J->mcux * J->mcuy;
+    int pred[3] = {0, 0, 0};
+    int16_t* blk = coefs;
+    for (long m = 0; m < nmcu; m++) {
+        if (J->ri && m > 0 && m % J->ri == 0) {
+            if (restart(&b)) return 6;
+            pred[0] = pred[1] = pred[2] = 0;
+        }
+        for (int k = 0; k < nb_mcu; k++, blk += 64) {
+            int c = comp_of[k];
+            memset(blk, 0, 64 * sizeof(int16_t));
+            int s = decode_sym(&b, &J->dc[J->td[c]]);
+            if (s < 0 || s > 15) return 6;
+            if (s) s = extend(get_bits(&b, s), s);
+            pred[c] += s;
+            blk[0] = (int16_t)pred[c];
+            for (int z = 1; z < 64; z++) {
+                int rs = decode_sym(&b, &J->ac[J->ta[c]]);
+                if (rs < 0) return 6;
+                int r = rs >> 4;
+                s = rs & 15;
+                if (s) {
+                    z += r;
+                    int v = extend(get_bits(&b, s), s);
+                    blk[ZZ_NAT[z]] = (int16_t)v;
+                } else {
+                    if (r != 15) break;
+                    z += 15;
+                }
+            }
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------ jidctint.c */
+#define CONST_BITS 13
+#define PASS1_BITS 2
+#define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
+
+static inline uint8_t idct_limit(int v)
+{
+    /* IDCT_range_limit(cinfo)[v & RANGE_MASK] of jdmaster.c prepare_range_limit_table */
+    int x = v & 1023;
+    if (x < 128) return (uint8_t)(x + 128);
+    if (x < 512) return 255;
+    if (x < 896) return 0;
+    return (uint8_t)(x - 896);
+}
+
+static void idct_islow(const int16_t* in, const uint16_t* qt, uint8_t* out, int ostride)
+{
+    int ws[64];
+    for (int c = 0; c < 8; c++) { /* pass 1: columns */
+        int d[8];
+        for (int r = 0; r < 8; r++) d[r] = in[r * 8 + c] * qt[r * 8 + c];
+        int z2 = d[2], z3 = d[6];
+        int z1 = (z2 + z3) * 4433;                 /* FIX_0_541196100 */
+        int t2 = z1 + z3 * (-15137);               /* FIX_1_847759065 */
+        int t3 = z1 + z2 * 6270;                   /* FIX_0_765366865 */
+        int t0 = (d[0] + d[4]) << CONST_BITS;
+        int t1 = (d[0] - d[4]) << CONST_BITS;
+        int t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+        int o0 = d[7], o1 = d[5], o2 = d[3], o3 = d[1];
+        int zz1 = o0 + o3, zz2 = o1 + o2, zz3 = o0 + o2, zz4 = o1 + o3;
+        int z5 = (zz3 + zz4) * 9633;               /* FIX_1_175875602 */
+        o0 *= 2446; o1 *= 16819; o2 *= 25172; o3 *= 12299;
+        zz1 *= -7373; zz2 *= -20995; zz3 *= -16069; zz4 *= -3196;
+        zz3 += z5; zz4 += z5;
+        o0 += zz1 + zz3; o1 += zz2 + zz4; o2 += zz2 + zz3; o3 += zz1 + zz4;
+        ws[0 * 8 + c] = DESCALE(t10 + o3, CONST_BITS - PASS1_BITS);
+        ws[7 * 8 + c] = DESCALE(t10 - o3, CONST_BITS - PASS1_BITS);
+        ws[1 * 8 + c] = DESCALE(t11 + o2, CONST_BITS - PASS1_BITS);
+        ws[6 * 8 + c] = DESCALE(t11 - o2, CONST_BITS - PASS1_BITS);
+        ws[2 * 8 + c] = DESCALE(t12 + o1, CONST_BITS - PASS1_BITS);
+        ws[5 * 8 + c] = DESCALE(t12 - o1, CONST_BITS - PASS1_BITS);
+        ws[3 * 8 + c] = DESCALE(t13 + o0, CONST_BITS - PASS1_BITS);
+        ws[4 * 8 + c] = DESCALE(t13 - o0, CONST_BITS - PASS1_BITS);
+    }
+    for (int r = 0; r < 8; r++) { /* pass 2: rows */
+        const int* d = ws + r * 8;
+        int z2 = d[2], z3 = d[6];
+        int z1 = (z2 + z3) * 4433;
+        int t2 = z1 + z3 * (-15137);
+        int t3 = z1 + z2 * 6270;
+        int t0 = (d[0] + d[4]) << CONST_BITS;
+        int t1 = (d[0] - d[4]) << CONST_BITS;
+        int t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+        int o0 = d[7], o1 = d[5], o2 = d[3], o3 = d[1];
+        int zz1 = o0 + o3, zz2 = o1 + o2, zz3 = o0 + o2, zz4 = o1 + o3;
+        int z5 = (zz3 + zz4) * 9633;
+        o0 *= 2446; o1 *= 16819; o2 *= 25172; o3 *= 12299;
+        zz1 *= -7373; zz2 *= -20995; zz3 *= -16069; zz4 *= -3196;
+        zz3 += z5; zz4 += z5;
+        o0 += zz1 + zz3; o1 += zz2 + zz4; o2 += zz2 + zz3; o3 += zz1 + zz4;
+        const int SH = CONST_BITS + PASS1_BITS + 3;
+        uint8_t* o = out + (size_t)r * ostride;
+        o[0] = idct_limit(DESCALE(t10 + o3, SH));
+        o[7] = idct_limit(DESCALE(t10 - o3, SH));
+        o[1] = idct_limit(DESCALE(t11 + o2, SH));
+        o[6] = idct_limit(DESCALE(t11 - o2, SH));
+        o[2] = idct_limit(DESCALE(t12 + o1, SH));
+        o[5] = idct_limit(DESCALE(t12 - o1, SH));
+        o[3] = idct_limit(DESCALE(t13 + o0, SH));
+        o[4] = idct_limit(DESCALE(t13 - o0, SH));
+    }
+}
+
+/* ------------------------------------------------------------- jdcolor.c */
+static inline uint8_t clamp255(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
+long oracle_jpeg_num_blocks(const uint8_t* jpg, size_t len)
+{
+    jinfo_t J;
+    if (parse(jpg, len, &J)) return -1;
+    int nb = J.ncomp == 3 ? J.hs[0] * J.vs[0] + 2 : 1;
+    return (long)J.mcux * J.mcuy * nb;
+}
+
+int oracle_jpeg_coefs(const uint8_t* jpg, size_t len, int16_t* coefs, size_t nblocks)
+{
+    jinfo_t J;
+    int rc = parse(jpg, len, &J);
+    if (rc) return rc;
+    int nb = J.ncomp == 3 ? J.hs[0] * J.vs[0] + 2 : 1;
+    if ((size_t)J.mcux * J.mcuy * nb > nblocks) return 4;
+    return decode_scan(&J, coefs);
+}
+
+int oracle_jpeg_decode(const uint8_t* jpg, size_t len, int s, uint8_t* out, size_t cap, int* ow,
+                       int* oh, int* ofmt)
+{
+    jinfo_t J;
+    int rc = parse(jpg, len, &J);
+    if (rc) return rc;
+    if (s < 1) return 1;
+    int W = J.w, H = J.h;
+    int dw = (W + s - 1) / s, dh = (H + s - 1) / s;
+    int nch = J.ncomp == 3 ? 3 : 1;
+    *ow = dw;
+    *oh = dh;
+    *ofmt = nch == 3 ? OR_BGR24 : OR_GRAY8;
+    if ((size_t)dw * dh * nch > cap) return 4;
+
+    int nb_mcu = J.ncomp == 3 ? J.hs[0] * J.vs[0] + 2 : 1;
+    long nblk = (long)J.mcux * J.mcuy * nb_mcu;
+    int16_t* coefs = (int16_t*)malloc((size_t)nblk * 64 * sizeof(int16_t));
+    if (!coefs) return 2;
+    rc = decode_scan(&J, coefs);
+    if (rc) {
+        free(coefs);
+        return rc;
+    }
+    /* component sample planes: width_in_blocks*8 x height_in_blocks*8; the
+     * real part is downsampled_width x downsampled_height (jdmaster.c) */
+    int cw[3], ch[3], pw[3], ph[3];
+    uint8_t* plane[3] = {0, 0, 0};
+    for (int c = 0; c < J.ncomp; c++) {
+        cw[c] = (W * J.hs[c] + J.hmax - 1) / J.hmax;
+        ch[c] = (H * J.vs[c] + J.vmax - 1) / J.vmax;
+        pw[c] = (cw[c] + 7) / 8 * 8;
+        ph[c] = (ch[c] + 7) / 8 * 8;
+        plane[c] = (uint8_t*)malloc((size_t)pw[c] * ph[c]);
+    }
+    /* IDCT of the real blocks of every MCU (jdcoefct.c decompress_onepass) */
+    const int16_t* blk = coefs;
+    for (int my = 0; my < J.mcuy; my++)
+        for (int mx = 0; mx < J.mcux; mx++)
+            for (int c = 0; c < J.ncomp; c++)
+                for (int by = 0; by < J.vs[c]; by++)
+                    for (int bx = 0; bx < J.hs[c]; bx++, blk += 64) {
+                        int X = (mx * J.hs[c] + bx) * 8, Y = (my * J.vs[c] + by) * 8;
+                        if (X >= pw[c] || Y >= ph[c]) continue; /* dummy block */
+                        idct_islow(blk, J.qt[J.tq[c]], plane[c] + (size_t)Y * pw[c] + X, pw[c]);
+                    }
+    free(coefs);
+
+    if (nch == 1) {
+        for (int y = 0; y < dh; y++)
+            for (int x = 0; x < dw; x++) out[(size_t)y * dw + x] = plane[0][(size_t)(y * s) * pw[0] + x * s];
+        free(plane[0]);
+        return 0;
+    }
+    /* upsample Cb/Cr to full width/height rows (jdsample.c), then convert */
+    int hx = J.hmax, vy = J.vmax;
+    int fancy = cw[1] > 2; /* do_fancy && downsampled_width > 2 */
+    int fullw = cw[1] * hx;
+    int* up[2];
+    up[0] = (int*)malloc(sizeof(int) * (size_t)fullw * 2);
+    up[1] = up[0] + fullw;
+    for (int y = 0; y < dh; y++) {
+        int Y = y * s; /* full-resolution output row */
+        for (int k = 0; k < 2; k++) {
+            const uint8_t* P = plane[1 + k];
+            int stride = pw[1 + k];
+            int* o = up[k];
+            int r0 = vy == 2 ? Y >> 1 : Y;
+            if (hx == 1 && vy == 1) {
+                for (int x = 0; x < cw[1]; x++) o[x] = P[(size_t)r0 * stride + x];
+            } else if (!fancy) { /* h2v1_upsample / h2v2_upsample: replication */
+                for (int x = 0; x < fullw; x++) o[x] = P[(size_t)r0 * stride + x / 2];
+            } else if (vy == 1) { /* h2v1_fancy_upsample */
+                const uint8_t* in = P + (size_t)r0 * stride;
+                int n = cw[1];
+                o[0] = in[0];
+                o[1] = (in[0] * 3 + in[1] + 2) >> 2;
+                for (int i = 1; i < n - 1; i++) {
+                    o[2 * i] = (in[i] * 3 + in[i - 1] + 1) >> 2;
+                    o[2 * i + 1] = (in[i] * 3 + in[i + 1] + 2) >> 2;
+                }
+                o[2 * n - 2] = (in[n - 1] * 3 + in[n - 2] + 1) >> 2;
+                o[2 * n - 1] = in[n - 1];
+            } else { /* h2v2_fancy_upsample with replicated context rows */
+                int rn = (Y & 1) ? r0 + 1 : r0 - 1;
+                if (rn < 0) rn = 0;
+                if (rn > ch[1] - 1) rn = ch[1] - 1;
+                const uint8_t* a = P + (size_t)r0 * stride;
+                const uint8_t* b = P + (size_t)rn * stride;
+                int n = cw[1];
+                int cs0 = a[0] * 3 + b[0], cs1 = a[1] * 3 + b[1];
+                o[0] = (cs0 * 4 + 8) >> 4;
+                o[1] = (cs0 * 3 + cs1 + 7) >> 4;
+                int last = cs0, cur = cs1;
+                for (int i = 1; i < n - 1; i++) {
+                    int nxt = a[i + 1] * 3 + b[i + 1];
+                    o[2 * i] = (cur * 3 + last + 8) >> 4;
+                    o[2 * i + 1] = (cur * 3 + nxt + 7) >> 4;
+                    last = cur;
+                    cur = nxt;
+                }
+                o[2 * n - 2] = (cur * 3 + last + 8) >> 4;
+                o[2 * n - 1] = (cur * 4 + 7) >> 4;
+            }
+        }
+        const uint8_t* yrow = plane[0] + (size_t)Y * pw[0];
+        uint8_t* orow = out + (size_t)y * dw * 3;
+        for (int x = 0; x < dw; x++) {
+            int X = x * s;
+            int yy = yrow[X], cb = up[0][X] - 128, cr = up[1][X] - 128;
+            /* ycc_rgb_convert: FIX(x) = (int)(x * 65536 + 0.5), ONE_HALF = 1 << 15 */
+            int rr = yy + ((91881 * cr + 32768) >> 16);
+            int gg = yy + ((-22554 * cb + 32768 - 46802 * cr) >> 16);
+            int bb = yy + ((116130 * cb + 32768) >> 16);
+            orow[3 * x + 0] = clamp255(bb);
+            orow[3 * x + 1] = clamp255(gg);
+            orow[3 * x + 2] = clamp255(rr);
+        }
+    }
+    free(up[0]);
+    for (int c = 0; c < 3; c++) free(plane[c]);
+    return 0;
+}

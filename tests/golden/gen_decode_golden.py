@@ -1,0 +1,121 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures for the JPEG decode row (A11).
+
+Test infrastructure only.  Run once in the build container; the output
+(decode_golden.npz, decode_golden.json) is committed and the GPU box never
+runs this script.
+
+The reference decodes through javax.imageio's JPEGImageReader, i.e. the JDK's
+bundled IJG libjpeg 6b (ImageCompression.java:113-155): ISLOW IDCT, fancy
+(triangle) upsampling, ycc_rgb_convert, then keeps pixels (x*s, y*s).  No JDK
+exists here; the independent pin is libjpeg-turbo 3.1.4 (6b API
+level, bundled in Pillow 12.2), whose decoder is of the same lineage
+ for every sampling layout covered here.  4:4:0 (h1v2) is left
+out on purpose: libjpeg-turbo upsamples it with a triangle filter where 6b
+replicates rows, so it cannot pin the JDK there.
+
+Inputs are synthetic (seeded), encoded by Pillow at several qualities,
+chroma layouts and restart intervals, plus a progressive file that the
+decoder must refuse (the device path is baseline-only; the JDK reads it).
+"""
+import io
+import json
+import os
+
+import numpy as np
+from PIL import Image, features
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def smooth(h, w, seed):
+    rng = np.random.default_rng(seed)
+    fx, fy, ph = rng.uniform(0.02, 0.2, 3)
+    y = np.arange(h, dtype=np.float32)[:, None]
+    x = np.arange(w, dtype=np.float32)[None, :]
+    r = 127 + 100 * np.sin(x * fx + ph) + 0 * y
+    g = 127 + 100 * np.sin(y * fy + 2 * ph) + 0 * x
+    b = 127 + 100 * np.sin((x + y) * fx / 2)
+    rgb = np.stack([r, g, b], -1) + rng.normal(0, 12, (h, w, 3)).astype(np.float32)
+    return np.clip(np.rint(rgb), 0, 255).astype(np.uint8)
+
+
+def noise(h, w, seed):
+    return np.random.default_rng(seed).integers(0, 256, (h, w, 3), dtype=np.uint8)
+
+
+def encode(rgb, **kw):
+    buf = io.BytesIO()
+    mode = "L" if rgb.ndim == 2 else "RGB"
+    Image.fromarray(rgb, mode).save(buf, "JPEG", **kw)
+    return buf.getvalue()
+
+
+def decode_bgr(data):
+    im = Image.open(io.BytesIO(data))
+    im.load()
+    a = np.asarray(im)
+    if a.ndim == 3:
+        a = a[:, :, ::-1]  # TYPE_3BYTE_BGR
+    return np.ascontiguousarray(a)
+
+
+def main():
+    cases = []
+    sizes = [(1, 1), (2, 2), (3, 5), (5, 3), (4, 6), (7, 9), (16, 16), (17, 33), (33, 17), (48, 64),
+             (47, 61), (66, 130), (130, 250)]
+    seed = 0
+    for (h, w) in sizes:
+        for sub in (2, 1, 0):
+            for q in (50, 95):
+                seed += 1
+                img = smooth(h, w, seed) if seed % 3 else noise(h, w, seed)
+                cases.append((f"c{h}x{w}_s{sub}_q{q}", img, dict(quality=q, subsampling=sub)))
+        seed += 1
+        g = smooth(h, w, seed)[:, :, 1]
+        cases.append((f"g{h}x{w}_q90", g, dict(quality=90)))
+    # restart intervals (DRI), including one MCU per interval
+    for (h, w), rb in [((48, 64), 1), ((66, 130), 3), ((130, 250), 7), ((17, 33), 2)]:
+        seed += 1
+        cases.append((f"rst{rb}_{h}x{w}", smooth(h, w, seed), dict(quality=85, subsampling=2,
+                                                                    restart_marker_blocks=rb)))
+        seed += 1
+        cases.append((f"rst{rb}_{h}x{w}_444", noise(h, w, seed), dict(quality=75, subsampling=0,
+                                                                       restart_marker_blocks=rb)))
+    seed += 1
+    cases.append(("rstrows_130x250", smooth(130, 250, seed), dict(quality=90, subsampling=2,
+                                                                   restart_marker_rows=1)))
+    seed += 1
+    cases.append(("grey_rst_66x130", smooth(66, 130, seed)[:, :, 0], dict(quality=70,
+                                                                        restart_marker_blocks=5)))
+    # extreme qualities: q=100 (all-ones tables, long AC codes), q=1
+    seed += 1
+    cases.append(("q100_noise_40x72", noise(40, 72, seed), dict(quality=100, subsampling=2)))
+    seed += 1
+    cases.append(("q1_smooth_40x72", smooth(40, 72, seed), dict(quality=1, subsampling=2)))
+
+    jpegs, expect, meta = {}, {}, {"libjpeg_turbo": features.version("libjpeg_turbo"),
+                                    "pillow": Image.__version__, "cases": {}}
+    for name, img, kw in cases:
+        data = encode(img, **kw)
+        out = decode_bgr(data)
+        jpegs[name] = np.frombuffer(data, np.uint8)
+        expect[name] = out
+        meta["cases"][name] = {"w": int(out.shape[1]), "h": int(out.shape[0]),
+                               "ncomp": 1 if out.ndim == 2 else 3, "params": kw, "bytes": len(data)}
+    # progressive: refused by the baseline decoder (status 5)
+    seed += 1
+    prog = encode(smooth(32, 48, seed), quality=80, progressive=True)
+    jpegs["progressive_32x48"] = np.frombuffer(prog, np.uint8)
+    meta["cases"]["progressive_32x48"] = {"w": 48, "h": 32, "ncomp": 3, "unsupported": True,
+                                          "params": {"progressive": True}, "bytes": len(prog)}
+    np.savez_compressed(os.path.join(HERE, "decode_golden.npz"),
+                        **{f"jpg:{k}": v for k, v in jpegs.items()},
+                        **{f"px:{k}": v for k, v in expect.items()})
+    with open(os.path.join(HERE, "decode_golden.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print(len(jpegs), "cases")
+
+
+if __name__ == "__main__":
+    main()

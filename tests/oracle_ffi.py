@@ -15,8 +15,8 @@ FMT = {"bgr": 0, "rgb": 1, "gray": 2}
 
 def build_oracle():
     lib = os.path.join(ORACLE_DIR, "liboracle.so")
-    src = os.path.join(ORACLE_DIR, "icx_oracle.c")
-    if not os.path.exists(lib) or os.path.getmtime(lib) < os.path.getmtime(src):
+    srcs = [os.path.join(ORACLE_DIR, f) for f in ("icx_oracle.c", "icx_oracle_decode.c", "icx_oracle.h")]
+    if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
     return lib
 
@@ -52,6 +52,12 @@ class Oracle:
         L.oracle_fit_batch.argtypes = [c.c_int, P(c.c_void_p), P(c.c_int), P(c.c_int), P(c.c_int), c.c_int,
                                        c.c_int64, c.c_float, c.c_int, c.c_float, c.c_double, c.c_int,
                                        P(c.c_int64), P(c.c_float), P(c.c_double)]
+        L.oracle_jpeg_info.argtypes = [c.c_void_p, c.c_size_t, P(c.c_int), P(c.c_int), P(c.c_int)]
+        L.oracle_jpeg_num_blocks.restype = c.c_long
+        L.oracle_jpeg_num_blocks.argtypes = [c.c_void_p, c.c_size_t]
+        L.oracle_jpeg_coefs.argtypes = [c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t]
+        L.oracle_jpeg_decode.argtypes = [c.c_void_p, c.c_size_t, c.c_int, c.c_void_p, c.c_size_t, P(c.c_int),
+                                         P(c.c_int), P(c.c_int)]
         self.L = L
 
     def encode(self, img, q):
@@ -122,6 +128,38 @@ class Oracle:
                 "quality": bq.value if rc == 1 else None, "scale": bs.value if rc == 1 else None,
                 "encodes": enc.value, "cache_hit": bool(hit.value)}
 
+    def jpeg_info(self, data):
+        data = np.frombuffer(bytes(data), np.uint8)
+        w, h, n = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        rc = self.L.oracle_jpeg_info(data.ctypes.data, data.size, ctypes.byref(w), ctypes.byref(h),
+                                     ctypes.byref(n))
+        return rc, w.value, h.value, n.value
+
+    def jpeg_coefs(self, data):
+        """Quantised coefficients (natural order) per scan block; None if refused."""
+        data = np.frombuffer(bytes(data), np.uint8)
+        nb = self.L.oracle_jpeg_num_blocks(data.ctypes.data, data.size)
+        if nb < 0:
+            return None
+        out = np.empty((nb, 64), np.int16)
+        rc = self.L.oracle_jpeg_coefs(data.ctypes.data, data.size, out.ctypes.data, nb)
+        return out if rc == 0 else None
+
+    def jpeg_decode(self, data, s=1):
+        """(status, pixels): BGR (H, W, 3) or grey (H, W) after source subsampling s."""
+        data = np.frombuffer(bytes(data), np.uint8)
+        rc, w, h, n = self.jpeg_info(data)
+        if rc:
+            return rc, None
+        dw, dh = -(-w // s), -(-h // s)
+        out = np.empty(dw * dh * n, np.uint8)
+        ow, oh, of = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        rc = self.L.oracle_jpeg_decode(data.ctypes.data, data.size, s, out.ctypes.data, out.size,
+                                       ctypes.byref(ow), ctypes.byref(oh), ctypes.byref(of))
+        if rc:
+            return rc, None
+        return 0, out.reshape((oh.value, ow.value, 3) if n == 3 else (oh.value, ow.value))
+
     def subsampling(self, w, h):
         return self.L.oracle_subsampling(w, h)
 
@@ -152,6 +190,14 @@ def load_golden():
     inputs = dict(np.load(os.path.join(GOLDEN_DIR, "inputs.npz")))
     jpegs = dict(np.load(os.path.join(GOLDEN_DIR, "jpeg_golden.npz")))
     return meta, inputs, jpegs
+
+
+def load_decode_golden():
+    meta = json.load(open(os.path.join(GOLDEN_DIR, "decode_golden.json")))
+    z = np.load(os.path.join(GOLDEN_DIR, "decode_golden.npz"))
+    jpgs = {k[4:]: z[k].tobytes() for k in z.files if k.startswith("jpg:")}
+    pxs = {k[3:]: z[k] for k in z.files if k.startswith("px:")}
+    return meta, jpgs, pxs
 
 
 def jdk_bytes(turbo_bytes, meta):
