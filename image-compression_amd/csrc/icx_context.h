@@ -1,0 +1,190 @@
+// icx_context.h — per-context state shared by the encode and decode drivers
+// (one HIP stream, device workspace arena, pinned staging arena, per-kernel
+// HIP-event timing) and the small helpers around it.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/icx.h"
+
+namespace icx {
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// ------------------------------------------------------------ arenas
+struct DevArena {
+    uint8_t* base = nullptr;
+    size_t cap = 0, used = 0;
+    hipError_t reserve(size_t bytes)
+    {
+        if (bytes <= cap) return hipSuccess;
+        if (base) hipFree(base);
+        base = nullptr;
+        cap = 0;
+        size_t want = std::max(bytes, cap * 3 / 2);
+        hipError_t e = hipMalloc(&base, want);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            e = hipMalloc(&base, bytes);
+            if (e != hipSuccess) return e;
+            want = bytes;
+        }
+        cap = want;
+        return hipSuccess;
+    }
+    void* take(size_t n)
+    {
+        used = align_up(used, 256);
+        void* p = base + used;
+        used += n;
+        return p;
+    }
+    ~DevArena() { if (base) hipFree(base); }
+};
+
+struct HostArena {
+    uint8_t* base = nullptr;
+    size_t cap = 0, used = 0;
+    hipError_t reserve(size_t bytes)
+    {
+        if (bytes <= cap) return hipSuccess;
+        if (base) hipHostFree(base);
+        base = nullptr;
+        size_t want = std::max(bytes, cap * 2);
+        hipError_t e = hipHostMalloc((void**)&base, want, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        cap = want;
+        return hipSuccess;
+    }
+    void* take(size_t n)
+    {
+        used = align_up(used, 64);
+        if (used + n > cap) return nullptr;
+        void* p = base + used;
+        used += n;
+        return p;
+    }
+    ~HostArena() { if (base) hipHostFree(base); }
+};
+
+struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+    int64_t units;
+};
+
+struct KStat {
+    int64_t launches = 0, units = 0;
+    double ms = 0;
+};
+
+
+inline bool is_device_ptr(const void* p)
+{
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+
+}  // namespace icx
+
+// ============================================================ context
+struct icx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::recursive_mutex mu;
+    std::string err;
+    icx::DevArena dev;
+    icx::HostArena host;
+    bool prof = false;
+    std::vector<icx::Pending> pending;
+    std::vector<hipEvent_t> evpool;
+    std::map<std::string, icx::KStat> stats;
+    size_t budget = 0;  // device workspace budget per sub-batch
+};
+
+namespace icx {
+
+inline icx_status fail(icx_ctx* c, icx_status s, const char* msg)
+{
+    if (c) c->err = msg;
+    return s;
+}
+
+inline icx_status hip_fail(icx_ctx* c, hipError_t e, const char* where)
+{
+    if (c) c->err = std::string(where) + ": " + hipGetErrorString(e);
+    (void)hipGetLastError();
+    return e == hipErrorOutOfMemory ? ICX_E_NOMEM : ICX_E_DEVICE;
+}
+
+inline hipEvent_t get_event(icx_ctx* c)
+{
+    if (!c->evpool.empty()) {
+        hipEvent_t e = c->evpool.back();
+        c->evpool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+}
+
+struct Timed {  // brackets one launch with events when profiling is on
+    icx_ctx* c;
+    Pending p;
+    bool on;
+    Timed(icx_ctx* ctx, const char* name, int64_t units) : c(ctx), on(ctx->prof)
+    {
+        if (!on) return;
+        p.name = name;
+        p.units = units;
+        p.a = get_event(c);
+        p.b = get_event(c);
+        hipEventRecord(p.a, c->stream);
+    }
+    ~Timed()
+    {
+        if (!on) return;
+        hipEventRecord(p.b, c->stream);
+        c->pending.push_back(p);
+    }
+};
+
+inline void resolve_profile(icx_ctx* c)  // call after a stream synchronisation
+{
+    for (auto& p : c->pending) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, p.a, p.b);
+        KStat& s = c->stats[p.name];
+        s.launches++;
+        s.ms += ms;
+        s.units += p.units;
+        c->evpool.push_back(p.a);
+        c->evpool.push_back(p.b);
+    }
+    c->pending.clear();
+}
+
+inline icx_status upload(icx_ctx* c, void* dst, const void* src, size_t n)
+{
+    void* h = c->host.take(n);
+    if (!h) return fail(c, ICX_E_NOMEM, "pinned staging exhausted");
+    memcpy(h, src, n);
+    hipError_t e = hipMemcpyAsync(dst, h, n, hipMemcpyHostToDevice, c->stream);
+    return e == hipSuccess ? ICX_OK : hip_fail(c, e, "hipMemcpyAsync(H2D)");
+}
+
+}  // namespace icx

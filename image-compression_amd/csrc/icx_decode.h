@@ -1,0 +1,278 @@
+// icx_decode.h — data structures and the entropy-decoding state machine of
+// the device JPEG decoder (row A11 of SURVEY.md §8a).
+//
+// Replaces the JDK JPEGImageReader decode reached from
+// ImageCompression.decodeImageWithSubsampling (core/ImageCompression.java:
+// 107-165); the arithmetic is IJG libjpeg 6b's baseline decompression, the
+// same algorithm oracle/icx_oracle_decode.c restates on the CPU.
+//
+// Parallel Huffman decoding without restart markers uses self-synchronisation
+// (a Huffman decoder started at an arbitrary bit soon falls onto the true
+// symbol boundaries): the unstuffed entropy stream of an image is cut into
+// subsequences of DEC_SUB_BITS bits, one per thread.  A decoder state is
+// (bit position, block-in-MCU, zig-zag index) at a symbol boundary;
+// walk(E[j], subsequence j) gives the state at which the decode leaves
+// subsequence j.  The entry states E[] are the fixed point of
+// E[j+1] = walk(E[j]) from the known E[0]; the sync kernel iterates it with
+// dirty flags (only threads whose entry changed re-walk), which settles in two
+// or three launches because wrong starts resynchronise within a subsequence.
+// Restart intervals need no special case: every RSTn marker is replaced by
+// DEC_PAD bytes of 0xFF, and an all-ones look-ahead is never a valid JPEG code
+// (T.81 C.2 forbids all-ones codes), so the decode of an interval ends with an
+// invalid code whose only transition is a jump to the next interval start.
+// A decoder started at a wrong state also meets invalid codes mid-interval
+// (e.g. nine 1-bits where a luma DC code is due); there it resumes one bit
+// later instead of ending, so wrong paths keep resynchronising rather than
+// collapsing into the end state.  The true path of a valid stream never meets
+// an invalid code more than 7 bits before its interval's end.
+//
+// Everything here is __host__ __device__ so tests/dec_emu.cpp can run the same
+// state machine serially on the CPU.
+#pragma once
+#include <stdint.h>
+
+#ifdef __HIPCC__
+#include <hip/hip_runtime.h>
+#define ICX_HD __host__ __device__ __forceinline__
+#else
+#define ICX_HD inline
+#endif
+
+namespace icx {
+
+constexpr int DEC_SUB_BITS = 1024;   // bits per subsequence (one thread)
+constexpr int DEC_LUT_BITS = 10;     // Huffman fast-lookup width
+constexpr int DEC_TILE = 4096;       // stuffed bytes per unstuff workgroup (256 x 16)
+constexpr int DEC_PAD = 8;           // 0xFF bytes standing in for each RSTn marker
+constexpr int DEC_TAIL = 16;         // 0xFF bytes after the last interval
+constexpr uint32_t DEC_END = 0xFFFFFFFFu;
+
+// One Huffman table prepared for decoding (jdhuff.c jpeg_make_d_derived_tbl):
+// lut[peek >> (16 - DEC_LUT_BITS)] = (symbol << 8) | code length for codes of at
+// most DEC_LUT_BITS bits, 0 otherwise; longer codes use maxcode/valoff.
+struct DecHuff {
+    uint16_t lut[1 << DEC_LUT_BITS];
+    int32_t maxcode[17];   // largest code of length l, -1 if none
+    int32_t valoff[17];    // index into vals of code c of length l: valoff[l] + c
+    uint8_t vals[256];
+};
+
+// Per-image tables: h[2*c] = DC table of component c, h[2*c+1] = AC table.
+struct DecTab {
+    DecHuff h[6];
+    uint16_t qt[3][64];    // dequantisation tables, natural order, per component
+};
+
+// Per-image descriptor (host-built, read-only on the device).
+struct DecDesc {
+    const uint8_t* scan;   // entropy-coded segment (stuffed), device
+    int64_t scan_len;
+    uint8_t* ent;          // unstuffed stream + pads, 4-byte aligned
+    int64_t ent_cap;       // bytes allocated for ent
+    uint32_t* tile_cnt;    // per unstuff tile: output bytes, then exclusive offsets
+    uint32_t* tile_rst;    // per unstuff tile: RSTn markers, then exclusive offsets
+    uint32_t* seg;         // interval start byte offsets in ent (nseg_max entries)
+    uint64_t* est;         // entry state per subsequence (nsub_max + 1)
+    uint8_t* dirty[2];
+    uint32_t* ncnt;        // blocks completed inside each subsequence
+    uint32_t* boff;        // blocks completed before each subsequence
+    int16_t* coefs;        // nblocks x 64, natural order, quantised (AC only)
+    int32_t* dc;           // nblocks: DC differences, then DC values
+    uint8_t* plane[3];     // IDCT output planes (pitch pw[c])
+    uint8_t* out;          // BGR24 / GRAY8 rows, stride ostride
+    const DecTab* tab;
+    int64_t nblocks;
+    int32_t ntiles, nsub_max, nseg_max;
+    int32_t w, h, ncomp, hs, vs, nby, nbmcu, mcux, mcuy, ri;
+    int32_t pw[3], ph[3], cw[3], ch[3];
+    int32_t fancy;         // chroma upsampled with the triangle filter (cw > 2)
+    int32_t s, ow, oh, ostride;
+};
+
+// Device-written per-image results.
+struct DecState {
+    int64_t end;           // stuffed offset of the terminating marker (or scan_len)
+    uint32_t ent_len;      // unstuffed bytes incl. pads
+    uint32_t nseg;         // intervals found (RSTn markers + 1)
+    uint32_t nsub;         // subsequences in use
+    uint32_t total_blocks; // blocks the entropy decode produced
+    int32_t status;        // 0 ok, 6 corrupt
+    int32_t pad;
+};
+
+ICX_HD uint64_t dec_pack(uint32_t pos, int b, int z) { return ((uint64_t)pos << 16) | ((uint64_t)b << 8) | (uint64_t)z; }
+ICX_HD uint32_t dec_pos(uint64_t st) { return (uint32_t)(st >> 16); }
+
+ICX_HD uint32_t dec_be32(uint32_t v)
+{
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__GNUC__)
+    return __builtin_bswap32(v);
+#else
+    return (v >> 24) | ((v >> 8) & 0xFF00u) | ((v << 8) & 0xFF0000u) | (v << 24);
+#endif
+}
+
+struct DecReader {
+    const uint32_t* w;
+    uint64_t buf;
+    int avail;
+    uint32_t wi;
+    ICX_HD void init(const uint32_t* words, uint32_t pos)
+    {
+        w = words;
+        wi = pos >> 5;
+        buf = ((uint64_t)dec_be32(w[wi]) << 32) | dec_be32(w[wi + 1]);
+        wi += 2;
+        buf <<= (pos & 31);
+        avail = 64 - (int)(pos & 31);
+    }
+    ICX_HD void refill()
+    {
+        if (avail < 32) {
+            buf |= (uint64_t)dec_be32(w[wi++]) << (32 - avail);
+            avail += 32;
+        }
+    }
+    ICX_HD uint32_t peek16() const { return (uint32_t)(buf >> 48); }
+    ICX_HD void skip(int n)
+    {
+        buf <<= n;
+        avail -= n;
+    }
+    ICX_HD int get(int n)  // 0 <= n <= 16
+    {
+        const int v = n ? (int)(buf >> (64 - n)) : 0;
+        buf <<= n;
+        avail -= n;
+        return v;
+    }
+};
+
+// HUFF_EXTEND (jdhuff.c)
+ICX_HD int dec_extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
+
+// Decode one symbol; returns (symbol << 8) | length, 0 if no valid code.
+ICX_HD uint32_t dec_symbol(const DecHuff* t, uint32_t pk)
+{
+    const uint32_t e = t->lut[pk >> (16 - DEC_LUT_BITS)];
+    if (e) return e;
+    for (int l = DEC_LUT_BITS + 1; l <= 16; l++) {
+        const int code = (int)(pk >> (16 - l));
+        if (code <= t->maxcode[l]) return ((uint32_t)t->vals[(t->valoff[l] + code) & 255] << 8) | (uint32_t)l;
+    }
+    return 0;
+}
+
+// zig-zag index -> natural index with jpeg_natural_order's tail (k > 63 -> 63)
+ICX_HD int dec_nat(int z)
+{
+    constexpr uint8_t N[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                               12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                               35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                               58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+    return N[z > 63 ? 63 : z];
+}
+
+// First interval start strictly after byte `byte` (DEC_END if none).
+ICX_HD uint32_t dec_next_seg(const uint32_t* seg, uint32_t nseg, uint32_t byte)
+{
+    uint32_t lo = 0, hi = nseg;  // find first k with seg[k] > byte
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (seg[mid] > byte) hi = mid; else lo = mid + 1;
+    }
+    return lo < nseg ? seg[lo] : DEC_END;
+}
+
+// Decode from state st until the first symbol boundary at or beyond `stop`
+// (jdhuff.c decode_mcu, symbol by symbol).  Returns the exit state; nblk =
+// blocks completed on the way.  WRITE: store AC coefficients (natural order)
+// and DC differences of block blk_base + (blocks completed so far).
+template <bool WRITE, class HuffPtr>
+ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const uint32_t* words, const uint32_t* seg, uint32_t nseg,
+                         uint32_t ent_bits, uint64_t st, uint32_t stop, uint32_t& nblk, int64_t blk_base)
+{
+    uint32_t pos = dec_pos(st);
+    nblk = 0;
+    if (pos >= stop) return st;
+    int b = (int)((st >> 8) & 7), z = (int)(st & 63);
+    DecReader R;
+    R.init(words, pos);
+    int comp = b < d.nby ? 0 : b - d.nby + 1;
+    uint32_t n = 0;
+    while (pos < stop) {
+        R.refill();
+        const uint32_t e = dec_symbol(&H[2 * comp + (z ? 1 : 0)], R.peek16());
+        const int len = (int)(e & 31), sym = (int)(e >> 8);
+        if (len == 0 || (z == 0 && sym > 11)) {  // no valid code here
+            const uint32_t nx = dec_next_seg(seg, nseg, pos >> 3);
+            const uint32_t bound = nx == DEC_END ? ent_bits : (nx - DEC_PAD) * 8;  // end of interval data
+            b = 0;
+            z = 0;
+            comp = 0;
+            if (pos + 8 < bound) {  // mid-interval: only a wrong-start path gets here; resume a bit later
+                pos++;
+                R.init(words, pos);
+                continue;
+            }
+            // the interval's 1-bit padding (< 8 bits) or its pad bytes: next interval
+            if (nx == DEC_END) {
+                pos = DEC_END;
+                break;
+            }
+            pos = nx * 8;
+            R.init(words, pos);
+            continue;
+        }
+        R.skip(len);
+        if (z == 0) {
+            const int v = R.get(sym);
+            pos += (uint32_t)(len + sym);
+            if (WRITE) {
+                const int64_t bi = blk_base + n;
+                if (bi < d.nblocks) d.dc[bi] = sym ? dec_extend(v, sym) : 0;
+            }
+            z = 1;
+        } else {
+            const int r = sym >> 4, s = sym & 15;
+            if (s) {
+                z += r;
+                const int v = R.get(s);
+                pos += (uint32_t)(len + s);
+                if (WRITE) {
+                    const int64_t bi = blk_base + n;
+                    if (bi < d.nblocks) d.coefs[bi * 64 + dec_nat(z)] = (int16_t)dec_extend(v, s);
+                }
+                z++;
+            } else {
+                pos += (uint32_t)len;
+                z = (r == 15) ? z + 16 : 64;
+            }
+        }
+        if (z >= 64) {
+            n++;
+            z = 0;
+            b = (b + 1 == d.nbmcu) ? 0 : b + 1;
+            comp = b < d.nby ? 0 : b - d.nby + 1;
+        }
+    }
+    nblk = n;
+    return dec_pack(pos, b, z);
+}
+
+// Unstuffing rule for stuffed byte i (jdhuff.c fill_bit_buffer / jdmarker.c):
+// returns output bytes it contributes (0, 1, or DEC_PAD for an RSTn code byte);
+// *rst = 1 for an RSTn code byte.
+ICX_HD int dec_unstuff_rule(int prev, int cur, int next, int* rst)
+{
+    *rst = 0;
+    if (prev == 0xFF && cur == 0x00) return 0;                 // stuffed zero
+    if (cur == 0xFF) return next == 0x00 ? 1 : 0;              // data 0xFF / marker prefix / fill
+    if (prev == 0xFF && cur >= 0xD0 && cur <= 0xD7) {          // RSTn code
+        *rst = 1;
+        return DEC_PAD;
+    }
+    return 1;
+}
+
+}  // namespace icx

@@ -1,0 +1,584 @@
+// icx_decode.hip — CDNA4 (gfx950) kernels of the device JPEG decoder (row A11:
+// the JDK JPEGImageReader decode behind ImageCompression.decodeImageWithSubsampling,
+// core/ImageCompression.java:107-165; IJG 6b arithmetic, see
+// oracle/icx_oracle_decode.c for the CPU statement of the same algorithm).
+//
+// Kernel map (per sub-batch of images, all launched on the context's stream):
+//   k_unstuff_end      first terminating marker of each entropy segment
+//   k_unstuff_count    per 4 KiB tile: unstuffed bytes (RSTn -> DEC_PAD bytes)
+//   k_unstuff_scan     per image: tile offsets, stream length, tail pad
+//   k_unstuff_scatter  compact the stream, record restart-interval starts
+//   k_dec_init         guessed entry state of every subsequence
+//   k_dec_sync         one relaxation step of E[j+1] = walk(E[j]) (icx_decode.h)
+//   k_dec_offsets      per image: blocks before each subsequence, block count check
+//   k_dec_write        decode again from the settled states, store coefficients
+//   k_dec_dc           per image: DC prediction (segmented per restart interval)
+//   k_dec_idct         jpeg_idct_islow of every real block into component planes
+//   k_dec_color        fancy upsampling + ycc_rgb_convert + source subsampling
+// Byte/bit-serial integer work; no MFMA.  The entropy stages are bound by the
+// dependent table look-ups of the bit-serial walk, the pixel stages by HBM.
+#include <hip/hip_runtime.h>
+
+#include "icx_decode.h"
+#include "icx_decode_kernels.h"
+
+namespace icx {
+
+namespace {
+
+__device__ __forceinline__ int slot_of(const int64_t* prefix, int m, int64_t item)
+{
+    int lo = 0, hi = m;  // prefix[lo] <= item < prefix[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (prefix[mid] <= item) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// Block-wide exclusive scan of one uint32 per thread (blockDim.x == NT).
+template <int NT>
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint32_t& total)
+{
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[w] = x;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t acc = 0;
+        for (int i = 0; i < NT / 64; i++) {
+            const uint32_t s = sh[i];
+            sh[i] = acc;
+            acc += s;
+        }
+        sh[NT / 64] = acc;
+    }
+    __syncthreads();
+    total = sh[NT / 64];
+    const uint32_t r = x - v + sh[w];
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ bool is_rst(int c) { return c >= 0xD0 && c <= 0xD7; }
+
+// 16 stuffed bytes of thread t of tile `tile` (zero beyond scan_len) plus neighbours.
+struct Bytes16 {
+    uint8_t b[16];
+    int prev, next;
+};
+__device__ __forceinline__ void load16(const DecDesc& d, int64_t base, Bytes16& B)
+{
+    const uint4 v = *(const uint4*)(d.scan + base);  // scan copy is 16-B aligned and padded
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 16; k++) B.b[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    B.prev = base > 0 ? d.scan[base - 1] : 0;
+    B.next = d.scan[base + 16];
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ unstuff
+__global__ void __launch_bounds__(256) k_unstuff_end(const DecDesc* D, DecState* S, Plan p)
+{
+    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    const int img = p.ids[slot];
+    const DecDesc& d = D[img];
+    const int64_t base = (blockIdx.x - p.prefix[slot]) * (int64_t)DEC_TILE + threadIdx.x * 16;
+    if (base >= d.scan_len) return;
+    Bytes16 B;
+    load16(d, base, B);
+    for (int k = 0; k < 16; k++) {
+        const int64_t i = base + k;
+        const int nx = k < 15 ? B.b[k + 1] : B.next;
+        if (i + 1 < d.scan_len && B.b[k] == 0xFF && nx != 0x00 && nx != 0xFF && !is_rst(nx)) {
+            atomicMin((unsigned long long*)&S[img].end, (unsigned long long)i);
+            return;
+        }
+    }
+}
+
+// Output bytes / RSTn markers of thread t's 16 stuffed bytes below `end`.
+__device__ __forceinline__ void unstuff_counts(const Bytes16& B, int64_t base, int64_t end, uint32_t& nb, uint32_t& nr)
+{
+    nb = nr = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        if (base + k >= end) break;
+        int rst;
+        nb += (uint32_t)dec_unstuff_rule(k ? B.b[k - 1] : B.prev, B.b[k], k < 15 ? B.b[k + 1] : B.next, &rst);
+        nr += (uint32_t)rst;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_unstuff_count(const DecDesc* D, const DecState* S, Plan p)
+{
+    __shared__ uint32_t sh[8];
+    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    const int img = p.ids[slot];
+    const DecDesc& d = D[img];
+    const int64_t tile = blockIdx.x - p.prefix[slot];
+    const int64_t base = tile * DEC_TILE + threadIdx.x * 16;
+    uint32_t nb = 0, nr = 0;
+    if (base < S[img].end) {
+        Bytes16 B;
+        load16(d, base, B);
+        unstuff_counts(B, base, S[img].end, nb, nr);
+    }
+    uint32_t tb, tr;
+    block_exscan<256>(nb, sh, tb);
+    block_exscan<256>(nr, sh, tr);
+    if (threadIdx.x == 0) {
+        d.tile_cnt[tile] = tb;
+        d.tile_rst[tile] = tr;
+    }
+}
+
+// One workgroup per image: tile offsets, stream length, subsequence count, tail pad.
+__global__ void __launch_bounds__(1024) k_unstuff_scan(const DecDesc* D, DecState* S, const int32_t* ids,
+                                                       uint32_t sub_bits)
+{
+    __shared__ uint32_t sh[24];
+    const int img = ids[blockIdx.x];
+    const DecDesc& d = D[img];
+    DecState& st = S[img];
+    uint32_t carry_b = 0, carry_r = 0;
+    for (int t0 = 0; t0 < d.ntiles; t0 += 1024) {
+        const int t = t0 + threadIdx.x;
+        const uint32_t b = t < d.ntiles ? d.tile_cnt[t] : 0, r = t < d.ntiles ? d.tile_rst[t] : 0;
+        uint32_t sb, sr;
+        const uint32_t eb = block_exscan<1024>(b, sh, sb);
+        const uint32_t er = block_exscan<1024>(r, sh, sr);
+        if (t < d.ntiles) {
+            d.tile_cnt[t] = carry_b + eb;
+            d.tile_rst[t] = carry_r + er;
+        }
+        carry_b += sb;
+        carry_r += sr;
+    }
+    const uint32_t len = carry_b;
+    const bool fits = (int64_t)len + DEC_TAIL + 8 <= d.ent_cap;  // more RSTn markers than intervals: corrupt
+    if (fits)
+        for (int k = threadIdx.x; k < DEC_TAIL + 8; k += blockDim.x) d.ent[len + k] = 0xFF;
+    if (threadIdx.x == 0) {
+        if (!fits) st.status = 6;
+        st.ent_len = len;
+        st.nseg = carry_r + 1 <= (uint32_t)d.nseg_max ? carry_r + 1 : (uint32_t)d.nseg_max;
+        if (carry_r + 1 > (uint32_t)d.nseg_max) st.status = 6;
+        uint32_t nsub = (uint32_t)(((uint64_t)len * 8 + sub_bits - 1) / sub_bits);
+        if (nsub > (uint32_t)d.nsub_max) {
+            nsub = d.nsub_max;
+            st.status = 6;
+        }
+        st.nsub = nsub;
+        d.seg[0] = 0;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const DecState* S, Plan p)
+{
+    __shared__ uint32_t sh[8];
+    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    const int img = p.ids[slot];
+    const DecDesc& d = D[img];
+    const int64_t tile = blockIdx.x - p.prefix[slot];
+    const int64_t base = tile * DEC_TILE + threadIdx.x * 16;
+    const int64_t end = S[img].end;
+    Bytes16 B;
+    uint32_t nb = 0, nr = 0;
+    if (base < end) {
+        load16(d, base, B);
+        unstuff_counts(B, base, end, nb, nr);
+    }
+    uint32_t tb, tr;
+    uint32_t ob = block_exscan<256>(nb, sh, tb) + d.tile_cnt[tile];
+    uint32_t orr = block_exscan<256>(nr, sh, tr) + d.tile_rst[tile];
+    if (base >= end) return;
+    for (int k = 0; k < 16; k++) {
+        if (base + k >= end) break;
+        int rst;
+        const int n = dec_unstuff_rule(k ? B.b[k - 1] : B.prev, B.b[k], k < 15 ? B.b[k + 1] : B.next, &rst);
+        if (rst) {
+            for (int q = 0; q < DEC_PAD; q++)
+                if (ob + q < d.ent_cap) d.ent[ob + q] = 0xFF;
+            ob += DEC_PAD;
+            if (orr + 1 < (uint32_t)d.nseg_max) d.seg[orr + 1] = ob;
+            orr++;
+        } else if (n) {
+            if (ob < d.ent_cap) d.ent[ob] = B.b[k];
+            ob++;
+        }
+    }
+}
+
+// ------------------------------------------------------------ entropy decode
+__global__ void __launch_bounds__(256) k_dec_init(const DecDesc* D, Plan p, uint32_t sub_bits)
+{
+    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    const int img = p.ids[slot];
+    const DecDesc& d = D[img];
+    const int64_t j = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
+    if (j > d.nsub_max) return;
+    d.est[j] = dec_pack((uint32_t)j * sub_bits, 0, 0);
+    d.dirty[0][j] = 1;
+    d.dirty[1][j] = 0;
+}
+
+// Stage the image's Huffman tables in LDS (all threads participate).
+__device__ __forceinline__ void load_tables(const DecTab* T, int ncomp, DecHuff* L)
+{
+    const uint4* src = (const uint4*)T->h;
+    uint4* dst = (uint4*)L;
+    const int n = (int)(sizeof(DecHuff) * 2 * ncomp / 16);
+    for (int k = threadIdx.x; k < n; k += blockDim.x) dst[k] = src[k];
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
+                                                  int parity, uint32_t* changed)
+{
+    __shared__ __attribute__((aligned(16))) DecHuff L[6];
+    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    const int img = p.ids[slot];
+    const DecDesc& d = D[img];
+    const DecState& st = S[img];
+    const int64_t j = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
+    const bool mine = j < st.nsub && st.status == 0 && d.dirty[parity][j];
+    if (!__syncthreads_or(mine)) return;
+    load_tables(d.tab, d.ncomp, L);
+    if (!mine) return;
+    d.dirty[parity][j] = 0;
+    const uint64_t e = __hip_atomic_load(&d.est[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t n;
+    const uint64_t x = dec_walk<false>(d, L, (const uint32_t*)d.ent, d.seg, st.nseg, st.ent_len * 8, e,
+                                       (uint32_t)(j + 1) * sub_bits, n, 0);
+    d.ncnt[j] = n;
+    const uint64_t old = __hip_atomic_load(&d.est[j + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (x != old) {
+        __hip_atomic_store(&d.est[j + 1], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        d.dirty[parity ^ 1][j + 1] = 1;
+        atomicAdd(changed, 1u);
+    }
+}
+
+// One workgroup per image: exclusive scan of blocks per subsequence.
+__global__ void __launch_bounds__(1024) k_dec_offsets(const DecDesc* D, DecState* S, const int32_t* ids)
+{
+    __shared__ uint32_t sh[24];
+    const int img = ids[blockIdx.x];
+    const DecDesc& d = D[img];
+    DecState& st = S[img];
+    const int n = (int)st.nsub;
+    uint32_t carry = 0;
+    for (int t0 = 0; t0 < n; t0 += 1024) {
+        const int t = t0 + threadIdx.x;
+        uint32_t tot;
+        const uint32_t e = block_exscan<1024>(t < n ? d.ncnt[t] : 0u, sh, tot);
+        if (t < n) d.boff[t] = carry + e;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        st.total_blocks = carry;
+        if ((int64_t)carry != d.nblocks) st.status = 6;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits)
+{
+    __shared__ __attribute__((aligned(16))) DecHuff L[6];
+    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    const int img = p.ids[slot];
+    const DecDesc& d = D[img];
+    const DecState& st = S[img];
+    if (st.status) return;
+    const int64_t j = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
+    if ((blockIdx.x - p.prefix[slot]) * 256 >= (int64_t)st.nsub) return;
+    load_tables(d.tab, d.ncomp, L);
+    if (j >= st.nsub) return;
+    uint32_t n;
+    dec_walk<true>(d, L, (const uint32_t*)d.ent, d.seg, st.nseg, st.ent_len * 8, d.est[j],
+                   (uint32_t)(j + 1) * sub_bits, n, d.boff[j]);
+}
+
+// One workgroup per image: DC values from differences, per component, the
+// predictor reset at every restart interval (jdhuff.c process_restart).
+__global__ void __launch_bounds__(1024) k_dec_dc(const DecDesc* D, const DecState* S, const int32_t* ids)
+{
+    __shared__ int32_t sv[3][1024];
+    __shared__ int32_t sf[1024];
+    const int img = ids[blockIdx.x];
+    const DecDesc& d = D[img];
+    if (S[img].status) return;
+    const int64_t nmcu = (int64_t)d.mcux * d.mcuy;
+    const int64_t per = (nmcu + 1023) / 1024;
+    const int64_t m0 = threadIdx.x * per, m1 = m0 + per < nmcu ? m0 + per : nmcu;
+    // pass 1: this thread's sums since its last reset
+    int32_t acc[3] = {0, 0, 0};
+    int reset = 0;
+    for (int64_t m = m0; m < m1; m++) {
+        if (d.ri && m % d.ri == 0) {
+            acc[0] = acc[1] = acc[2] = 0;
+            reset = 1;
+        }
+        for (int k = 0; k < d.nbmcu; k++) acc[k < d.nby ? 0 : k - d.nby + 1] += d.dc[m * d.nbmcu + k];
+    }
+    for (int c = 0; c < 3; c++) sv[c][threadIdx.x] = acc[c];
+    sf[threadIdx.x] = reset;
+    __syncthreads();
+    // segmented inclusive scan (Hillis-Steele): (a, fa) + (b, fb) = (fb ? b : a + b, fa | fb)
+    for (int o = 1; o < 1024; o <<= 1) {
+        int32_t v[3];
+        int f = 0;
+        const bool has = (int)threadIdx.x >= o;
+        if (has) {
+            for (int c = 0; c < 3; c++) v[c] = sv[c][threadIdx.x - o];
+            f = sf[threadIdx.x - o];
+        }
+        __syncthreads();
+        if (has && !sf[threadIdx.x]) {
+            for (int c = 0; c < 3; c++) sv[c][threadIdx.x] += v[c];
+            sf[threadIdx.x] = f;
+        } else if (has) {
+            sf[threadIdx.x] = 1;
+        }
+        __syncthreads();
+    }
+    int32_t pred[3] = {0, 0, 0};
+    if (threadIdx.x > 0)
+        for (int c = 0; c < 3; c++) pred[c] = sv[c][threadIdx.x - 1];
+    // pass 2: write DC values
+    for (int64_t m = m0; m < m1; m++) {
+        if (d.ri && m % d.ri == 0) pred[0] = pred[1] = pred[2] = 0;
+        for (int k = 0; k < d.nbmcu; k++) {
+            const int c = k < d.nby ? 0 : k - d.nby + 1;
+            pred[c] += d.dc[m * d.nbmcu + k];
+            d.dc[m * d.nbmcu + k] = (int32_t)(int16_t)pred[c];
+        }
+    }
+}
+
+// ------------------------------------------------------------------- IDCT
+#define CONST_BITS 13
+#define PASS1_BITS 2
+#define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
+
+// One 1-D pass of jpeg_idct_islow (jidctint.c, IJG 6b); d[0..7] in place.
+template <int SH>
+__device__ __forceinline__ void idct8(int32_t* v)
+{
+    int32_t z2 = v[2], z3 = v[6];
+    int32_t z1 = (z2 + z3) * 4433;                   // FIX_0_541196100
+    const int32_t t2 = z1 + z3 * (-15137);           // FIX_1_847759065
+    const int32_t t3 = z1 + z2 * 6270;               // FIX_0_765366865
+    const int32_t t0 = (v[0] + v[4]) << CONST_BITS;
+    const int32_t t1 = (v[0] - v[4]) << CONST_BITS;
+    const int32_t t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+    int32_t o0 = v[7], o1 = v[5], o2 = v[3], o3 = v[1];
+    int32_t q1 = o0 + o3, q2 = o1 + o2, q3 = o0 + o2, q4 = o1 + o3;
+    const int32_t z5 = (q3 + q4) * 9633;             // FIX_1_175875602
+    o0 *= 2446; o1 *= 16819; o2 *= 25172; o3 *= 12299;
+    q1 *= -7373; q2 *= -20995; q3 *= -16069; q4 *= -3196;
+    q3 += z5; q4 += z5;
+    o0 += q1 + q3; o1 += q2 + q4; o2 += q2 + q3; o3 += q1 + q4;
+    v[0] = DESCALE(t10 + o3, SH);
+    v[7] = DESCALE(t10 - o3, SH);
+    v[1] = DESCALE(t11 + o2, SH);
+    v[6] = DESCALE(t11 - o2, SH);
+    v[2] = DESCALE(t12 + o1, SH);
+    v[5] = DESCALE(t12 - o1, SH);
+    v[3] = DESCALE(t13 + o0, SH);
+    v[4] = DESCALE(t13 - o0, SH);
+}
+
+// IDCT_range_limit(cinfo)[x & RANGE_MASK] (jdmaster.c prepare_range_limit_table)
+__device__ __forceinline__ uint32_t idct_limit(int32_t v)
+{
+    const int x = v & 1023;
+    return x < 128 ? (uint32_t)(x + 128) : x < 512 ? 255u : x < 896 ? 0u : (uint32_t)(x - 896);
+}
+
+// 8 threads per block (thread r owns row r), 32 blocks per workgroup; one image per workgroup.
+__global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecState* S, Plan p)
+{
+    __shared__ int32_t ws[32][8 * 9];
+    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    const int img = p.ids[slot];
+    const DecDesc& d = D[img];
+    if (S[img].status) return;
+    const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;
+    const int64_t b = (blockIdx.x - p.prefix[slot]) * 32 + lb;
+    const bool valid = b < d.nblocks;
+    int comp = 0, bx = 0, by = 0;
+    if (valid) {
+        const int64_t m = b / d.nbmcu;
+        const int k = (int)(b - m * d.nbmcu);
+        const int mx = (int)(m % d.mcux), my = (int)(m / d.mcux);
+        if (k < d.nby) {
+            bx = mx * d.hs + k % d.hs;
+            by = my * d.vs + k / d.hs;
+        } else {
+            comp = k - d.nby + 1;
+            bx = mx;
+            by = my;
+        }
+    }
+    const bool real = valid && bx * 8 < d.pw[comp] && by * 8 < d.ph[comp];  // dummy blocks: no IDCT (jdcoefct.c)
+    int32_t v[8];
+    if (real) {
+        const uint4 q = *(const uint4*)(d.coefs + b * 64 + r * 8);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+        const uint16_t* qt = d.tab->qt[comp] + r * 8;
+#pragma unroll
+        for (int c = 0; c < 8; c++) v[c] = (int32_t)(int16_t)(w[c >> 1] >> (16 * (c & 1))) * (int32_t)qt[c];
+        if (r == 0) v[0] = d.dc[b] * (int32_t)qt[0];
+#pragma unroll
+        for (int c = 0; c < 8; c++) ws[lb][r * 9 + c] = v[c];
+    }
+    __syncthreads();
+    if (real) {  // pass 1: column r
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = ws[lb][k * 9 + r];
+        idct8<CONST_BITS - PASS1_BITS>(v);
+#pragma unroll
+        for (int k = 0; k < 8; k++) ws[lb][k * 9 + r] = v[k];
+    }
+    __syncthreads();
+    if (real) {  // pass 2: row r
+#pragma unroll
+        for (int c = 0; c < 8; c++) v[c] = ws[lb][r * 9 + c];
+        idct8<CONST_BITS + PASS1_BITS + 3>(v);
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            lo |= idct_limit(v[c]) << (8 * c);
+            hi |= idct_limit(v[c + 4]) << (8 * c);
+        }
+        uint8_t* dst = d.plane[comp] + (int64_t)(by * 8 + r) * d.pw[comp] + bx * 8;
+        *(uint2*)dst = make_uint2(lo, hi);
+    }
+}
+
+// ----------------------------------------------------------- colour output
+// Upsampled chroma sample of component plane P at full-resolution (X, Y)
+// (jdsample.c: h2v2/h2v1 fancy when cw > 2, else replication; 1x1 direct).
+__device__ __forceinline__ int chroma_at(const DecDesc& d, const uint8_t* P, int pitch, int cw, int ch, int X, int Y)
+{
+    if (d.hs == 1 && d.vs == 1) return P[(int64_t)Y * pitch + X];
+    const int i = X >> 1;
+    if (!d.fancy) return P[(int64_t)(d.vs == 2 ? Y >> 1 : Y) * pitch + i];
+    if (d.vs == 1) {  // h2v1_fancy_upsample
+        const uint8_t* in = P + (int64_t)Y * pitch;
+        const int c = in[i];
+        if (!(X & 1)) return i == 0 ? c : (c * 3 + in[i - 1] + 1) >> 2;
+        return i == cw - 1 ? c : (c * 3 + in[i + 1] + 2) >> 2;
+    }
+    // h2v2_fancy_upsample: context row above (even Y) / below (odd Y), replicated at the edges
+    const int r0 = Y >> 1;
+    int rn = (Y & 1) ? r0 + 1 : r0 - 1;
+    rn = rn < 0 ? 0 : rn > ch - 1 ? ch - 1 : rn;
+    const uint8_t* a = P + (int64_t)r0 * pitch;
+    const uint8_t* bb = P + (int64_t)rn * pitch;
+    const int cs = a[i] * 3 + bb[i];
+    if (!(X & 1)) return i == 0 ? (cs * 4 + 8) >> 4 : (cs * 3 + a[i - 1] * 3 + bb[i - 1] + 8) >> 4;
+    return i == cw - 1 ? (cs * 4 + 7) >> 4 : (cs * 3 + a[i + 1] * 3 + bb[i + 1] + 7) >> 4;
+}
+
+__device__ __forceinline__ uint8_t clamp255(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
+// Thread per 4 output pixels of one output row; one image per workgroup.
+__global__ void __launch_bounds__(256) k_dec_color(const DecDesc* D, const DecState* S, Plan p)
+{
+    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    const int img = p.ids[slot];
+    const DecDesc& d = D[img];
+    if (S[img].status) return;
+    const int64_t item = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
+    const int gpr = (d.ow + 3) >> 2;
+    const int y = (int)(item / gpr), x0 = (int)(item % gpr) * 4;
+    if (y >= d.oh) return;
+    const int Y = y * d.s;
+    uint8_t* orow = d.out + (int64_t)y * d.ostride;
+    const uint8_t* yrow = d.plane[0] + (int64_t)Y * d.pw[0];
+    if (d.ncomp == 1) {
+        for (int k = 0; k < 4 && x0 + k < d.ow; k++) orow[x0 + k] = yrow[(x0 + k) * d.s];
+        return;
+    }
+    uint8_t px[12];
+    const int n = d.ow - x0 < 4 ? d.ow - x0 : 4;
+    for (int k = 0; k < n; k++) {
+        const int X = (x0 + k) * d.s;
+        const int yy = yrow[X];
+        const int cb = chroma_at(d, d.plane[1], d.pw[1], d.cw[1], d.ch[1], X, Y) - 128;
+        const int cr = chroma_at(d, d.plane[2], d.pw[2], d.cw[1], d.ch[1], X, Y) - 128;
+        // ycc_rgb_convert (jdcolor.c), SCALEBITS 16
+        px[3 * k + 0] = clamp255(yy + ((116130 * cb + 32768) >> 16));
+        px[3 * k + 1] = clamp255(yy + ((-22554 * cb + 32768 - 46802 * cr) >> 16));
+        px[3 * k + 2] = clamp255(yy + ((91881 * cr + 32768) >> 16));
+    }
+    uint8_t* o = orow + x0 * 3;
+    if (n == 4 && (((uintptr_t)o) & 3) == 0) {
+        uint32_t w[3];
+        for (int q = 0; q < 3; q++)
+            w[q] = px[4 * q] | (px[4 * q + 1] << 8) | (px[4 * q + 2] << 16) | ((uint32_t)px[4 * q + 3] << 24);
+        *(uint3*)o = make_uint3(w[0], w[1], w[2]);
+    } else {
+        for (int k = 0; k < 3 * n; k++) o[k] = px[k];
+    }
+}
+
+// ---------------------------------------------------------------- launchers
+void launch_unstuff(const DecDesc* d, DecState* s, const Plan& tiles, int64_t ntiles, const int32_t* ids, int m,
+                    uint32_t sub_bits, hipStream_t st)
+{
+    if (ntiles <= 0 || m <= 0) return;
+    hipLaunchKernelGGL(k_unstuff_end, dim3((unsigned)ntiles), dim3(256), 0, st, d, s, tiles);
+    hipLaunchKernelGGL(k_unstuff_count, dim3((unsigned)ntiles), dim3(256), 0, st, d, s, tiles);
+    hipLaunchKernelGGL(k_unstuff_scan, dim3((unsigned)m), dim3(1024), 0, st, d, s, ids, sub_bits);
+    hipLaunchKernelGGL(k_unstuff_scatter, dim3((unsigned)ntiles), dim3(256), 0, st, d, s, tiles);
+}
+
+void launch_dec_init(const DecDesc* d, const Plan& subs, int64_t nwg, uint32_t sub_bits, hipStream_t st)
+{
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_init, dim3((unsigned)nwg), dim3(256), 0, st, d, subs, sub_bits);
+}
+
+void launch_dec_sync(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
+                     int parity, uint32_t* changed, hipStream_t st)
+{
+    if (nwg > 0)
+        hipLaunchKernelGGL(k_dec_sync, dim3((unsigned)nwg), dim3(256), 0, st, d, s, subs, sub_bits, parity, changed);
+}
+
+void launch_dec_offsets(const DecDesc* d, DecState* s, const int32_t* ids, int m, hipStream_t st)
+{
+    if (m > 0) hipLaunchKernelGGL(k_dec_offsets, dim3((unsigned)m), dim3(1024), 0, st, d, s, ids);
+}
+
+void launch_dec_write(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
+                      hipStream_t st)
+{
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_write, dim3((unsigned)nwg), dim3(256), 0, st, d, s, subs, sub_bits);
+}
+
+void launch_dec_dc(const DecDesc* d, const DecState* s, const int32_t* ids, int m, hipStream_t st)
+{
+    if (m > 0) hipLaunchKernelGGL(k_dec_dc, dim3((unsigned)m), dim3(1024), 0, st, d, s, ids);
+}
+
+void launch_dec_idct(const DecDesc* d, const DecState* s, const Plan& blocks, int64_t nwg, hipStream_t st)
+{
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_idct, dim3((unsigned)nwg), dim3(256), 0, st, d, s, blocks);
+}
+
+void launch_dec_color(const DecDesc* d, const DecState* s, const Plan& px, int64_t nwg, hipStream_t st)
+{
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_color, dim3((unsigned)nwg), dim3(256), 0, st, d, s, px);
+}
+
+}  // namespace icx

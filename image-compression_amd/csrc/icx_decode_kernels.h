@@ -1,0 +1,26 @@
+// icx_decode_kernels.h — launch wrappers of the device JPEG decoder (icx_decode.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "icx_decode.h"
+#include "icx_internal.h"
+
+namespace icx {
+
+// tiles: per image ntiles work items (one workgroup per 4 KiB stuffed tile)
+void launch_unstuff(const DecDesc* d, DecState* s, const Plan& tiles, int64_t ntiles, const int32_t* ids, int m,
+                    uint32_t sub_bits, hipStream_t st);
+// subs: per image ceil((nsub_max + 1) / 256) workgroups
+void launch_dec_init(const DecDesc* d, const Plan& subs, int64_t nwg, uint32_t sub_bits, hipStream_t st);
+void launch_dec_sync(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
+                     int parity, uint32_t* changed, hipStream_t st);
+void launch_dec_offsets(const DecDesc* d, DecState* s, const int32_t* ids, int m, hipStream_t st);
+void launch_dec_write(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
+                      hipStream_t st);
+void launch_dec_dc(const DecDesc* d, const DecState* s, const int32_t* ids, int m, hipStream_t st);
+// blocks: per image ceil(nblocks / 32) workgroups
+void launch_dec_idct(const DecDesc* d, const DecState* s, const Plan& blocks, int64_t nwg, hipStream_t st);
+// px: per image ceil(oh * ceil(ow / 4) / 256) workgroups
+void launch_dec_color(const DecDesc* d, const DecState* s, const Plan& px, int64_t nwg, hipStream_t st);
+
+}  // namespace icx

@@ -1,0 +1,174 @@
+// icx_jpeg_parse.cpp — see icx_jpeg_parse.h.
+#include "icx_jpeg_parse.h"
+
+#include <string.h>
+
+namespace icx {
+
+namespace {
+const uint8_t kNat[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                          12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                          35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                          58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+}
+
+icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& J)
+{
+    J = JpegHeader{};
+    if (total < 4) return ICX_E_CORRUPT;
+    if (avail < 4) return ICX_E_BUFFER;
+    if (p[0] != 0xFF || p[1] != 0xD8) return ICX_E_CORRUPT;
+    size_t i = 2;
+    bool sof = false, unsupported = false, adobe_rgb = false, jfif = false;
+    for (;;) {
+        // next marker: skip non-0xFF garbage, then fill bytes (jdmarker.c next_marker)
+        while (i < avail && p[i] != 0xFF) i++;
+        while (i < avail && p[i] == 0xFF) i++;
+        if (i >= avail) return avail < total ? ICX_E_BUFFER : ICX_E_CORRUPT;
+        const int m = p[i++];
+        if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+        if (m == 0xD9) return ICX_E_CORRUPT;
+        if (i + 2 > avail) return avail < total ? ICX_E_BUFFER : ICX_E_CORRUPT;
+        const size_t seg = ((size_t)p[i] << 8) | p[i + 1];
+        if (seg < 2) return ICX_E_CORRUPT;
+        if (i + seg > avail) return avail < total ? ICX_E_BUFFER : ICX_E_CORRUPT;
+        const uint8_t* s = p + i + 2;
+        const size_t n = seg - 2;
+        i += seg;
+        switch (m) {
+        case 0xDB: {  // DQT
+            size_t o = 0;
+            while (o < n) {
+                const int pq = s[o] >> 4, tq = s[o] & 15;
+                if (tq > 3 || pq > 1) return ICX_E_CORRUPT;
+                const size_t need = 1 + (pq ? 128 : 64);
+                if (o + need > n) return ICX_E_CORRUPT;
+                for (int k = 0; k < 64; k++)
+                    J.qt[tq][kNat[k]] = pq ? (uint16_t)((s[o + 1 + 2 * k] << 8) | s[o + 2 + 2 * k]) : s[o + 1 + k];
+                J.qt_ok[tq] = true;
+                o += need;
+            }
+            break;
+        }
+        case 0xC4: {  // DHT
+            size_t o = 0;
+            while (o < n) {
+                if (o + 17 > n) return ICX_E_CORRUPT;
+                const int tc = s[o] >> 4, th = s[o] & 15;
+                if (tc > 1 || th > 3) return ICX_E_CORRUPT;
+                int cnt = 0;
+                for (int l = 0; l < 16; l++) cnt += s[o + 1 + l];
+                if (cnt > 256 || o + 17 + (size_t)cnt > n) return ICX_E_CORRUPT;
+                memcpy(J.hbits[tc][th], s + o + 1, 16);
+                memcpy(J.hvals[tc][th], s + o + 17, (size_t)cnt);
+                J.hn[tc][th] = cnt;
+                J.h_ok[tc][th] = true;
+                o += 17 + (size_t)cnt;
+            }
+            break;
+        }
+        case 0xC0:
+        case 0xC1: {  // baseline / extended sequential, Huffman
+            if (n < 6) return ICX_E_CORRUPT;
+            J.h = (s[1] << 8) | s[2];
+            J.w = (s[3] << 8) | s[4];
+            J.ncomp = s[5];
+            if (s[0] != 8 || J.w == 0 || J.h == 0 || (J.ncomp != 1 && J.ncomp != 3)) unsupported = true;
+            if (J.ncomp >= 1 && J.ncomp <= 3) {
+                if (n < 6 + 3 * (size_t)J.ncomp) return ICX_E_CORRUPT;
+                for (int c = 0; c < J.ncomp; c++) {
+                    J.id[c] = s[6 + 3 * c];
+                    J.hs[c] = s[7 + 3 * c] >> 4;
+                    J.vs[c] = s[7 + 3 * c] & 15;
+                    J.tq[c] = s[8 + 3 * c];
+                    if (J.tq[c] > 3 || J.hs[c] < 1 || J.vs[c] < 1 || J.hs[c] > 4 || J.vs[c] > 4)
+                        return ICX_E_CORRUPT;
+                }
+            }
+            sof = true;
+            break;
+        }
+        case 0xDD:  // DRI
+            if (n < 2) return ICX_E_CORRUPT;
+            J.ri = (s[0] << 8) | s[1];
+            break;
+        case 0xE0:  // APP0: JFIF
+            if (n >= 5 && !memcmp(s, "JFIF\0", 5)) jfif = true;
+            break;
+        case 0xEE:  // APP14: Adobe colour transform (jdmarker.c examine_app14)
+            if (n >= 12 && !memcmp(s, "Adobe", 5) && s[11] == 0) adobe_rgb = true;
+            break;
+        case 0xDA: {  // SOS
+            if (!sof) return ICX_E_CORRUPT;
+            if (unsupported) return ICX_E_UNSUPPORTED;
+            const int ns = n >= 1 ? s[0] : 0;
+            if (ns != J.ncomp || n < 1 + 2 * (size_t)ns + 3) return ICX_E_UNSUPPORTED;  // multi-scan
+            for (int k = 0; k < ns; k++) {
+                if (s[1 + 2 * k] != J.id[k]) return ICX_E_UNSUPPORTED;
+                J.td[k] = s[2 + 2 * k] >> 4;
+                J.ta[k] = s[2 + 2 * k] & 15;
+                if (J.td[k] > 3 || J.ta[k] > 3) return ICX_E_CORRUPT;
+            }
+            if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0) return ICX_E_UNSUPPORTED;
+            J.scan_off = i;
+            // colour space (jdapimin.c default_decompress_parms): JFIF or ids 1,2,3 -> YCbCr
+            if (J.ncomp == 3) {
+                const bool rgb_ids = J.id[0] == 'R' && J.id[1] == 'G' && J.id[2] == 'B';
+                if (!jfif && (adobe_rgb || rgb_ids)) return ICX_E_UNSUPPORTED;
+                if (J.hs[1] != 1 || J.vs[1] != 1 || J.hs[2] != 1 || J.vs[2] != 1) return ICX_E_UNSUPPORTED;
+                if (J.hs[0] > 2 || J.vs[0] > 2 || (J.hs[0] == 1 && J.vs[0] == 2)) return ICX_E_UNSUPPORTED;
+            }
+            for (int c = 0; c < J.ncomp; c++)
+                if (!J.qt_ok[J.tq[c]] || !J.h_ok[0][J.td[c]] || !J.h_ok[1][J.ta[c]]) return ICX_E_CORRUPT;
+            return ICX_OK;
+        }
+        default:
+            if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+                // progressive / lossless / arithmetic: dimensions only
+                if (n >= 6) {
+                    J.h = (s[1] << 8) | s[2];
+                    J.w = (s[3] << 8) | s[4];
+                    J.ncomp = s[5];
+                }
+                return ICX_E_UNSUPPORTED;
+            }
+            break;  // APPn, COM, DNL: skipped (ignoreMetadata, ImageCompression.java:126)
+        }
+    }
+}
+
+bool build_dec_huff(const uint8_t* bits, const uint8_t* vals, int n, DecHuff& t)
+{
+    memset(&t, 0, sizeof(t));
+    int code = 0, k = 0;
+    for (int l = 1; l <= 16; l++) {
+        const int cnt = bits[l - 1];
+        t.valoff[l] = k - code;
+        for (int i = 0; i < cnt; i++, code++, k++) {
+            if (l <= DEC_LUT_BITS) {
+                const int sh = DEC_LUT_BITS - l;
+                for (int f = 0; f < (1 << sh); f++)
+                    t.lut[(code << sh) | f] = (uint16_t)((vals[k] << 8) | l);
+            }
+        }
+        t.maxcode[l] = cnt ? code - 1 : -1;
+        if (code >= (1 << l)) return false;  // all-ones code or over-subscribed (jdhuff.c)
+        code <<= 1;
+    }
+    if (k != n) return false;
+    memcpy(t.vals, vals, (size_t)n);
+    return true;
+}
+
+bool build_dec_tab(const JpegHeader& J, DecTab& T)
+{
+    memset(&T, 0, sizeof(T));
+    for (int c = 0; c < J.ncomp; c++) {
+        if (!build_dec_huff(J.hbits[0][J.td[c]], J.hvals[0][J.td[c]], J.hn[0][J.td[c]], T.h[2 * c])) return false;
+        if (!build_dec_huff(J.hbits[1][J.ta[c]], J.hvals[1][J.ta[c]], J.hn[1][J.ta[c]], T.h[2 * c + 1])) return false;
+        memcpy(T.qt[c], J.qt[J.tq[c]], sizeof(T.qt[c]));
+    }
+    return true;
+}
+
+}  // namespace icx

@@ -1,0 +1,43 @@
+// icx_jpeg_parse.h — host-side JPEG marker parsing for the device decoder.
+//
+// The JDK reader (reached from ImageCompression.java:119-155) parses the
+// header with libjpeg's jdmarker.c; this is the baseline subset the device
+// decoder implements: SOF0/SOF1 8-bit, one interleaved scan (or a single grey
+// component), Huffman coding, optional DRI.  Everything else (progressive,
+// arithmetic, lossless, 12-bit, CMYK/YCCK, Adobe RGB, multi-scan sequential,
+// 4:4:0 and exotic sampling) is reported as ICX_E_UNSUPPORTED with the image
+// dimensions filled in, so the caller can still apply the dimension gate
+// (ImageCompression.java:131) and route the file to a host decoder.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/icx.h"
+#include "icx_decode.h"
+
+namespace icx {
+
+struct JpegHeader {
+    int w = 0, h = 0, ncomp = 0, ri = 0;
+    int id[3] = {}, hs[3] = {}, vs[3] = {}, tq[3] = {}, td[3] = {}, ta[3] = {};
+    uint16_t qt[4][64] = {};  // natural order
+    bool qt_ok[4] = {};
+    uint8_t hbits[2][4][16] = {};   // [dc|ac][slot] counts per code length
+    uint8_t hvals[2][4][256] = {};
+    int hn[2][4] = {};
+    bool h_ok[2][4] = {};
+    size_t scan_off = 0;  // first byte of the entropy-coded segment
+};
+
+// Parse markers up to the SOS.  `avail` bytes of the file are present at p
+// (the file is `total` bytes long).  Returns ICX_OK, ICX_E_UNSUPPORTED (w, h,
+// ncomp valid), ICX_E_CORRUPT, or ICX_E_BUFFER when more bytes are needed.
+icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& J);
+
+// jpeg_make_d_derived_tbl equivalent; false if the table is invalid.
+bool build_dec_huff(const uint8_t* bits, const uint8_t* vals, int n, DecHuff& t);
+
+// Per-image decode tables (Huffman per component, dequantisation per component).
+bool build_dec_tab(const JpegHeader& J, DecTab& T);
+
+}  // namespace icx

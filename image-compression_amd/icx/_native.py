@@ -22,6 +22,7 @@ EXPORTS = [
     "icx_compress_jpg_with_target_size", "icx_compress_jpg_batch", "icx_resize_image",
     "icx_resize_bilinear", "icx_png_fit", "icx_num_blocks", "icx_debug_fdct",
     "icx_profile_enable", "icx_profile_reset", "icx_profile_query",
+    "icx_jpeg_info", "icx_decode_jpg", "icx_decode_jpg_batch", "icx_debug_decode_coefs",
 ]
 
 
@@ -56,6 +57,14 @@ class FitJob(ctypes.Structure):
                 ("success", ctypes.c_int32), ("cache_hit", ctypes.c_int32),
                 ("out_len", ctypes.c_size_t), ("learned", LearnedParams),
                 ("encodes", ctypes.c_int32), ("status", ctypes.c_int32)]
+
+
+class DecodeJob(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_size_t), ("subsampling", ctypes.c_int32),
+                ("out", ctypes.c_void_p), ("cap", ctypes.c_size_t),
+                ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("fmt", ctypes.c_int32),
+                ("src_width", ctypes.c_int32), ("src_height", ctypes.c_int32),
+                ("out_len", ctypes.c_size_t), ("status", ctypes.c_int32)]
 
 
 _lib = None
@@ -101,6 +110,10 @@ def load():
         "icx_profile_enable": (c.c_int, [c.c_void_p, c.c_int32]),
         "icx_profile_reset": (c.c_int, [c.c_void_p]),
         "icx_profile_query": (c.c_int, [c.c_void_p, c.c_char_p, P(c.c_int64), P(c.c_double), P(c.c_int64)]),
+        "icx_jpeg_info": (c.c_int, [c.c_void_p, c.c_size_t, P(c.c_int32), P(c.c_int32), P(c.c_int32)]),
+        "icx_decode_jpg": (c.c_int, [c.c_void_p, P(DecodeJob)]),
+        "icx_decode_jpg_batch": (c.c_int, [c.c_void_p, P(DecodeJob), c.c_int32]),
+        "icx_debug_decode_coefs": (c.c_int, [c.c_void_p, c.c_void_p, c.c_size_t, P(c.c_int16), c.c_size_t]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -298,6 +298,63 @@ class Codec:
         write_png(output_file, resized)
         return True
 
+    # -------------------------------------------------------------- A11 decode
+    def decode_jpg_batch(self, datas, subsampling: int = 0, device_out: bool = False):
+        """Decode JPEG files (bytes / uint8 arrays / CUDA uint8 tensors) on the
+        GPU: decodeImageWithSubsampling's read (ImageCompression.java:113-155).
+        subsampling 0 = the reference's rule.  Returns one (status, image) per
+        file; image is (H, W, 3) BGR or (H, W) grey, a CUDA tensor when
+        device_out (then it stays in HBM for the encoder), else numpy."""
+        n = len(datas)
+        jobs = (N.DecodeJob * n)()
+        keep, outs = [], [None] * n
+        for i, d in enumerate(datas):
+            if d is None:
+                raise TypeError("data must not be null")
+            if hasattr(d, "data_ptr"):
+                keep.append(d)
+                jobs[i].data, jobs[i].len = d.data_ptr(), d.numel()
+            else:
+                a = np.frombuffer(d, np.uint8) if isinstance(d, (bytes, bytearray, memoryview)) else d
+                keep.append(a)
+                jobs[i].data, jobs[i].len = a.ctypes.data, a.nbytes
+            jobs[i].subsampling = int(subsampling)
+            info = jpeg_info(_host_header(d))
+            if info[0] == N.OK:
+                _, w, h, nc = info
+                s = subsampling if subsampling > 0 else subsampling_factor(w, h)
+                shape = (-(-h // s), -(-w // s), 3) if nc == 3 else (-(-h // s), -(-w // s))
+                if device_out:
+                    import torch
+                    out = torch.empty(shape, dtype=torch.uint8, device=f"cuda:{self.device}")
+                    jobs[i].out, jobs[i].cap = out.data_ptr(), out.numel()
+                else:
+                    out = np.empty(shape, np.uint8)
+                    jobs[i].out, jobs[i].cap = out.ctypes.data, out.nbytes
+                outs[i] = out
+            else:
+                jobs[i].out, jobs[i].cap = None, 0
+        with self._lock:
+            st = self._lib.icx_decode_jpg_batch(self._ctx, jobs, n)
+        self._check(st, "icx_decode_jpg_batch")
+        return [(jobs[i].status, outs[i] if jobs[i].status == N.OK else None) for i in range(n)]
+
+    def decode_jpg(self, data, subsampling: int = 0, device_out: bool = False):
+        st, img = self.decode_jpg_batch([data], subsampling, device_out)[0]
+        self._check(st, "icx_decode_jpg")
+        return img
+
+    def debug_decode_coefs(self, data) -> np.ndarray:
+        a = np.frombuffer(bytes(data), np.uint8)
+        st, w, h, nc = jpeg_info(a)
+        self._check(st, "icx_jpeg_info")
+        nb = _scan_blocks(a)
+        out = np.zeros((nb, 64), np.int16)
+        st = self._lib.icx_debug_decode_coefs(self._ctx, a.ctypes.data, a.nbytes,
+                                              out.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)), out.size)
+        self._check(st, "icx_debug_decode_coefs")
+        return out
+
     # -------------------------------------------------------------- parity / metrics
     def debug_fdct(self, image) -> np.ndarray:
         img, keep = _image_struct(image)
@@ -321,6 +378,51 @@ class Codec:
         self._check(self._lib.icx_profile_query(self._ctx, kernel.encode(), ctypes.byref(n), ctypes.byref(ms),
                                                 ctypes.byref(u)), "icx_profile_query")
         return {"launches": n.value, "ms": ms.value, "units": u.value}
+
+
+def jpeg_info(data):
+    """(status, width, height, ncomp) from the JPEG header (host bytes)."""
+    lib = N.load()
+    a = np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) else data
+    w, h, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    st = lib.icx_jpeg_info(a.ctypes.data, a.nbytes, ctypes.byref(w), ctypes.byref(h), ctypes.byref(n))
+    return st, w.value, h.value, n.value
+
+
+def _host_header(d):
+    """Host bytes holding at least the JPEG header of d (a CUDA tensor is
+    copied up to its SOS, in growing pieces)."""
+    if not hasattr(d, "data_ptr"):
+        return np.frombuffer(d, np.uint8) if isinstance(d, (bytes, bytearray, memoryview)) else d
+    n = min(d.numel(), 1 << 16)
+    while True:
+        a = d[:n].cpu().numpy()
+        if n == d.numel() or jpeg_info(a)[0] != N.E_CORRUPT:
+            return a
+        n = min(d.numel(), n * 4)
+
+
+def _scan_blocks(a):
+    """Blocks in the scan of a supported JPEG (MCU order incl. dummy blocks)."""
+    i = 2
+    while i + 4 <= len(a):
+        if a[i] != 0xFF:
+            i += 1
+            continue
+        m = int(a[i + 1])
+        if m in (0xC0, 0xC1):
+            h = int(a[i + 5]) << 8 | int(a[i + 6])
+            w = int(a[i + 7]) << 8 | int(a[i + 8])
+            nc = int(a[i + 9])
+            if nc == 1:
+                return -(-w // 8) * -(-h // 8)
+            hs, vs = int(a[i + 11]) >> 4, int(a[i + 11]) & 15
+            return -(-w // (8 * hs)) * -(-h // (8 * vs)) * (hs * vs + 2)
+        if m == 0xFF or m == 0xD8:
+            i += 1
+            continue
+        i += 2 + (int(a[i + 2]) << 8 | int(a[i + 3]))
+    raise ValueError("no SOF0/SOF1 marker")
 
 
 def quality_tables(quality: float):

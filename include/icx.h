@@ -168,7 +168,45 @@ icx_status icx_png_fit(icx_ctx* ctx, const icx_image* src, int32_t min_width, in
                        uint8_t* dst, size_t cap, int32_t* out_w, int32_t* out_h,
                        int32_t* resized);
 
+/* ------------------------------------------------------------- decode (A11) */
+/* ImageCompression.decodeImageWithSubsampling (ImageCompression.java:107-165)
+ * for JPEG: the JDK JPEGImageReader (IJG 6b: ISLOW IDCT, fancy upsampling,
+ * ycc_rgb_convert) with ImageReadParam.setSourceSubsampling(s, s, 0, 0) —
+ * pixels (x*s, y*s) of the full decode — and ignoreMetadata = true.
+ * Baseline/extended-sequential Huffman JPEGs with one interleaved scan
+ * (4:2:0, 4:2:2, 4:4:4) or one grey component, with or without restart
+ * intervals; anything else returns ICX_E_UNSUPPORTED. */
+typedef struct icx_decode_job {
+    /* inputs */
+    const uint8_t* data;   /* the whole JPEG file; host or device memory */
+    size_t len;
+    int32_t subsampling;   /* s >= 1; 0 = the reference's rule icx_subsampling_factor(w, h) */
+    uint8_t* out;          /* host or device; rows of width*channels bytes, packed */
+    size_t cap;
+    /* outputs */
+    int32_t width, height; /* decoded image: ceil(W/s) x ceil(H/s) */
+    int32_t fmt;           /* ICX_BGR24 (TYPE_3BYTE_BGR) or ICX_GRAY8 (TYPE_BYTE_GRAY) */
+    int32_t src_width, src_height; /* SOF dimensions (reader.getWidth(0)/getHeight(0)) */
+    size_t out_len;        /* width*height*channels */
+    icx_status status;
+} icx_decode_job;
+
+/* Header-only parse (host memory): SOF dimensions and components.  Returns
+ * ICX_OK when the device decoder supports the file, ICX_E_UNSUPPORTED (with
+ * the dimensions filled in) when it does not, ICX_E_CORRUPT otherwise. */
+icx_status icx_jpeg_info(const uint8_t* data, size_t len, int32_t* width, int32_t* height, int32_t* ncomp);
+
+icx_status icx_decode_jpg(icx_ctx* ctx, icx_decode_job* job);
+/* Batched decode: all files of the batch share the launches.  Per-job status
+ * is filled in; the return value is ICX_OK unless a context-level failure
+ * occurred. */
+icx_status icx_decode_jpg_batch(icx_ctx* ctx, icx_decode_job* jobs, int32_t n);
+
 /* ------------------------------------------------------- parity / metrics */
+/* Quantised coefficients after DC prediction (natural order, 64 per block,
+ * scan/MCU block order incl. dummy blocks) as the device decoder produced them. */
+icx_status icx_debug_decode_coefs(icx_ctx* ctx, const uint8_t* data, size_t len, int16_t* coefs, size_t ncoefs);
+
 /* Raw jpeg_fdct_islow coefficients (x8 scale, before quantisation) in scan
  * block order (MCU: Y0 Y1 Y2 Y3 Cb Cr), zig-zag within each block: the
  * device-resident layout the search re-quantises every trial. */

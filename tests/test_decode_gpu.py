@@ -1,0 +1,104 @@
+"""Parity of the device JPEG decoder (row A11, libicx.so through the C ABI)
+with the oracle and the golden decodes.  Bit-exact: quantised coefficients
+after DC prediction, and decoded BGR / grey pixels, with and without restart
+intervals, with source subsampling, for batches mixing layouts."""
+import io
+
+import numpy as np
+import pytest
+
+from icx import _native as N
+from tests.oracle_ffi import load_decode_golden, noise, smooth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dgolden():
+    return load_decode_golden()
+
+
+def test_decode_coefficients_match_oracle(codec, oracle, dgolden):
+    meta, jpgs, _ = dgolden
+    for name, data in jpgs.items():
+        if meta["cases"][name].get("unsupported"):
+            continue
+        ref = oracle.jpeg_coefs(data)
+        got = codec.debug_decode_coefs(data)
+        assert got.shape == ref.shape and np.array_equal(got, ref), name
+
+
+def test_decode_pixels_match_golden_batch(codec, dgolden):
+    """All golden files in one batch (grey, 4:2:0, 4:2:2, 4:4:4, DRI, q1..q100)."""
+    meta, jpgs, pxs = dgolden
+    names = list(jpgs)
+    res = codec.decode_jpg_batch([jpgs[k] for k in names], subsampling=1)
+    for name, (st, img) in zip(names, res):
+        if meta["cases"][name].get("unsupported"):
+            assert st == N.E_UNSUPPORTED, name
+            continue
+        assert st == N.OK, (name, st)
+        assert img.shape == pxs[name].shape and np.array_equal(img, pxs[name]), name
+
+
+def test_decode_to_device_and_subsampling(codec, oracle, dgolden):
+    import torch
+    meta, jpgs, pxs = dgolden
+    for s in (1, 2, 3):
+        for name in ("c130x250_s2_q95", "c66x130_s1_q50", "g47x61_q90", "rst7_130x250_444", "c7x9_s2_q95"):
+            img = codec.decode_jpg(jpgs[name], subsampling=s, device_out=True)
+            assert isinstance(img, torch.Tensor) and img.is_cuda
+            assert np.array_equal(img.cpu().numpy(), pxs[name][::s, ::s]), (name, s)
+            # device-resident compressed input as well
+            dev_in = torch.from_numpy(np.frombuffer(jpgs[name], np.uint8).copy()).cuda()
+            img2 = codec.decode_jpg(dev_in, subsampling=s)
+            assert np.array_equal(img2, pxs[name][::s, ::s]), (name, s, "device input")
+
+
+def _jpeg(rgb, **kw):
+    from PIL import Image
+    b = io.BytesIO()
+    Image.fromarray(rgb).save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+@pytest.mark.parametrize("kind", ["smooth", "noise"])
+def test_decode_4k_q95_matches_oracle(codec, oracle, kind):
+    """BASELINE sources: 4K, q95, 4:2:0 — the noise frame has almost no EOBs,
+    the hardest case for self-synchronisation."""
+    img = (smooth if kind == "smooth" else noise)(2160, 3840, 5)[:, :, ::-1].copy()
+    data = _jpeg(img, quality=95, subsampling=2)
+    rc, ref = oracle.jpeg_decode(data)
+    assert rc == 0
+    got = codec.decode_jpg(data)
+    assert np.array_equal(got, ref)
+
+
+def test_decode_8k_reference_subsampling_rule(codec, oracle):
+    """decodeImageWithSubsampling's rule (ImageCompression.java:140-153):
+    s = 2 for an 8192-wide image, 1 below."""
+    img = smooth(520, 8200, 9)[:, :, ::-1].copy()
+    data = _jpeg(img, quality=80, subsampling=2)
+    got = codec.decode_jpg(data)  # subsampling 0 = the reference's rule
+    rc, ref = oracle.jpeg_decode(data, 2)
+    assert rc == 0 and got.shape == (260, 4100, 3) and np.array_equal(got, ref)
+
+
+def test_decode_of_own_encodes_round_trip(codec, oracle):
+    """decode(encode(img)) on the GPU: coefficients equal the oracle decode of
+    the same bytes, for smooth/noise at low and full quality, colour and grey."""
+    for img, q in [(smooth(136, 200, 3), 0.25), (noise(64, 96, 4), 1.0), (smooth(50, 70, 5)[:, :, 0].copy(), 0.5)]:
+        data = codec.compress_jpg_to_stream(img, q)
+        assert np.array_equal(codec.debug_decode_coefs(data), oracle.jpeg_coefs(data))
+        rc, ref = oracle.jpeg_decode(data)
+        assert rc == 0 and np.array_equal(codec.decode_jpg(data), ref)
+
+
+def test_decode_refusals_and_corrupt_input(codec, dgolden):
+    meta, jpgs, _ = dgolden
+    good = jpgs["c130x250_s2_q95"]
+    bad = [good[: len(good) // 2], good[:700], b"\xff\xd8\xff\xd9", good[:2] + b"\x00" * 100]
+    res = codec.decode_jpg_batch(bad + [good], subsampling=1)
+    for st, img in res[:-1]:
+        assert st in (N.E_CORRUPT, N.E_UNSUPPORTED), st
+    assert res[-1][0] == N.OK  # a bad file does not spoil the batch
