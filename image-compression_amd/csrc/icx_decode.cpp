@@ -93,7 +93,7 @@ uint32_t pick_sub_bits(uint64_t total_bits)
         if (v >= 64 && (v & (v - 1)) == 0) return (uint32_t)v;
     }
     uint32_t S = 2048;  // enough subsequences to fill the chip, as few as possible (less re-walking)
-    while (S < 16384 && total_bits / S > 262144) S *= 2;
+    while (S < 16384 && total_bits / S > 524288) S *= 2;
     return S;
 }
 
@@ -124,6 +124,32 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
     if (he != hipSuccess) return hip_fail(c, he, "hipSetDevice");
     std::vector<DecItem> items;
     items.reserve(n);
+    // headers of device-resident files: one batched download of their first 64 KiB
+    const size_t HEAD = 64 << 10;
+    std::vector<char> dev_in(n, 0);
+    std::vector<const uint8_t*> head(n, nullptr);
+    {
+        size_t total = 0;
+        for (int i = 0; i < n; i++)
+            if (jobs[i].data && is_device_ptr(jobs[i].data)) {
+                dev_in[i] = 1;
+                total += align_up(std::min(jobs[i].len, HEAD), 64);
+            }
+        if (total) {
+            hipError_t e = c->host.reserve(std::max<size_t>(total + 4096, 64 << 20));
+            if (e != hipSuccess) return hip_fail(c, e, "hipHostMalloc");
+            c->host.used = 0;
+            for (int i = 0; i < n; i++)
+                if (dev_in[i]) {
+                    uint8_t* h = (uint8_t*)c->host.take(std::min(jobs[i].len, HEAD));
+                    e = hipMemcpyAsync(h, jobs[i].data, std::min(jobs[i].len, HEAD), hipMemcpyDeviceToHost, c->stream);
+                    if (e != hipSuccess) return hip_fail(c, e, "header download");
+                    head[i] = h;
+                }
+            e = hipStreamSynchronize(c->stream);
+            if (e != hipSuccess) return hip_fail(c, e, "header download");
+        }
+    }
     for (int i = 0; i < n; i++) {
         icx_decode_job& j = jobs[i];
         j.width = j.height = j.src_width = j.src_height = 0;
@@ -135,8 +161,13 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         }
         DecItem it;
         it.job = &j;
-        it.dev_in = is_device_ptr(j.data);
-        j.status = read_header(c, j.data, j.len, it.dev_in, it.J);
+        it.dev_in = dev_in[i];
+        if (it.dev_in) {
+            j.status = parse_jpeg(head[i], std::min(j.len, HEAD), j.len, it.J);
+            if (j.status == ICX_E_BUFFER) j.status = read_header(c, j.data, j.len, true, it.J);  // header > 64 KiB
+        } else {
+            j.status = parse_jpeg(j.data, j.len, j.len, it.J);
+        }
         j.src_width = it.J.w;
         j.src_height = it.J.h;
         if (j.status != ICX_OK) continue;
@@ -242,9 +273,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
                 d.ostride = d.ow * it.nch;
             }
             d.tab = d_tab + k;
-            states[k].end = scan_len;
-            e = hipMemsetAsync(d.coefs, 0, (size_t)d.nblocks * 128, c->stream);
-            if (e != hipSuccess) return hip_fail(c, e, "coefficient clear");
+            states[k].end = scan_len;  // coefficients need no clearing: the write pass stores whole blocks
         }
         DecDesc* d_desc = (DecDesc*)c->dev.take(sizeof(DecDesc) * m);
         DecState* d_state = (DecState*)c->dev.take(sizeof(DecState) * m);

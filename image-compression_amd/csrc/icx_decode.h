@@ -47,20 +47,33 @@ constexpr int DEC_PAD = 8;           // 0xFF bytes standing in for each RSTn mar
 constexpr int DEC_TAIL = 16;         // 0xFF bytes after the last interval
 constexpr uint32_t DEC_END = 0xFFFFFFFFu;
 
-// One Huffman table prepared for decoding (jdhuff.c jpeg_make_d_derived_tbl):
-// lut[peek >> (16 - DEC_LUT_BITS)] = (symbol << 8) | code length for codes of at
-// most DEC_LUT_BITS bits, 0 otherwise; longer codes use maxcode/valoff.
+// One Huffman table prepared for decoding (jdhuff.c jpeg_make_d_derived_tbl),
+// two-level: lut[peek >> 6] (the next 10 bits) is (length << 8) | symbol for
+// codes of at most 10 bits; for a 10-bit prefix of longer codes it is
+// DEC_SUB | k and lut2[k][next 6 bits] holds (length << 8) | symbol.  0 = no
+// valid code.  Tables with more than DEC_NSUB long-code prefixes mark the rest
+// DEC_SLOW and decode those codes with the canonical maxcode loop (DecSlow).
+constexpr int DEC_NSUB = 16;
+constexpr uint32_t DEC_SUB = 0x2000u, DEC_SLOW = 0x4000u;
 struct DecHuff {
     uint16_t lut[1 << DEC_LUT_BITS];
+    uint16_t lut2[DEC_NSUB][1 << (16 - DEC_LUT_BITS)];
+};
+struct DecSlow {
     int32_t maxcode[17];   // largest code of length l, -1 if none
     int32_t valoff[17];    // index into vals of code c of length l: valoff[l] + c
     uint8_t vals[256];
 };
 
-// Per-image tables: h[2*c] = DC table of component c, h[2*c+1] = AC table.
+// Per-image tables.  Components share tables (Cb/Cr normally do): h[] holds
+// the distinct ones, sel[2*c] / sel[2*c+1] index the DC / AC table of component c.
 struct DecTab {
-    DecHuff h[6];
+    DecHuff h[4];
+    DecSlow slow[4];
     uint16_t qt[3][64];    // dequantisation tables, natural order, per component
+    uint8_t sel[6];
+    uint8_t ntab;
+    uint8_t pad[9];
 };
 
 // Per-image descriptor (host-built, read-only on the device).
@@ -112,25 +125,37 @@ ICX_HD uint32_t dec_be32(uint32_t v)
 #endif
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+#define ICX_GLOBAL __attribute__((address_space(1)))
+#else
+#define ICX_GLOBAL
+#endif
+
+// MSB-first bit reader over the unstuffed stream (big-endian 32-bit words).
+// One word is always in flight (nxt), so a refill never waits on the load it
+// issues; the stream is padded so the look-ahead stays inside the buffer.
 struct DecReader {
-    const uint32_t* w;
+    const ICX_GLOBAL uint32_t* w;
     uint64_t buf;
     int avail;
     uint32_t wi;
+    uint32_t nxt;
     ICX_HD void init(const uint32_t* words, uint32_t pos)
     {
-        w = words;
+        w = (const ICX_GLOBAL uint32_t*)words;
         wi = pos >> 5;
         buf = ((uint64_t)dec_be32(w[wi]) << 32) | dec_be32(w[wi + 1]);
-        wi += 2;
+        nxt = w[wi + 2];
+        wi += 3;
         buf <<= (pos & 31);
         avail = 64 - (int)(pos & 31);
     }
     ICX_HD void refill()
     {
         if (avail < 32) {
-            buf |= (uint64_t)dec_be32(w[wi++]) << (32 - avail);
+            buf |= (uint64_t)dec_be32(nxt) << (32 - avail);
             avail += 32;
+            nxt = w[wi++];
         }
     }
     ICX_HD uint32_t peek16() const { return (uint32_t)(buf >> 48); }
@@ -151,16 +176,23 @@ struct DecReader {
 // HUFF_EXTEND (jdhuff.c)
 ICX_HD int dec_extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
-// Decode one symbol; returns (symbol << 8) | length, 0 if no valid code.
-ICX_HD uint32_t dec_symbol(const DecHuff* t, uint32_t pk)
+// Decode one symbol: (length << 8) | symbol, 0 if no valid code.
+template <class HuffPtr>
+ICX_HD uint32_t dec_symbol(HuffPtr t, const DecSlow* slow, uint32_t pk)
 {
-    const uint32_t e = t->lut[pk >> (16 - DEC_LUT_BITS)];
-    if (e) return e;
-    for (int l = DEC_LUT_BITS + 1; l <= 16; l++) {
-        const int code = (int)(pk >> (16 - l));
-        if (code <= t->maxcode[l]) return ((uint32_t)t->vals[(t->valoff[l] + code) & 255] << 8) | (uint32_t)l;
+    uint32_t e = t->lut[pk >> (16 - DEC_LUT_BITS)];
+    if (e & DEC_SUB) e = t->lut2[e & (DEC_NSUB - 1)][pk & ((1u << (16 - DEC_LUT_BITS)) - 1)];
+    if (e & DEC_SLOW) {
+        e = 0;
+        for (int l = DEC_LUT_BITS + 1; l <= 16; l++) {
+            const int code = (int)(pk >> (16 - l));
+            if (code <= slow->maxcode[l]) {
+                e = ((uint32_t)l << 8) | slow->vals[(slow->valoff[l] + code) & 255];
+                break;
+            }
+        }
     }
-    return 0;
+    return e;
 }
 
 // zig-zag index -> natural index with jpeg_natural_order's tail (k > 63 -> 63)
@@ -186,30 +218,49 @@ ICX_HD uint32_t dec_next_seg(const uint32_t* seg, uint32_t nseg, uint32_t byte)
 
 // Decode from state st until the first symbol boundary at or beyond `stop`
 // (jdhuff.c decode_mcu, symbol by symbol).  Returns the exit state; nblk =
-// blocks completed on the way.  WRITE: store AC coefficients (natural order)
-// and DC differences of block blk_base + (blocks completed so far).
-template <bool WRITE, class HuffPtr>
-ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const uint32_t* words, const uint32_t* seg, uint32_t nseg,
-                         uint32_t ent_bits, uint64_t st, uint32_t stop, uint32_t& nblk, int64_t blk_base)
+// blocks completed on the way.
+//
+// OWNED (the write pass): a block belongs to the subsequence in which its DC
+// symbol starts, so every block is written whole by exactly one thread.  The
+// walk skips the stores of a block it enters mid-way (its owner is the
+// previous subsequence), and after `stop` it keeps decoding until the block in
+// progress is complete.  AC coefficients go to sink.coef(natural index, value),
+// a finished owned block to sink.flush(block index); DC differences are
+// stored directly in d.dc[block].
+// Table index of (component, DC or AC) from the packed selector (dec_selector).
+ICX_HD int dec_sel(uint32_t selp, int comp, int ac) { return (int)((selp >> (4 * (2 * comp + ac))) & 3); }
+
+struct NoSink {
+    ICX_HD void coef(int, int) {}
+    ICX_HD void flush(int64_t) {}
+};
+
+template <bool OWNED, class HuffPtr, class Sink>
+ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, uint32_t selp, const uint32_t* words,
+                         const uint32_t* seg, uint32_t nseg, uint32_t ent_bits, uint64_t st, uint32_t stop,
+                         uint32_t& nblk, int64_t blk_base, Sink& sink)
 {
     uint32_t pos = dec_pos(st);
     nblk = 0;
-    if (pos >= stop) return st;
     int b = (int)((st >> 8) & 7), z = (int)(st & 63);
+    if (pos >= stop && (!OWNED || z == 0)) return st;
+    bool own = z == 0;
     DecReader R;
     R.init(words, pos);
     int comp = b < d.nby ? 0 : b - d.nby + 1;
     uint32_t n = 0;
-    while (pos < stop) {
+    while (pos < stop || (OWNED && z != 0)) {
         R.refill();
-        const uint32_t e = dec_symbol(&H[2 * comp + (z ? 1 : 0)], R.peek16());
-        const int len = (int)(e & 31), sym = (int)(e >> 8);
+        const int ti = dec_sel(selp, comp, z ? 1 : 0);
+        const uint32_t e = dec_symbol(&H[ti], &slow[ti], R.peek16());
+        const int len = (int)(e >> 8), sym = (int)(e & 255);
         if (len == 0 || (z == 0 && sym > 11)) {  // no valid code here
             const uint32_t nx = dec_next_seg(seg, nseg, pos >> 3);
             const uint32_t bound = nx == DEC_END ? ent_bits : (nx - DEC_PAD) * 8;  // end of interval data
             b = 0;
             z = 0;
             comp = 0;
+            own = true;
             if (pos + 8 < bound) {  // mid-interval: only a wrong-start path gets here; resume a bit later
                 pos++;
                 R.init(words, pos);
@@ -228,7 +279,7 @@ ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const uint32_t* words, con
         if (z == 0) {
             const int v = R.get(sym);
             pos += (uint32_t)(len + sym);
-            if (WRITE) {
+            if (OWNED) {
                 const int64_t bi = blk_base + n;
                 if (bi < d.nblocks) d.dc[bi] = sym ? dec_extend(v, sym) : 0;
             }
@@ -239,10 +290,7 @@ ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const uint32_t* words, con
                 z += r;
                 const int v = R.get(s);
                 pos += (uint32_t)(len + s);
-                if (WRITE) {
-                    const int64_t bi = blk_base + n;
-                    if (bi < d.nblocks) d.coefs[bi * 64 + dec_nat(z)] = (int16_t)dec_extend(v, s);
-                }
+                if (OWNED && own) sink.coef(dec_nat(z), dec_extend(v, s));
                 z++;
             } else {
                 pos += (uint32_t)len;
@@ -250,6 +298,11 @@ ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const uint32_t* words, con
             }
         }
         if (z >= 64) {
+            if (OWNED && own) {
+                const int64_t bi = blk_base + n;
+                if (bi < d.nblocks) sink.flush(bi);
+            }
+            own = true;
             n++;
             z = 0;
             b = (b + 1 == d.nbmcu) ? 0 : b + 1;

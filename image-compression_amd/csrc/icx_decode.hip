@@ -230,20 +230,27 @@ __global__ void __launch_bounds__(256) k_dec_init(const DecDesc* D, Plan p, uint
     d.dirty[1][j] = 0;
 }
 
-// Stage the image's Huffman tables in LDS (all threads participate).
-__device__ __forceinline__ void load_tables(const DecTab* T, int ncomp, DecHuff* L)
+// Stage the image's distinct Huffman tables in LDS (all threads participate).
+__device__ __forceinline__ void load_tables(const DecTab* T, DecHuff* L)
 {
     const uint4* src = (const uint4*)T->h;
     uint4* dst = (uint4*)L;
-    const int n = (int)(sizeof(DecHuff) * 2 * ncomp / 16);
+    const int n = (int)(sizeof(DecHuff) * T->ntab / 16);
     for (int k = threadIdx.x; k < n; k += blockDim.x) dst[k] = src[k];
     __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t selector(const DecTab* T)
+{
+    uint32_t s = 0;
+    for (int k = 0; k < 6; k++) s |= (uint32_t)(T->sel[k] & 3) << (4 * k);
+    return s;
 }
 
 __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
                                                   int parity, uint32_t* changed)
 {
-    __shared__ __attribute__((aligned(16))) DecHuff L[6];
+    __shared__ __attribute__((aligned(16))) DecHuff L[4];
     const int slot = slot_of(p.prefix, p.m, blockIdx.x);
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
@@ -251,13 +258,14 @@ __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecSta
     const int64_t j = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
     const bool mine = j < st.nsub && st.status == 0 && d.dirty[parity][j];
     if (!__syncthreads_or(mine)) return;
-    load_tables(d.tab, d.ncomp, L);
+    load_tables(d.tab, L);
     if (!mine) return;
     d.dirty[parity][j] = 0;
     const uint64_t e = __hip_atomic_load(&d.est[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t n;
-    const uint64_t x = dec_walk<false>(d, L, (const uint32_t*)d.ent, d.seg, st.nseg, st.ent_len * 8, e,
-                                       (uint32_t)(j + 1) * sub_bits, n, 0);
+    NoSink ns;
+    const uint64_t x = dec_walk<false>(d, L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
+                                       st.ent_len * 8, e, (uint32_t)(j + 1) * sub_bits, n, 0, ns);
     d.ncnt[j] = n;
     const uint64_t old = __hip_atomic_load(&d.est[j + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (x != old) {
@@ -289,9 +297,29 @@ __global__ void __launch_bounds__(1024) k_dec_offsets(const DecDesc* D, DecState
     }
 }
 
+// Per-thread block assembly slot in LDS: 64 int16 at a stride of 33 dwords
+// (consecutive threads' slots start on consecutive banks).
+constexpr int SLOT_DW = 33;
+struct LdsBlockSink {
+    int16_t* slot;   // this thread's slot
+    int16_t* coefs;  // d.coefs
+    __device__ __forceinline__ void coef(int k, int v) { slot[k] = (int16_t)v; }
+    __device__ __forceinline__ void flush(int64_t bi)
+    {
+        uint32_t* s32 = (uint32_t*)slot;
+        uint4* dst = (uint4*)(coefs + bi * 64);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            dst[q] = make_uint4(s32[4 * q], s32[4 * q + 1], s32[4 * q + 2], s32[4 * q + 3]);
+            s32[4 * q] = s32[4 * q + 1] = s32[4 * q + 2] = s32[4 * q + 3] = 0;
+        }
+    }
+};
+
 __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits)
 {
-    __shared__ __attribute__((aligned(16))) DecHuff L[6];
+    __shared__ __attribute__((aligned(16))) DecHuff L[4];
+    __shared__ uint32_t slots[256 * SLOT_DW];
     const int slot = slot_of(p.prefix, p.m, blockIdx.x);
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
@@ -299,11 +327,14 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, const DecSt
     if (st.status) return;
     const int64_t j = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
     if ((blockIdx.x - p.prefix[slot]) * 256 >= (int64_t)st.nsub) return;
-    load_tables(d.tab, d.ncomp, L);
+    uint32_t* mys = slots + threadIdx.x * SLOT_DW;
+    for (int k = 0; k < 32; k++) mys[k] = 0;
+    load_tables(d.tab, L);
     if (j >= st.nsub) return;
     uint32_t n;
-    dec_walk<true>(d, L, (const uint32_t*)d.ent, d.seg, st.nseg, st.ent_len * 8, d.est[j],
-                   (uint32_t)(j + 1) * sub_bits, n, d.boff[j]);
+    LdsBlockSink sink{(int16_t*)mys, d.coefs};
+    dec_walk<true>(d, L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg, st.ent_len * 8,
+                   d.est[j], (uint32_t)(j + 1) * sub_bits, n, d.boff[j], sink);
 }
 
 // One workgroup per image: DC values from differences, per component, the

@@ -137,38 +137,67 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
     }
 }
 
-bool build_dec_huff(const uint8_t* bits, const uint8_t* vals, int n, DecHuff& t)
+bool build_dec_huff(const uint8_t* bits, const uint8_t* vals, int n, DecHuff& t, DecSlow& slow)
 {
     memset(&t, 0, sizeof(t));
-    int code = 0, k = 0;
+    memset(&slow, 0, sizeof(slow));
+    int code = 0, k = 0, nsub = 0;
     for (int l = 1; l <= 16; l++) {
         const int cnt = bits[l - 1];
-        t.valoff[l] = k - code;
+        slow.valoff[l] = k - code;
         for (int i = 0; i < cnt; i++, code++, k++) {
+            const uint16_t e = (uint16_t)((l << 8) | vals[k]);
             if (l <= DEC_LUT_BITS) {
                 const int sh = DEC_LUT_BITS - l;
-                for (int f = 0; f < (1 << sh); f++)
-                    t.lut[(code << sh) | f] = (uint16_t)((vals[k] << 8) | l);
+                for (int f = 0; f < (1 << sh); f++) t.lut[(code << sh) | f] = e;
+            } else {
+                const int pre = code >> (l - DEC_LUT_BITS);  // its 10-bit prefix
+                uint16_t& p = t.lut[pre];
+                if (p == 0) p = nsub < DEC_NSUB ? (uint16_t)(DEC_SUB | nsub++) : (uint16_t)DEC_SLOW;
+                if (p & DEC_SUB) {
+                    const int rest = 16 - l, low = (code & ((1 << (l - DEC_LUT_BITS)) - 1)) << rest;
+                    for (int f = 0; f < (1 << rest); f++) t.lut2[p & (DEC_NSUB - 1)][low | f] = e;
+                }
             }
         }
-        t.maxcode[l] = cnt ? code - 1 : -1;
+        slow.maxcode[l] = cnt ? code - 1 : -1;
         if (code >= (1 << l)) return false;  // all-ones code or over-subscribed (jdhuff.c)
         code <<= 1;
     }
     if (k != n) return false;
-    memcpy(t.vals, vals, (size_t)n);
+    memcpy(slow.vals, vals, (size_t)n);
     return true;
 }
 
 bool build_dec_tab(const JpegHeader& J, DecTab& T)
 {
     memset(&T, 0, sizeof(T));
+    int slot_of[2][4];  // (class, table id) -> slot
+    for (int a = 0; a < 2; a++)
+        for (int b = 0; b < 4; b++) slot_of[a][b] = -1;
+    int ntab = 0;
     for (int c = 0; c < J.ncomp; c++) {
-        if (!build_dec_huff(J.hbits[0][J.td[c]], J.hvals[0][J.td[c]], J.hn[0][J.td[c]], T.h[2 * c])) return false;
-        if (!build_dec_huff(J.hbits[1][J.ta[c]], J.hvals[1][J.ta[c]], J.hn[1][J.ta[c]], T.h[2 * c + 1])) return false;
+        for (int ac = 0; ac < 2; ac++) {
+            const int id = ac ? J.ta[c] : J.td[c];
+            int& sl = slot_of[ac][id];
+            if (sl < 0) {
+                if (ntab == 4) return false;
+                sl = ntab++;
+                if (!build_dec_huff(J.hbits[ac][id], J.hvals[ac][id], J.hn[ac][id], T.h[sl], T.slow[sl])) return false;
+            }
+            T.sel[2 * c + ac] = (uint8_t)sl;
+        }
         memcpy(T.qt[c], J.qt[J.tq[c]], sizeof(T.qt[c]));
     }
+    T.ntab = (uint8_t)ntab;
     return true;
+}
+
+uint32_t dec_selector(const DecTab& T)
+{
+    uint32_t s = 0;
+    for (int k = 0; k < 6; k++) s |= (uint32_t)(T.sel[k] & 3) << (4 * k);
+    return s;
 }
 
 }  // namespace icx

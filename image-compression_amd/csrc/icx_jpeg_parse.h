@@ -35,9 +35,13 @@ struct JpegHeader {
 icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& J);
 
 // jpeg_make_d_derived_tbl equivalent; false if the table is invalid.
-bool build_dec_huff(const uint8_t* bits, const uint8_t* vals, int n, DecHuff& t);
+bool build_dec_huff(const uint8_t* bits, const uint8_t* vals, int n, DecHuff& t, DecSlow& slow);
 
-// Per-image decode tables (Huffman per component, dequantisation per component).
+// Per-image decode tables (distinct Huffman tables + per-component selectors,
+// dequantisation per component).
 bool build_dec_tab(const JpegHeader& J, DecTab& T);
+
+// DecTab::sel packed 4 bits per entry, as dec_walk takes it.
+uint32_t dec_selector(const DecTab& T);
 
 }  // namespace icx

@@ -339,6 +339,11 @@ class Codec:
         self._check(st, "icx_decode_jpg_batch")
         return [(jobs[i].status, outs[i] if jobs[i].status == N.OK else None) for i in range(n)]
 
+    def prepare_decode(self, datas, outputs, subsampling: int = 0):
+        """A reusable decode job array over preallocated inputs/outputs
+        (numpy arrays or CUDA tensors), for repeated timed runs (bench)."""
+        return PreparedDecode(self, datas, outputs, subsampling)
+
     def decode_jpg(self, data, subsampling: int = 0, device_out: bool = False):
         st, img = self.decode_jpg_batch([data], subsampling, device_out)[0]
         self._check(st, "icx_decode_jpg")
@@ -477,3 +482,31 @@ class PreparedBatch:
         return [{"status": j.status, "success": bool(j.success), "cache_hit": bool(j.cache_hit),
                  "out_len": j.out_len, "encodes": j.encodes,
                  "learned": LearnedParams(j.learned.quality, j.learned.scale)} for j in self.jobs]
+
+
+class PreparedDecode:
+    """icx_decode_jpg_batch over fixed buffers: run() decodes all files again."""
+
+    def __init__(self, codec, datas, outputs, subsampling=0):
+        self.codec = codec
+        n = len(datas)
+        self.n = n
+        self.jobs = (N.DecodeJob * n)()
+        self.keep = list(datas) + list(outputs)
+        for i, (d, o) in enumerate(zip(datas, outputs)):
+            j = self.jobs[i]
+            if hasattr(d, "data_ptr"):
+                j.data, j.len = d.data_ptr(), d.numel()
+            else:
+                j.data, j.len = d.ctypes.data, d.nbytes
+            if hasattr(o, "data_ptr"):
+                j.out, j.cap = o.data_ptr(), o.numel()
+            else:
+                j.out, j.cap = o.ctypes.data, o.nbytes
+            j.subsampling = int(subsampling)
+
+    def run(self):
+        with self.codec._lock:
+            st = self.codec._lib.icx_decode_jpg_batch(self.codec._ctx, self.jobs, self.n)
+        self.codec._check(st, "icx_decode_jpg_batch")
+        return [self.jobs[i].status for i in range(self.n)]

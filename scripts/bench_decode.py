@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Device JPEG decode throughput (row A11) on synthetic 4K q95 4:2:0 sources
+(half smooth = sinusoids + Gaussian sigma 16, half uniform
+noise), compressed bytes and decoded frames resident in HBM.  Prints one JSON
+line with MP/s, per-kernel HIP-event times and the sync iteration count."""
+import argparse
+import io
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "image-compression_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+
+def sources(h, w, distinct):
+    from PIL import Image
+    from tests.oracle_ffi import noise, smooth
+    out = []
+    for i in range(distinct):
+        img = (smooth if i % 2 == 0 else noise)(h, w, 100 + i)[:, :, ::-1]
+        b = io.BytesIO()
+        Image.fromarray(np.ascontiguousarray(img)).save(b, "JPEG", quality=95, subsampling=2)
+        out.append(b.getvalue())
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=200)
+    ap.add_argument("--distinct", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--kind", default="mixed", choices=["mixed", "smooth", "noise"])
+    a = ap.parse_args()
+    import torch
+    import icx
+    srcs = sources(a.height, a.width, a.distinct)
+    if a.kind != "mixed":
+        srcs = [s for i, s in enumerate(srcs) if (i % 2 == 0) == (a.kind == "smooth")]
+    codec = icx.Codec(0)
+    dev = [torch.from_numpy(np.frombuffer(s, np.uint8).copy()).cuda() for s in srcs]
+    ins = [dev[i % len(dev)] for i in range(a.frames)]
+    outs = [torch.empty((a.height, a.width, 3), dtype=torch.uint8, device="cuda") for _ in range(a.frames)]
+    P = codec.prepare_decode(ins, outs, subsampling=1)
+    for _ in range(a.warmup):
+        assert all(s == 0 for s in P.run())
+    torch.cuda.synchronize()
+    codec.profile(True)
+    codec.profile_reset()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        P.run()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    kern = {k: codec.profile_query(k) for k in ("dec_unstuff", "dec_sync", "dec_write", "dec_dc", "dec_idct",
+                                                 "dec_color", "dec_sync_iters")}
+    mp = a.frames * a.height * a.width / 1e6
+    stuffed = sum(len(srcs[i % len(srcs)]) for i in range(a.frames))
+    print(json.dumps({"metric": "megapixels/sec JPEG decode (4K q95 4:2:0, HBM-resident)", "value": round(mp / dt, 1),
+                      "unit": "MP/s", "ms_per_step": round(dt * 1e3, 3), "frames": a.frames, "kind": a.kind,
+                      "mean_jpeg_bytes": stuffed // a.frames,
+                      "kernels_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in kern.items()
+                                              if k != "dec_sync_iters"},
+                      "sync_launches_per_step": kern["dec_sync_iters"]["launches"] / a.steps}))
+    codec.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -28,6 +28,7 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
     if (st) return (int)st;
     static DecTab T;
     if (!build_dec_tab(J, T)) return ICX_E_CORRUPT;
+    const uint32_t sel = dec_selector(T);
     DecDesc d{};
     d.ncomp = J.ncomp;
     if (J.ncomp == 3) {
@@ -95,8 +96,9 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
             if (!cur[j]) continue;
             cur[j] = 0;
             uint32_t n;
-            const uint64_t x = dec_walk<false>(d, T.h, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8, est[j],
-                                               (j + 1) * S, n, 0);
+            NoSink ns;
+            const uint64_t x = dec_walk<false>(d, T.h, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(),
+                                               ent_len * 8, est[j], (j + 1) * S, n, 0, ns);
             ncnt[j] = n;
             if (x != est[j + 1]) {
                 est[j + 1] = x;
@@ -111,15 +113,29 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
     for (uint32_t j = 0; j < nsub; j++) boff[j + 1] = boff[j] + ncnt[j];
     if ((int64_t)boff[nsub] != d.nblocks) return ICX_E_CORRUPT;
 
-    // ---- write pass
-    std::vector<int16_t> coefs((size_t)d.nblocks * 64, 0);
-    std::vector<int32_t> dc((size_t)d.nblocks, 0);
+    // ---- write pass: blocks owned by the subsequence where their DC starts,
+    // assembled in a per-thread buffer and flushed whole (no pre-zeroing:
+    // the coefficient array starts as garbage to prove every block is written)
+    std::vector<int16_t> coefs((size_t)d.nblocks * 64, (int16_t)0x5A5A);
+    std::vector<int32_t> dc((size_t)d.nblocks, 0x5A5A5A5A);
     d.coefs = coefs.data();
     d.dc = dc.data();
-    for (uint32_t j = 0; j < nsub; j++) {
+    struct Sink {
+        int16_t buf[64] = {};
+        int16_t* out;
+        void coef(int k, int v) { buf[k] = (int16_t)v; }
+        void flush(int64_t bi)
+        {
+            memcpy(out + bi * 64, buf, sizeof(buf));
+            memset(buf, 0, sizeof(buf));
+        }
+    };
+    for (uint32_t j : order) {
         uint32_t n;
-        dec_walk<true>(d, T.h, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8, est[j], (j + 1) * S, n,
-                       boff[j]);
+        Sink sk;
+        sk.out = coefs.data();
+        dec_walk<true>(d, T.h, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8, est[j],
+                       (j + 1) * S, n, boff[j], sk);
     }
     // ---- DC prediction per component, reset every restart interval
     int pred[3] = {0, 0, 0};
