@@ -89,13 +89,61 @@ def cpu_baseline(frames, n_sample, threads):
                       f"{enc} full encodes, {dt:.2f} s wall"}, sizes
 
 
+def e2e_leg(codec, dev, n_frames, steps, distinct=8):
+    """Secondary measurement: the whole per-image hot loop of processImage on
+    the device — q95 4:2:0 4K JPEG files resident in HBM -> decode (A11,
+    decodeImageWithSubsampling) -> compressJpgWithTargetSize at -t 1 MiB with
+    the cached q = 0.25 (A2-A10) -> output bytes in HBM.  Sources: `distinct`
+    synthetic frames (half smooth, half noise) encoded by libjpeg-turbo at
+    q95, repeated to n_frames."""
+    import io
+    from PIL import Image
+    srcs = []
+    for i in range(distinct):
+        f = make_frames(1, 777 + i * 2 + (i % 2), dev)[0] if i % 2 == 0 else \
+            torch.randint(0, 256, (H, W, 3), generator=torch.Generator(device=dev).manual_seed(555 + i),
+                          device=dev, dtype=torch.uint8)
+        b = io.BytesIO()
+        Image.fromarray(f.cpu().numpy()[:, :, ::-1].copy()).save(b, "JPEG", quality=95, subsampling=2)
+        srcs.append(torch.from_numpy(np.frombuffer(b.getvalue(), np.uint8).copy()).to(dev))
+    ins = [srcs[i % distinct] for i in range(n_frames)]
+    px = [torch.empty((H, W, 3), dtype=torch.uint8, device=dev) for _ in range(n_frames)]
+    outs = torch.empty((n_frames, TARGET + 1), dtype=torch.uint8, device=dev)
+    dec = codec.prepare_decode(ins, px, subsampling=0)
+    fit = codec.prepare(px, TARGET, Q0, cached=[icx.LearnedParams(Q0, 1.0)] * n_frames,
+                        outputs=[outs[i] for i in range(n_frames)])
+    assert all(s == 0 for s in dec.run())
+    fit.run()
+    assert all(r["success"] and r["status"] == 0 for r in fit.results())
+    torch.cuda.synchronize()
+    td = tf = 0.0
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        dec.run()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        fit.run()
+        torch.cuda.synchronize()
+        td += t1 - t0
+        tf += time.perf_counter() - t1
+    mp = n_frames * W * H / 1e6
+    return {"metric": "megapixels/sec 4K q95 JPEG bytes in HBM -> device decode -> target-size encode (-t 1MiB, "
+                      "q=0.25 cached)",
+            "value": round(mp * steps / (td + tf), 1), "unit": "MP/s", "frames": n_frames, "steps": steps,
+            "ms_per_step": round((td + tf) / steps * 1e3, 3), "decode_ms_per_step": round(td / steps * 1e3, 3),
+            "encode_ms_per_step": round(tf / steps * 1e3, 3),
+            "decode_mp_s": round(mp * steps / td, 1),
+            "mean_src_jpeg_bytes": int(np.mean([s.numel() for s in srcs]))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--images", type=int, default=1000, help="4K frames per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=16)
+    ap.add_argument("--cpu-sample", type=int, default=320, help="4K frames for the CPU baseline (~10 s on 16 cores)")
+    ap.add_argument("--e2e", type=int, default=200, help="frames of the decode+encode leg (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
     ap.add_argument("--target", type=int, default=TARGET, help="-t bytes (default 1 MiB)")
@@ -190,6 +238,9 @@ def main():
         "roofline": roof,
         "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k, v in kstats.items()},
     }
+    if rank == 0 and world == 1 and args.e2e and not args.host_io:
+        batch = None
+        line["e2e"] = e2e_leg(codec, dev, args.e2e, args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         cb, _ = cpu_baseline(frames, args.cpu_sample, threads)

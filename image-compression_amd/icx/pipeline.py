@@ -13,9 +13,15 @@ Differences that are design, not semantics:
   * the learned-cache lookup for an image happens when its group is formed
     (the reference's lookups also race with other tasks' puts: results of
     both depend on completion order).
-Decoding uses libjpeg-turbo through Pillow (6b-lineage ISLOW IDCT + h2v2 fancy
-upsampling, the JDK decoder's arithmetic); device decode is the
-next row of the plan.
+JPEG files the device decoder supports (baseline/extended Huffman, one
+interleaved scan or grey, any restart interval — icx_jpeg_info) are only read
+and header-parsed on the host threads; each device group decodes them on the
+GPU (icx_decode_jpg_batch: the JDK reader's IJG 6b arithmetic plus source
+subsampling) straight into HBM tensors that the encoder then reads, so no
+decoded pixel crosses PCIe.  Other files (progressive/CMYK JPEG, PNG, GIF,
+BMP, ...) and JPEGs the device decoder rejects as corrupt are decoded on the
+host with libjpeg-turbo / Pillow (6b-lineage ISLOW IDCT + h2v2 fancy
+upsampling for JPEG).
 """
 import concurrent.futures as cf
 import logging
@@ -41,12 +47,22 @@ IMAGEIO_FORMATS = {"JPEG": "jpeg", "PNG": "png", "GIF": "gif", "BMP": "bmp", "TI
 
 @dataclass
 class DecodedImage:
-    """core/DecodedImage.java:7-16: pixels + the reader's format name."""
-    image: np.ndarray
+    """core/DecodedImage.java:7-16: pixels + the reader's format name.
+
+    For a JPEG left to the device decoder, image is None until its group is
+    decoded and `data` holds the file bytes."""
+    image: Optional[np.ndarray]
     format_name: str
     width: int
     height: int
     subsampling: int
+    data: Optional[bytes] = None
+
+    @property
+    def decoded_dims(self):
+        """Dimensions after source subsampling (what reader.read(0, param) returns)."""
+        s = self.subsampling
+        return -(-self.width // s), -(-self.height // s)
 
 
 def format_file_size(size: int) -> str:
@@ -72,14 +88,42 @@ def _to_array(im):
     return np.ascontiguousarray(rgb[:, :, ::-1])  # TYPE_3BYTE_BGR
 
 
-def decode_image_with_subsampling(input_path, params: CompressionParams, file_size: int) -> Optional[DecodedImage]:
+def _device_jpeg(input_path, params: CompressionParams):
+    """The header of a JPEG the device decoder supports, else None."""
+    from .core import jpeg_info
+    with open(input_path, "rb") as f:
+        data = f.read()
+    if data[:2] != b"\xff\xd8":
+        return None
+    st, w, h, _ = jpeg_info(data)
+    if st != N.OK:
+        return None
+    if w <= params.min_width or h <= params.min_height:  # ImageCompression.java:131
+        log.debug("%s - 跳過: 圖片尺寸 %dx%d 未超過最小壓縮門檻 %dx%d", input_path, w, h, params.min_width,
+                  params.min_height)
+        return False
+    s = subsampling_factor(w, h)
+    if s > 1:
+        log.debug("%s - 對圖片應用二次取樣，比率: %d", os.path.basename(str(input_path)), s)
+    return DecodedImage(None, "jpeg", w, h, s, data)
+
+
+def decode_image_with_subsampling(input_path, params: CompressionParams, file_size: int,
+                                  device_jpeg: bool = False) -> Optional[DecodedImage]:
     """ImageCompression.decodeImageWithSubsampling: None when the file is at or
-    below -s, has no reader, or is not larger than (-w, -i) on both axes."""
+    below -s, has no reader, or is not larger than (-w, -i) on both axes.
+    device_jpeg: leave supported JPEGs undecoded for the GPU (DecodedImage.data)."""
     from PIL import Image
     if file_size <= params.min_size_bytes:
         log.info("%s - 跳過: 檔案大小 %s 未超過最小壓縮門檻 %s", input_path, format_file_size(file_size),
                  format_file_size(params.min_size_bytes))
         return None
+    if device_jpeg:
+        d = _device_jpeg(input_path, params)
+        if d is False:
+            return None
+        if d is not None:
+            return d
     try:
         im = Image.open(input_path)
     except (Image.UnidentifiedImageError, ValueError):
@@ -113,7 +157,7 @@ class _Item:
     output: Optional[str] = None
 
 
-def _prepare(index, path, output_dir, params) -> _Item:
+def _prepare(index, path, output_dir, params, device_jpeg=False) -> _Item:
     """processImage up to and including the decode (ImageCompression.java:53-76)."""
     it = _Item(index, path)
     try:
@@ -126,7 +170,7 @@ def _prepare(index, path, output_dir, params) -> _Item:
         it.report = CompressionReport(CompressionResult.FAILED_IO_ERROR, 0, 0)
         return it
     try:
-        d = decode_image_with_subsampling(path, params, it.original_size)
+        d = decode_image_with_subsampling(path, params, it.original_size, device_jpeg)
     except MemoryError:
         it.report = CompressionReport(CompressionResult.FAILED_OUT_OF_MEMORY, it.original_size, 0)
         return it
@@ -179,8 +223,38 @@ def _fail(it: _Item, exc: BaseException):
     it.decoded = None
 
 
+def _host_decode(path, s):
+    """libjpeg-turbo decode + source subsampling (files the device decoder refused)."""
+    from PIL import Image
+    with Image.open(path) as im:
+        arr = _to_array(im)
+    return np.ascontiguousarray(arr[::s, ::s]) if s > 1 else arr
+
+
+def decode_group(codec, items: List[_Item]):
+    """Decode the group's device-decodable JPEGs on the GPU (one batch, output
+    left in HBM); a file the device decoder rejects is decoded on the host."""
+    todo = [it for it in items if it.decoded.image is None]
+    if not todo:
+        return
+    res = codec.decode_jpg_batch([it.decoded.data for it in todo], subsampling=0, device_out=True)
+    for it, (st, img) in zip(todo, res):
+        if st == N.OK:
+            it.decoded.image = img
+        else:
+            log.warning("%s - GPU 解碼失敗 (icx status %d)，改用主機解碼", it.path, st)
+            it.decoded.image = _host_decode(it.path, it.decoded.subsampling)
+        it.decoded.data = None
+
+
 def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, cache):
     """compressJpgWithTargetSize for a group of decoded JPEGs in one device batch."""
+    try:
+        decode_group(codec, items)
+    except Exception as e:  # context-level failure: every image of the group fails alike
+        for it in items:
+            _fail(it, e)
+        return
     keys = [create_key(it.decoded.image, it.original_size) for it in items]
     with cache.lock:
         cached = [cache.get(k) for k in keys]
@@ -232,7 +306,7 @@ def process_image(input_path, output_dir, params: CompressionParams, cache, code
     from .cache import LockedDict
     if not hasattr(cache, "lock"):
         cache = LockedDict(cache) if cache is not None else LockedDict()
-    it = _prepare(0, str(input_path), output_dir, params)
+    it = _prepare(0, str(input_path), output_dir, params, hasattr(codec, "decode_jpg_batch"))
     if it.report is None:
         compress_image_iteratively(codec, it, params, cache)
     return it.report
@@ -307,7 +381,8 @@ class CompressionBatch:
 
     def __init__(self, file_list_path, save_dir, params: CompressionParams, time_out_hr: float = 24,
                  h2_cache_path="image-compression-cache", codecs=None, group_size: int = 16,
-                 decode_threads: Optional[int] = None, rank: int = 0, world: int = 1):
+                 decode_threads: Optional[int] = None, rank: int = 0, world: int = 1,
+                 device_decode: Optional[bool] = None):
         self.file_list_path = file_list_path
         self.save_dir = save_dir
         self.params = params
@@ -317,6 +392,10 @@ class CompressionBatch:
         self.group_size = max(1, group_size)
         self.decode_threads = decode_threads or min(16, os.cpu_count() or 1)
         self.rank, self.world = rank, world
+        # JPEG decode on the GPU when every codec can (the default for icx.Codec)
+        if device_decode is None:
+            device_decode = bool(self.codecs) and all(hasattr(c, "decode_jpg_batch") for c in self.codecs)
+        self.device_decode = device_decode
 
     def execute(self, cache=None, save_cache: bool = True) -> BatchReport:
         from .cache import CacheManager, LockedDict
@@ -378,7 +457,7 @@ class CompressionBatch:
             w.start()
         pending_jpeg: List[_Item] = []
         with cf.ThreadPoolExecutor(self.decode_threads) as pool:
-            futs = [pool.submit(_prepare, i, p, self.save_dir, self.params) for i, p in mine]
+            futs = [pool.submit(_prepare, i, p, self.save_dir, self.params, self.device_decode) for i, p in mine]
             try:
                 for f in cf.as_completed(futs, timeout=max(0.0, deadline - time.perf_counter())):
                     it = f.result()
@@ -386,7 +465,7 @@ class CompressionBatch:
                         done_items.append(it)
                     if it.report is not None:
                         continue
-                    it.mp = it.decoded.width * it.decoded.height / 1e6
+                    it.mp = it.decoded.width * it.decoded.height / 1e6  # source pixels
                     if not self.codecs:
                         raise RuntimeError("no GPU codec available to compress decoded images")
                     fmt = it.decoded.format_name

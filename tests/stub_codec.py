@@ -24,6 +24,18 @@ class OracleCodec:
                         "data": r["data"]})
         return res
 
+    def decode_jpg_batch(self, datas, subsampling=0, device_out=False):
+        """The oracle's IJG 6b decode (+ the reference's subsampling rule)."""
+        out = []
+        for d in datas:
+            rc, w, h, _ = self.o.jpeg_info(d)
+            if rc:
+                out.append((rc, None))
+                continue
+            s = subsampling if subsampling > 0 else self.o.subsampling(w, h)
+            out.append(self.o.jpeg_decode(d, s))
+        return out
+
     def compress_png_with_target_size(self, img, output_file, params):
         w, h = image_dims(img)
         if w <= params.min_width and h <= params.min_height:
