@@ -92,9 +92,20 @@ uint32_t pick_sub_bits(uint64_t total_bits)
         const long v = atol(e);
         if (v >= 64 && (v & (v - 1)) == 0) return (uint32_t)v;
     }
-    uint32_t S = 2048;  // enough subsequences to fill the chip, as few as possible (less re-walking)
-    while (S < 16384 && total_bits / S > 524288) S *= 2;
+    // Long subsequences re-walk least (measured on 4K q95: 16384 beats 8192 for
+    // smooth and noise content); shorter ones only when the batch would not
+    // give the chip ~64k threads.
+    uint32_t S = 16384;
+    while (S > 2048 && total_bits / S < 65536) S /= 2;
     return S;
+}
+
+// Warm-up walk before each subsequence (k_dec_init): long enough for typical
+// content to resynchronise, short against the subsequence.
+uint32_t warm_bits(uint32_t sub_bits)
+{
+    if (const char* e = getenv("ICX_DEC_WARM")) return (uint32_t)atol(e);
+    return std::min<uint32_t>(4096, sub_bits / 4);
 }
 
 struct WPlan {
@@ -292,24 +303,32 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         e = hipMemsetAsync(d_changed, 0, (size_t)max_it * 4, c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "counter clear");
 
-        std::vector<int64_t> cnt_tiles(m), cnt_subs(m), cnt_blk(m), cnt_px(m);
+        std::vector<int64_t> cnt_tiles(m), cnt_subs(m), cnt_blk(m), cnt_px(m), cnt_rows(m);
         int64_t stuffed = 0;
         for (int k = 0; k < m; k++) {
             cnt_tiles[k] = sub[k]->ntiles;
             cnt_subs[k] = (desc[k].nsub_max + 1 + 255) / 256;
             cnt_blk[k] = (desc[k].nblocks + 31) / 32;
-            cnt_px[k] = ((int64_t)desc[k].oh * ((desc[k].ow + 3) / 4) + 255) / 256;
+            // colour: the row-pair kernel for s == 1 4:2:0 fancy, the per-pixel gather kernel otherwise
+            const bool rows = desc[k].s == 1 && desc[k].ncomp == 3 && desc[k].hs == 2 && desc[k].vs == 2 &&
+                              desc[k].fancy;
+            cnt_px[k] = rows ? 0 : ((int64_t)desc[k].oh * ((desc[k].ow + 3) / 4) + 255) / 256;
+            cnt_rows[k] = rows ? (int64_t)((desc[k].oh + 1) / 2) * ((desc[k].ow + 1023) / 1024) : 0;
             stuffed += desc[k].scan_len;
         }
-        WPlan Pt, Ps, Pb, Pp;
+        WPlan Pt, Ps, Pb, Pp, Pr;
         if ((st = plan_of(c, cnt_tiles, d_ids, Pt)) || (st = plan_of(c, cnt_subs, d_ids, Ps)) ||
-            (st = plan_of(c, cnt_blk, d_ids, Pb)) || (st = plan_of(c, cnt_px, d_ids, Pp)))
+            (st = plan_of(c, cnt_blk, d_ids, Pb)) || (st = plan_of(c, cnt_px, d_ids, Pp)) ||
+            (st = plan_of(c, cnt_rows, d_ids, Pr)))
             return st;
         {
             Timed tm(c, "dec_unstuff", stuffed);
             launch_unstuff(d_desc, d_state, Pt.p, Pt.total, d_ids, m, S, c->stream);
         }
-        launch_dec_init(d_desc, Ps.p, Ps.total, S, c->stream);
+        {
+            Timed tm(c, "dec_init", stuffed);
+            launch_dec_init(d_desc, d_state, Ps.p, Ps.total, S, warm_bits(S), c->stream);
+        }
         // ---- settle the subsequence entry states
         int it = 0;
         for (;;) {
@@ -342,6 +361,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             }
             {
                 Timed tm(c, "dec_color", px);
+                launch_dec_color_420(d_desc, d_state, Pr.p, Pr.total, c->stream);
                 launch_dec_color(d_desc, d_state, Pp.p, Pp.total, c->stream);
             }
         }

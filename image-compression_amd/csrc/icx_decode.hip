@@ -218,16 +218,39 @@ __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const
 }
 
 // ------------------------------------------------------------ entropy decode
-__global__ void __launch_bounds__(256) k_dec_init(const DecDesc* D, Plan p, uint32_t sub_bits)
+// Initial entry-state estimates: subsequence j starts decoding `warm` bits
+// before its first bit from a guessed state (block 0, DC next) and takes the
+// state at which that walk reaches j * sub_bits.  A Huffman decoder
+// resynchronises within a few hundred bits on typical content, so most
+// estimates are already the fixed point and the first sync launch confirms
+// them; the rest are repaired by the relaxation like any other guess.
+__device__ __forceinline__ void load_tables(const DecTab* T, DecHuff* L);
+__device__ __forceinline__ uint32_t selector(const DecTab* T);
+
+__global__ void __launch_bounds__(256) k_dec_init(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
+                                                  uint32_t warm)
 {
+    __shared__ __attribute__((aligned(16))) DecHuff L[4];
     const int slot = slot_of(p.prefix, p.m, blockIdx.x);
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
+    const DecState& st = S[img];
     const int64_t j = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
+    const bool live = st.status == 0 && (blockIdx.x - p.prefix[slot]) * 256 < (int64_t)st.nsub;
+    if (live) load_tables(d.tab, L);
     if (j > d.nsub_max) return;
-    d.est[j] = dec_pack((uint32_t)j * sub_bits, 0, 0);
     d.dirty[0][j] = 1;
     d.dirty[1][j] = 0;
+    const uint32_t start = (uint32_t)j * sub_bits;
+    uint64_t e = dec_pack(start, 0, 0);
+    if (live && j > 0 && j < st.nsub && warm > 0) {
+        const uint32_t from = start > warm ? start - warm : 0;
+        uint32_t n;
+        NoSink ns;
+        e = dec_walk<false>(d, L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
+                            st.ent_len * 8, dec_pack(from, 0, 0), start, n, 0, ns);
+    }
+    d.est[j] = e;
 }
 
 // Stage the image's distinct Huffman tables in LDS (all threads participate).
@@ -297,8 +320,11 @@ __global__ void __launch_bounds__(1024) k_dec_offsets(const DecDesc* D, DecState
     }
 }
 
-// Per-thread block assembly slot in LDS: 64 int16 at a stride of 33 dwords
-// (consecutive threads' slots start on consecutive banks).
+// Per-thread block assembly slot in LDS: 64 int16 at a stride of 33 dwords, so
+// the 64 lanes' slots start on 64 distinct banks and lanes storing the same
+// zig-zag position (they walk in near lockstep) do not collide.  (A 16-B
+// aligned 36-dword stride allows 128-bit flushes but measured 25 % slower:
+// 4-way conflicts on those coefficient stores.)
 constexpr int SLOT_DW = 33;
 struct LdsBlockSink {
     int16_t* slot;   // this thread's slot
@@ -310,8 +336,12 @@ struct LdsBlockSink {
         uint4* dst = (uint4*)(coefs + bi * 64);
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-            dst[q] = make_uint4(s32[4 * q], s32[4 * q + 1], s32[4 * q + 2], s32[4 * q + 3]);
-            s32[4 * q] = s32[4 * q + 1] = s32[4 * q + 2] = s32[4 * q + 3] = 0;
+            const uint4 v = make_uint4(s32[4 * q], s32[4 * q + 1], s32[4 * q + 2], s32[4 * q + 3]);
+            s32[4 * q] = 0;
+            s32[4 * q + 1] = 0;
+            s32[4 * q + 2] = 0;
+            s32[4 * q + 3] = 0;
+            dst[q] = v;
         }
     }
 };
@@ -319,7 +349,7 @@ struct LdsBlockSink {
 __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits)
 {
     __shared__ __attribute__((aligned(16))) DecHuff L[4];
-    __shared__ uint32_t slots[256 * SLOT_DW];
+    __shared__ __attribute__((aligned(16))) uint32_t slots[256 * SLOT_DW];
     const int slot = slot_of(p.prefix, p.m, blockIdx.x);
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
@@ -563,6 +593,93 @@ __global__ void __launch_bounds__(256) k_dec_color(const DecDesc* D, const DecSt
     }
 }
 
+// s == 1, 4:2:0 with fancy upsampling (the JDK decode of nearly every photo):
+// one workgroup per output row pair (2r, 2r+1) x 1024 columns.  Both luma rows
+// and chroma rows r-1, r, r+1 (edge-replicated, jdmainct.c context rows) are
+// staged in LDS with coalesced loads; each thread converts a 4 x 2 pixel tile
+// from the 3 x 4 chroma neighbourhood it shares (h2v2_fancy_upsample).
+constexpr int CT_PX = 1024;
+__global__ void __launch_bounds__(256) k_dec_color_420(const DecDesc* D, const DecState* S, Plan p)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t ly[2][CT_PX];
+    __shared__ uint8_t lc[2][3][CT_PX / 2 + 8];  // [cb|cr][row r-1|r|r+1], chroma column c at c - cbase
+    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    const int img = p.ids[slot];
+    const DecDesc& d = D[img];
+    if (S[img].status) return;
+    const int tpr = (d.ow + CT_PX - 1) / CT_PX;
+    const int64_t item = blockIdx.x - p.prefix[slot];
+    const int r = (int)(item / tpr), x0 = (int)(item % tpr) * CT_PX;
+    const int n = d.ow - x0 < CT_PX ? d.ow - x0 : CT_PX;
+    const int t = threadIdx.x;
+    const int y0 = 2 * r, rows = d.oh - y0 < 2 ? 1 : 2;
+    for (int q = 0; q < rows; q++) {
+        const uint32_t* yr = (const uint32_t*)(d.plane[0] + (int64_t)(y0 + q) * d.pw[0] + x0);
+        if (4 * t < n) ((uint32_t*)ly[q])[t] = yr[t];
+    }
+    const int cw = d.cw[1], ch = d.ch[1];
+    const int cbase = (x0 >> 1) - 1, cn = (n + 1) / 2 + 2;
+    for (int q = 0; q < 6; q++) {
+        const int comp = q / 3, dr = q % 3 - 1;
+        int rr = r + dr;
+        rr = rr < 0 ? 0 : rr > ch - 1 ? ch - 1 : rr;
+        const uint8_t* P = d.plane[1 + comp] + (int64_t)rr * d.pw[1 + comp];
+        for (int c = t; c < cn; c += 256) {
+            int col = cbase + c;
+            col = col < 0 ? 0 : col > cw - 1 ? cw - 1 : col;  // edge columns are special-cased below
+            lc[comp][dr + 1][c] = P[col];
+        }
+    }
+    __syncthreads();
+    const int xt = 4 * t;  // first of this thread's 4 columns (local)
+    if (xt >= n) return;
+    const int i0 = ((x0 + xt) >> 1);  // chroma columns i0, i0 + 1
+    const int li = i0 - cbase;        // local index of i0 (>= 1)
+    int cv[2][2][4];                  // [comp][top|bottom row][column]
+#pragma unroll
+    for (int comp = 0; comp < 2; comp++) {
+        int cs_t[4], cs_b[4];  // column sums for i0-1 .. i0+2
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int a = lc[comp][1][li - 1 + k] * 3;
+            cs_t[k] = a + lc[comp][0][li - 1 + k];
+            cs_b[k] = a + lc[comp][2][li - 1 + k];
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int* cs = h ? cs_b : cs_t;
+#pragma unroll
+            for (int u = 0; u < 2; u++) {  // chroma column i0 + u -> output columns 2u, 2u + 1
+                const int i = i0 + u, c = cs[1 + u];
+                cv[comp][h][2 * u] = i == 0 ? (c * 4 + 8) >> 4 : (c * 3 + cs[u] + 8) >> 4;
+                cv[comp][h][2 * u + 1] = i == cw - 1 ? (c * 4 + 7) >> 4 : (c * 3 + cs[2 + u] + 7) >> 4;
+            }
+        }
+    }
+    const int m = n - xt < 4 ? n - xt : 4;
+    for (int h = 0; h < rows; h++) {
+        uint32_t w[3] = {0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int yy = ly[h][xt + k];
+            const int cb = cv[0][h][k] - 128, cr = cv[1][h][k] - 128;
+            const uint32_t B = clamp255(yy + ((116130 * cb + 32768) >> 16));
+            const uint32_t G = clamp255(yy + ((-22554 * cb + 32768 - 46802 * cr) >> 16));
+            const uint32_t R = clamp255(yy + ((91881 * cr + 32768) >> 16));
+            const int o = 3 * k;  // byte offset inside the 12-byte group
+            w[o >> 2] |= B << (8 * (o & 3));
+            w[(o + 1) >> 2] |= G << (8 * ((o + 1) & 3));
+            w[(o + 2) >> 2] |= R << (8 * ((o + 2) & 3));
+        }
+        uint8_t* o = d.out + (int64_t)(y0 + h) * d.ostride + (int64_t)(x0 + xt) * 3;
+        if (m == 4 && (((uintptr_t)o) & 3) == 0) {
+            *(uint3*)o = make_uint3(w[0], w[1], w[2]);
+        } else {
+            for (int k = 0; k < 3 * m; k++) o[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+}
+
 // ---------------------------------------------------------------- launchers
 void launch_unstuff(const DecDesc* d, DecState* s, const Plan& tiles, int64_t ntiles, const int32_t* ids, int m,
                     uint32_t sub_bits, hipStream_t st)
@@ -574,9 +691,10 @@ void launch_unstuff(const DecDesc* d, DecState* s, const Plan& tiles, int64_t nt
     hipLaunchKernelGGL(k_unstuff_scatter, dim3((unsigned)ntiles), dim3(256), 0, st, d, s, tiles);
 }
 
-void launch_dec_init(const DecDesc* d, const Plan& subs, int64_t nwg, uint32_t sub_bits, hipStream_t st)
+void launch_dec_init(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
+                     uint32_t warm, hipStream_t st)
 {
-    if (nwg > 0) hipLaunchKernelGGL(k_dec_init, dim3((unsigned)nwg), dim3(256), 0, st, d, subs, sub_bits);
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_init, dim3((unsigned)nwg), dim3(256), 0, st, d, s, subs, sub_bits, warm);
 }
 
 void launch_dec_sync(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
@@ -610,6 +728,11 @@ void launch_dec_idct(const DecDesc* d, const DecState* s, const Plan& blocks, in
 void launch_dec_color(const DecDesc* d, const DecState* s, const Plan& px, int64_t nwg, hipStream_t st)
 {
     if (nwg > 0) hipLaunchKernelGGL(k_dec_color, dim3((unsigned)nwg), dim3(256), 0, st, d, s, px);
+}
+
+void launch_dec_color_420(const DecDesc* d, const DecState* s, const Plan& rows, int64_t nwg, hipStream_t st)
+{
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_color_420, dim3((unsigned)nwg), dim3(256), 0, st, d, s, rows);
 }
 
 }  // namespace icx

@@ -11,7 +11,9 @@ namespace icx {
 void launch_unstuff(const DecDesc* d, DecState* s, const Plan& tiles, int64_t ntiles, const int32_t* ids, int m,
                     uint32_t sub_bits, hipStream_t st);
 // subs: per image ceil((nsub_max + 1) / 256) workgroups
-void launch_dec_init(const DecDesc* d, const Plan& subs, int64_t nwg, uint32_t sub_bits, hipStream_t st);
+// warm: bits decoded before each subsequence start to estimate its entry state
+void launch_dec_init(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
+                     uint32_t warm, hipStream_t st);
 void launch_dec_sync(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
                      int parity, uint32_t* changed, hipStream_t st);
 void launch_dec_offsets(const DecDesc* d, DecState* s, const int32_t* ids, int m, hipStream_t st);
@@ -20,7 +22,9 @@ void launch_dec_write(const DecDesc* d, const DecState* s, const Plan& subs, int
 void launch_dec_dc(const DecDesc* d, const DecState* s, const int32_t* ids, int m, hipStream_t st);
 // blocks: per image ceil(nblocks / 32) workgroups
 void launch_dec_idct(const DecDesc* d, const DecState* s, const Plan& blocks, int64_t nwg, hipStream_t st);
-// px: per image ceil(oh * ceil(ow / 4) / 256) workgroups
+// px: per image ceil(oh * ceil(ow / 4) / 256) workgroups (any source subsampling)
 void launch_dec_color(const DecDesc* d, const DecState* s, const Plan& px, int64_t nwg, hipStream_t st);
+// rows: per image ceil(oh / 2) * ceil(ow / 1024) workgroups (s == 1, 4:2:0 fancy only)
+void launch_dec_color_420(const DecDesc* d, const DecState* s, const Plan& rows, int64_t nwg, hipStream_t st);
 
 }  // namespace icx

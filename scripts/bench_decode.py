@@ -59,7 +59,7 @@ def main():
         P.run()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
-    kern = {k: codec.profile_query(k) for k in ("dec_unstuff", "dec_sync", "dec_write", "dec_dc", "dec_idct",
+    kern = {k: codec.profile_query(k) for k in ("dec_unstuff", "dec_init", "dec_sync", "dec_write", "dec_dc", "dec_idct",
                                                  "dec_color", "dec_sync_iters")}
     mp = a.frames * a.height * a.width / 1e6
     stuffed = sum(len(srcs[i % len(srcs)]) for i in range(a.frames))

@@ -11,6 +11,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <random>
 #include <vector>
@@ -20,9 +22,15 @@
 
 using namespace icx;
 
+extern "C" {
+long dec_emu_walks = 0;  // subsequence walks in the sync launches of the last call (work measure)
+long dec_emu_nsub = 0;
+}
+
 extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_t nblocks_cap, int seed,
                              int sub_bits, int* iterations)
 {
+    const bool warm_up = seed % 2 == 0;  // odd seeds: plain guesses, even seeds: warm-up estimates (k_dec_init)
     JpegHeader J;
     icx_status st = parse_jpeg(jpg, len, len, J);
     if (st) return (int)st;
@@ -81,11 +89,23 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
     std::vector<uint64_t> est(nsub + 1);
     std::vector<uint8_t> dirty[2] = {std::vector<uint8_t>(nsub + 1, 1), std::vector<uint8_t>(nsub + 1, 0)};
     std::vector<uint32_t> ncnt(nsub, 0);
-    for (uint32_t j = 0; j <= nsub; j++) est[j] = dec_pack(j * S, 0, 0);
+    uint32_t warm = std::min<uint32_t>(4096, S / 4);  // as icx_decode.cpp warm_bits
+    if (const char* e = getenv("ICX_DEC_WARM")) warm = (uint32_t)atol(e);
+    for (uint32_t j = 0; j <= nsub; j++) {
+        est[j] = dec_pack(j * S, 0, 0);
+        if (j > 0 && j < nsub && warm_up) {
+            uint32_t n;
+            NoSink ns;
+            est[j] = dec_walk<false>(d, T.h, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8,
+                                     dec_pack(j * S > warm ? j * S - warm : 0, 0, 0), j * S, n, 0, ns);
+        }
+    }
     std::mt19937 rng((uint32_t)seed);
     std::vector<uint32_t> order(nsub);
     for (uint32_t j = 0; j < nsub; j++) order[j] = j;
     int it = 0;
+    dec_emu_walks = 0;
+    dec_emu_nsub = nsub;
     for (;; it++) {
         if (it > (int)nsub + 2) return ICX_E_CORRUPT;  // cannot happen: one subsequence settles per launch
         std::vector<uint8_t>& cur = dirty[it & 1];
@@ -95,6 +115,7 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
         for (uint32_t j : order) {
             if (!cur[j]) continue;
             cur[j] = 0;
+            dec_emu_walks++;
             uint32_t n;
             NoSink ns;
             const uint64_t x = dec_walk<false>(d, T.h, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(),
