@@ -235,21 +235,41 @@ struct NoSink {
     ICX_HD void flush(int64_t) {}
 };
 
-template <bool OWNED, class HuffPtr, class Sink>
-ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, uint32_t selp, const uint32_t* words,
-                         const uint32_t* seg, uint32_t nseg, uint32_t ent_bits, uint64_t st, uint32_t stop,
-                         uint32_t& nblk, int64_t blk_base, Sink& sink)
-{
-    uint32_t pos = dec_pos(st);
-    nblk = 0;
-    int b = (int)((st >> 8) & 7), z = (int)(st & 63);
-    if (pos >= stop && (!OWNED || z == 0)) return st;
-    bool own = z == 0;
+// The walk as a state object, one symbol per step() (the device write pass
+// drives it from a wave-uniform loop so finished blocks can be flushed by the
+// whole wave between steps).
+template <bool OWNED, class HuffPtr>
+struct DecWalker {
+    const DecDesc* d;
+    HuffPtr H;
+    const DecSlow* slow;
+    uint32_t selp;
+    const uint32_t* words;
+    const uint32_t* seg;
+    uint32_t nseg, ent_bits;
+    uint32_t pos, n;
+    int b, z, comp;
+    bool own;
+    int64_t blk_base;
     DecReader R;
-    R.init(words, pos);
-    int comp = b < d.nby ? 0 : b - d.nby + 1;
-    uint32_t n = 0;
-    while (pos < stop || (OWNED && z != 0)) {
+
+    ICX_HD void start(uint64_t st)
+    {
+        pos = dec_pos(st);
+        b = (int)((st >> 8) & 7);
+        z = (int)(st & 63);
+        n = 0;
+        own = z == 0;
+        comp = b < d->nby ? 0 : b - d->nby + 1;
+        R.init(words, pos);
+    }
+    ICX_HD bool running(uint32_t stop) const { return pos < stop || (OWNED && z != 0); }
+    ICX_HD uint64_t state() const { return dec_pack(pos, b, z); }
+
+    // Decode one symbol (or take one invalid-code transition).
+    template <class Sink>
+    ICX_HD void step(Sink& sink)
+    {
         R.refill();
         const int ti = dec_sel(selp, comp, z ? 1 : 0);
         const uint32_t e = dec_symbol(&H[ti], &slow[ti], R.peek16());
@@ -264,16 +284,16 @@ ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, uint3
             if (pos + 8 < bound) {  // mid-interval: only a wrong-start path gets here; resume a bit later
                 pos++;
                 R.init(words, pos);
-                continue;
+                return;
             }
             // the interval's 1-bit padding (< 8 bits) or its pad bytes: next interval
             if (nx == DEC_END) {
                 pos = DEC_END;
-                break;
+                return;
             }
             pos = nx * 8;
             R.init(words, pos);
-            continue;
+            return;
         }
         R.skip(len);
         if (z == 0) {
@@ -281,7 +301,7 @@ ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, uint3
             pos += (uint32_t)(len + sym);
             if (OWNED) {
                 const int64_t bi = blk_base + n;
-                if (bi < d.nblocks) d.dc[bi] = sym ? dec_extend(v, sym) : 0;
+                if (bi < d->nblocks) d->dc[bi] = sym ? dec_extend(v, sym) : 0;
             }
             z = 1;
         } else {
@@ -300,17 +320,47 @@ ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, uint3
         if (z >= 64) {
             if (OWNED && own) {
                 const int64_t bi = blk_base + n;
-                if (bi < d.nblocks) sink.flush(bi);
+                if (bi < d->nblocks) sink.flush(bi);
             }
             own = true;
             n++;
             z = 0;
-            b = (b + 1 == d.nbmcu) ? 0 : b + 1;
-            comp = b < d.nby ? 0 : b - d.nby + 1;
+            b = (b + 1 == d->nbmcu) ? 0 : b + 1;
+            comp = b < d->nby ? 0 : b - d->nby + 1;
         }
     }
-    nblk = n;
-    return dec_pack(pos, b, z);
+};
+
+template <bool OWNED, class HuffPtr>
+ICX_HD DecWalker<OWNED, HuffPtr> dec_walker(const DecDesc& d, HuffPtr H, const DecSlow* slow, uint32_t selp,
+                                            const uint32_t* words, const uint32_t* seg, uint32_t nseg,
+                                            uint32_t ent_bits, int64_t blk_base)
+{
+    DecWalker<OWNED, HuffPtr> w;
+    w.d = &d;
+    w.H = H;
+    w.slow = slow;
+    w.selp = selp;
+    w.words = words;
+    w.seg = seg;
+    w.nseg = nseg;
+    w.ent_bits = ent_bits;
+    w.blk_base = blk_base;
+    return w;
+}
+
+template <bool OWNED, class HuffPtr, class Sink>
+ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, uint32_t selp, const uint32_t* words,
+                         const uint32_t* seg, uint32_t nseg, uint32_t ent_bits, uint64_t st, uint32_t stop,
+                         uint32_t& nblk, int64_t blk_base, Sink& sink)
+{
+    nblk = 0;
+    if (dec_pos(st) >= stop && (!OWNED || (st & 63) == 0)) return st;
+    DecWalker<OWNED, HuffPtr> w = dec_walker<OWNED>(d, H, slow, selp, words, seg, nseg, ent_bits, blk_base);
+    w.start(st);
+    while (w.running(stop)) w.step(sink);
+    nblk = w.n;
+    return w.state();
 }
 
 // Unstuffing rule for stuffed byte i (jdhuff.c fill_bit_buffer / jdmarker.c):

@@ -181,9 +181,14 @@ __global__ void __launch_bounds__(1024) k_unstuff_scan(const DecDesc* D, DecStat
     }
 }
 
+// Compact one tile: each thread applies the unstuffing rule to its 16 bytes
+// (fully unrolled, no dynamic register indexing), writes its output bytes at
+// its workgroup-local offset in LDS, and the workgroup then copies the tile's
+// contiguous output to HBM with consecutive lanes on consecutive bytes.
 __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const DecState* S, Plan p)
 {
     __shared__ uint32_t sh[8];
+    __shared__ uint8_t buf[DEC_TILE / 2 * DEC_PAD + 64];  // worst case: an RSTn marker every 2 bytes
     const int slot = slot_of(p.prefix, p.m, blockIdx.x);
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
@@ -191,30 +196,40 @@ __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const
     const int64_t base = tile * DEC_TILE + threadIdx.x * 16;
     const int64_t end = S[img].end;
     Bytes16 B;
+    for (int k = 0; k < 16; k++) B.b[k] = 0;
+    B.prev = B.next = 0;
+    if (base < end) load16(d, base, B);
+    int out[16], rsts[16];
     uint32_t nb = 0, nr = 0;
-    if (base < end) {
-        load16(d, base, B);
-        unstuff_counts(B, base, end, nb, nr);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        int rst = 0;
+        const int c = base + k < end
+                          ? dec_unstuff_rule(k ? B.b[k - 1] : B.prev, B.b[k], k < 15 ? B.b[k + 1] : B.next, &rst)
+                          : 0;
+        out[k] = c;
+        rsts[k] = rst;
+        nb += (uint32_t)c;
+        nr += (uint32_t)rst;
     }
     uint32_t tb, tr;
-    uint32_t ob = block_exscan<256>(nb, sh, tb) + d.tile_cnt[tile];
+    uint32_t ob = block_exscan<256>(nb, sh, tb);
     uint32_t orr = block_exscan<256>(nr, sh, tr) + d.tile_rst[tile];
-    if (base >= end) return;
+    const uint32_t tile_off = d.tile_cnt[tile];
+#pragma unroll
     for (int k = 0; k < 16; k++) {
-        if (base + k >= end) break;
-        int rst;
-        const int n = dec_unstuff_rule(k ? B.b[k - 1] : B.prev, B.b[k], k < 15 ? B.b[k + 1] : B.next, &rst);
-        if (rst) {
-            for (int q = 0; q < DEC_PAD; q++)
-                if (ob + q < d.ent_cap) d.ent[ob + q] = 0xFF;
+        if (rsts[k]) {
+            for (int q = 0; q < DEC_PAD; q++) buf[ob + q] = 0xFF;
             ob += DEC_PAD;
-            if (orr + 1 < (uint32_t)d.nseg_max) d.seg[orr + 1] = ob;
+            if (orr + 1 < (uint32_t)d.nseg_max) d.seg[orr + 1] = tile_off + ob;
             orr++;
-        } else if (n) {
-            if (ob < d.ent_cap) d.ent[ob] = B.b[k];
-            ob++;
+        } else if (out[k]) {
+            buf[ob++] = B.b[k];
         }
     }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < tb; k += 256)
+        if ((int64_t)(tile_off + k) < d.ent_cap) d.ent[tile_off + k] = buf[k];
 }
 
 // ------------------------------------------------------------ entropy decode
@@ -322,34 +337,28 @@ __global__ void __launch_bounds__(1024) k_dec_offsets(const DecDesc* D, DecState
 
 // Per-thread block assembly slot in LDS: 64 int16 at a stride of 33 dwords, so
 // the 64 lanes' slots start on 64 distinct banks and lanes storing the same
-// zig-zag position (they walk in near lockstep) do not collide.  (A 16-B
-// aligned 36-dword stride allows 128-bit flushes but measured 25 % slower:
-// 4-way conflicts on those coefficient stores.)
+// zig-zag position (they walk in near lockstep) do not collide.
 constexpr int SLOT_DW = 33;
-struct LdsBlockSink {
-    int16_t* slot;   // this thread's slot
-    int16_t* coefs;  // d.coefs
+
+// A lane that finishes an owned block only records its index; the wave then
+// copies every finished slot together (below).
+struct PendSink {
+    int16_t* slot;
+    int64_t pend;  // block waiting for the wave flush, -1 = none
     __device__ __forceinline__ void coef(int k, int v) { slot[k] = (int16_t)v; }
-    __device__ __forceinline__ void flush(int64_t bi)
-    {
-        uint32_t* s32 = (uint32_t*)slot;
-        uint4* dst = (uint4*)(coefs + bi * 64);
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const uint4 v = make_uint4(s32[4 * q], s32[4 * q + 1], s32[4 * q + 2], s32[4 * q + 3]);
-            s32[4 * q] = 0;
-            s32[4 * q + 1] = 0;
-            s32[4 * q + 2] = 0;
-            s32[4 * q + 3] = 0;
-            dst[q] = v;
-        }
-    }
+    __device__ __forceinline__ void flush(int64_t bi) { pend = bi; }
 };
 
+// Write pass.  The walk runs in a wave-uniform loop, one symbol per lane per
+// iteration; after each step the wave ballots the lanes that finished a block
+// and copies each of those 128-byte slots with 32 lanes (one coalesced dword
+// store each), zeroing it behind.  A per-lane flush would cost every lane of
+// the wave ~70 instructions whenever any lane finishes a block, which on
+// q95 content is most iterations.
 __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits)
 {
     __shared__ __attribute__((aligned(16))) DecHuff L[4];
-    __shared__ __attribute__((aligned(16))) uint32_t slots[256 * SLOT_DW];
+    __shared__ uint32_t slots[256 * SLOT_DW];
     const int slot = slot_of(p.prefix, p.m, blockIdx.x);
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
@@ -357,14 +366,47 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, const DecSt
     if (st.status) return;
     const int64_t j = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
     if ((blockIdx.x - p.prefix[slot]) * 256 >= (int64_t)st.nsub) return;
+    const int lane = threadIdx.x & 63;
+    uint32_t* wave_slots = slots + (threadIdx.x - lane) * SLOT_DW;
     uint32_t* mys = slots + threadIdx.x * SLOT_DW;
     for (int k = 0; k < 32; k++) mys[k] = 0;
     load_tables(d.tab, L);
-    if (j >= st.nsub) return;
-    uint32_t n;
-    LdsBlockSink sink{(int16_t*)mys, d.coefs};
-    dec_walk<true>(d, L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg, st.ent_len * 8,
-                   d.est[j], (uint32_t)(j + 1) * sub_bits, n, d.boff[j], sink);
+    const uint32_t stop = (uint32_t)(j + 1) * sub_bits;
+    DecWalker<true, DecHuff*> w = dec_walker<true>(d, (DecHuff*)L, d.tab->slow, selector(d.tab),
+                                                   (const uint32_t*)d.ent, d.seg, st.nseg, st.ent_len * 8,
+                                                   j < st.nsub ? (int64_t)d.boff[j] : 0);
+    bool run = false;
+    if (j < st.nsub) {
+        const uint64_t e = d.est[j];
+        run = !(dec_pos(e) >= stop && (e & 63) == 0);
+        if (run) {
+            w.start(e);
+            run = w.running(stop);
+        }
+    }
+    PendSink sk{(int16_t*)mys, -1};
+    uint32_t* coefs32 = (uint32_t*)d.coefs;
+    while (__any(run)) {
+        if (run) {
+            w.step(sk);
+            run = w.running(stop);
+        }
+        uint64_t m = __ballot(sk.pend >= 0);
+        while (m) {
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)sk.pend, l);
+            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)sk.pend >> 32), l);
+            const int64_t bi = (int64_t)(((uint64_t)hi << 32) | lo);
+            uint32_t* src = wave_slots + l * SLOT_DW;
+            if (lane < 32) {
+                const uint32_t v = src[lane];
+                src[lane] = 0;
+                coefs32[bi * 32 + lane] = v;
+            }
+        }
+        sk.pend = -1;
+    }
 }
 
 // One workgroup per image: DC values from differences, per component, the
