@@ -250,6 +250,7 @@ struct DecWalker {
     uint32_t pos, n;
     int b, z, comp;
     bool own;
+    bool bad;  // met an invalid code mid-interval (corrupt data if this is the true path)
     int64_t blk_base;
     DecReader R;
 
@@ -260,6 +261,7 @@ struct DecWalker {
         z = (int)(st & 63);
         n = 0;
         own = z == 0;
+        bad = false;
         comp = b < d->nby ? 0 : b - d->nby + 1;
         R.init(words, pos);
     }
@@ -282,6 +284,7 @@ struct DecWalker {
             comp = 0;
             own = true;
             if (pos + 8 < bound) {  // mid-interval: only a wrong-start path gets here; resume a bit later
+                bad = true;
                 pos++;
                 R.init(words, pos);
                 return;

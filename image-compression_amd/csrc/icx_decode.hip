@@ -355,7 +355,7 @@ struct PendSink {
 // store each), zeroing it behind.  A per-lane flush would cost every lane of
 // the wave ~70 instructions whenever any lane finishes a block, which on
 // q95 content is most iterations.
-__global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits)
+__global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S, Plan p, uint32_t sub_bits)
 {
     __shared__ __attribute__((aligned(16))) DecHuff L[4];
     __shared__ uint32_t slots[256 * SLOT_DW];
@@ -407,6 +407,10 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, const DecSt
         }
         sk.pend = -1;
     }
+    // The settled states are the true decode: an invalid code met on it
+    // (outside an interval's padding) means corrupt data (jdhuff.c warns and
+    // zero-fills there; the caller decides what to do with the file).
+    if (w.bad) atomicOr(&S[img].status, 6);
 }
 
 // One workgroup per image: DC values from differences, per component, the
@@ -751,7 +755,7 @@ void launch_dec_offsets(const DecDesc* d, DecState* s, const int32_t* ids, int m
     if (m > 0) hipLaunchKernelGGL(k_dec_offsets, dim3((unsigned)m), dim3(1024), 0, st, d, s, ids);
 }
 
-void launch_dec_write(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
+void launch_dec_write(const DecDesc* d, DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
                       hipStream_t st)
 {
     if (nwg > 0) hipLaunchKernelGGL(k_dec_write, dim3((unsigned)nwg), dim3(256), 0, st, d, s, subs, sub_bits);

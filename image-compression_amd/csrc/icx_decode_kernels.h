@@ -17,7 +17,7 @@ void launch_dec_init(const DecDesc* d, const DecState* s, const Plan& subs, int6
 void launch_dec_sync(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
                      int parity, uint32_t* changed, hipStream_t st);
 void launch_dec_offsets(const DecDesc* d, DecState* s, const int32_t* ids, int m, hipStream_t st);
-void launch_dec_write(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
+void launch_dec_write(const DecDesc* d, DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
                       hipStream_t st);
 void launch_dec_dc(const DecDesc* d, const DecState* s, const int32_t* ids, int m, hipStream_t st);
 // blocks: per image ceil(nblocks / 32) workgroups

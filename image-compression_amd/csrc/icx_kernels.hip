@@ -399,6 +399,12 @@ struct LdsSink {
     }
 };
 
+struct CountSink {  // timing experiments only (ICX_HUFF_EXP == 2)
+    int n;
+    __device__ __forceinline__ void put(uint32_t, int len) { n += len; }
+    __device__ __forceinline__ void finish() {}
+};
+
 struct GlobalSink {
     uint64_t acc;
     int n, widx;
@@ -545,6 +551,15 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
 
     // ---- 1. encode_one_block into the slot (rarely: into the block's HBM spill)
     int bits = 0;
+#if ICX_HUFF_EXP == 2  // timing only: code lengths counted, no bit packing, nothing after
+    if (valid) {
+        CountSink cs{0};
+        encode_block(cs, quad, dq - qprev, s_qf[tb], s_ac[tb], s_dc[tb]);
+        bits = cs.n;
+    }
+    if (t == 0) D.chunk_bits[cur][chunk] = (uint32_t)bits;
+    return;
+#endif
     if (valid) {
         const uint32_t sb = (uint32_t)(t * SLOT_WORDS * 4);
         LdsSink sink{0, 0, sb, sb + (SLOT_WORDS - 1) * 4, slots};

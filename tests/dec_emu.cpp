@@ -151,13 +151,19 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
             memset(buf, 0, sizeof(buf));
         }
     };
+    bool bad = false;
     for (uint32_t j : order) {
-        uint32_t n;
         Sink sk;
         sk.out = coefs.data();
-        dec_walk<true>(d, T.h, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8, est[j],
-                       (j + 1) * S, n, boff[j], sk);
+        const uint64_t e = est[j];
+        if (dec_pos(e) >= (j + 1) * S && (e & 63) == 0) continue;
+        DecWalker<true, const DecHuff*> w = dec_walker<true>(d, (const DecHuff*)T.h, T.slow, sel, words.data(),
+                                                             seg.data(), (uint32_t)seg.size(), ent_len * 8, boff[j]);
+        w.start(e);
+        while (w.running((j + 1) * S)) w.step(sk);
+        bad |= w.bad;  // as k_dec_write: an invalid code on the true path = corrupt data
     }
+    if (bad) return ICX_E_CORRUPT;
     // ---- DC prediction per component, reset every restart interval
     int pred[3] = {0, 0, 0};
     for (int64_t b = 0; b < d.nblocks; b++) {

@@ -63,3 +63,70 @@ def test_emulated_decode_of_own_encodes(emu, oracle):
         ref = oracle.jpeg_coefs(data)
         rc, got, _ = run(emu, data, ref.shape[0], seed=3, sub=256)
         assert rc == 0 and np.array_equal(got, ref), (h, w, q)
+
+
+def test_fuzzed_streams_never_read_out_of_bounds(oracle, tmp_path):
+    """Corrupted files through the product parser + walker under
+    AddressSanitizer: every call must end (status 0 or corrupt/unsupported)
+    without an out-of-bounds access.  Guards the device kernels' indexing,
+    which share this code."""
+    lib = os.path.join(BUILD, "dec_emu_asan.so")
+    srcs = [os.path.join(ROOT, "tests", "dec_emu.cpp"), os.path.join(CSRC, "icx_jpeg_parse.cpp")]
+    exe = str(tmp_path / "fuzz")
+    main = tmp_path / "fuzz_main.cpp"
+    main.write_text(r'''
+#include <stdio.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <vector>
+extern "C" int dec_emu_coefs(const uint8_t*, size_t, int16_t*, size_t, int, int, int*);
+int main(int argc, char** argv) {
+    FILE* f = fopen(argv[1], "rb");
+    std::vector<uint8_t> buf(1 << 22);
+    size_t n = fread(buf.data(), 1, buf.size(), f);
+    fclose(f);
+    std::vector<int16_t> out((size_t)64 * 200000);
+    int it = 0, bad = 0;
+    size_t pos = 0;
+    while (pos + 4 <= n) {  // records: u32 length, bytes
+        uint32_t len = buf[pos] | buf[pos + 1] << 8 | buf[pos + 2] << 16 | (uint32_t)buf[pos + 3] << 24;
+        pos += 4;
+        std::vector<uint8_t> one(buf.begin() + pos, buf.begin() + pos + len);  // exact-size copy: ASan sees overruns
+        int rc = dec_emu_coefs(one.data(), one.size(), out.data(), 200000, 2, 256, &it);
+        if (rc != 0 && rc != 4 && rc != 5 && rc != 6) bad++;
+        pos += len;
+    }
+    printf("bad=%d\n", bad);
+    return bad != 0;
+}
+''')
+    r = subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address", "-fno-omit-frame-pointer", "-I", CSRC,
+                        "-o", exe, str(main)] + srcs, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    meta, jpgs, _ = load_decode_golden()
+    rng = np.random.default_rng(1234)
+    recs = []
+    names = [k for k in jpgs if not meta["cases"][k].get("unsupported")]
+    for i in range(400):
+        d = bytearray(jpgs[names[i % len(names)]])
+        mode = i % 4
+        if mode == 0:    # flip random bytes in the entropy-coded data
+            for _ in range(int(rng.integers(1, 8))):
+                p = int(rng.integers(len(d) // 2, len(d)))
+                d[p] = int(rng.integers(0, 256))
+        elif mode == 1:  # truncate
+            d = d[: int(rng.integers(4, len(d)))]
+        elif mode == 2:  # insert stray markers (RSTn, fill, EOI)
+            for _ in range(int(rng.integers(1, 4))):
+                p = int(rng.integers(len(d) // 2, len(d)))
+                d[p:p] = bytes([0xFF, int(rng.choice([0xD0, 0xD3, 0xD9, 0xFF, 0xC4]))])
+        else:            # corrupt header bytes (tables, dimensions, sampling)
+            for _ in range(int(rng.integers(1, 4))):
+                p = int(rng.integers(2, min(len(d), 700)))
+                d[p] = int(rng.integers(0, 256))
+        recs.append(len(d).to_bytes(4, "little") + bytes(d))
+    fz = tmp_path / "cases.bin"
+    fz.write_bytes(b"".join(recs))
+    r = subprocess.run([exe, str(fz)], capture_output=True, text=True, timeout=600,
+                       env={**os.environ, "ASAN_OPTIONS": "detect_leaks=0"})
+    assert r.returncode == 0 and "bad=0" in r.stdout, (r.stdout[-500:], r.stderr[-3000:])

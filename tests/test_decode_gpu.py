@@ -102,3 +102,44 @@ def test_decode_refusals_and_corrupt_input(codec, dgolden):
     for st, img in res[:-1]:
         assert st in (N.E_CORRUPT, N.E_UNSUPPORTED), st
     assert res[-1][0] == N.OK  # a bad file does not spoil the batch
+
+
+def test_decode_fuzzed_batch(codec, oracle, dgolden):
+    """400 corrupted files in one device batch (flipped entropy bytes,
+    truncation, stray RSTn/EOI/fill markers, corrupted headers): every file
+    ends with OK, UNSUPPORTED or CORRUPT, a bad file never spoils its
+    neighbours, and whatever the device accepts decodes exactly as the oracle
+    does."""
+    meta, jpgs, pxs = dgolden
+    rng = np.random.default_rng(99)
+    names = [k for k in jpgs if not meta["cases"][k].get("unsupported")]
+    datas = []
+    for i in range(400):
+        d = bytearray(jpgs[names[i % len(names)]])
+        mode = i % 5
+        if mode == 0:
+            for _ in range(int(rng.integers(1, 8))):
+                p = int(rng.integers(len(d) // 2, len(d)))
+                d[p] = int(rng.integers(0, 256))
+        elif mode == 1:
+            d = d[: int(rng.integers(4, len(d)))]
+        elif mode == 2:
+            for _ in range(int(rng.integers(1, 4))):
+                p = int(rng.integers(len(d) // 2, len(d)))
+                d[p:p] = bytes([0xFF, int(rng.choice([0xD0, 0xD3, 0xD9, 0xFF, 0xC4]))])
+        elif mode == 3:
+            for _ in range(int(rng.integers(1, 4))):
+                p = int(rng.integers(2, min(len(d), 700)))
+                d[p] = int(rng.integers(0, 256))
+        datas.append(bytes(d))  # mode 4: intact
+    res = codec.decode_jpg_batch(datas, subsampling=1)
+    ok = 0
+    for i, (d, (st, img)) in enumerate(zip(datas, res)):
+        assert st in (N.OK, N.E_UNSUPPORTED, N.E_CORRUPT), (i, st)
+        if i % 5 == 4:
+            assert st == N.OK and np.array_equal(img, pxs[names[i % len(names)]]), i
+        if st == N.OK:
+            rc, ref = oracle.jpeg_decode(d)
+            assert rc == 0 and np.array_equal(img, ref), i
+            ok += 1
+    assert ok >= 80
