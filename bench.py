@@ -89,7 +89,7 @@ def cpu_baseline(frames, n_sample, threads):
                       f"{enc} full encodes, {dt:.2f} s wall"}, sizes
 
 
-def e2e_leg(codec, dev, n_frames, steps, distinct=8):
+def e2e_leg(codec, dev, n_frames, steps, distinct=8, cpu_sample=0, threads=16):
     """Secondary measurement: the whole per-image hot loop of processImage on
     the device — q95 4:2:0 4K JPEG files resident in HBM -> decode (A11,
     decodeImageWithSubsampling) -> compressJpgWithTargetSize at -t 1 MiB with
@@ -127,13 +127,40 @@ def e2e_leg(codec, dev, n_frames, steps, distinct=8):
         td += t1 - t0
         tf += time.perf_counter() - t1
     mp = n_frames * W * H / 1e6
-    return {"metric": "megapixels/sec 4K q95 JPEG bytes in HBM -> device decode -> target-size encode (-t 1MiB, "
+    line = {"metric": "megapixels/sec 4K q95 JPEG bytes in HBM -> device decode -> target-size encode (-t 1MiB, "
                       "q=0.25 cached)",
             "value": round(mp * steps / (td + tf), 1), "unit": "MP/s", "frames": n_frames, "steps": steps,
             "ms_per_step": round((td + tf) / steps * 1e3, 3), "decode_ms_per_step": round(td / steps * 1e3, 3),
             "encode_ms_per_step": round(tf / steps * 1e3, 3),
             "decode_mp_s": round(mp * steps / td, 1),
             "mean_src_jpeg_bytes": int(np.mean([s.numel() for s in srcs]))}
+    if cpu_sample:
+        line["cpu_baseline"] = e2e_cpu_baseline([s.cpu().numpy().tobytes() for s in srcs], cpu_sample, threads)
+    return line
+
+
+def e2e_cpu_baseline(srcs, n_sample, threads):
+    """The same per-image loop on host cores with the oracle (test
+    infrastructure): IJG-6b decode restatement + compressJpgWithTargetSize
+    restatement, one image per thread task."""
+    import concurrent.futures as cf
+    from tests.oracle_ffi import Oracle
+    o = Oracle()
+
+    def one(i):
+        rc, img = o.jpeg_decode(srcs[i % len(srcs)])
+        assert rc == 0
+        return o.fit(img, TARGET, Q0, cached=(Q0, 1.0))["success"]
+
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        ok = sum(ex.map(one, range(n_sample)))
+    dt = time.perf_counter() - t0
+    assert ok == n_sample
+    return {"value": round(n_sample * W * H / 1e6 / dt, 3), "unit": "MP/s", "cores": threads, "kind": "port",
+            "sample": f"{n_sample} of the q95 sources ({len(srcs)} distinct, half smooth, half noise): oracle "
+                      f"decode + compressJpgWithTargetSize with cache (0.25, 1.0), {threads} threads, "
+                      f"{dt:.2f} s wall"}
 
 
 def main():
@@ -240,7 +267,8 @@ def main():
     }
     if rank == 0 and world == 1 and args.e2e and not args.host_io:
         batch = None
-        line["e2e"] = e2e_leg(codec, dev, args.e2e, args.steps)
+        line["e2e"] = e2e_leg(codec, dev, args.e2e, args.steps,
+                              cpu_sample=0 if args.no_cpu_baseline else 64, threads=min(16, os.cpu_count() or 1))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         cb, _ = cpu_baseline(frames, args.cpu_sample, threads)

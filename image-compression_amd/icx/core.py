@@ -288,15 +288,25 @@ class Codec:
             raise TypeError("outputFile must not be null")
         if params is None:
             raise TypeError("params must not be null")
-        w, h = image_dims(original_image)
-        if w <= params.min_width and h <= params.min_height:
-            log.info("PNG 圖片尺寸 %dx%d 未超過目標 %dx%d，不處理。", w, h, params.min_width, params.min_height)
+        resized = self.png_resize(original_image, params)
+        if resized is None:
             return False
-        scale = min(params.min_width / w, params.min_height / h)
-        resized = self.resize_image(original_image, scale)
         from .pngio import write_png
         write_png(output_file, resized)
         return True
+
+    def png_resize(self, original_image, params: CompressionParams):
+        """The device part of compressPngWithTargetSize (ImageCompressionPng.java:
+        45-67): None when the image already fits the (minWidth x minHeight) box,
+        else the bilinear resize by min(minWidth/w, minHeight/h)."""
+        if original_image is None:
+            raise TypeError("originalImage must not be null")
+        w, h = image_dims(original_image)
+        if w <= params.min_width and h <= params.min_height:
+            log.info("PNG 圖片尺寸 %dx%d 未超過目標 %dx%d，不處理。", w, h, params.min_width, params.min_height)
+            return None
+        scale = min(params.min_width / w, params.min_height / h)
+        return self.resize_image(original_image, scale)
 
     # -------------------------------------------------------------- A11 decode
     def decode_jpg_batch(self, datas, subsampling: int = 0, device_out: bool = False):

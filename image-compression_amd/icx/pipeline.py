@@ -282,9 +282,29 @@ def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, ca
             _fail(it, e)
 
 
-def compress_png_item(codec, it: _Item, params: CompressionParams):
+def _png_write(it: _Item, resized):
     try:
-        _finish(it, codec.compress_png_with_target_size(it.decoded.image, it.output, params))
+        from .pngio import write_png
+        write_png(it.output, resized)
+        _finish(it, True)
+    except Exception as e:
+        _fail(it, e)
+
+
+def compress_png_item(codec, it: _Item, params: CompressionParams, writer=None):
+    """compressPngWithTargetSize (ImageCompressionPng.java:37-75): the resize on
+    the device, the PNG filter + deflate + file write on `writer` (a host
+    thread pool) when given, so the device worker never waits on deflate."""
+    try:
+        if writer is None or not hasattr(codec, "png_resize"):
+            _finish(it, codec.compress_png_with_target_size(it.decoded.image, it.output, params))
+            return
+        resized = codec.png_resize(it.decoded.image, params)
+        if resized is None:
+            _finish(it, False)
+            return
+        it.decoded = None
+        writer.submit(_png_write, it, resized)
     except Exception as e:
         _fail(it, e)
 
@@ -435,6 +455,8 @@ class CompressionBatch:
         done_items: List[_Item] = []
         lock = threading.Lock()
 
+        writer = cf.ThreadPoolExecutor(self.decode_threads)  # PNG filter + deflate + write
+
         def gpu_worker(codec):
             while True:
                 grp = work.get()
@@ -447,7 +469,7 @@ class CompressionBatch:
                     compress_jpeg_group(codec, its, self.params, cache)
                 elif kind == "png":
                     for it in its:
-                        compress_png_item(codec, it, self.params)
+                        compress_png_item(codec, it, self.params, writer)
                 else:
                     for it in its:
                         compress_image_iteratively(codec, it, self.params, cache)
@@ -488,4 +510,5 @@ class CompressionBatch:
             work.put(None)
         for w in workers:
             w.join(timeout=max(1.0, deadline - time.perf_counter()))
+        writer.shutdown(wait=True)
         return done_items

@@ -36,12 +36,18 @@ class OracleCodec:
             out.append(self.o.jpeg_decode(d, s))
         return out
 
-    def compress_png_with_target_size(self, img, output_file, params):
+    def png_resize(self, img, params):
         w, h = image_dims(img)
         if w <= params.min_width and h <= params.min_height:
-            return False
+            return None
         s = min(params.min_width / w, params.min_height / h)
         dw, dh = self.o.scaled_dims(w, h, s)
+        return self.o.resize(img, dw, dh)
+
+    def compress_png_with_target_size(self, img, output_file, params):
+        r = self.png_resize(img, params)
+        if r is None:
+            return False
         from icx.pngio import write_png
-        write_png(output_file, self.o.resize(img, dw, dh))
+        write_png(output_file, r)
         return True
