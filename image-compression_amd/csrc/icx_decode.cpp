@@ -271,8 +271,8 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             d.nsub_max = (int32_t)((it.ent_cap * 8 + S - 1) / S);
             max_nsub = std::max<int64_t>(max_nsub, d.nsub_max);
             d.est = (uint64_t*)c->dev.take((size_t)(d.nsub_max + 1) * 8);
-            d.dirty[0] = (uint8_t*)c->dev.take((size_t)d.nsub_max + 1);
-            d.dirty[1] = (uint8_t*)c->dev.take((size_t)d.nsub_max + 1);
+            d.wl[0] = (uint32_t*)c->dev.take((size_t)(d.nsub_max + 1) * 4);
+            d.wl[1] = (uint32_t*)c->dev.take((size_t)(d.nsub_max + 1) * 4);
             d.ncnt = (uint32_t*)c->dev.take((size_t)(d.nsub_max + 1) * 4);
             d.boff = (uint32_t*)c->dev.take((size_t)(d.nsub_max + 1) * 4);
             d.coefs = (int16_t*)c->dev.take((size_t)d.nblocks * 128);
@@ -288,8 +288,10 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         }
         DecDesc* d_desc = (DecDesc*)c->dev.take(sizeof(DecDesc) * m);
         DecState* d_state = (DecState*)c->dev.take(sizeof(DecState) * m);
-        const int max_it = (int)max_nsub + 8;
+        const int max_it = (int)max_nsub + 8;  // each launch settles at least one more subsequence
         uint32_t* d_changed = (uint32_t*)c->dev.take((size_t)max_it * 4);
+        uint32_t* d_wlcnt = (uint32_t*)c->dev.take((size_t)m * max_it * 4);
+        for (int k = 0; k < m; k++) desc[k].wl_cnt = d_wlcnt;
         uint32_t* h_changed = (uint32_t*)c->host.take(4);
         int32_t* d_ids = (int32_t*)c->dev.take((size_t)m * 4);
         std::vector<int32_t> ids(m);
@@ -301,6 +303,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             (st = upload(c, d_ids, ids.data(), (size_t)m * 4)))
             return st;
         e = hipMemsetAsync(d_changed, 0, (size_t)max_it * 4, c->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(d_wlcnt, 0, (size_t)m * max_it * 4, c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "counter clear");
 
         std::vector<int64_t> cnt_tiles(m), cnt_subs(m), cnt_blk(m), cnt_px(m), cnt_rows(m);
@@ -334,7 +337,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         for (;;) {
             for (int k = 0; k < 4 && it < max_it; k++, it++) {
                 Timed tm(c, "dec_sync", 0);
-                launch_dec_sync(d_desc, d_state, Ps.p, Ps.total, S, it & 1, d_changed + it, c->stream);
+                launch_dec_sync(d_desc, d_state, Ps.p, Ps.total, S, it, max_it, d_changed + it, c->stream);
             }
             e = hipMemcpyAsync(h_changed, d_changed + it - 1, 4, hipMemcpyDeviceToHost, c->stream);
             if (e == hipSuccess) e = hipStreamSynchronize(c->stream);

@@ -13,9 +13,10 @@
 // (bit position, block-in-MCU, zig-zag index) at a symbol boundary;
 // walk(E[j], subsequence j) gives the state at which the decode leaves
 // subsequence j.  The entry states E[] are the fixed point of
-// E[j+1] = walk(E[j]) from the known E[0]; the sync kernel iterates it with
-// dirty flags (only threads whose entry changed re-walk), which settles in two
-// or three launches because wrong starts resynchronise within a subsequence.
+// E[j+1] = walk(E[j]) from the known E[0]; the sync kernel iterates it, the
+// first launch over every subsequence and each later one over a worklist of
+// the subsequences whose entry changed (so re-walks pack densely into waves);
+// it settles in a few launches because wrong starts resynchronise quickly.
 // Restart intervals need no special case: every RSTn marker is replaced by
 // DEC_PAD bytes of 0xFF, and an all-ones look-ahead is never a valid JPEG code
 // (T.81 C.2 forbids all-ones codes), so the decode of an interval ends with an
@@ -86,7 +87,8 @@ struct DecDesc {
     uint32_t* tile_rst;    // per unstuff tile: RSTn markers, then exclusive offsets
     uint32_t* seg;         // interval start byte offsets in ent (nseg_max entries)
     uint64_t* est;         // entry state per subsequence (nsub_max + 1)
-    uint8_t* dirty[2];
+    uint32_t* wl[2];       // subsequences to re-walk in the next sync launch (ping-pong)
+    uint32_t* wl_cnt;      // entries appended to the worklist by sync launch r: wl_cnt[r]
     uint32_t* ncnt;        // blocks completed inside each subsequence
     uint32_t* boff;        // blocks completed before each subsequence
     int16_t* coefs;        // nblocks x 64, natural order, quantised (AC only)

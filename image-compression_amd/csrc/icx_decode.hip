@@ -254,8 +254,6 @@ __global__ void __launch_bounds__(256) k_dec_init(const DecDesc* D, const DecSta
     const bool live = st.status == 0 && (blockIdx.x - p.prefix[slot]) * 256 < (int64_t)st.nsub;
     if (live) load_tables(d.tab, L);
     if (j > d.nsub_max) return;
-    d.dirty[0][j] = 1;
-    d.dirty[1][j] = 0;
     const uint32_t start = (uint32_t)j * sub_bits;
     uint64_t e = dec_pack(start, 0, 0);
     if (live && j > 0 && j < st.nsub && warm > 0) {
@@ -285,30 +283,40 @@ __device__ __forceinline__ uint32_t selector(const DecTab* T)
     return s;
 }
 
+// One relaxation launch.  Launch 0 walks every subsequence; launch r > 0 walks
+// the worklist launch r-1 built (entry k of workgroup w: wl[r & 1][256 w + k]),
+// so the few subsequences still moving fill whole waves.  A thread whose exit
+// differs from the stored next entry stores it and appends j + 1 to the next
+// worklist (only thread j writes E[j+1], so entries are unique per launch).
 __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
-                                                  int parity, uint32_t* changed)
+                                                  int iter, int max_it, uint32_t* changed)
 {
     __shared__ __attribute__((aligned(16))) DecHuff L[4];
     const int slot = slot_of(p.prefix, p.m, blockIdx.x);
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
     const DecState& st = S[img];
-    const int64_t j = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
-    const bool mine = j < st.nsub && st.status == 0 && d.dirty[parity][j];
-    if (!__syncthreads_or(mine)) return;
+    if (st.status) return;
+    const int64_t k = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
+    const uint32_t n = iter == 0 ? st.nsub : d.wl_cnt[(int64_t)img * max_it + iter - 1];
+    if ((blockIdx.x - p.prefix[slot]) * 256 >= (int64_t)n) return;
     load_tables(d.tab, L);
-    if (!mine) return;
-    d.dirty[parity][j] = 0;
+    if (k >= n) return;
+    const uint32_t j = iter == 0 ? (uint32_t)k : d.wl[iter & 1][k];
+    if (j >= st.nsub) return;
     const uint64_t e = __hip_atomic_load(&d.est[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t n;
+    uint32_t nb;
     NoSink ns;
     const uint64_t x = dec_walk<false>(d, L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
-                                       st.ent_len * 8, e, (uint32_t)(j + 1) * sub_bits, n, 0, ns);
-    d.ncnt[j] = n;
+                                       st.ent_len * 8, e, (j + 1) * sub_bits, nb, 0, ns);
+    d.ncnt[j] = nb;
     const uint64_t old = __hip_atomic_load(&d.est[j + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (x != old) {
         __hip_atomic_store(&d.est[j + 1], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        d.dirty[parity ^ 1][j + 1] = 1;
+        if (j + 1 < st.nsub) {
+            const uint32_t pos = atomicAdd(&d.wl_cnt[(int64_t)img * max_it + iter], 1u);
+            d.wl[(iter + 1) & 1][pos] = j + 1;
+        }
         atomicAdd(changed, 1u);
     }
 }
@@ -744,10 +752,11 @@ void launch_dec_init(const DecDesc* d, const DecState* s, const Plan& subs, int6
 }
 
 void launch_dec_sync(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
-                     int parity, uint32_t* changed, hipStream_t st)
+                     int iter, int max_it, uint32_t* changed, hipStream_t st)
 {
     if (nwg > 0)
-        hipLaunchKernelGGL(k_dec_sync, dim3((unsigned)nwg), dim3(256), 0, st, d, s, subs, sub_bits, parity, changed);
+        hipLaunchKernelGGL(k_dec_sync, dim3((unsigned)nwg), dim3(256), 0, st, d, s, subs, sub_bits, iter, max_it,
+                           changed);
 }
 
 void launch_dec_offsets(const DecDesc* d, DecState* s, const int32_t* ids, int m, hipStream_t st)

@@ -87,7 +87,6 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
     const uint32_t S = (uint32_t)sub_bits;
     const uint32_t nsub = (ent_len * 8 + S - 1) / S;
     std::vector<uint64_t> est(nsub + 1);
-    std::vector<uint8_t> dirty[2] = {std::vector<uint8_t>(nsub + 1, 1), std::vector<uint8_t>(nsub + 1, 0)};
     std::vector<uint32_t> ncnt(nsub, 0);
     uint32_t warm = std::min<uint32_t>(4096, S / 4);  // as icx_decode.cpp warm_bits
     if (const char* e = getenv("ICX_DEC_WARM")) warm = (uint32_t)atol(e);
@@ -101,20 +100,17 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
         }
     }
     std::mt19937 rng((uint32_t)seed);
-    std::vector<uint32_t> order(nsub);
-    for (uint32_t j = 0; j < nsub; j++) order[j] = j;
+    // launch 0 walks everything; launch r > 0 walks the worklist launch r-1 appended to (as k_dec_sync)
+    std::vector<uint32_t> work(nsub);
+    for (uint32_t j = 0; j < nsub; j++) work[j] = j;
     int it = 0;
     dec_emu_walks = 0;
     dec_emu_nsub = nsub;
     for (;; it++) {
         if (it > (int)nsub + 2) return ICX_E_CORRUPT;  // cannot happen: one subsequence settles per launch
-        std::vector<uint8_t>& cur = dirty[it & 1];
-        std::vector<uint8_t>& nxt = dirty[(it + 1) & 1];
-        if (seed) std::shuffle(order.begin(), order.end(), rng);
-        uint32_t changed = 0;
-        for (uint32_t j : order) {
-            if (!cur[j]) continue;
-            cur[j] = 0;
+        if (seed) std::shuffle(work.begin(), work.end(), rng);
+        std::vector<uint32_t> next;
+        for (uint32_t j : work) {
             dec_emu_walks++;
             uint32_t n;
             NoSink ns;
@@ -123,11 +119,11 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
             ncnt[j] = n;
             if (x != est[j + 1]) {
                 est[j + 1] = x;
-                nxt[j + 1] = 1;
-                changed++;
+                if (j + 1 < nsub) next.push_back(j + 1);
             }
         }
-        if (!changed) break;
+        if (next.empty()) break;
+        work.swap(next);
     }
     if (iterations) *iterations = it + 1;
     std::vector<uint32_t> boff(nsub + 1, 0);
@@ -152,6 +148,9 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
         }
     };
     bool bad = false;
+    std::vector<uint32_t> order(nsub);
+    for (uint32_t j = 0; j < nsub; j++) order[j] = j;
+    if (seed) std::shuffle(order.begin(), order.end(), rng);
     for (uint32_t j : order) {
         Sink sk;
         sk.out = coefs.data();
