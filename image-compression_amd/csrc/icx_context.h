@@ -101,6 +101,40 @@ inline bool is_device_ptr(const void* p)
 }  // namespace icx
 
 // ============================================================ context
+// Caching allocator behind icx_device_alloc/free: freed buffers are kept by
+// size class (power of two) and handed out again, so a pipeline that
+// allocates a frame buffer per image never pays hipMalloc/hipFree (which
+// synchronise the device) after warm-up.
+struct DevPool {
+    std::map<size_t, std::vector<void*>> free_;
+    std::map<void*, size_t> live_;
+    size_t cached = 0, limit = (size_t)16 << 30;
+    static size_t cls(size_t n)
+    {
+        size_t c = 1 << 16;
+        while (c < n) c <<= 1;
+        return c;
+    }
+    bool host = false;  // pinned host pool (hipHostMalloc) instead of device memory
+    ~DevPool()
+    {
+        for (auto& kv : free_)
+            for (void* p : kv.second) (void)(host ? hipHostFree(p) : hipFree(p));
+        for (auto& kv : live_) (void)(host ? hipHostFree(kv.first) : hipFree(kv.first));
+    }
+};
+
+inline bool is_pinned_ptr(const void* p)
+{
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
 struct icx_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -113,6 +147,8 @@ struct icx_ctx {
     std::vector<hipEvent_t> evpool;
     std::map<std::string, icx::KStat> stats;
     size_t budget = 0;  // device workspace budget per sub-batch
+    DevPool pool;
+    DevPool hpool;  // pinned host buffers (hpool.host = true)
 };
 
 namespace icx {

@@ -238,7 +238,10 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             continue;
         }
         c->dev.used = 0;
-        e = c->host.reserve(64 << 20);
+        size_t host_need = 64 << 20;
+        for (DecItem* it : sub)
+            if (!it->dev_in && !is_pinned_ptr(it->job->data)) host_need += align_up(it->job->len, 64);
+        e = c->host.reserve(host_need);
         if (e != hipSuccess) return hip_fail(c, e, "hipHostMalloc");
         c->host.used = 0;
 
@@ -258,9 +261,17 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             d.ntiles = (int32_t)it.ntiles;
             uint8_t* scan = (uint8_t*)c->dev.take(align_up(scan_len + 64, 256));
             e = hipMemsetAsync(scan + scan_len, 0, 64, c->stream);
+            const uint8_t* src = it.job->data + it.J.scan_off;
+            if (!it.dev_in && !is_pinned_ptr(it.job->data)) {  // pageable: via pinned staging (DMA at link speed)
+                uint8_t* h = (uint8_t*)c->host.take(scan_len);
+                if (h) {
+                    memcpy(h, src, scan_len);
+                    src = h;
+                }
+            }
             if (e == hipSuccess)
-                e = hipMemcpyAsync(scan, it.job->data + it.J.scan_off, scan_len,
-                                   it.dev_in ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream);
+                e = hipMemcpyAsync(scan, src, scan_len, it.dev_in ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                   c->stream);
             if (e != hipSuccess) return hip_fail(c, e, "scan upload");
             d.scan = scan;
             d.ent = (uint8_t*)c->dev.take(align_up(it.ent_cap, 256));
@@ -434,6 +445,77 @@ icx_status icx_decode_jpg(icx_ctx* ctx, icx_decode_job* job)
     if (!ctx || !job) return ICX_E_NULL;
     const icx_status s = run_decode(ctx, job, 1, nullptr, 0);
     return s != ICX_OK ? s : job->status;
+}
+
+namespace {
+icx_status pool_alloc(icx_ctx* ctx, DevPool& P, size_t bytes, void** ptr)
+{
+    if (!ctx || !ptr) return ICX_E_NULL;
+    *ptr = nullptr;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    const size_t c = DevPool::cls(bytes);
+    auto f = P.free_.find(c);
+    if (f != P.free_.end() && !f->second.empty()) {
+        *ptr = f->second.back();
+        f->second.pop_back();
+        P.cached -= c;
+    } else {
+        hipError_t e = hipSetDevice(ctx->device);
+        if (e == hipSuccess) e = P.host ? hipHostMalloc(ptr, c, hipHostMallocPortable) : hipMalloc(ptr, c);
+        if (e != hipSuccess) return hip_fail(ctx, e, P.host ? "hipHostMalloc" : "hipMalloc");
+    }
+    P.live_[*ptr] = c;
+    return ICX_OK;
+}
+
+icx_status pool_free(icx_ctx* ctx, DevPool& P, void* ptr)
+{
+    if (!ctx) return ICX_E_NULL;
+    if (!ptr) return ICX_OK;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    auto l = P.live_.find(ptr);
+    if (l == P.live_.end()) return fail(ctx, ICX_E_INVALID, "free of a buffer this context did not allocate");
+    const size_t c = l->second;
+    P.live_.erase(l);
+    // A recycled buffer's next use is a copy or launch on this context's
+    // stream, ordered after every launch that used it before, so recycling
+    // needs no synchronisation.  (Host buffers: every call that reads one
+    // synchronises before returning.)
+    if (P.cached + c <= P.limit) {
+        P.free_[c].push_back(ptr);
+        P.cached += c;
+        return ICX_OK;
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = P.host ? hipHostFree(ptr) : hipFree(ptr);
+    return e == hipSuccess ? ICX_OK : hip_fail(ctx, e, "free");
+}
+}  // namespace
+
+icx_status icx_device_alloc(icx_ctx* ctx, size_t bytes, void** ptr)
+{
+    return ctx ? pool_alloc(ctx, ctx->pool, bytes, ptr) : ICX_E_NULL;
+}
+
+icx_status icx_device_free(icx_ctx* ctx, void* ptr) { return ctx ? pool_free(ctx, ctx->pool, ptr) : ICX_E_NULL; }
+
+icx_status icx_host_alloc(icx_ctx* ctx, size_t bytes, void** ptr)
+{
+    return ctx ? pool_alloc(ctx, ctx->hpool, bytes, ptr) : ICX_E_NULL;
+}
+
+icx_status icx_host_free(icx_ctx* ctx, void* ptr) { return ctx ? pool_free(ctx, ctx->hpool, ptr) : ICX_E_NULL; }
+
+icx_status icx_memcpy(icx_ctx* ctx, void* dst, const void* src, size_t bytes)
+{
+    if (!ctx || ((!dst || !src) && bytes)) return ICX_E_NULL;
+    if (!bytes) return ICX_OK;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return e == hipSuccess ? ICX_OK : hip_fail(ctx, e, "hipMemcpy");
 }
 
 icx_status icx_debug_decode_coefs(icx_ctx* ctx, const uint8_t* data, size_t len, int16_t* coefs, size_t ncoefs)

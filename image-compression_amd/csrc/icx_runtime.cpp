@@ -728,6 +728,7 @@ icx_status icx_create(int device, icx_ctx** out)
     if (hipSetDevice(device) != hipSuccess) return ICX_E_DEVICE;
     icx_ctx* c = new icx_ctx();
     c->device = device;
+    c->hpool.host = true;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return ICX_E_DEVICE;

@@ -99,13 +99,113 @@ def _fmt_of(img):
     raise ValueError(f"unsupported image shape {tuple(img.shape)}")
 
 
+class DeviceImage:
+    """A frame (or byte string) in the codec GPU's HBM, allocated through the
+    C ABI (icx_device_alloc): (H, W, 3) BGR or (H, W) grey uint8, contiguous.
+    Decoded frames stay here between icx_decode_jpg_batch and
+    icx_compress_jpg_batch; the product path needs no PyTorch."""
+    icx_device = True
+
+    def __init__(self, codec, shape):
+        self.codec = codec
+        self.shape = tuple(int(x) for x in shape)
+        self.nbytes = int(np.prod(self.shape))
+        p = ctypes.c_void_p()
+        codec._check(codec._lib.icx_device_alloc(codec._ctx, self.nbytes, ctypes.byref(p)), "icx_device_alloc")
+        self.ptr = p.value
+
+    @property
+    def ndim(self):
+        return len(self.shape)
+
+    def data_ptr(self):
+        return self.ptr
+
+    def numel(self):
+        return self.nbytes
+
+    def numpy(self, nbytes=None) -> np.ndarray:
+        """Copy to host (the first nbytes as a flat array when given)."""
+        n = self.nbytes if nbytes is None else min(int(nbytes), self.nbytes)
+        out = np.empty(self.shape if nbytes is None else (n,), np.uint8)
+        self.codec._check(self.codec._lib.icx_memcpy(self.codec._ctx, out.ctypes.data, self.ptr, n), "icx_memcpy")
+        return out
+
+    @classmethod
+    def from_host(cls, codec, arr) -> "DeviceImage":
+        a = np.ascontiguousarray(np.frombuffer(arr, np.uint8) if isinstance(arr, (bytes, bytearray)) else arr)
+        d = cls(codec, a.shape)
+        codec._check(codec._lib.icx_memcpy(codec._ctx, d.ptr, a.ctypes.data, d.nbytes), "icx_memcpy")
+        return d
+
+    def free(self):
+        if self.ptr and self.codec._ctx:
+            self.codec._lib.icx_device_free(self.codec._ctx, self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class PinnedBuffer:
+    """Page-locked host bytes from the codec's pool (icx_host_alloc): a file
+    read into one is uploaded by DMA with no staging copy.  `array` is a
+    numpy view of the first `size` bytes."""
+
+    def __init__(self, codec, size):
+        self.codec = codec
+        self.size = int(size)
+        p = ctypes.c_void_p()
+        codec._check(codec._lib.icx_host_alloc(codec._ctx, max(1, self.size), ctypes.byref(p)), "icx_host_alloc")
+        self.ptr = p.value
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, self.size)).from_address(self.ptr))[:self.size]
+
+    @classmethod
+    def read_file(cls, codec, path) -> "PinnedBuffer":
+        import os
+        size = os.path.getsize(path)
+        b = cls(codec, size)
+        with open(path, "rb", buffering=0) as f:
+            n = f.readinto(memoryview(b.array))
+        b.size = n
+        b.array = b.array[:n]
+        return b
+
+    @property
+    def nbytes(self):
+        return self.size
+
+    def __getitem__(self, k):
+        return self.array[k]
+
+    def __len__(self):
+        return self.size
+
+    def free(self):
+        if self.ptr and self.codec._ctx:
+            self.array = None
+            self.codec._lib.icx_host_free(self.codec._ctx, self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 def _image_struct(img, fmt=None):
-    """Describe a numpy array or CUDA tensor as an icx_image (no copy)."""
+    """Describe a numpy array, DeviceImage or CUDA tensor as an icx_image (no copy)."""
     if img is None:
         raise TypeError("image must not be null")
     if fmt is None:
         fmt = _fmt_of(img)
     h, w = int(img.shape[0]), int(img.shape[1])
+    if getattr(img, "icx_device", False):
+        return N.Image(img.data_ptr(), w, h, w * (1 if fmt == N.GRAY8 else 3), fmt), img
     if isinstance(img, np.ndarray):
         if img.dtype != np.uint8:
             raise ValueError("image must be uint8")
@@ -310,18 +410,22 @@ class Codec:
 
     # -------------------------------------------------------------- A11 decode
     def decode_jpg_batch(self, datas, subsampling: int = 0, device_out: bool = False):
-        """Decode JPEG files (bytes / uint8 arrays / CUDA uint8 tensors) on the
-        GPU: decodeImageWithSubsampling's read (ImageCompression.java:113-155).
-        subsampling 0 = the reference's rule.  Returns one (status, image) per
-        file; image is (H, W, 3) BGR or (H, W) grey, a CUDA tensor when
-        device_out (then it stays in HBM for the encoder), else numpy."""
+        """Decode JPEG files (bytes / uint8 arrays / DeviceImage / CUDA uint8
+        tensors) on the GPU: decodeImageWithSubsampling's read
+        (ImageCompression.java:113-155).  subsampling 0 = the reference's
+        rule.  Returns one (status, image) per file; image is (H, W, 3) BGR or
+        (H, W) grey, a DeviceImage when device_out (it stays in HBM for the
+        encoder), else numpy."""
         n = len(datas)
         jobs = (N.DecodeJob * n)()
         keep, outs = [], [None] * n
         for i, d in enumerate(datas):
             if d is None:
                 raise TypeError("data must not be null")
-            if hasattr(d, "data_ptr"):
+            if isinstance(d, PinnedBuffer):
+                keep.append(d)
+                jobs[i].data, jobs[i].len = d.ptr, d.size
+            elif hasattr(d, "data_ptr"):
                 keep.append(d)
                 jobs[i].data, jobs[i].len = d.data_ptr(), d.numel()
             else:
@@ -335,8 +439,7 @@ class Codec:
                 s = subsampling if subsampling > 0 else subsampling_factor(w, h)
                 shape = (-(-h // s), -(-w // s), 3) if nc == 3 else (-(-h // s), -(-w // s))
                 if device_out:
-                    import torch
-                    out = torch.empty(shape, dtype=torch.uint8, device=f"cuda:{self.device}")
+                    out = DeviceImage(self, shape)
                     jobs[i].out, jobs[i].cap = out.data_ptr(), out.numel()
                 else:
                     out = np.empty(shape, np.uint8)
@@ -407,11 +510,13 @@ def jpeg_info(data):
 def _host_header(d):
     """Host bytes holding at least the JPEG header of d (a CUDA tensor is
     copied up to its SOS, in growing pieces)."""
+    if isinstance(d, PinnedBuffer):
+        return d.array
     if not hasattr(d, "data_ptr"):
         return np.frombuffer(d, np.uint8) if isinstance(d, (bytes, bytearray, memoryview)) else d
     n = min(d.numel(), 1 << 16)
     while True:
-        a = d[:n].cpu().numpy()
+        a = d.numpy(n) if getattr(d, "icx_device", False) else d[:n].cpu().numpy()
         if n == d.numel() or jpeg_info(a)[0] != N.E_CORRUPT:
             return a
         n = min(d.numel(), n * 4)

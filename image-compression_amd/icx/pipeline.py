@@ -88,14 +88,19 @@ def _to_array(im):
     return np.ascontiguousarray(rgb[:, :, ::-1])  # TYPE_3BYTE_BGR
 
 
-def _device_jpeg(input_path, params: CompressionParams):
-    """The header of a JPEG the device decoder supports, else None."""
+def _device_jpeg(input_path, params: CompressionParams, reader=None):
+    """The file bytes (read by `reader`: into pinned host memory when the codec
+    provides it) and header of a JPEG the device decoder supports, else None."""
     from .core import jpeg_info
-    with open(input_path, "rb") as f:
-        data = f.read()
-    if data[:2] != b"\xff\xd8":
+    if reader is None:
+        with open(input_path, "rb") as f:
+            data = f.read()
+    else:
+        data = reader(input_path)
+    head = data[:2] if isinstance(data, bytes) else bytes(data[:2])
+    if head != b"\xff\xd8":
         return None
-    st, w, h, _ = jpeg_info(data)
+    st, w, h, _ = jpeg_info(data if isinstance(data, bytes) else data.array)
     if st != N.OK:
         return None
     if w <= params.min_width or h <= params.min_height:  # ImageCompression.java:131
@@ -109,7 +114,7 @@ def _device_jpeg(input_path, params: CompressionParams):
 
 
 def decode_image_with_subsampling(input_path, params: CompressionParams, file_size: int,
-                                  device_jpeg: bool = False) -> Optional[DecodedImage]:
+                                  device_jpeg=False) -> Optional[DecodedImage]:
     """ImageCompression.decodeImageWithSubsampling: None when the file is at or
     below -s, has no reader, or is not larger than (-w, -i) on both axes.
     device_jpeg: leave supported JPEGs undecoded for the GPU (DecodedImage.data)."""
@@ -118,8 +123,8 @@ def decode_image_with_subsampling(input_path, params: CompressionParams, file_si
         log.info("%s - 跳過: 檔案大小 %s 未超過最小壓縮門檻 %s", input_path, format_file_size(file_size),
                  format_file_size(params.min_size_bytes))
         return None
-    if device_jpeg:
-        d = _device_jpeg(input_path, params)
+    if device_jpeg:  # True, or a reader callable (path -> bytes / PinnedBuffer)
+        d = _device_jpeg(input_path, params, None if device_jpeg is True else device_jpeg)
         if d is False:
             return None
         if d is not None:
@@ -247,8 +252,18 @@ def decode_group(codec, items: List[_Item]):
         it.decoded.data = None
 
 
-def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, cache):
-    """compressJpgWithTargetSize for a group of decoded JPEGs in one device batch."""
+def _jpeg_write(it: _Item, data: bytes, success: bool):
+    try:
+        with open(it.output, "wb") as f:
+            f.write(data)
+        _finish(it, success)
+    except Exception as e:
+        _fail(it, e)
+
+
+def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, cache, writer=None):
+    """compressJpgWithTargetSize for a group of decoded JPEGs in one device batch
+    (file writes on `writer`, a host thread pool, when given)."""
     try:
         decode_group(codec, items)
     except Exception as e:  # context-level failure: every image of the group fails alike
@@ -272,11 +287,15 @@ def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, ca
             if r["status"] != N.OK:
                 raise OSError(f"encode failed (icx status {r['status']})")
             if r["success"]:
-                with open(it.output, "wb") as f:
-                    f.write(r["data"])
                 if not r["cache_hit"]:
                     with cache.lock:
                         cache[key] = r["learned"]
+                it.decoded = None  # the frame's HBM buffer goes back to the pool now
+                if writer is not None:
+                    writer.submit(_jpeg_write, it, r["data"], True)
+                    continue
+                with open(it.output, "wb") as f:
+                    f.write(r["data"])
             _finish(it, r["success"])
         except Exception as e:
             _fail(it, e)
@@ -416,6 +435,10 @@ class CompressionBatch:
         if device_decode is None:
             device_decode = bool(self.codecs) and all(hasattr(c, "decode_jpg_batch") for c in self.codecs)
         self.device_decode = device_decode
+        if device_decode and self.codecs and hasattr(self.codecs[0], "_ctx"):
+            from .core import PinnedBuffer
+            c0 = self.codecs[0]  # portable pinned memory: DMA-able to every codec's GPU
+            self.device_decode = lambda path: PinnedBuffer.read_file(c0, path)
 
     def execute(self, cache=None, save_cache: bool = True) -> BatchReport:
         from .cache import CacheManager, LockedDict
@@ -466,7 +489,7 @@ class CompressionBatch:
                 if time.perf_counter() > deadline:  # shutdownNow(): unfinished tasks are dropped
                     continue
                 if kind == "jpeg":
-                    compress_jpeg_group(codec, its, self.params, cache)
+                    compress_jpeg_group(codec, its, self.params, cache, writer)
                 elif kind == "png":
                     for it in its:
                         compress_png_item(codec, it, self.params, writer)

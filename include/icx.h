@@ -202,6 +202,19 @@ icx_status icx_decode_jpg(icx_ctx* ctx, icx_decode_job* job);
  * occurred. */
 icx_status icx_decode_jpg_batch(icx_ctx* ctx, icx_decode_job* jobs, int32_t n);
 
+/* ------------------------------------------------------------ device memory */
+/* Buffers in the context GPU's HBM, so a decoded frame can stay on the device
+ * between icx_decode_jpg_batch and icx_compress_jpg_batch (pass the pointer
+ * as icx_decode_job.out and then as icx_image.px). */
+icx_status icx_device_alloc(icx_ctx* ctx, size_t bytes, void** ptr);
+icx_status icx_device_free(icx_ctx* ctx, void* ptr);
+/* Pinned (page-locked, portable) host buffers: file bytes read straight into
+ * one upload by DMA at link speed, with no staging copy. */
+icx_status icx_host_alloc(icx_ctx* ctx, size_t bytes, void** ptr);
+icx_status icx_host_free(icx_ctx* ctx, void* ptr);
+/* Synchronous copy between any two of host / this context's device memory. */
+icx_status icx_memcpy(icx_ctx* ctx, void* dst, const void* src, size_t bytes);
+
 /* ------------------------------------------------------- parity / metrics */
 /* Quantised coefficients after DC prediction (natural order, 64 per block,
  * scan/MCU block order incl. dummy blocks) as the device decoder produced them. */

@@ -43,16 +43,32 @@ def test_decode_pixels_match_golden_batch(codec, dgolden):
 
 def test_decode_to_device_and_subsampling(codec, oracle, dgolden):
     import torch
+
+    import icx
     meta, jpgs, pxs = dgolden
     for s in (1, 2, 3):
         for name in ("c130x250_s2_q95", "c66x130_s1_q50", "g47x61_q90", "rst7_130x250_444", "c7x9_s2_q95"):
             img = codec.decode_jpg(jpgs[name], subsampling=s, device_out=True)
-            assert isinstance(img, torch.Tensor) and img.is_cuda
-            assert np.array_equal(img.cpu().numpy(), pxs[name][::s, ::s]), (name, s)
-            # device-resident compressed input as well
-            dev_in = torch.from_numpy(np.frombuffer(jpgs[name], np.uint8).copy()).cuda()
-            img2 = codec.decode_jpg(dev_in, subsampling=s)
-            assert np.array_equal(img2, pxs[name][::s, ::s]), (name, s, "device input")
+            assert isinstance(img, icx.DeviceImage)
+            assert np.array_equal(img.numpy(), pxs[name][::s, ::s]), (name, s)
+            # device-resident compressed input: libicx buffer and CUDA tensor
+            dev_in = icx.DeviceImage.from_host(codec, jpgs[name])
+            assert np.array_equal(codec.decode_jpg(dev_in, subsampling=s), pxs[name][::s, ::s]), (name, s)
+            t_in = torch.from_numpy(np.frombuffer(jpgs[name], np.uint8).copy()).cuda()
+            assert np.array_equal(codec.decode_jpg(t_in, subsampling=s), pxs[name][::s, ::s]), (name, s)
+
+
+def test_decode_then_fit_in_hbm_matches_oracle(codec, oracle, dgolden):
+    """decode -> compressJpgWithTargetSize with the frame kept in HBM
+    (DeviceImage), as icx.pipeline runs it: same bytes as the oracle on the
+    oracle's decode."""
+    meta, jpgs, pxs = dgolden
+    for name in ("c130x250_s2_q95", "c130x250_s0_q95", "g130x250_q90"):
+        img = codec.decode_jpg(jpgs[name], device_out=True)
+        target = len(jpgs[name]) // 3
+        r = codec.fit([img], target, 0.25)[0]
+        o = oracle.fit(pxs[name], target, 0.25)
+        assert r["success"] == o["success"] and r.get("data") == o["data"], name
 
 
 def _jpeg(rgb, **kw):
