@@ -27,6 +27,9 @@ __constant__ uint8_t c_nat_to_zz[64];
 __constant__ uint8_t c_zz_to_nat[64];
 __constant__ uint32_t c_dc[2][16];    // (code << 8) | length, by category
 __constant__ uint32_t c_ac[2][256];   // (code << 8) | length, by run/size symbol
+// k_huff's AC table, pre-shifted per (run, size) slot: (code << size, len + size)
+// at [run * 11 + size]; built once by upload_constants.
+__constant__ uint2 c_acx[2][16 * 11];
 __constant__ uint8_t c_hdr[2][HDR_COLOR];  // [0] grey template, [1] colour template
 
 // ------------------------------------------------------------------ helpers
@@ -511,11 +514,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         s_qf[c][k] = make_float4(N.thr[c][k], N.frcp[c][k], N.fbias[c][k], 0.0f);
     }
     // AC codes pre-shifted for their (run, size) slot: (code << size, len + size)
-    for (int i = t; i < 2 * AC_ENTRIES; i += CHUNK_BLOCKS) {
-        const int c = i / AC_ENTRIES, r = i - c * AC_ENTRIES, run = r / AC_SIZES, sz = r - run * AC_SIZES;
-        const uint32_t h = c_ac[c][(run << 4) | sz];
-        s_ac[c][r] = make_uint2((h >> 8) << sz, (h & 255) + sz);
-    }
+    for (int i = t; i < 2 * AC_ENTRIES; i += CHUNK_BLOCKS) (&s_ac[0][0])[i] = (&c_acx[0][0])[i];
     if (t < 32) s_dc[t >> 4][t & 15] = c_dc[t >> 4][t & 15];
     if (t < 8) s_ffa[t] = 0;
 
@@ -962,6 +961,14 @@ hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_zz_to_nat), zz_to_nat, 64))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_dc), dc, sizeof(uint32_t) * 2 * 16))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_ac), ac, sizeof(uint32_t) * 2 * 256))) return e;
+    uint2 acx[2][16 * 11];
+    for (int c = 0; c < 2; c++)
+        for (int run = 0; run < 16; run++)
+            for (int sz = 0; sz < 11; sz++) {
+                const uint32_t h = ac[c][(run << 4) | sz];
+                acx[c][run * 11 + sz] = make_uint2((h >> 8) << sz, (h & 255) + sz);
+            }
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_acx), acx, sizeof(acx)))) return e;
     return hipMemcpyToSymbol(HIP_SYMBOL(c_hdr), hdr, 2 * HDR_COLOR);
 }
 
