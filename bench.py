@@ -74,6 +74,30 @@ def pmc_traffic(kernel, units_per_launch):
     return int(per_unit * units_per_launch)
 
 
+VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 256 CUs x 4 SIMD-32, 2 cycles each (MI355X_MICROARCH.md)
+SALU_PEAK = 256 * 2.4e9          # scalar instructions/s: one scalar unit per CU
+
+
+def issue_rates(kernel, units_per_launch, launch_s):
+    """Instruction-issue rates of the dominant kernel from the committed SQ
+    counter summary (profiles/sq_issue_summary.json, scripts/sq_issue.py):
+    instructions per unit of work x this run's units per launch / launch time,
+    against the chip's issue peaks.  None when no summary exists."""
+    path = os.path.join(ROOT, "profiles", "sq_issue_summary.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        pu = json.load(open(path))["per_unit"][kernel]
+    except (KeyError, ValueError):
+        return None
+    valu = pu["SQ_INSTS_VALU"] * units_per_launch / launch_s
+    salu = pu["SQ_INSTS_SALU"] * units_per_launch / launch_s
+    return {"valu_per_s": round(valu / 1e9, 1), "valu_peak_per_s": round(VALU_PEAK / 1e9, 1),
+            "valu_frac": round(valu / VALU_PEAK, 4), "salu_per_s": round(salu / 1e9, 1),
+            "salu_peak_per_s": round(SALU_PEAK / 1e9, 1), "salu_frac": round(salu / SALU_PEAK, 4),
+            "unit": "G wave-instructions/s"}
+
+
 def cpu_baseline(frames, n_sample, threads):
     """Oracle (scalar C restatement, test infrastructure) on host cores."""
     from tests.oracle_ffi import Oracle
@@ -247,6 +271,7 @@ def main():
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(dom, ks["units"] / ks["launches"]),
+                "issue": issue_rates(dom, ks["units"] / ks["launches"], ks["ms"] / ks["launches"] / 1e3),
                 "avg_launch_ms": round(ks["ms"] / ks["launches"], 4), "algo_bytes_per_launch": int(algo_launch)}
     res = batch.results()
     line = {
