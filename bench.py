@@ -273,6 +273,12 @@ def main():
                 "traffic": pmc_traffic(dom, ks["units"] / ks["launches"]),
                 "issue": issue_rates(dom, ks["units"] / ks["launches"], ks["ms"] / ks["launches"] / 1e3),
                 "avg_launch_ms": round(ks["ms"] / ks["launches"], 4), "algo_bytes_per_launch": int(algo_launch)}
+    # every kernel with an algorithmic-bytes model, against the HBM roofline
+    # (the north star's >= 60 % target is for the DCT stage, k_fdct)
+    stages = {k: {"achieved_GBps": round(ALGO_BYTES[k] * v["units"] / (v["ms"] / 1e3) / 1e9, 1),
+                  "frac": round(ALGO_BYTES[k] * v["units"] / (v["ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                  "avg_launch_ms": round(v["ms"] / v["launches"], 4), "algo_bytes_per_unit": ALGO_BYTES[k]}
+              for k, v in kstats.items() if k in ALGO_BYTES and v["units"]}
     res = batch.results()
     line = {
         "metric": "megapixels/sec JPEG encode (4K, -t 1MiB, q=0.25 cached)",
@@ -288,6 +294,7 @@ def main():
                    "encodes_per_image": round(sum(r["encodes"] for r in res) / len(res), 3),
                    "mean_out_bytes": int(np.mean([r["out_len"] for r in res]))},
         "roofline": roof,
+        "stages": stages,
         "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k, v in kstats.items()},
     }
     if rank == 0 and world == 1 and args.e2e and not args.host_io:

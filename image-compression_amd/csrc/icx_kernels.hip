@@ -293,13 +293,21 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
     const uint32_t bbase = (uint32_t)(my * D.mcux + tx * FDC_MCU) * 6;  // < 2^31 blocks per image
     const bool plain = nmcu == FDC_MCU && !bottom && 2 * (tx * FDC_MCU + FDC_MCU - 1) + 1 < D.ywb;
     if (plain) {  // full interior tile: no dummy blocks, constant-divisor indexing
+        // 16-B stores: quad k of blocks b, b+1 (b even: bbase is a multiple of
+        // 6, so a pair never straddles a 256-block chunk) is 16 contiguous,
+        // 16-B aligned bytes of the interleaved layout
 #pragma unroll
-        for (int i = 0; i < FDC_BLK * 16 / 256; i++) {
-            const int e = t + 256 * i, quad = e / FDC_BLK, blk = e - quad * FDC_BLK;
+        for (int i = 0; i < FDC_BLK * 8 / 256; i++) {
+            const int e = t + 256 * i, quad = e / (FDC_BLK / 2), pr = e - quad * (FDC_BLK / 2), blk = 2 * pr;
             const uint32_t b = bbase + blk;
-            st8(D.coefs + ((size_t)(b / CHUNK_BLOCKS) * (CHUNK_BLOCKS * 64) + quad * (CHUNK_BLOCKS * 4) +
-                           (b % CHUNK_BLOCKS) * 4),
-                *(const int2*)&oz[blk][quad * 4]);
+            const int2 lo = *(const int2*)&oz[blk][quad * 4], hi = *(const int2*)&oz[blk + 1][quad * 4];
+            u32x4_t v;
+            v.x = lo.x;
+            v.y = lo.y;
+            v.z = hi.x;
+            v.w = hi.y;
+            *(GAS u32x4_t*)(D.coefs + ((size_t)(b / CHUNK_BLOCKS) * (CHUNK_BLOCKS * 64) + quad * (CHUNK_BLOCKS * 4) +
+                                       (b % CHUNK_BLOCKS) * 4)) = v;
         }
     } else {
         for (int e = t; e < nblk * 16; e += 256) {  // (quad, block) pieces of 8 B, block fastest
