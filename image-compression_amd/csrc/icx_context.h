@@ -223,4 +223,53 @@ inline icx_status upload(icx_ctx* c, void* dst, const void* src, size_t n)
     return e == hipSuccess ? ICX_OK : hip_fail(c, e, "hipMemcpyAsync(H2D)");
 }
 
+// Packs a launch's small host->device arguments (descriptors, tables, work
+// plans) into one pinned block and one copy.  alloc() hands out the device
+// address at once (so descriptors can point at each other) and the host slot
+// to fill before flush().
+struct Uploader {
+    icx_ctx* c;
+    uint8_t *h = nullptr, *d = nullptr;
+    size_t cap = 0, used = 0;
+    bool overflow = false;
+    Uploader(icx_ctx* ctx, size_t bytes) : c(ctx), cap(bytes)
+    {
+        h = (uint8_t*)c->host.take(bytes);
+        d = (uint8_t*)c->dev.take(bytes);
+    }
+    template <class T>
+    T* alloc(size_t count, T** host)
+    {
+        used = align_up(used, 64);
+        const size_t n = sizeof(T) * count;
+        if (!h || used + n > cap) {
+            overflow = true;
+            *host = nullptr;
+            return nullptr;
+        }
+        *host = (T*)(h + used);
+        T* p = (T*)(d + used);
+        used += n;
+        return p;
+    }
+    template <class T>
+    T* put(const T* src, size_t count)
+    {
+        T* hp;
+        T* p = alloc<T>(count, &hp);
+        if (hp) memcpy((void*)hp, (const void*)src, sizeof(T) * count);
+        return p;
+    }
+    // Bytes to reserve for `count` objects of T (with the 64-byte alignment).
+    template <class T>
+    static size_t need(size_t count) { return align_up(sizeof(T) * count, 64); }
+    icx_status flush()
+    {
+        if (overflow) return fail(c, ICX_E_NOMEM, "upload staging exhausted");
+        if (!used) return ICX_OK;
+        hipError_t e = hipMemcpyAsync(d, h, used, hipMemcpyHostToDevice, c->stream);
+        return e == hipSuccess ? ICX_OK : hip_fail(c, e, "hipMemcpyAsync(H2D)");
+    }
+};
+
 }  // namespace icx

@@ -36,19 +36,65 @@ struct DecItem {
     size_t ent_cap = 0;
 };
 
-icx_status read_header(icx_ctx* c, const uint8_t* data, size_t len, bool dev, JpegHeader& J)
+// Headers of device-resident files: their first bytes are gathered into one
+// device buffer by k_stage and downloaded in one copy; a file whose header runs
+// past what was fetched goes again with 8x more (4 KiB, 32 KiB, ...).
+icx_status fetch_headers(icx_ctx* c, const icx_decode_job* jobs, int n, const std::vector<char>& dev_in,
+                         std::vector<JpegHeader>& J, std::vector<icx_status>& st)
 {
-    if (!dev) return parse_jpeg(data, len, len, J);
-    std::vector<uint8_t> tmp;
-    size_t avail = std::min<size_t>(len, 64 << 10);
-    for (;;) {
-        tmp.resize(avail);
-        hipError_t e = hipMemcpy(tmp.data(), data, avail, hipMemcpyDeviceToHost);
+    std::vector<int> pend;
+    std::vector<size_t> avail(n, 0);
+    for (int i = 0; i < n; i++)
+        if (dev_in[i]) {
+            pend.push_back(i);
+            avail[i] = std::min<size_t>(jobs[i].len, 4096);
+        }
+    while (!pend.empty()) {
+        const int m = (int)pend.size();
+        size_t bytes = 0;
+        for (int i : pend) bytes += align_up(avail[i], 64);
+        const size_t up = Uploader::need<StageJob>(m) + Uploader::need<int64_t>(m + 1);
+        hipError_t e = c->dev.reserve(bytes + up + 4096);
+        if (e == hipSuccess) e = c->host.reserve(bytes + up + 4096);
+        if (e != hipSuccess) return hip_fail(c, e, "header staging");
+        c->dev.used = c->host.used = 0;
+        uint8_t* dbuf = (uint8_t*)c->dev.take(bytes);
+        uint8_t* hbuf = (uint8_t*)c->host.take(bytes);
+        Uploader U(c, up);
+        StageJob* hj;
+        int64_t* hp;
+        const StageJob* dj = U.alloc<StageJob>(m, &hj);
+        const int64_t* dp = U.alloc<int64_t>(m + 1, &hp);
+        if (U.overflow || !hbuf) return fail(c, ICX_E_NOMEM, "header staging exhausted");
+        std::vector<size_t> at(m);
+        size_t off = 0;
+        hp[0] = 0;
+        for (int k = 0; k < m; k++) {
+            const int i = pend[k];
+            const int64_t dl = (int64_t)align_up(avail[i], 16);
+            hj[k] = StageJob{jobs[i].data, dbuf + off, (int64_t)avail[i], dl};
+            hp[k + 1] = hp[k] + (dl + STAGE_TILE - 1) / STAGE_TILE;
+            at[k] = off;
+            off += align_up(avail[i], 64);
+        }
+        const int64_t nwg = hp[m];
+        if (icx_status s = U.flush()) return s;
+        launch_stage(dj, Plan{nullptr, dp, m}, nwg, c->stream);
+        e = hipMemcpyAsync(hbuf, dbuf, bytes, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "header download");
-        icx_status s = parse_jpeg(tmp.data(), avail, len, J);
-        if (s != ICX_E_BUFFER || avail >= len) return s;
-        avail = std::min(len, avail * 4);
+        std::vector<int> next;
+        for (int k = 0; k < m; k++) {
+            const int i = pend[k];
+            st[i] = parse_jpeg(hbuf + at[k], avail[i], jobs[i].len, J[i]);
+            if (st[i] == ICX_E_BUFFER && avail[i] < jobs[i].len) {
+                avail[i] = std::min<size_t>(jobs[i].len, avail[i] * 8);
+                next.push_back(i);
+            }
+        }
+        pend.swap(next);
     }
+    return ICX_OK;
 }
 
 // Geometry of the decode (jdmaster.c jpeg_calc_output_dimensions / per-component dims).
@@ -81,6 +127,7 @@ void dec_geometry(const JpegHeader& J, int s, DecDesc& d)
         d.ph[c] = (d.ch[c] + 7) / 8 * 8;
     }
     d.fancy = J.ncomp == 3 && d.hs == 2 && d.cw[1] > 2;  // do_fancy_upsampling && downsampled_width > 2
+    d.fuse420 = s == 1 && J.ncomp == 3 && d.hs == 2 && d.vs == 2 && d.fancy;
     d.s = s;
     d.ow = (J.w + s - 1) / s;
     d.oh = (J.h + s - 1) / s;
@@ -113,18 +160,16 @@ struct WPlan {
     int64_t total;
 };
 
-icx_status plan_of(icx_ctx* c, const std::vector<int64_t>& counts, const int32_t* d_ids, WPlan& out)
+WPlan plan_of(Uploader& U, const std::vector<int64_t>& counts, const int32_t* d_ids)
 {
     std::vector<int64_t> pre(counts.size() + 1, 0);
     for (size_t i = 0; i < counts.size(); i++) pre[i + 1] = pre[i] + counts[i];
-    int64_t* d_pre = (int64_t*)c->dev.take(pre.size() * 8);
-    icx_status s = upload(c, d_pre, pre.data(), pre.size() * 8);
-    if (s) return s;
+    WPlan out;
     out.p.ids = d_ids;
-    out.p.prefix = d_pre;
+    out.p.prefix = U.put(pre.data(), pre.size());
     out.p.m = (int32_t)counts.size();
     out.total = pre.back();
-    return ICX_OK;
+    return out;
 }
 
 // mode 0: decode to pixels; mode 1: coefficients only (debug: natural order, DC in [0])
@@ -135,32 +180,11 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
     if (he != hipSuccess) return hip_fail(c, he, "hipSetDevice");
     std::vector<DecItem> items;
     items.reserve(n);
-    // headers of device-resident files: one batched download of their first 64 KiB
-    const size_t HEAD = 64 << 10;
     std::vector<char> dev_in(n, 0);
-    std::vector<const uint8_t*> head(n, nullptr);
-    {
-        size_t total = 0;
-        for (int i = 0; i < n; i++)
-            if (jobs[i].data && is_device_ptr(jobs[i].data)) {
-                dev_in[i] = 1;
-                total += align_up(std::min(jobs[i].len, HEAD), 64);
-            }
-        if (total) {
-            hipError_t e = c->host.reserve(std::max<size_t>(total + 4096, 64 << 20));
-            if (e != hipSuccess) return hip_fail(c, e, "hipHostMalloc");
-            c->host.used = 0;
-            for (int i = 0; i < n; i++)
-                if (dev_in[i]) {
-                    uint8_t* h = (uint8_t*)c->host.take(std::min(jobs[i].len, HEAD));
-                    e = hipMemcpyAsync(h, jobs[i].data, std::min(jobs[i].len, HEAD), hipMemcpyDeviceToHost, c->stream);
-                    if (e != hipSuccess) return hip_fail(c, e, "header download");
-                    head[i] = h;
-                }
-            e = hipStreamSynchronize(c->stream);
-            if (e != hipSuccess) return hip_fail(c, e, "header download");
-        }
-    }
+    for (int i = 0; i < n; i++) dev_in[i] = jobs[i].data && is_device_ptr(jobs[i].data);
+    std::vector<JpegHeader> hdr(n);
+    std::vector<icx_status> hst(n, ICX_OK);
+    if (icx_status s = fetch_headers(c, jobs, n, dev_in, hdr, hst)) return s;
     for (int i = 0; i < n; i++) {
         icx_decode_job& j = jobs[i];
         j.width = j.height = j.src_width = j.src_height = 0;
@@ -174,8 +198,8 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         it.job = &j;
         it.dev_in = dev_in[i];
         if (it.dev_in) {
-            j.status = parse_jpeg(head[i], std::min(j.len, HEAD), j.len, it.J);
-            if (j.status == ICX_E_BUFFER) j.status = read_header(c, j.data, j.len, true, it.J);  // header > 64 KiB
+            it.J = hdr[i];
+            j.status = hst[i];
         } else {
             j.status = parse_jpeg(j.data, j.len, j.len, it.J);
         }
@@ -230,7 +254,11 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         }
         const int m = (int)sub.size();
         const uint32_t S = pick_sub_bits(bits);
-        hipError_t e = c->dev.reserve(need + (size_t)m * 64 * 1024 + (16 << 20));
+        // every small argument array of the sub-batch travels in one packed upload
+        const size_t up = Uploader::need<DecTab>(m) + Uploader::need<DecDesc>(m) + Uploader::need<DecState>(m) +
+                          Uploader::need<int32_t>(m) + Uploader::need<StageJob>(m) +
+                          6 * Uploader::need<int64_t>(m + 1);
+        hipError_t e = c->dev.reserve(need + up + (size_t)m * 64 * 1024 + (16 << 20));
         if (e != hipSuccess) {
             for (DecItem* it : sub) it->job->status = ICX_E_NOMEM;
             (void)hipGetLastError();
@@ -238,41 +266,53 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             continue;
         }
         c->dev.used = 0;
-        size_t host_need = 64 << 20;
+        size_t host_need = (64 << 20) + up;
         for (DecItem* it : sub)
             if (!it->dev_in && !is_pinned_ptr(it->job->data)) host_need += align_up(it->job->len, 64);
         e = c->host.reserve(host_need);
         if (e != hipSuccess) return hip_fail(c, e, "hipHostMalloc");
         c->host.used = 0;
+        Uploader U(c, up);
 
-        std::vector<DecTab> tabs(m);
+        DecTab* h_tab;
+        DecTab* d_tab = U.alloc<DecTab>(m, &h_tab);
+        StageJob* h_stage;
+        const StageJob* d_stage = U.alloc<StageJob>(m, &h_stage);
+        if (U.overflow) return fail(c, ICX_E_NOMEM, "upload staging exhausted");
         std::vector<DecState> states(m);
-        DecTab* d_tab = (DecTab*)c->dev.take(sizeof(DecTab) * m);
+        std::vector<int64_t> cnt_stage(m);
         int64_t max_nsub = 0;
         for (int k = 0; k < m; k++) {
             DecItem& it = *sub[k];
             DecDesc& d = desc[k];
-            if (!build_dec_tab(it.J, tabs[k])) {
+            h_tab[k] = DecTab{};
+            if (!build_dec_tab(it.J, h_tab[k])) {
                 it.job->status = ICX_E_CORRUPT;
                 states[k].status = 6;
             }
             const int64_t scan_len = (int64_t)(it.job->len - it.J.scan_off);
             d.scan_len = scan_len;
             d.ntiles = (int32_t)it.ntiles;
+            // the scan copy: 16-B aligned, zero-padded by 64 bytes (k_unstuff_* read past the end)
+            const int64_t padded = (int64_t)align_up(scan_len + 64, 16);
             uint8_t* scan = (uint8_t*)c->dev.take(align_up(scan_len + 64, 256));
-            e = hipMemsetAsync(scan + scan_len, 0, 64, c->stream);
             const uint8_t* src = it.job->data + it.J.scan_off;
-            if (!it.dev_in && !is_pinned_ptr(it.job->data)) {  // pageable: via pinned staging (DMA at link speed)
-                uint8_t* h = (uint8_t*)c->host.take(scan_len);
-                if (h) {
-                    memcpy(h, src, scan_len);
-                    src = h;
+            if (it.dev_in) {  // device file: k_stage copies and pads
+                h_stage[k] = StageJob{src, scan, scan_len, padded};
+            } else {  // host file: one DMA (pageable: via pinned staging), k_stage pads the tail in place
+                if (!is_pinned_ptr(it.job->data)) {
+                    uint8_t* h = (uint8_t*)c->host.take(scan_len);
+                    if (h) {
+                        memcpy(h, src, scan_len);
+                        src = h;
+                    }
                 }
+                e = hipMemcpyAsync(scan, src, scan_len, hipMemcpyHostToDevice, c->stream);
+                if (e != hipSuccess) return hip_fail(c, e, "scan upload");
+                const int64_t t0 = scan_len & ~(int64_t)15;
+                h_stage[k] = StageJob{scan + t0, scan + t0, scan_len - t0, padded - t0};
             }
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(scan, src, scan_len, it.dev_in ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                                   c->stream);
-            if (e != hipSuccess) return hip_fail(c, e, "scan upload");
+            cnt_stage[k] = (h_stage[k].dst_len + STAGE_TILE - 1) / STAGE_TILE;
             d.scan = scan;
             d.ent = (uint8_t*)c->dev.take(align_up(it.ent_cap, 256));
             d.ent_cap = (int64_t)it.ent_cap;
@@ -289,7 +329,8 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             d.coefs = (int16_t*)c->dev.take((size_t)d.nblocks * 128);
             d.dc = (int32_t*)c->dev.take((size_t)d.nblocks * 4);
             if (!coef_out) {
-                for (int q = 0; q < d.ncomp; q++) d.plane[q] = (uint8_t*)c->dev.take((size_t)d.pw[q] * d.ph[q]);
+                for (int q = d.fuse420 ? 1 : 0; q < d.ncomp; q++)  // fuse420: luma stays in LDS
+                    d.plane[q] = (uint8_t*)c->dev.take((size_t)d.pw[q] * d.ph[q]);
                 it.host_out = !is_device_ptr(it.job->out);
                 d.out = it.host_out ? (uint8_t*)c->dev.take(it.job->out_len) : it.job->out;
                 d.ostride = d.ow * it.nch;
@@ -297,44 +338,40 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             d.tab = d_tab + k;
             states[k].end = scan_len;  // coefficients need no clearing: the write pass stores whole blocks
         }
-        DecDesc* d_desc = (DecDesc*)c->dev.take(sizeof(DecDesc) * m);
-        DecState* d_state = (DecState*)c->dev.take(sizeof(DecState) * m);
         const int max_it = (int)max_nsub + 8;  // each launch settles at least one more subsequence
         uint32_t* d_changed = (uint32_t*)c->dev.take((size_t)max_it * 4);
         uint32_t* d_wlcnt = (uint32_t*)c->dev.take((size_t)m * max_it * 4);
         for (int k = 0; k < m; k++) desc[k].wl_cnt = d_wlcnt;
         uint32_t* h_changed = (uint32_t*)c->host.take(4);
-        int32_t* d_ids = (int32_t*)c->dev.take((size_t)m * 4);
         std::vector<int32_t> ids(m);
         for (int k = 0; k < m; k++) ids[k] = k;
-        icx_status st;
-        if ((st = upload(c, d_tab, tabs.data(), sizeof(DecTab) * m)) ||
-            (st = upload(c, d_desc, desc.data(), sizeof(DecDesc) * m)) ||
-            (st = upload(c, d_state, states.data(), sizeof(DecState) * m)) ||
-            (st = upload(c, d_ids, ids.data(), (size_t)m * 4)))
-            return st;
-        e = hipMemsetAsync(d_changed, 0, (size_t)max_it * 4, c->stream);
-        if (e == hipSuccess) e = hipMemsetAsync(d_wlcnt, 0, (size_t)m * max_it * 4, c->stream);
-        if (e != hipSuccess) return hip_fail(c, e, "counter clear");
+        const DecDesc* d_desc = U.put(desc.data(), m);
+        DecState* d_state = U.put(states.data(), m);
+        const int32_t* d_ids = U.put(ids.data(), m);
 
         std::vector<int64_t> cnt_tiles(m), cnt_subs(m), cnt_blk(m), cnt_px(m), cnt_rows(m);
         int64_t stuffed = 0;
         for (int k = 0; k < m; k++) {
             cnt_tiles[k] = sub[k]->ntiles;
             cnt_subs[k] = (desc[k].nsub_max + 1 + 255) / 256;
-            cnt_blk[k] = (desc[k].nblocks + 31) / 32;
-            // colour: the row-pair kernel for s == 1 4:2:0 fancy, the per-pixel gather kernel otherwise
-            const bool rows = desc[k].s == 1 && desc[k].ncomp == 3 && desc[k].hs == 2 && desc[k].vs == 2 &&
-                              desc[k].fancy;
-            cnt_px[k] = rows ? 0 : ((int64_t)desc[k].oh * ((desc[k].ow + 3) / 4) + 255) / 256;
-            cnt_rows[k] = rows ? (int64_t)((desc[k].oh + 1) / 2) * ((desc[k].ow + 1023) / 1024) : 0;
+            // colour: luma IDCT fused with upsampling + conversion for s == 1 4:2:0 fancy (chroma
+            // blocks alone go through k_dec_idct), the per-pixel gather kernel otherwise
+            const DecDesc& q = desc[k];
+            const int64_t nmcu = (int64_t)q.mcux * q.mcuy;
+            cnt_blk[k] = q.fuse420 ? (2 * nmcu + 31) / 32 : (q.nblocks + 31) / 32;
+            cnt_px[k] = q.fuse420 ? 0 : ((int64_t)q.oh * ((q.ow + 3) / 4) + 255) / 256;
+            cnt_rows[k] = q.fuse420 ? (int64_t)q.mcuy * ((q.mcux + 7) / 8) : 0;
             stuffed += desc[k].scan_len;
         }
-        WPlan Pt, Ps, Pb, Pp, Pr;
-        if ((st = plan_of(c, cnt_tiles, d_ids, Pt)) || (st = plan_of(c, cnt_subs, d_ids, Ps)) ||
-            (st = plan_of(c, cnt_blk, d_ids, Pb)) || (st = plan_of(c, cnt_px, d_ids, Pp)) ||
-            (st = plan_of(c, cnt_rows, d_ids, Pr)))
-            return st;
+        const WPlan Pg = plan_of(U, cnt_stage, d_ids), Pt = plan_of(U, cnt_tiles, d_ids),
+                    Ps = plan_of(U, cnt_subs, d_ids), Pb = plan_of(U, cnt_blk, d_ids),
+                    Pp = plan_of(U, cnt_px, d_ids), Pr = plan_of(U, cnt_rows, d_ids);
+        icx_status st = U.flush();
+        if (st) return st;
+        e = hipMemsetAsync(d_changed, 0, (size_t)max_it * 4, c->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(d_wlcnt, 0, (size_t)m * max_it * 4, c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "counter clear");
+        launch_stage(d_stage, Pg.p, Pg.total, c->stream);
         {
             Timed tm(c, "dec_unstuff", stuffed);
             launch_unstuff(d_desc, d_state, Pt.p, Pt.total, d_ids, m, S, c->stream);
@@ -375,7 +412,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             }
             {
                 Timed tm(c, "dec_color", px);
-                launch_dec_color_420(d_desc, d_state, Pr.p, Pr.total, c->stream);
+                launch_dec_luma_color_420(d_desc, d_state, Pr.p, Pr.total, c->stream);
                 launch_dec_color(d_desc, d_state, Pp.p, Pp.total, c->stream);
             }
         }

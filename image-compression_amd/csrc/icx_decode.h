@@ -101,8 +101,19 @@ struct DecDesc {
     int32_t w, h, ncomp, hs, vs, nby, nbmcu, mcux, mcuy, ri;
     int32_t pw[3], ph[3], cw[3], ch[3];
     int32_t fancy;         // chroma upsampled with the triangle filter (cw > 2)
+    int32_t fuse420;       // s == 1, 4:2:0, fancy: luma IDCT fused into the colour pass (no luma plane)
     int32_t s, ow, oh, ostride;
 };
+
+// One k_stage copy: len bytes from src (any alignment, device memory) to dst
+// (16-byte aligned), then zeros up to dst_len (a multiple of 16).  src may
+// equal dst (in-place padding of an uploaded scan's last partial 16 bytes).
+struct StageJob {
+    const uint8_t* src;
+    uint8_t* dst;
+    int64_t len, dst_len;
+};
+constexpr int STAGE_TILE = 4096;  // bytes per k_stage workgroup
 
 // Device-written per-image results.
 struct DecState {

@@ -14,6 +14,9 @@
 //   k_dec_write        decode again from the settled states, store coefficients
 //   k_dec_dc           per image: DC prediction (segmented per restart interval)
 //   k_dec_idct         jpeg_idct_islow of every real block into component planes
+//                      (chroma blocks only when k_dec_luma_color_420 runs)
+//   k_dec_luma_color_420  s == 1 4:2:0 fancy: luma IDCT + h2v2 fancy upsampling
+//                      + ycc_rgb_convert, one MCU row x 8 MCUs per workgroup
 //   k_dec_color        fancy upsampling + ycc_rgb_convert + source subsampling
 // Byte/bit-serial integer work; no MFMA.  The entropy stages are bound by the
 // dependent table look-ups of the bit-serial walk, the pixel stages by HBM.
@@ -83,6 +86,37 @@ __device__ __forceinline__ void load16(const DecDesc& d, int64_t base, Bytes16& 
 }
 
 }  // namespace
+
+// -------------------------------------------------------------------- stage
+// Gathers file bytes into aligned, zero-padded device buffers for a whole
+// sub-batch in one launch (headers for the host parser, entropy segments for
+// k_unstuff_*): 16 bytes per thread from five aligned dwords and a byte
+// funnel shift; a dword is read only if it holds a byte of the source.
+__global__ void __launch_bounds__(256) k_stage(const StageJob* J, Plan p)
+{
+    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    const StageJob j = J[slot];
+    const int64_t o = (blockIdx.x - p.prefix[slot]) * (int64_t)STAGE_TILE + threadIdx.x * 16;
+    if (o >= j.dst_len) return;
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (o < j.len) {
+        const uintptr_t s = (uintptr_t)(j.src + o), end = (uintptr_t)(j.src + j.len);
+        const uintptr_t a = s & ~(uintptr_t)3;
+        const uint32_t sh = (uint32_t)(s & 3);
+        uint32_t x[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) x[k] = a + 4 * k < end ? *(const uint32_t*)(a + 4 * k) : 0u;
+        const int64_t rem = j.len - o;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint32_t v = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
+            const int64_t nb = rem - 4 * k;  // valid bytes in this dword
+            if (nb < 4) v = nb <= 0 ? 0u : v & ((1u << (8 * nb)) - 1);
+            w[k] = v;
+        }
+    }
+    *(uint4*)(j.dst + o) = make_uint4(w[0], w[1], w[2], w[3]);
+}
 
 // ------------------------------------------------------------------ unstuff
 __global__ void __launch_bounds__(256) k_unstuff_end(const DecDesc* D, DecState* S, Plan p)
@@ -518,7 +552,50 @@ __device__ __forceinline__ uint32_t idct_limit(int32_t v)
     return x < 128 ? (uint32_t)(x + 128) : x < 512 ? 255u : x < 896 ? 0u : (uint32_t)(x - 896);
 }
 
-// 8 threads per block (thread r owns row r), 32 blocks per workgroup; one image per workgroup.
+// jpeg_idct_islow of one block by 8 threads (thread r owns coefficient row r,
+// then column r, then output row r); ws = this block's 8 x 9 LDS workspace.
+// Returns output row r as 8 range-limited samples packed in two dwords.  The
+// caller's 8 threads must all reach the barriers (real == false: no work).
+__device__ __forceinline__ uint2 idct_block_row(const DecDesc& d, int64_t b, int comp, int r, bool real,
+                                                int32_t* ws)
+{
+    int32_t v[8];
+    if (real) {
+        const uint4 q = *(const uint4*)(d.coefs + b * 64 + r * 8);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+        const uint16_t* qt = d.tab->qt[comp] + r * 8;
+#pragma unroll
+        for (int c = 0; c < 8; c++) v[c] = (int32_t)(int16_t)(w[c >> 1] >> (16 * (c & 1))) * (int32_t)qt[c];
+        if (r == 0) v[0] = d.dc[b] * (int32_t)qt[0];
+#pragma unroll
+        for (int c = 0; c < 8; c++) ws[r * 9 + c] = v[c];
+    }
+    __syncthreads();
+    if (real) {  // pass 1: column r
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = ws[k * 9 + r];
+        idct8<CONST_BITS - PASS1_BITS>(v);
+#pragma unroll
+        for (int k = 0; k < 8; k++) ws[k * 9 + r] = v[k];
+    }
+    __syncthreads();
+    uint32_t lo = 0, hi = 0;
+    if (real) {  // pass 2: row r
+#pragma unroll
+        for (int c = 0; c < 8; c++) v[c] = ws[r * 9 + c];
+        idct8<CONST_BITS + PASS1_BITS + 3>(v);
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            lo |= idct_limit(v[c]) << (8 * c);
+            hi |= idct_limit(v[c + 4]) << (8 * c);
+        }
+    }
+    return make_uint2(lo, hi);
+}
+
+// 8 threads per block, 32 blocks per workgroup, one image per workgroup, into
+// the component planes.  fuse420 images: chroma blocks only (their luma IDCT
+// runs inside k_dec_luma_color_420).
 __global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecState* S, Plan p)
 {
     __shared__ int32_t ws[32][8 * 9];
@@ -527,13 +604,20 @@ __global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecSta
     const DecDesc& d = D[img];
     if (S[img].status) return;
     const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;
-    const int64_t b = (blockIdx.x - p.prefix[slot]) * 32 + lb;
+    const int i = (int)(blockIdx.x - p.prefix[slot]) * 32 + lb;  // < 2^31: at most 65535^2 * 3 / 64 blocks
+    int m, k;
+    if (d.fuse420) {
+        m = i >> 1;
+        k = d.nby + (i & 1);
+    } else {
+        m = i / d.nbmcu;
+        k = i - m * d.nbmcu;
+    }
+    const int64_t b = (int64_t)m * d.nbmcu + k;
     const bool valid = b < d.nblocks;
     int comp = 0, bx = 0, by = 0;
     if (valid) {
-        const int64_t m = b / d.nbmcu;
-        const int k = (int)(b - m * d.nbmcu);
-        const int mx = (int)(m % d.mcux), my = (int)(m / d.mcux);
+        const int mx = m % d.mcux, my = m / d.mcux;
         if (k < d.nby) {
             bx = mx * d.hs + k % d.hs;
             by = my * d.vs + k / d.hs;
@@ -544,39 +628,8 @@ __global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecSta
         }
     }
     const bool real = valid && bx * 8 < d.pw[comp] && by * 8 < d.ph[comp];  // dummy blocks: no IDCT (jdcoefct.c)
-    int32_t v[8];
-    if (real) {
-        const uint4 q = *(const uint4*)(d.coefs + b * 64 + r * 8);
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-        const uint16_t* qt = d.tab->qt[comp] + r * 8;
-#pragma unroll
-        for (int c = 0; c < 8; c++) v[c] = (int32_t)(int16_t)(w[c >> 1] >> (16 * (c & 1))) * (int32_t)qt[c];
-        if (r == 0) v[0] = d.dc[b] * (int32_t)qt[0];
-#pragma unroll
-        for (int c = 0; c < 8; c++) ws[lb][r * 9 + c] = v[c];
-    }
-    __syncthreads();
-    if (real) {  // pass 1: column r
-#pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = ws[lb][k * 9 + r];
-        idct8<CONST_BITS - PASS1_BITS>(v);
-#pragma unroll
-        for (int k = 0; k < 8; k++) ws[lb][k * 9 + r] = v[k];
-    }
-    __syncthreads();
-    if (real) {  // pass 2: row r
-#pragma unroll
-        for (int c = 0; c < 8; c++) v[c] = ws[lb][r * 9 + c];
-        idct8<CONST_BITS + PASS1_BITS + 3>(v);
-        uint32_t lo = 0, hi = 0;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            lo |= idct_limit(v[c]) << (8 * c);
-            hi |= idct_limit(v[c + 4]) << (8 * c);
-        }
-        uint8_t* dst = d.plane[comp] + (int64_t)(by * 8 + r) * d.pw[comp] + bx * 8;
-        *(uint2*)dst = make_uint2(lo, hi);
-    }
+    const uint2 row = idct_block_row(d, b, comp, r, real, ws[lb]);
+    if (real) *(uint2*)(d.plane[comp] + (int64_t)(by * 8 + r) * d.pw[comp] + bx * 8) = row;
 }
 
 // ----------------------------------------------------------- colour output
@@ -648,56 +701,69 @@ __global__ void __launch_bounds__(256) k_dec_color(const DecDesc* D, const DecSt
 }
 
 // s == 1, 4:2:0 with fancy upsampling (the JDK decode of nearly every photo):
-// one workgroup per output row pair (2r, 2r+1) x 1024 columns.  Both luma rows
-// and chroma rows r-1, r, r+1 (edge-replicated, jdmainct.c context rows) are
-// staged in LDS with coalesced loads; each thread converts a 4 x 2 pixel tile
-// from the 3 x 4 chroma neighbourhood it shares (h2v2_fancy_upsample).
-constexpr int CT_PX = 1024;
-__global__ void __launch_bounds__(256) k_dec_color_420(const DecDesc* D, const DecState* S, Plan p)
+// one workgroup per MCU row x LC_NM MCUs (16 x 128 output pixels).  The 32
+// luma blocks are inverse-transformed straight into an LDS tile (the luma
+// plane never reaches HBM); chroma rows cy0-1 .. cy0+8 (edge-replicated,
+// jdmainct.c context rows) and columns cx0-4 .. cx0+67 of both chroma planes
+// (written by k_dec_idct) are staged as dwords; each thread then converts a
+// 4 x 2 pixel tile from the 3 x 4 chroma neighbourhood it shares
+// (h2v2_fancy_upsample + ycc_rgb_convert).
+constexpr int LC_NM = 8;
+constexpr int LC_W = 16 * LC_NM;      // output columns per tile
+constexpr int LC_CD = LC_W / 8 + 2;   // chroma dwords per staged row
+__global__ void __launch_bounds__(256) k_dec_luma_color_420(const DecDesc* D, const DecState* S, Plan p)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t ly[2][CT_PX];
-    __shared__ uint8_t lc[2][3][CT_PX / 2 + 8];  // [cb|cr][row r-1|r|r+1], chroma column c at c - cbase
+    __shared__ int32_t ws[32][8 * 9];
+    __shared__ __attribute__((aligned(16))) uint32_t ly[16][LC_W / 4];
+    __shared__ uint32_t lc[2][10][LC_CD];  // [cb|cr][chroma row cy0-1+j][dword]; byte q <-> column cx0-4+q
     const int slot = slot_of(p.prefix, p.m, blockIdx.x);
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
     if (S[img].status) return;
-    const int tpr = (d.ow + CT_PX - 1) / CT_PX;
-    const int64_t item = blockIdx.x - p.prefix[slot];
-    const int r = (int)(item / tpr), x0 = (int)(item % tpr) * CT_PX;
-    const int n = d.ow - x0 < CT_PX ? d.ow - x0 : CT_PX;
+    const int tpr = (d.mcux + LC_NM - 1) / LC_NM;
+    const int item = (int)(blockIdx.x - p.prefix[slot]);
+    const int my = item / tpr, mx0 = (item - my * tpr) * LC_NM;
     const int t = threadIdx.x;
-    const int y0 = 2 * r, rows = d.oh - y0 < 2 ? 1 : 2;
-    for (int q = 0; q < rows; q++) {
-        const uint32_t* yr = (const uint32_t*)(d.plane[0] + (int64_t)(y0 + q) * d.pw[0] + x0);
-        if (4 * t < n) ((uint32_t*)ly[q])[t] = yr[t];
-    }
-    const int cw = d.cw[1], ch = d.ch[1];
-    const int cbase = (x0 >> 1) - 1, cn = (n + 1) / 2 + 2;
-    for (int q = 0; q < 6; q++) {
-        const int comp = q / 3, dr = q % 3 - 1;
-        int rr = r + dr;
+    // chroma staging first: its loads overlap the luma IDCT
+    const int cw = d.cw[1], ch = d.ch[1], cx0 = mx0 * 8, cy0 = my * 8;
+    const int pwd = d.pw[1] >> 2;
+    for (int e = t; e < 2 * 10 * LC_CD; e += 256) {
+        const int comp = e / (10 * LC_CD), rem = e - comp * (10 * LC_CD);
+        const int j = rem / LC_CD, q = rem - j * LC_CD;
+        int rr = cy0 - 1 + j;
         rr = rr < 0 ? 0 : rr > ch - 1 ? ch - 1 : rr;
-        const uint8_t* P = d.plane[1 + comp] + (int64_t)rr * d.pw[1 + comp];
-        for (int c = t; c < cn; c += 256) {
-            int col = cbase + c;
-            col = col < 0 ? 0 : col > cw - 1 ? cw - 1 : col;  // edge columns are special-cased below
-            lc[comp][dr + 1][c] = P[col];
-        }
+        int dw = (cx0 >> 2) - 1 + q;
+        dw = dw < 0 ? 0 : dw > pwd - 1 ? pwd - 1 : dw;  // clamped dwords hold only unused columns
+        lc[comp][j][q] = ((const uint32_t*)(d.plane[1 + comp] + (int64_t)rr * d.pw[1 + comp]))[dw];
+    }
+    {  // luma: block lb = MCU lb / 4, block k = lb % 4 of it
+        const int lb = t >> 3, r = t & 7, mx = mx0 + (lb >> 2), k = lb & 3;
+        const int bx = mx * 2 + (k & 1), by = my * 2 + (k >> 1);
+        const bool real = mx < d.mcux && bx * 8 < d.pw[0] && by * 8 < d.ph[0];
+        const int64_t b = ((int64_t)my * d.mcux + mx) * d.nbmcu + k;
+        const uint2 row = idct_block_row(d, b, 0, r, real, ws[lb]);
+        *(uint2*)&ly[(k >> 1) * 8 + r][(lb >> 2) * 4 + (k & 1) * 2] = row;
     }
     __syncthreads();
-    const int xt = 4 * t;  // first of this thread's 4 columns (local)
-    if (xt >= n) return;
-    const int i0 = ((x0 + xt) >> 1);  // chroma columns i0, i0 + 1
-    const int li = i0 - cbase;        // local index of i0 (>= 1)
-    int cv[2][2][4];                  // [comp][top|bottom row][column]
+    const int rp = t >> 5, xt = 4 * (t & 31);  // chroma row cy0 + rp -> output rows 2rp, 2rp+1; columns xt..xt+3
+    const int x0 = mx0 * 16;
+    const int n = d.ow - x0 - xt;
+    const int y0 = my * 16 + 2 * rp;
+    if (n <= 0 || y0 >= d.oh) return;
+    const int i0 = (x0 + xt) >> 1;       // chroma columns i0, i0 + 1
+    const int li = (xt >> 1) + 4;        // local byte of i0
+    int cv[2][2][4];                     // [comp][top|bottom row][column]
 #pragma unroll
     for (int comp = 0; comp < 2; comp++) {
+        const uint8_t* c0 = (const uint8_t*)lc[comp][rp];  // rows cy0+rp-1, cy0+rp, cy0+rp+1
+        const uint8_t* c1 = c0 + LC_CD * 4;
+        const uint8_t* c2 = c1 + LC_CD * 4;
         int cs_t[4], cs_b[4];  // column sums for i0-1 .. i0+2
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const int a = lc[comp][1][li - 1 + k] * 3;
-            cs_t[k] = a + lc[comp][0][li - 1 + k];
-            cs_b[k] = a + lc[comp][2][li - 1 + k];
+            const int a = c1[li - 1 + k] * 3;
+            cs_t[k] = a + c0[li - 1 + k];
+            cs_b[k] = a + c2[li - 1 + k];
         }
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -710,12 +776,16 @@ __global__ void __launch_bounds__(256) k_dec_color_420(const DecDesc* D, const D
             }
         }
     }
-    const int m = n - xt < 4 ? n - xt : 4;
-    for (int h = 0; h < rows; h++) {
+    const int m = n < 4 ? n : 4;
+    const int rows = d.oh - y0 < 2 ? 1 : 2;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {  // unrolled: cv stays in registers
+        if (h >= rows) break;
+        const uint32_t yq = ly[2 * rp + h][xt >> 2];
         uint32_t w[3] = {0, 0, 0};
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const int yy = ly[h][xt + k];
+            const int yy = (yq >> (8 * k)) & 255;
             const int cb = cv[0][h][k] - 128, cr = cv[1][h][k] - 128;
             const uint32_t B = clamp255(yy + ((116130 * cb + 32768) >> 16));
             const uint32_t G = clamp255(yy + ((-22554 * cb + 32768 - 46802 * cr) >> 16));
@@ -735,6 +805,11 @@ __global__ void __launch_bounds__(256) k_dec_color_420(const DecDesc* D, const D
 }
 
 // ---------------------------------------------------------------- launchers
+void launch_stage(const StageJob* jobs, const Plan& tiles, int64_t nwg, hipStream_t st)
+{
+    if (nwg > 0) hipLaunchKernelGGL(k_stage, dim3((unsigned)nwg), dim3(256), 0, st, jobs, tiles);
+}
+
 void launch_unstuff(const DecDesc* d, DecState* s, const Plan& tiles, int64_t ntiles, const int32_t* ids, int m,
                     uint32_t sub_bits, hipStream_t st)
 {
@@ -785,9 +860,9 @@ void launch_dec_color(const DecDesc* d, const DecState* s, const Plan& px, int64
     if (nwg > 0) hipLaunchKernelGGL(k_dec_color, dim3((unsigned)nwg), dim3(256), 0, st, d, s, px);
 }
 
-void launch_dec_color_420(const DecDesc* d, const DecState* s, const Plan& rows, int64_t nwg, hipStream_t st)
+void launch_dec_luma_color_420(const DecDesc* d, const DecState* s, const Plan& tiles, int64_t nwg, hipStream_t st)
 {
-    if (nwg > 0) hipLaunchKernelGGL(k_dec_color_420, dim3((unsigned)nwg), dim3(256), 0, st, d, s, rows);
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_luma_color_420, dim3((unsigned)nwg), dim3(256), 0, st, d, s, tiles);
 }
 
 }  // namespace icx

@@ -7,6 +7,8 @@
 
 namespace icx {
 
+// tiles: per job ceil(dst_len / STAGE_TILE) workgroups (Plan.ids unused)
+void launch_stage(const StageJob* jobs, const Plan& tiles, int64_t nwg, hipStream_t st);
 // tiles: per image ntiles work items (one workgroup per 4 KiB stuffed tile)
 void launch_unstuff(const DecDesc* d, DecState* s, const Plan& tiles, int64_t ntiles, const int32_t* ids, int m,
                     uint32_t sub_bits, hipStream_t st);
@@ -22,11 +24,11 @@ void launch_dec_offsets(const DecDesc* d, DecState* s, const int32_t* ids, int m
 void launch_dec_write(const DecDesc* d, DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
                       hipStream_t st);
 void launch_dec_dc(const DecDesc* d, const DecState* s, const int32_t* ids, int m, hipStream_t st);
-// blocks: per image ceil(nblocks / 32) workgroups
+// blocks: per image ceil(nblocks / 32) workgroups (fuse420 images: ceil(2 * mcux * mcuy / 32))
 void launch_dec_idct(const DecDesc* d, const DecState* s, const Plan& blocks, int64_t nwg, hipStream_t st);
 // px: per image ceil(oh * ceil(ow / 4) / 256) workgroups (any source subsampling)
 void launch_dec_color(const DecDesc* d, const DecState* s, const Plan& px, int64_t nwg, hipStream_t st);
-// rows: per image ceil(oh / 2) * ceil(ow / 1024) workgroups (s == 1, 4:2:0 fancy only)
-void launch_dec_color_420(const DecDesc* d, const DecState* s, const Plan& rows, int64_t nwg, hipStream_t st);
+// tiles: per image mcuy * ceil(mcux / 8) workgroups (fuse420 images only)
+void launch_dec_luma_color_420(const DecDesc* d, const DecState* s, const Plan& tiles, int64_t nwg, hipStream_t st);
 
 }  // namespace icx

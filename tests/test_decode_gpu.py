@@ -159,3 +159,36 @@ def test_decode_fuzzed_batch(codec, oracle, dgolden):
             assert rc == 0 and np.array_equal(img, ref), i
             ok += 1
     assert ok >= 80
+
+
+def _with_comments(data, sizes):
+    """data with COM segments of the given payload sizes inserted after SOI."""
+    segs = b"".join(b"\xff\xfe" + (n + 2).to_bytes(2, "big") + bytes((i * 7) & 0x7F for i in range(n))
+                    for n in sizes)
+    return data[:2] + segs + data[2:]
+
+
+def test_decode_device_inputs_unaligned_and_long_headers(codec, dgolden):
+    """Device-resident files at every address alignment, and headers longer
+    than the first 4 KiB header fetch (re-fetched at 32 KiB, then 256 KiB),
+    in one batch: the k_stage gather/copy paths."""
+    import torch
+    meta, jpgs, pxs = dgolden
+    names = ["c130x250_s2_q95", "c66x130_s1_q50", "g47x61_q90", "rst7_130x250_444", "c7x9_s2_q95"]
+    datas, want = [], []
+    for k, name in enumerate(names):
+        for extra in ([], [5000], [60000, 60000, 3000]):
+            data = _with_comments(jpgs[name], extra)
+            off = (k + len(extra)) % 4 + 4 * (len(extra) == 1)
+            buf = torch.zeros(len(data) + off + 3, dtype=torch.uint8)
+            buf[off:off + len(data)] = torch.from_numpy(np.frombuffer(data, np.uint8).copy())
+            datas.append(buf.cuda()[off:off + len(data)])
+            want.append(pxs[name])
+    res = codec.decode_jpg_batch(datas, subsampling=1)
+    for i, (st, img) in enumerate(res):
+        assert st == N.OK, (i, st)
+        assert np.array_equal(img, want[i]), i
+    # the same files from pageable host memory (scan tail padded in place on the device)
+    res = codec.decode_jpg_batch([d.cpu().numpy().tobytes() for d in datas], subsampling=1)
+    for i, (st, img) in enumerate(res):
+        assert st == N.OK and np.array_equal(img, want[i]), i
