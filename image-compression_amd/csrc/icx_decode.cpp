@@ -237,13 +237,14 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             const int64_t scan_len = (int64_t)(it.job->len - it.J.scan_off);
             const int64_t nmcu = (int64_t)d.mcux * d.mcuy;
             d.nseg_max = it.J.ri ? (int32_t)((nmcu + it.J.ri - 1) / it.J.ri) + 1 : 1;
-            it.ent_cap = (size_t)scan_len + (size_t)(DEC_PAD - 2) * d.nseg_max + DEC_TAIL + 64;
+            it.ent_cap = (size_t)scan_len + (size_t)(DEC_PAD - 2) * d.nseg_max + DEC_TAIL + 64 + 4 * DEC_WIN;
             it.ntiles = (scan_len + DEC_TILE - 1) / DEC_TILE;
             it.nblocks = d.nblocks;
             size_t per = align_up(scan_len + 64, 256) + align_up(it.ent_cap, 256) + it.ntiles * 8 + 512 +
                          (size_t)d.nseg_max * 4 + (size_t)d.nblocks * (128 + 4) + sizeof(DecTab) + 4096;
             for (int k = 0; k < 3; k++) per += align_up((size_t)d.pw[k] * d.ph[k], 256);
             per += (size_t)(it.ent_cap * 8 / 2048 + 2) * (8 + 2 + 4 + 4);  // subsequence arrays at S >= 2048
+            per += (size_t)(it.ent_cap * 8 / 2048 + 2) * DEC_CK_MAX * 8;  // checkpoints
             if (!coef_out && !is_device_ptr(it.job->out)) per += align_up(it.job->out_len, 256);
             if (!sub.empty() && need + per > c->budget) break;
             need += per;
@@ -322,6 +323,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             d.nsub_max = (int32_t)((it.ent_cap * 8 + S - 1) / S);
             max_nsub = std::max<int64_t>(max_nsub, d.nsub_max);
             d.est = (uint64_t*)c->dev.take((size_t)(d.nsub_max + 1) * 8);
+            d.ck = (uint64_t*)c->dev.take((size_t)(d.nsub_max + 1) * DEC_CK_MAX * 8);
             d.wl[0] = (uint32_t*)c->dev.take((size_t)(d.nsub_max + 1) * 4);
             d.wl[1] = (uint32_t*)c->dev.take((size_t)(d.nsub_max + 1) * 4);
             d.ncnt = (uint32_t*)c->dev.take((size_t)(d.nsub_max + 1) * 4);

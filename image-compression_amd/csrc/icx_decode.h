@@ -87,12 +87,13 @@ struct DecDesc {
     uint32_t* tile_rst;    // per unstuff tile: RSTn markers, then exclusive offsets
     uint32_t* seg;         // interval start byte offsets in ent (nseg_max entries)
     uint64_t* est;         // entry state per subsequence (nsub_max + 1)
+    uint64_t* ck;          // sync-walk checkpoints, DEC_CK_MAX per subsequence (dec_sync_walk)
     uint32_t* wl[2];       // subsequences to re-walk in the next sync launch (ping-pong)
     uint32_t* wl_cnt;      // entries appended to the worklist by sync launch r: wl_cnt[r]
     uint32_t* ncnt;        // blocks completed inside each subsequence
     uint32_t* boff;        // blocks completed before each subsequence
-    int16_t* coefs;        // nblocks x 64, natural order, quantised (AC only)
-    int32_t* dc;           // nblocks: DC differences, then DC values
+    int16_t* coefs;        // nblocks x 64, natural order, quantised; [0] = DC difference
+    int32_t* dc;           // nblocks: DC differences (write pass), then DC values (k_dec_dc)
     uint8_t* plane[3];     // IDCT output planes (pitch pw[c])
     uint8_t* out;          // BGR24 / GRAY8 rows, stride ostride
     const DecTab* tab;
@@ -145,31 +146,73 @@ ICX_HD uint32_t dec_be32(uint32_t v)
 #endif
 
 // MSB-first bit reader over the unstuffed stream (big-endian 32-bit words).
-// One word is always in flight (nxt), so a refill never waits on the load it
-// issues; the stream is padded so the look-ahead stays inside the buffer.
+// The words ahead of the 64-bit bit buffer sit in an 8-word register window
+// (q[0] next).  On the device the window is reloaded only at wave-uniform
+// points (top_up() when low(), driven by the caller's loop) followed at once by
+// an explicit vmcnt(0): vector-memory counters are in-order and count stores
+// too, so a load consumed one symbol later would also wait for every block
+// store issued in between.  A step consumes at most one window word and the
+// device loops top up every lane once any holds <= 1, so a device refill never
+// finds the window empty; host loops (no top-ups) reload inside refill().  The stream buffer extends 64 + 4 DEC_WIN
+// bytes past its padded end, so a window never reads outside it.
+#ifndef ICX_DEC_WIN
+#define ICX_DEC_WIN 8
+#endif
+constexpr int DEC_WIN = ICX_DEC_WIN;
 struct DecReader {
     const ICX_GLOBAL uint32_t* w;
     uint64_t buf;
     int avail;
-    uint32_t wi;
-    uint32_t nxt;
+    uint32_t wi;    // stream word index of q[0]
+    int nq;         // valid words in q
+    uint32_t q[DEC_WIN];
+
+    ICX_HD void fetch(uint32_t at)
+    {
+        wi = at;
+        nq = DEC_WIN;
+#pragma unroll
+        for (int j = 0; j < DEC_WIN; j++) q[j] = w[at + j];
+#if defined(__HIP_DEVICE_COMPILE__)
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing later waits on q
+#endif
+    }
+    ICX_HD uint32_t pop()  // next window word, byte-swapped
+    {
+        const uint32_t v = q[0];
+#pragma unroll
+        for (int j = 0; j + 1 < DEC_WIN; j++) q[j] = q[j + 1];
+        wi++;
+        nq--;
+        return dec_be32(v);
+    }
     ICX_HD void init(const uint32_t* words, uint32_t pos)
     {
         w = (const ICX_GLOBAL uint32_t*)words;
-        wi = pos >> 5;
-        buf = ((uint64_t)dec_be32(w[wi]) << 32) | dec_be32(w[wi + 1]);
-        nxt = w[wi + 2];
-        wi += 3;
-        buf <<= (pos & 31);
+        fetch(pos >> 5);
+        const uint64_t hi = pop();
+        buf = ((hi << 32) | pop()) << (pos & 31);
         avail = 64 - (int)(pos & 31);
     }
-    ICX_HD void refill()
+    ICX_HD bool low() const { return nq <= 1; }
+#ifndef ICX_DEC_TOPUP_HALF
+#define ICX_DEC_TOPUP_HALF 0
+#endif
+    ICX_HD bool wants() const { return !ICX_DEC_TOPUP_HALF || nq <= DEC_WIN / 2; }  // joins a top-up
+    ICX_HD void top_up() { fetch(wi); }
+    ICX_HD void refill()  // select-based: the common case takes no branch
     {
-        if (avail < 32) {
-            buf |= (uint64_t)dec_be32(nxt) << (32 - avail);
-            avail += 32;
-            nxt = w[wi++];
-        }
+#if !defined(__HIP_DEVICE_COMPILE__)
+        if (nq == 0 && avail < 32) top_up();  // device loops top up first: nq >= 1 here
+#endif
+        const bool need = avail < 32;
+        const uint32_t v = dec_be32(q[0]);
+#pragma unroll
+        for (int j = 0; j + 1 < DEC_WIN; j++) q[j] = need ? q[j + 1] : q[j];
+        buf |= need ? (uint64_t)v << (32 - avail) : 0ull;
+        wi += need ? 1u : 0u;
+        nq -= need ? 1 : 0;
+        avail += need ? 32 : 0;
     }
     ICX_HD uint32_t peek16() const { return (uint32_t)(buf >> 48); }
     ICX_HD void skip(int n)
@@ -191,7 +234,7 @@ ICX_HD int dec_extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) +
 
 // Decode one symbol: (length << 8) | symbol, 0 if no valid code.
 template <class HuffPtr>
-ICX_HD uint32_t dec_symbol(HuffPtr t, const DecSlow* slow, uint32_t pk)
+ICX_HD uint32_t dec_symbol(HuffPtr t, const ICX_GLOBAL DecSlow* slow, uint32_t pk)
 {
     uint32_t e = t->lut[pk >> (16 - DEC_LUT_BITS)];
     if (e & DEC_SUB) e = t->lut2[e & (DEC_NSUB - 1)][pk & ((1u << (16 - DEC_LUT_BITS)) - 1)];
@@ -219,7 +262,7 @@ ICX_HD int dec_nat(int z)
 }
 
 // First interval start strictly after byte `byte` (DEC_END if none).
-ICX_HD uint32_t dec_next_seg(const uint32_t* seg, uint32_t nseg, uint32_t byte)
+ICX_HD uint32_t dec_next_seg(const ICX_GLOBAL uint32_t* seg, uint32_t nseg, uint32_t byte)
 {
     uint32_t lo = 0, hi = nseg;  // find first k with seg[k] > byte
     while (lo < hi) {
@@ -227,6 +270,16 @@ ICX_HD uint32_t dec_next_seg(const uint32_t* seg, uint32_t nseg, uint32_t byte)
         if (seg[mid] > byte) hi = mid; else lo = mid + 1;
     }
     return lo < nseg ? seg[lo] : DEC_END;
+}
+
+// natural index -> zig-zag index (inverse of dec_nat on 0..63)
+ICX_HD int dec_zz(int n)
+{
+    constexpr uint8_t Z[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
+                               3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
+                               10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+                               21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+    return Z[n];
 }
 
 // Decode from state st until the first symbol boundary at or beyond `stop`
@@ -237,15 +290,17 @@ ICX_HD uint32_t dec_next_seg(const uint32_t* seg, uint32_t nseg, uint32_t byte)
 // symbol starts, so every block is written whole by exactly one thread.  The
 // walk skips the stores of a block it enters mid-way (its owner is the
 // previous subsequence), and after `stop` it keeps decoding until the block in
-// progress is complete.  AC coefficients go to sink.coef(natural index, value),
-// a finished owned block to sink.flush(block index); DC differences are
-// stored directly in d.dc[block].
+// progress is complete.  An owned block's DC difference goes to sink.put(0, v),
+// its AC coefficients to sink.put(zig-zag index, v) (indices past 63 clamp to
+// 63, as jpeg_natural_order's tail), the finished block to sink.flush_if.
 // Table index of (component, DC or AC) from the packed selector (dec_selector).
 ICX_HD int dec_sel(uint32_t selp, int comp, int ac) { return (int)((selp >> (4 * (2 * comp + ac))) & 3); }
 
+// Sink of an owned walk: put(zig-zag index, value) per symbol (index 0 = the
+// DC difference, 64 = nothing), flush_if(block complete and owned, index).
 struct NoSink {
-    ICX_HD void coef(int, int) {}
-    ICX_HD void flush(int64_t) {}
+    ICX_HD void put(int, int) {}
+    ICX_HD void flush_if(bool, int64_t) {}
 };
 
 // The walk as a state object, one symbol per step() (the device write pass
@@ -253,13 +308,14 @@ struct NoSink {
 // whole wave between steps).
 template <bool OWNED, class HuffPtr>
 struct DecWalker {
-    const DecDesc* d;
     HuffPtr H;
-    const DecSlow* slow;
+    const ICX_GLOBAL DecSlow* slow;
     uint32_t selp;
     const uint32_t* words;
-    const uint32_t* seg;
+    const ICX_GLOBAL uint32_t* seg;
     uint32_t nseg, ent_bits;
+    int nby, nbmcu;    // descriptor fields the walk uses, held in registers
+    int64_t nblocks;
     uint32_t pos, n;
     int b, z, comp;
     bool own;
@@ -275,75 +331,74 @@ struct DecWalker {
         n = 0;
         own = z == 0;
         bad = false;
-        comp = b < d->nby ? 0 : b - d->nby + 1;
+        comp = b < nby ? 0 : b - nby + 1;
         R.init(words, pos);
     }
     ICX_HD bool running(uint32_t stop) const { return pos < stop || (OWNED && z != 0); }
     ICX_HD uint64_t state() const { return dec_pack(pos, b, z); }
 
-    // Decode one symbol (or take one invalid-code transition).
+    // Decode one symbol (or take one invalid-code transition).  Straight-line
+    // apart from the rare paths (second-level / slow code tables, invalid
+    // code): DC and AC symbols, runs, ZRL / EOB and the block end are all
+    // selects, and every symbol makes exactly one sink.put (index 64 = nothing
+    // to store), so a wave pays no branch bookkeeping on the common path.
     template <class Sink>
     ICX_HD void step(Sink& sink)
     {
         R.refill();
-        const int ti = dec_sel(selp, comp, z ? 1 : 0);
+        const bool ac = z != 0;
+        const int ti = dec_sel(selp, comp, ac ? 1 : 0);
         const uint32_t e = dec_symbol(&H[ti], &slow[ti], R.peek16());
         const int len = (int)(e >> 8), sym = (int)(e & 255);
-        if (len == 0 || (z == 0 && sym > 11)) {  // no valid code here
-            const uint32_t nx = dec_next_seg(seg, nseg, pos >> 3);
-            const uint32_t bound = nx == DEC_END ? ent_bits : (nx - DEC_PAD) * 8;  // end of interval data
-            b = 0;
-            z = 0;
-            comp = 0;
-            own = true;
-            if (pos + 8 < bound) {  // mid-interval: only a wrong-start path gets here; resume a bit later
-                bad = true;
-                pos++;
-                R.init(words, pos);
-                return;
-            }
-            // the interval's 1-bit padding (< 8 bits) or its pad bytes: next interval
-            if (nx == DEC_END) {
-                pos = DEC_END;
-                return;
-            }
-            pos = nx * 8;
+        if (len == 0 || (!ac && sym > 11)) {  // no valid code here
+            invalid();
+            return;
+        }
+        const int sz = ac ? (sym & 15) : sym;   // extra bits
+        const int run = ac ? (sym >> 4) : 0;
+        R.skip(len);
+        const int v = R.get(sz);
+        pos += (uint32_t)(len + sz);
+        const int x = sz ? dec_extend(v, sz) : 0;
+        const int zc = z + run;                 // zig-zag index of an AC coefficient
+        if (OWNED) sink.put(!own ? 64 : !ac ? 0 : sz ? (zc > 63 ? 63 : zc) : 64, x);
+        z = !ac ? 1 : sz ? zc + 1 : (run == 15 ? z + 16 : 64);
+        const bool end = z >= 64;
+        if (OWNED) {
+            const int64_t bi = blk_base + n;
+            sink.flush_if(end && own && bi < nblocks, bi);
+        }
+        own = own || end;
+        n += end ? 1u : 0u;
+        const int bn = b + 1 == nbmcu ? 0 : b + 1;
+        b = end ? bn : b;
+        z = end ? 0 : z;
+        comp = b < nby ? 0 : b - nby + 1;
+    }
+
+    // An invalid code: on a wrong-start path resume one bit later (flagged),
+    // in an interval's padding move to the next interval or the end.
+    ICX_HD void invalid()
+    {
+        const uint32_t nx = dec_next_seg(seg, nseg, pos >> 3);
+        const uint32_t bound = nx == DEC_END ? ent_bits : (nx - DEC_PAD) * 8;  // end of interval data
+        b = 0;
+        z = 0;
+        comp = 0;
+        own = true;
+        if (pos + 8 < bound) {  // mid-interval: only a wrong-start path gets here; resume a bit later
+            bad = true;
+            pos++;
             R.init(words, pos);
             return;
         }
-        R.skip(len);
-        if (z == 0) {
-            const int v = R.get(sym);
-            pos += (uint32_t)(len + sym);
-            if (OWNED) {
-                const int64_t bi = blk_base + n;
-                if (bi < d->nblocks) d->dc[bi] = sym ? dec_extend(v, sym) : 0;
-            }
-            z = 1;
-        } else {
-            const int r = sym >> 4, s = sym & 15;
-            if (s) {
-                z += r;
-                const int v = R.get(s);
-                pos += (uint32_t)(len + s);
-                if (OWNED && own) sink.coef(dec_nat(z), dec_extend(v, s));
-                z++;
-            } else {
-                pos += (uint32_t)len;
-                z = (r == 15) ? z + 16 : 64;
-            }
+        // the interval's 1-bit padding (< 8 bits) or its pad bytes: next interval
+        if (nx == DEC_END) {
+            pos = DEC_END;
+            return;
         }
-        if (z >= 64) {
-            if (OWNED && own) {
-                const int64_t bi = blk_base + n;
-                if (bi < d->nblocks) sink.flush(bi);
-            }
-            own = true;
-            n++;
-            z = 0;
-            b = (b + 1 == d->nbmcu) ? 0 : b + 1;
-            comp = b < d->nby ? 0 : b - d->nby + 1;
-        }
+        pos = nx * 8;
+        R.init(words, pos);
     }
 };
 
@@ -353,28 +408,164 @@ ICX_HD DecWalker<OWNED, HuffPtr> dec_walker(const DecDesc& d, HuffPtr H, const D
                                             uint32_t ent_bits, int64_t blk_base)
 {
     DecWalker<OWNED, HuffPtr> w;
-    w.d = &d;
     w.H = H;
-    w.slow = slow;
+    w.slow = (const ICX_GLOBAL DecSlow*)slow;
     w.selp = selp;
     w.words = words;
-    w.seg = seg;
+    w.seg = (const ICX_GLOBAL uint32_t*)seg;
     w.nseg = nseg;
     w.ent_bits = ent_bits;
+    w.nby = d.nby;
+    w.nbmcu = d.nbmcu;
+    w.nblocks = d.nblocks;
     w.blk_base = blk_base;
     return w;
 }
 
+// The walk of one thread (active == false: this lane only keeps the wave's
+// uniform loop company).  On the device the loop is wave-uniform so the
+// window top-ups happen together (DecReader).
 template <bool OWNED, class HuffPtr, class Sink>
 ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, uint32_t selp, const uint32_t* words,
                          const uint32_t* seg, uint32_t nseg, uint32_t ent_bits, uint64_t st, uint32_t stop,
-                         uint32_t& nblk, int64_t blk_base, Sink& sink)
+                         uint32_t& nblk, int64_t blk_base, Sink& sink, bool active = true)
 {
     nblk = 0;
-    if (dec_pos(st) >= stop && (!OWNED || (st & 63) == 0)) return st;
     DecWalker<OWNED, HuffPtr> w = dec_walker<OWNED>(d, H, slow, selp, words, seg, nseg, ent_bits, blk_base);
-    w.start(st);
-    while (w.running(stop)) w.step(sink);
+    const bool started = active && !(dec_pos(st) >= stop && (!OWNED || (st & 63) == 0));
+    bool run = false;
+    if (started) {
+        w.start(st);
+        run = w.running(stop);
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    while (__any(run)) {
+        if (run) {
+            w.step(sink);
+            run = w.running(stop);
+        }
+        if (__any(run && w.R.low()) && run && w.R.wants()) w.R.top_up();
+    }
+#else
+    while (run) {
+        w.step(sink);
+        run = w.running(stop);
+    }
+#endif
+    if (!started) return st;
+    nblk = w.n;
+    return w.state();
+}
+
+// ---------------------------------------------------------------------------
+// Sync-walk checkpoints.  A walk records its state at the first symbol boundary
+// at or beyond each interior mark base + (k + 1) * dec_ck_bits of its
+// subsequence, with the blocks completed before it in bits 48..63.  The state
+// (pos, block in MCU, zig-zag index) determines the rest of the walk, so a
+// later walk of the same subsequence that reaches a recorded state can stop
+// there: its exit is the recorded walk's exit, and its block count that walk's
+// count plus the difference at the checkpoint.  A re-walk from a corrected
+// entry state typically resynchronises within a few hundred bits, so relaunch
+// walks cost about one checkpoint interval instead of a whole subsequence.
+constexpr int DEC_CK_MAX = 7;
+constexpr uint64_t DEC_CK_NONE = ~0ull;
+constexpr uint64_t DEC_CK_STATE = (1ull << 48) - 1;
+ICX_HD uint32_t dec_ck_bits(uint32_t sub_bits) { return sub_bits / 8 > 2048 ? sub_bits / 8 : 2048; }
+ICX_HD int dec_ck_slots(uint32_t sub_bits)
+{
+    const uint32_t c = dec_ck_bits(sub_bits);
+    return sub_bits > c ? (int)(sub_bits / c) - 1 : 0;
+}
+
+// Checkpoint store of a subsequence's first walk: records, never matches.
+template <class P>
+struct CkRecord {
+    P ck;  // DEC_CK_MAX slots
+    int nck;
+    ICX_HD bool visit(int k, uint64_t s, uint32_t&) { ck[k] = s; return false; }
+    ICX_HD void finish(int k, bool)
+    {
+        for (; k < nck; k++) ck[k] = DEC_CK_NONE;
+    }
+};
+
+// Checkpoints of a re-walk: old = the previous walk's (a private copy), total =
+// its block count.  A match fixes up the later checkpoints' counts and sets
+// total to the new count.
+template <class P, class Q>
+struct CkCompare {
+    P ck;
+    Q old;
+    int nck;
+    uint32_t total;
+    ICX_HD bool visit(int k, uint64_t s, uint32_t& nblk)
+    {
+        const uint64_t o = old[k];
+        if (o != DEC_CK_NONE && ((o ^ s) & DEC_CK_STATE) == 0) {
+            const int32_t delta = (int32_t)(s >> 48) - (int32_t)(o >> 48);
+            for (int q = k + 1; q < nck; q++)
+                if (old[q] != DEC_CK_NONE) ck[q] = old[q] + ((uint64_t)(int64_t)delta << 48);
+            ck[k] = s;
+            nblk = total + (uint32_t)delta;
+            return true;
+        }
+        ck[k] = s;
+        return false;
+    }
+    ICX_HD void finish(int k, bool early)
+    {
+        if (!early)
+            for (; k < nck; k++) ck[k] = DEC_CK_NONE;
+    }
+};
+
+// One sync walk of subsequence [base, base + sub_bits) from entry state st,
+// with checkpoints (policy ck).  Returns the exit state, or st with early ==
+// true when the walk met the previous walk (exit unchanged); nblk = blocks
+// completed inside the subsequence either way.
+template <class HuffPtr, class Ck>
+ICX_HD uint64_t dec_sync_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, uint32_t selp,
+                              const uint32_t* words, const uint32_t* seg, uint32_t nseg, uint32_t ent_bits,
+                              uint64_t st, uint32_t base, uint32_t sub_bits, uint32_t& nblk, bool& early, Ck& ck,
+                              bool active = true)
+{
+    const uint32_t stop = base + sub_bits, ckb = dec_ck_bits(sub_bits);
+    const int nck = dec_ck_slots(sub_bits);
+    nblk = 0;
+    early = false;
+    DecWalker<false, HuffPtr> w = dec_walker<false>(d, H, slow, selp, words, seg, nseg, ent_bits, 0);
+    const bool started = active && dec_pos(st) < stop;
+    bool run = false;
+    if (started) {
+        w.start(st);
+        run = w.running(stop);
+    }
+    int k = 0;
+    uint32_t ckpos = base + ckb;
+    NoSink ns;
+#if defined(__HIP_DEVICE_COMPILE__)
+    while (__any(run)) {
+#else
+    while (run) {
+#endif
+        if (run) {
+            w.step(ns);
+            while (k < nck && w.pos >= ckpos) {  // a jump (END, next interval) may pass several marks
+                if (ck.visit(k, w.state() | ((uint64_t)w.n << 48), nblk)) {
+                    early = true;
+                    break;
+                }
+                k++;
+                ckpos += ckb;
+            }
+            run = !early && w.running(stop);
+        }
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (__any(run && w.R.low()) && run && w.R.wants()) w.R.top_up();
+#endif
+    }
+    if (active) ck.finish(k, early);
+    if (!started || early) return st;
     nblk = w.n;
     return w.state();
 }

@@ -322,28 +322,45 @@ __device__ __forceinline__ uint32_t selector(const DecTab* T)
 // so the few subsequences still moving fill whole waves.  A thread whose exit
 // differs from the stored next entry stores it and appends j + 1 to the next
 // worklist (only thread j writes E[j+1], so entries are unique per launch).
+// Launch 0 records each walk's checkpoints; a re-walk compares against them
+// (staged in LDS) and stops where it meets its previous walk (dec_sync_walk).
+template <bool FIRST>
 __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
                                                   int iter, int max_it, uint32_t* changed)
 {
     __shared__ __attribute__((aligned(16))) DecHuff L[4];
+    __shared__ uint64_t ckl[FIRST ? 1 : 256][DEC_CK_MAX];
     const int slot = slot_of(p.prefix, p.m, blockIdx.x);
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
     const DecState& st = S[img];
     if (st.status) return;
     const int64_t k = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
-    const uint32_t n = iter == 0 ? st.nsub : d.wl_cnt[(int64_t)img * max_it + iter - 1];
+    const uint32_t n = FIRST ? st.nsub : d.wl_cnt[(int64_t)img * max_it + iter - 1];
     if ((blockIdx.x - p.prefix[slot]) * 256 >= (int64_t)n) return;
     load_tables(d.tab, L);
     if (k >= n) return;
-    const uint32_t j = iter == 0 ? (uint32_t)k : d.wl[iter & 1][k];
+    const uint32_t j = FIRST ? (uint32_t)k : d.wl[iter & 1][k];
     if (j >= st.nsub) return;
     const uint64_t e = __hip_atomic_load(&d.est[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int nck = dec_ck_slots(sub_bits);
+    ICX_GLOBAL uint64_t* ckg = (ICX_GLOBAL uint64_t*)d.ck + (int64_t)j * DEC_CK_MAX;
     uint32_t nb;
-    NoSink ns;
-    const uint64_t x = dec_walk<false>(d, L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
-                                       st.ent_len * 8, e, (j + 1) * sub_bits, nb, 0, ns);
+    bool early;
+    uint64_t x;
+    if (FIRST) {
+        CkRecord<ICX_GLOBAL uint64_t*> ck{ckg, nck};
+        x = dec_sync_walk(d, L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
+                          st.ent_len * 8, e, j * sub_bits, sub_bits, nb, early, ck);
+    } else {
+        uint64_t* mine = ckl[FIRST ? 0 : threadIdx.x];
+        for (int q = 0; q < nck; q++) mine[q] = ckg[q];
+        CkCompare<ICX_GLOBAL uint64_t*, uint64_t*> ck{ckg, mine, nck, d.ncnt[j]};
+        x = dec_sync_walk(d, L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
+                          st.ent_len * 8, e, j * sub_bits, sub_bits, nb, early, ck);
+    }
     d.ncnt[j] = nb;
+    if (early) return;  // met the previous walk: same exit as before
     const uint64_t old = __hip_atomic_load(&d.est[j + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (x != old) {
         __hip_atomic_store(&d.est[j + 1], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -382,21 +399,27 @@ __global__ void __launch_bounds__(1024) k_dec_offsets(const DecDesc* D, DecState
 // zig-zag position (they walk in near lockstep) do not collide.
 constexpr int SLOT_DW = 33;
 
-// A lane that finishes an owned block only records its index; the wave then
-// copies every finished slot together (below).
+// Slots hold a block in zig-zag order (no index table per coefficient), the
+// DC difference at [0]; a lane that finishes an owned block only records its
+// index, and the wave then copies every finished slot together (below),
+// permuting to natural order on the way.
 struct PendSink {
-    int16_t* slot;
-    int64_t pend;  // block waiting for the wave flush, -1 = none
-    __device__ __forceinline__ void coef(int k, int v) { slot[k] = (int16_t)v; }
-    __device__ __forceinline__ void flush(int64_t bi) { pend = bi; }
+    int16_t* slot;  // 64 int16 + the pad dword, which takes put(64, .)
+    int64_t pend;   // block waiting for the wave flush, -1 = none
+    __device__ __forceinline__ void put(int z, int v) { slot[z] = (int16_t)v; }
+    __device__ __forceinline__ void flush_if(bool c, int64_t bi) { pend = c ? bi : pend; }
 };
 
 // Write pass.  The walk runs in a wave-uniform loop, one symbol per lane per
-// iteration; after each step the wave ballots the lanes that finished a block
-// and copies each of those 128-byte slots with 32 lanes (one coalesced dword
-// store each), zeroing it behind.  A per-lane flush would cost every lane of
-// the wave ~70 instructions whenever any lane finishes a block, which on
-// q95 content is most iterations.
+// iteration; after each step the wave tops up the bit windows if any lane runs
+// low (DecReader), then ballots the lanes that finished a block and copies
+// each of those 128-byte slots with 32 lanes (one coalesced dword store each,
+// natural order: coefficient pair 2l, 2l+1 read from its zig-zag positions),
+// zeroing it behind (lane 0 also stores the DC difference into d.dc).  The
+// block stores are the only vector-memory traffic between top-ups, so no
+// symbol waits for them.  A per-lane flush would cost
+// every lane of the wave ~70 instructions whenever any lane finishes a block,
+// which on q95 content is most iterations.
 __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S, Plan p, uint32_t sub_bits)
 {
     __shared__ __attribute__((aligned(16))) DecHuff L[4];
@@ -427,12 +450,15 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
         }
     }
     PendSink sk{(int16_t*)mys, -1};
-    uint32_t* coefs32 = (uint32_t*)d.coefs;
+    ICX_GLOBAL uint32_t* coefs32 = (ICX_GLOBAL uint32_t*)d.coefs;  // global_store: vmcnt only, not lgkmcnt
+    ICX_GLOBAL int32_t* dcs = (ICX_GLOBAL int32_t*)d.dc;
+    const int zl = dec_zz((2 * lane) & 63), zh = dec_zz((2 * lane + 1) & 63);  // this lane's flush pair
     while (__any(run)) {
         if (run) {
             w.step(sk);
             run = w.running(stop);
         }
+        if (__any(run && w.R.low()) && run && w.R.wants()) w.R.top_up();
         uint64_t m = __ballot(sk.pend >= 0);
         while (m) {
             const int l = __builtin_ctzll(m);
@@ -442,9 +468,12 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
             const int64_t bi = (int64_t)(((uint64_t)hi << 32) | lo);
             uint32_t* src = wave_slots + l * SLOT_DW;
             if (lane < 32) {
-                const uint32_t v = src[lane];
+                const uint16_t* s16 = (const uint16_t*)src;
+                const uint32_t v = s16[zl] | ((uint32_t)s16[zh] << 16);
+                __builtin_amdgcn_wave_barrier();  // every lane's reads before the zeroing
                 src[lane] = 0;
                 coefs32[bi * 32 + lane] = v;
+                if (lane == 0) dcs[bi] = (int16_t)v;  // the DC difference, also for k_dec_dc's dense reads
             }
         }
         sk.pend = -1;
@@ -455,8 +484,9 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
     if (w.bad) atomicOr(&S[img].status, 6);
 }
 
-// One workgroup per image: DC values from differences, per component, the
-// predictor reset at every restart interval (jdhuff.c process_restart).
+// One workgroup per image: DC values from the differences the write pass left
+// in d.dc, in place, per component, the predictor reset at every restart
+// interval (jdhuff.c process_restart).
 __global__ void __launch_bounds__(1024) k_dec_dc(const DecDesc* D, const DecState* S, const int32_t* ids)
 {
     __shared__ int32_t sv[3][1024];
@@ -830,8 +860,8 @@ void launch_dec_sync(const DecDesc* d, const DecState* s, const Plan& subs, int6
                      int iter, int max_it, uint32_t* changed, hipStream_t st)
 {
     if (nwg > 0)
-        hipLaunchKernelGGL(k_dec_sync, dim3((unsigned)nwg), dim3(256), 0, st, d, s, subs, sub_bits, iter, max_it,
-                           changed);
+        hipLaunchKernelGGL(iter == 0 ? k_dec_sync<true> : k_dec_sync<false>, dim3((unsigned)nwg), dim3(256), 0, st,
+                           d, s, subs, sub_bits, iter, max_it, changed);
 }
 
 void launch_dec_offsets(const DecDesc* d, DecState* s, const int32_t* ids, int m, hipStream_t st)

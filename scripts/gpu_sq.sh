@@ -1,7 +1,8 @@
 #!/bin/bash
 # GPU-box helper: SQ counters for the icx kernels of one bench config, for one
 # or more builds of libicx (ICX_LIBS="lib/a.so lib/b.so").  One counter group
-# per rocprofv3 pass, kernel-trace only alongside.
+# per rocprofv3 pass, kernel-trace only alongside.  SQ_PROG: the script to
+# profile (default bench.py; e.g. scripts/bench_decode.py with its own SQ_ARGS).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
@@ -16,7 +17,7 @@ for lib in ${ICX_LIBS:-image-compression_amd/lib/libicx.so}; do
   g=0
   for grp in $GROUPS_; do
     g=$((g+1))
-    ICX_LIB="$R/$lib" timeout -k 10 ${T_SQ:-300} rocprofv3 --pmc ${grp//,/ } --kernel-trace --output-format csv -d "$R/gpurun_out/$TAG/$name/g$g" -o run -- python3 "$R/bench.py" $ARGS > "$R/gpurun_out/$TAG/$name.g$g.out" 2>&1 || { echo "sq $name g$g failed rc=$?"; tail -20 "$R/gpurun_out/$TAG/$name.g$g.out"; exit 1; }
+    ICX_LIB="$R/$lib" timeout -k 10 ${T_SQ:-300} rocprofv3 --pmc ${grp//,/ } --kernel-trace --output-format csv -d "$R/gpurun_out/$TAG/$name/g$g" -o run -- python3 "$R/${SQ_PROG:-bench.py}" $ARGS > "$R/gpurun_out/$TAG/$name.g$g.out" 2>&1 || { echo "sq $name g$g failed rc=$?"; tail -20 "$R/gpurun_out/$TAG/$name.g$g.out"; exit 1; }
   done
 done
 cd "$R"

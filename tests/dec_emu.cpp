@@ -25,6 +25,7 @@ using namespace icx;
 extern "C" {
 long dec_emu_walks = 0;  // subsequence walks in the sync launches of the last call (work measure)
 long dec_emu_nsub = 0;
+long dec_emu_early = 0;  // re-walks that stopped at a checkpoint of their previous walk
 }
 
 extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_t nblocks_cap, int seed,
@@ -78,7 +79,7 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
         }
     }
     const uint32_t ent_len = (uint32_t)ent.size();
-    for (int p = 0; p < DEC_TAIL + 64; p++) ent.push_back(0xFF);
+    for (int p = 0; p < DEC_TAIL + 64 + 4 * DEC_WIN; p++) ent.push_back(0xFF);
     while (ent.size() % 4) ent.push_back(0xFF);
     std::vector<uint32_t> words(ent.size() / 4 + 2, 0xFFFFFFFFu);
     memcpy(words.data(), ent.data(), ent.size());
@@ -106,6 +107,10 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
     int it = 0;
     dec_emu_walks = 0;
     dec_emu_nsub = nsub;
+    // checkpoints as k_dec_sync: launch 0 records, later launches compare and stop early
+    const int nck = dec_ck_slots(S);
+    std::vector<uint64_t> ck((size_t)(nsub + 1) * DEC_CK_MAX, 0x5A5A5A5A5A5A5A5Aull);
+    dec_emu_early = 0;
     for (;; it++) {
         if (it > (int)nsub + 2) return ICX_E_CORRUPT;  // cannot happen: one subsequence settles per launch
         if (seed) std::shuffle(work.begin(), work.end(), rng);
@@ -113,11 +118,23 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
         for (uint32_t j : work) {
             dec_emu_walks++;
             uint32_t n;
-            NoSink ns;
-            const uint64_t x = dec_walk<false>(d, T.h, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(),
-                                               ent_len * 8, est[j], (j + 1) * S, n, 0, ns);
+            bool early;
+            uint64_t x;
+            uint64_t* mine = ck.data() + (size_t)j * DEC_CK_MAX;
+            if (it == 0) {
+                CkRecord<uint64_t*> rec{mine, nck};
+                x = dec_sync_walk(d, T.h, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8,
+                                  est[j], j * S, S, n, early, rec);
+            } else {
+                uint64_t old[DEC_CK_MAX];
+                memcpy(old, mine, sizeof(old));
+                CkCompare<uint64_t*, uint64_t*> cmp{mine, old, nck, ncnt[j]};
+                x = dec_sync_walk(d, T.h, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8,
+                                  est[j], j * S, S, n, early, cmp);
+                if (early) dec_emu_early++;
+            }
             ncnt[j] = n;
-            if (x != est[j + 1]) {
+            if (!early && x != est[j + 1]) {
                 est[j + 1] = x;
                 if (j + 1 < nsub) next.push_back(j + 1);
             }
@@ -138,12 +155,15 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
     d.coefs = coefs.data();
     d.dc = dc.data();
     struct Sink {
-        int16_t buf[64] = {};
+        int16_t buf[65] = {};  // [64]: the discard slot
         int16_t* out;
-        void coef(int k, int v) { buf[k] = (int16_t)v; }
-        void flush(int64_t bi)
+        int32_t* dcs;
+        void put(int z, int v) { buf[z < 64 ? dec_nat(z) : 64] = (int16_t)v; }
+        void flush_if(bool c, int64_t bi)
         {
-            memcpy(out + bi * 64, buf, sizeof(buf));
+            if (!c) return;
+            memcpy(out + bi * 64, buf, 64 * sizeof(int16_t));
+            dcs[bi] = buf[0];
             memset(buf, 0, sizeof(buf));
         }
     };
@@ -154,6 +174,7 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
     for (uint32_t j : order) {
         Sink sk;
         sk.out = coefs.data();
+        sk.dcs = dc.data();
         const uint64_t e = est[j];
         if (dec_pos(e) >= (j + 1) * S && (e & 63) == 0) continue;
         DecWalker<true, const DecHuff*> w = dec_walker<true>(d, (const DecHuff*)T.h, T.slow, sel, words.data(),

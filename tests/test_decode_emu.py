@@ -130,3 +130,20 @@ int main(int argc, char** argv) {
     r = subprocess.run([exe, str(fz)], capture_output=True, text=True, timeout=600,
                        env={**os.environ, "ASAN_OPTIONS": "detect_leaks=0"})
     assert r.returncode == 0 and "bad=0" in r.stdout, (r.stdout[-500:], r.stderr[-3000:])
+
+
+@pytest.mark.parametrize("sub", [4096, 16384])
+def test_emulated_checkpoint_early_exit(emu, oracle, sub):
+    """Subsequences long enough to carry sync checkpoints (dec_sync_walk):
+    re-walks stop where they meet their previous walk, and the coefficients
+    (block counts spliced from the checkpoints included) still match the
+    oracle, with and without warm-up estimates (odd / even seeds)."""
+    early = 0
+    for (h, w), q, gen in [((320, 480), 0.95, noise), ((360, 640), 0.9, smooth), ((256, 256), 1.0, noise)]:
+        data = oracle.encode(gen(h, w, 11), q)
+        ref = oracle.jpeg_coefs(data)
+        for seed in (1, 2, 5):
+            rc, got, _ = run(emu, data, ref.shape[0], seed=seed, sub=sub)
+            assert rc == 0 and np.array_equal(got, ref), (h, w, q, seed)
+            early += ctypes.c_long.in_dll(emu, "dec_emu_early").value
+    assert early > 0
