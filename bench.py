@@ -33,10 +33,20 @@ W, H = 3840, 2160
 TARGET = 1 << 20
 Q0 = 0.25
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s
-# algorithmic bytes per unit of each kernel
-ALGO_BYTES = {"fdct": 6.0,      # per pixel: 3 B BGR read + 1.5 coef x 2 B write
-              "huff": 128.0,    # per scan block: 64 int16 coefficients read
-              "resize": 6.0}    # per destination pixel (~3 B read + 3 B write)
+# Algorithmic bytes of each kernel.  fdct and huff move
+# content-dependent amounts (candidate lists), so the library counts them per
+# launch ("<kernel>.bytes" profile entries): fdct = pixels read + lists, list
+# offsets and lengths written; huff = per trial, every block's padded list +
+# offset + length read.  resize: a fixed 6 B per destination pixel.
+ALGO_BYTES_FIXED = {"resize": 6.0}
+UNIT_NAME = {"fdct": "pixel", "huff": "scan block (per trial)", "resize": "destination pixel"}
+
+
+def algo_bytes(codec, kernel, stat):
+    """Algorithmic bytes of `kernel` over the profiled launches."""
+    if kernel in ALGO_BYTES_FIXED:
+        return ALGO_BYTES_FIXED[kernel] * stat["units"]
+    return codec.profile_query(kernel + ".bytes")["units"]
 
 
 def make_frames(n, seed0, device):
@@ -262,23 +272,24 @@ def main():
                                                   "stuff", "resize")}
     kstats = {k: v for k, v in kstats.items() if v["launches"]}
     roof = None
-    cands = [k for k in kstats if k in ALGO_BYTES]
-    if cands:
-        dom = max(cands, key=lambda k: kstats[k]["ms"])
+    bytes_of = {k: algo_bytes(codec, k, v) for k, v in kstats.items() if k in UNIT_NAME and v["units"]}
+    if bytes_of:
+        dom = max(bytes_of, key=lambda k: kstats[k]["ms"])
         ks = kstats[dom]
-        achieved = ALGO_BYTES[dom] * ks["units"] / (ks["ms"] / 1e3) / 1e9
-        algo_launch = ALGO_BYTES[dom] * ks["units"] / ks["launches"]
+        achieved = bytes_of[dom] / (ks["ms"] / 1e3) / 1e9
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(dom, ks["units"] / ks["launches"]),
                 "issue": issue_rates(dom, ks["units"] / ks["launches"], ks["ms"] / ks["launches"] / 1e3),
-                "avg_launch_ms": round(ks["ms"] / ks["launches"], 4), "algo_bytes_per_launch": int(algo_launch)}
+                "avg_launch_ms": round(ks["ms"] / ks["launches"], 4),
+                "algo_bytes_per_launch": int(bytes_of[dom] / ks["launches"])}
     # every kernel with an algorithmic-bytes model, against the HBM roofline
     # (the north star's >= 60 % target is for the DCT stage, k_fdct)
-    stages = {k: {"achieved_GBps": round(ALGO_BYTES[k] * v["units"] / (v["ms"] / 1e3) / 1e9, 1),
-                  "frac": round(ALGO_BYTES[k] * v["units"] / (v["ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                  "avg_launch_ms": round(v["ms"] / v["launches"], 4), "algo_bytes_per_unit": ALGO_BYTES[k]}
-              for k, v in kstats.items() if k in ALGO_BYTES and v["units"]}
+    stages = {k: {"achieved_GBps": round(b / (kstats[k]["ms"] / 1e3) / 1e9, 1),
+                  "frac": round(b / (kstats[k]["ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                  "avg_launch_ms": round(kstats[k]["ms"] / kstats[k]["launches"], 4),
+                  "algo_bytes_per_unit": round(b / kstats[k]["units"], 2), "unit": UNIT_NAME[k]}
+              for k, b in bytes_of.items()}
     res = batch.results()
     line = {
         "metric": "megapixels/sec JPEG encode (4K, -t 1MiB, q=0.25 cached)",

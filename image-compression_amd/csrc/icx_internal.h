@@ -2,13 +2,17 @@
 //
 // HBM layout per image (DESIGN.md §Data layout):
 //   px          u8 BGR/RGB/grey rows (caller's buffer, or the resize buffer)
-//   coefs       int16 raw jpeg_fdct_islow output (3 B per pixel for 4:2:0),
-//               scan blocks in MCU order (Y0 Y1 Y2 Y3 Cb Cr), chunk-interleaved:
-//               inside a chunk of CHUNK_BLOCKS blocks, zig-zag coefficients
-//               4k..4k+3 of block j sit at quad k, lane j (8 B), so the
-//               thread-per-block Huffman kernel reads 512 contiguous bytes per
-//               wave-load.  Written once per visited scale, re-read by every
-//               quality trial (quantisation happens in the trial kernel).
+//   coefs       sparse jpeg_fdct_islow output (raw, x8): per scan block
+//               (MCU order Y0 Y1 Y2 Y3 Cb Cr) a list of int32 entries
+//               (c << 6) | k in zig-zag order k — entry 0 is the DC, then every
+//               AC coefficient that can quantise to nonzero in ANY trial this
+//               image may run (|c| >= the smallest threshold over the image's
+//               reachable quality nodes, `cand_node`), zero-padded to a
+//               multiple of 4.  The lists of one FDCT tile are packed back to
+//               back inside the tile's region (room for 64 entries per block);
+//               block b's list starts at entry 4 * coff[b] and holds ncoef[b]
+//               entries.  Written once per visited scale by the FDCT, re-read
+//               by every quality trial (quantisation happens there).
 //   scratch[2]  per-chunk packed Huffman bitstreams (chunk = CHUNK_BLOCKS
 //               scan blocks, MSB-first 32-bit words, chunk-local bit 0),
 //               double-buffered: [best] holds the best fitting trial so the
@@ -31,12 +35,7 @@ constexpr int MAX_BLOCK_BITS = 1664;     // >= 22 (DC) + 63 * 26 (AC) bits, mult
 constexpr int BLOCK_WORDS = MAX_BLOCK_BITS / 32;               // 52
 constexpr int CHUNK_WORDS = CHUNK_BLOCKS * BLOCK_WORDS;        // 13312 words = 52 KiB
 
-// int16 index of zig-zag coefficient k of scan block b (chunk-interleaved)
-__host__ __device__ inline int64_t coef_index(int64_t b, int k)
-{
-    return (b / CHUNK_BLOCKS) * (CHUNK_BLOCKS * 64) + (k >> 2) * (CHUNK_BLOCKS * 4) +
-           (b % CHUNK_BLOCKS) * 4 + (k & 3);
-}
+constexpr int COEF_SLOTS = 64;           // int32 entries reserved per block in `coefs` (tile regions)
 constexpr int FD_TILE_PX = 128;          // FDCT tile width in pixels (8 colour MCUs)
 constexpr int MAX_TRIALS = 8;            // findBestQualityByBinarySearch loop bound (:167)
 constexpr int HDR_COLOR = 623;           // SOI+APP0+2 DQT+SOF0+4 DHT+SOS
@@ -64,10 +63,12 @@ struct ImgDesc {
     const uint8_t* px;     // pixels for the current stage (original or resized)
     int32_t w, h, stride, fmt;
     int32_t ncomp, mcux, mcuy, ywb, yhb;
-    int32_t nchunks, hdr_len, pad0;
+    int32_t nchunks, hdr_len, cand_node;  // cand_node: QNode whose thr[] filters the FDCT's lists
     int64_t nblocks;
     int64_t target;
-    int16_t* coefs;
+    int32_t* coefs;        // candidate lists, COEF_SLOTS entries reserved per block (see above)
+    uint32_t* coff;        // start of each block's list, in 4-entry (16-B) units
+    uint8_t* ncoef;        // list length per block (1..64)
     uint32_t* scratch[2];
     uint32_t* chunk_bits[2];
     uint64_t* chunk_off[2];   // nchunks + 1 entries
@@ -91,6 +92,7 @@ struct ImgState {
     int64_t best_size;
     int64_t out_len;
     uint64_t total_bits[2];
+    uint64_t list_entries; // candidate-list entries the last FDCT wrote (padded; algorithmic bytes)
     uint32_t ff_total[2];
     float trial_q[MAX_TRIALS + 1];
     int64_t trial_size[MAX_TRIALS + 1];

@@ -170,6 +170,13 @@ int64_t fdct_tiles(const ImgDesc& d)
     return d.ncomp == 1 ? (int64_t)((d.mcux + 15) / 16) * d.mcuy : (int64_t)((d.mcux + 15) / 16) * d.mcuy;
 }
 
+// candidate-list region: COEF_SLOTS int32 entries for every block of every
+// FDCT tile (16 colour MCUs = 96 blocks, or 16 grey blocks), partial tiles included
+size_t coef_bytes(const ImgDesc& d)
+{
+    return (size_t)fdct_tiles(d) * (d.ncomp == 1 ? 16 : 96) * COEF_SLOTS * 4;
+}
+
 // worst-case entropy bytes after stuffing
 uint64_t worst_file(const ImgDesc& d) { return (uint64_t)d.hdr_len + (uint64_t)d.nblocks * (MAX_BLOCK_BITS / 8) * 2 + 16; }
 
@@ -191,6 +198,7 @@ struct Item {
     int depth;
     int cached_node;
     double coef_scale;     // scale whose coefficients are resident, NaN = none
+    int64_t entries;       // candidate-list entries of the resident coefficients (padded)
     bool done, found, hit;
     float best_q;
     double best_scale;
@@ -281,6 +289,9 @@ void stage_pixels(Batch& B, int i, double scale)
     }
     // buffers and limits stay those sized for the original image
     d.coefs = keep.coefs;
+    d.coff = keep.coff;
+    d.ncoef = keep.ncoef;
+    d.cand_node = keep.cand_node;
     for (int k = 0; k < 2; k++) {
         d.scratch[k] = keep.scratch[k];
         d.chunk_bits[k] = keep.chunk_bits[k];
@@ -312,20 +323,40 @@ icx_status run_fdct(Batch& B, const std::vector<int>& ids)
         int64_t px = 0;
         for (int i : sel) px += (int64_t)B.desc[i].w * B.desc[i].h;
         Timed tm(B.c, "fdct", px);
-        launch_fdct(B.d_desc, P.p, P.total, kind, B.c->stream);
+        launch_fdct(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, kind, B.c->stream);
     }
     return ICX_OK;
 }
 
+// After the synchronisation of a stage whose FDCT covered `ids`: the list
+// entries each image's FDCT wrote (device counter), and the FDCT's algorithmic
+// bytes - pixels read + lists, list offsets and lengths written.
+void credit_fdct(Batch& B, const std::vector<int>& ids)
+{
+    int64_t bytes = 0;
+    for (int i : ids) {
+        const ImgDesc& d = B.desc[i];
+        B.it[i].entries = (int64_t)B.state[i].list_entries;
+        bytes += (int64_t)d.w * d.h * B.it[i].nch + 4 * B.it[i].entries + 5 * d.nblocks;
+    }
+    if (B.c->prof) B.c->stats["fdct.bytes"].units += bytes;
+}
+
 // Blocks actually quantised+coded by the trials of `ids` since their state
 // was initialised (inactive images exit k_huff at once): the huff kernel's
-// algorithmic work, credited after the stage's synchronisation.
+// algorithmic work - and bytes: every trial reads each block's list (padded
+// entries), its offset and its length - credited after the stage's
+// synchronisation.
 void credit_huff(Batch& B, const std::vector<int>& ids)
 {
     if (!B.c->prof) return;
-    int64_t blocks = 0;
-    for (int i : ids) blocks += (int64_t)B.state[i].ntrials * B.desc[i].nblocks;
+    int64_t blocks = 0, bytes = 0;
+    for (int i : ids) {
+        blocks += (int64_t)B.state[i].ntrials * B.desc[i].nblocks;
+        bytes += (int64_t)B.state[i].ntrials * (4 * B.it[i].entries + 5 * B.desc[i].nblocks);
+    }
     B.c->stats["huff"].units += blocks;
+    B.c->stats["huff.bytes"].units += bytes;
 }
 
 icx_status run_trials(Batch& B, const std::vector<int>& ids, int depth)
@@ -410,7 +441,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             ImgDesc g{};
             geometry(g, j.img.width, j.img.height, j.img.fmt);
             const int nch = channels(j.img.fmt);
-            size_t per = (size_t)g.nchunks * CHUNK_BLOCKS * 128 + (size_t)g.nblocks * BLOCK_WORDS * 4 + 1024 +
+            size_t per = coef_bytes(g) + (size_t)g.nchunks * CHUNK_BLOCKS * 5 + (size_t)g.nblocks * BLOCK_WORDS * 4 + 1024 +
                          2 * ((size_t)g.nchunks * CHUNK_WORDS + 1) * 4 +
                          (size_t)g.nchunks * (2 * 4 + 2 * 8 + 2 * 4 + 2 * 32 + 8) + 64 + 8 * 256;
             per += (size_t)j.img.width * j.img.height * nch * 2;  // input staging + resize buffer
@@ -463,13 +494,16 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             I.best_scale = 0;
             I.encodes = 0;
             I.coef_scale = NAN;
+            I.entries = 0;
             I.root = I.cached_node = -1;
             I.depth = 0;
             ImgDesc& d = B.desc[k];
             geometry(d, j.img.width, j.img.height, j.img.fmt);
             d.stride = j.img.stride;
             d.target = j.target_max_size;
-            d.coefs = (int16_t*)c->dev.take((size_t)d.nchunks * CHUNK_BLOCKS * 128);
+            d.coefs = (int32_t*)c->dev.take(coef_bytes(d));
+            d.coff = (uint32_t*)c->dev.take((size_t)d.nchunks * CHUNK_BLOCKS * 4);
+            d.ncoef = (uint8_t*)c->dev.take((size_t)d.nchunks * CHUNK_BLOCKS);
             d.ovf = (uint32_t*)c->dev.take((size_t)d.nblocks * BLOCK_WORDS * 4 + 1024);
             for (int b = 0; b < 2; b++) {
                 d.scratch[b] = (uint32_t*)c->dev.take(((size_t)d.nchunks * CHUNK_WORDS + 1) * 4);
@@ -532,7 +566,39 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                 I.cached_node = single(j.quality);
             }
         }
-        if (B.nodes.empty()) B.nodes.emplace_back();
+        // Candidate filter of each image: per coefficient, the smallest
+        // quantiser threshold over every node a trial of this image can reach
+        // (cached probe + search tree).  The FDCT keeps only coefficients at or
+        // above it - every one that can quantise to nonzero in some trial.  No
+        // reachable node (debug FDCT): all-zero thresholds keep every coefficient.
+        std::map<std::pair<int, int>, int> cand_of;
+        for (int k = 0; k < m; k++) {
+            Item& I = B.it[k];
+            const auto key = std::make_pair(I.root, I.cached_node);
+            auto f = cand_of.find(key);
+            if (f == cand_of.end()) {
+                QNode cn{};
+                std::vector<int> todo;
+                if (I.root >= 0) todo.push_back(I.root);
+                if (I.cached_node >= 0) todo.push_back(I.cached_node);
+                bool first = true;
+                while (!todo.empty()) {
+                    const int n = todo.back();
+                    todo.pop_back();
+                    for (int c = 0; c < 2; c++)
+                        for (int z = 0; z < 64; z++)
+                            cn.thr[c][z] = first ? B.nodes[n].thr[c][z] : std::min(cn.thr[c][z], B.nodes[n].thr[c][z]);
+                    first = false;
+                    if (B.nodes[n].child_fit >= 0) todo.push_back(B.nodes[n].child_fit);
+                    if (B.nodes[n].child_nofit >= 0) todo.push_back(B.nodes[n].child_nofit);
+                }
+                cn.child_fit = cn.child_nofit = -1;
+                B.nodes.push_back(cn);
+                f = cand_of.emplace(key, (int)B.nodes.size() - 1).first;
+            }
+            B.desc[k].cand_node = f->second;
+            I.orig.cand_node = f->second;
+        }
         B.d_desc = (ImgDesc*)c->dev.take(sizeof(ImgDesc) * m);
         B.d_state = (ImgState*)c->dev.take(sizeof(ImgState) * m);
         B.d_nodes = (QNode*)c->dev.take(sizeof(QNode) * B.nodes.size());
@@ -548,11 +614,21 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             for (int k = 0; k < m; k++) init_state(B.state[k], -1, false);
             if ((s = push_desc_state(B)) || (s = run_fdct(B, all)) || (s = sync_states(B))) return s;
             const ImgDesc& d0 = B.desc[0];
-            std::vector<int16_t> raw((size_t)d0.nchunks * CHUNK_BLOCKS * 64);
-            e = hipMemcpy(raw.data(), d0.coefs, raw.size() * 2, hipMemcpyDeviceToHost);
+            std::vector<int32_t> raw(coef_bytes(d0) / 4);
+            std::vector<uint32_t> off((size_t)d0.nblocks);
+            std::vector<uint8_t> cnt((size_t)d0.nblocks);
+            e = hipMemcpy(raw.data(), d0.coefs, raw.size() * 4, hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(off.data(), d0.coff, off.size() * 4, hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(cnt.data(), d0.ncoef, cnt.size(), hipMemcpyDeviceToHost);
             if (e != hipSuccess) return hip_fail(c, e, "coef download");
-            for (int64_t blk = 0; blk < d0.nblocks; blk++)  // chunk-interleaved -> block-major
-                for (int k = 0; k < 64; k++) fdct_out[blk * 64 + k] = raw[coef_index(blk, k)];
+            for (int64_t blk = 0; blk < d0.nblocks; blk++) {  // lists -> block-major zig-zag
+                if (cnt[blk] != 64 || (size_t)off[blk] * 4 + 64 > raw.size())
+                    return fail(c, ICX_E_DEVICE, "debug FDCT list is not complete");
+                for (int i = 0; i < 64; i++) {
+                    const int32_t v = raw[(size_t)off[blk] * 4 + i];
+                    fdct_out[blk * 64 + (v & 63)] = (int16_t)(v >> 6);
+                }
+            }
             continue;
         }
 
@@ -568,6 +644,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             if ((s = push_desc_state(B)) || (s = run_fdct(B, all)) || (s = run_trials(B, all, 1)) ||
                 (s = sync_states(B)))
                 return s;
+            credit_fdct(B, all);
             credit_huff(B, all);
             if ((s = finish_found(all))) return s;
             for (int k = 0; k < m; k++) {
@@ -593,6 +670,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                 if ((s = push_desc_state(B)) || (s = run_fdct(B, probe)) || (s = run_trials(B, probe, 1)) ||
                     (s = sync_states(B)))
                     return s;
+                credit_fdct(B, probe);
                 credit_huff(B, probe);
                 std::vector<int> hits;
                 for (int k : probe) {
@@ -627,6 +705,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                 if ((s = push_desc_state(B)) || (s = run_fdct(B, need_fdct)) || (s = run_trials(B, pend, depth)) ||
                     (s = sync_states(B)))
                     return s;
+                credit_fdct(B, need_fdct);
                 credit_huff(B, pend);
                 std::vector<int> found, rest;
                 for (int k : pend) {

@@ -17,7 +17,10 @@ import icx  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 target = int(sys.argv[2]) if len(sys.argv) > 2 else bench.TARGET  # a huge target: one probe trial per frame
 dev = torch.device("cuda:0")
-frames = bench.make_frames(n, 1000, dev)
+kind = sys.argv[3] if len(sys.argv) > 3 else "mixed"  # mixed | smooth | noise
+frames = bench.make_frames(n if kind == "mixed" else 2 * n, 1000, dev)
+if kind != "mixed":
+    frames = frames[0 if kind == "smooth" else 1::2]
 codec = icx.Codec(0)
 outs = [torch.empty(min(target, 1 << 25) + 1, dtype=torch.uint8, device=dev) for _ in range(n)]
 cached = [icx.LearnedParams(bench.Q0, 1.0)] * n
@@ -29,5 +32,5 @@ for _ in range(2):
     codec.fit(frames, target, bench.Q0, cached=cached, outputs=outs)
 torch.cuda.synchronize()
 res = {k: codec.profile_query(k) for k in ("fdct", "huff", "scan", "decide", "ffscan", "stuff")}
-print(json.dumps({"lib": os.path.basename(os.environ.get("ICX_LIB", "libicx.so")), "images": n,
+print(json.dumps({"lib": os.path.basename(os.environ.get("ICX_LIB", "libicx.so")), "images": n, "kind": kind,
                   "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k, v in res.items()}}))
