@@ -271,6 +271,7 @@ def main():
     kstats = {k: codec.profile_query(k) for k in ("fdct", "huff", "scan", "decide", "ffscan",
                                                   "stuff", "resize")}
     kstats = {k: v for k, v in kstats.items() if v["launches"]}
+    sb = codec.profile_query("subbatch")
     roof = None
     bytes_of = {k: algo_bytes(codec, k, v) for k, v in kstats.items() if k in UNIT_NAME and v["units"]}
     if bytes_of:
@@ -303,7 +304,9 @@ def main():
                    "images_per_gpu": args.images, "global_images": world * args.images,
                    "target_bytes": TARGET, "quality": Q0, "parallelism": f"file-list shard x{world}",
                    "encodes_per_image": round(sum(r["encodes"] for r in res) / len(res), 3),
-                   "mean_out_bytes": int(np.mean([r["out_len"] for r in res]))},
+                   "mean_out_bytes": int(np.mean([r["out_len"] for r in res])),
+                   "subbatches_per_step": round(sb["launches"] / args.steps, 2),
+                   "workspace_mb_per_subbatch": int(sb["units"] / max(1, sb["launches"]))},
         "roofline": roof,
         "stages": stages,
         "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k, v in kstats.items()},

@@ -205,81 +205,78 @@ __device__ __forceinline__ void fdct_load(const FdctTile& T, uint32_t (&wv)[2][6
 }
 
 // Candidate lists of one FDCT tile (nblk scan blocks from bbase; the tile's
-// list region starts at entry `base`).  oz[blk] holds block blk's raw
-// coefficients in zig-zag order (fix(blk, lane, c) applies dummy blocks),
-// luma(blk) its component.  The DC and every AC coefficient with |c| >= thr
+// list region starts at entry `base`, COEF_SLOTS entries reserved per block).
+// oz[blk] holds block blk's raw coefficients in zig-zag order (fix(blk, lane,
+// c) applies dummy blocks).  The DC and every AC coefficient with |c| >= thr
 // (lane 0's thr is negative; the others hold the smallest quantiser
-// threshold of k over the qualities this image may be coded at) become
-// entries (c << 6) | k, in k order, zero-padded to a multiple of 4 entries
-// (k_huff reads 16-B groups; a zero entry never quantises to nonzero).
-//   1. one wave per block, lane = k, four blocks per step: ballot/mbcnt
-//      compaction of the values in place in oz and of k into s_k; lengths
-//   2. exclusive scan of the padded lengths -> packed offsets in the region
-//   3. every thread forms four entries at a time and stores them as one
-//      16-B piece; the tile's lists lie back to back
+// threshold of k over the qualities this image may be coded at) form the
+// block's list, entries (c << 6) | k in k order, padded to a multiple of 4
+// entries (k_huff reads 16-B groups) with the block's first non-candidates,
+// which cannot quantise to nonzero in any trial.
+// One wave per group of STEP blocks (one MCU for colour; luma(a): block
+// blk0 + a is luma), lane = k: per block a ballot/mbcnt partition
+// (candidates first, then the rest) into the wave's LDS stage, the group's
+// lists back to back; then the group leaves as 16-B pieces into the group's
+// own reserved region.  No cross-wave scan: lists are packed per group.
+// Lengths and offsets go to s_len / s_off and, after the caller's barrier,
+// to ncoef / coff (store_list_meta).
 template <int NB, int STEP, class Fix, class Luma>
-__device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, uint32_t bbase, int nblk,
-                                           int16_t (*oz)[WSTR_OF<NB>], uint8_t (*s_k)[64], uint8_t* s_len,
+__device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int nblk, int16_t (*oz)[WSTR_OF<NB>],
+                                           uint32_t (*stg)[STEP * 64], uint8_t* s_len,
                                            uint16_t* s_off, const float (&thr)[2], unsigned long long* ent,
                                            Fix fix, Luma luma)
 {
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    uint32_t* st = stg[wave];
+    uint32_t total = 0;
     for (int blk0 = wave * STEP; blk0 < nblk; blk0 += 4 * STEP) {
         int c[STEP];
 #pragma unroll
         for (int a = 0; a < STEP; a++) c[a] = blk0 + a < nblk ? fix(blk0 + a, lane, (int)oz[blk0 + a][lane]) : 0;
-        int len = 0;
+        int run = 0, len = 0, off = 0;  // run: padded entries of the group so far (wave-uniform)
 #pragma unroll
         for (int a = 0; a < STEP; a++) {
-            // blocks past nblk (grey tiles only) are partitioned too but never read back
+            if (blk0 + a >= nblk) break;  // wave-uniform (partial grey tiles)
             const bool cand = fabsf((float)c[a]) >= (luma(a) ? thr[0] : thr[1]);
             const uint64_t mask = __ballot(cand);
-            const int cnt = __popcll(mask);
+            const int cnt = __popcll(mask), r4 = (cnt + 3) & ~3;
             const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-            const int slot = cand ? pos : cnt + lane - pos;  // every lane has read the row already
-            oz[blk0 + a][slot] = (int16_t)c[a];
-            s_k[blk0 + a][slot] = (uint8_t)lane;
-            if (lane == a) len = cnt;
+            const int slot = cand ? pos : cnt + lane - pos;
+            if (slot < r4) st[run + slot] = ((uint32_t)c[a] << 6) | (uint32_t)lane;
+            if (lane == a) {
+                len = cnt;
+                off = run;
+            }
+            run += r4;
         }
-        if (lane < STEP && blk0 + lane < nblk) s_len[blk0 + lane] = (uint8_t)len;
-    }
-    __syncthreads();
-    if (t < 64) {
-        const int n0 = 2 * t < nblk ? (s_len[2 * t] + 3) & ~3 : 0;
-        const int n1 = 2 * t + 1 < nblk ? (s_len[2 * t + 1] + 3) & ~3 : 0;
-        int incl = n0 + n1;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int y = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += y;
+        if (lane < STEP && blk0 + lane < nblk) {
+            s_len[blk0 + lane] = (uint8_t)len;
+            s_off[blk0 + lane] = (uint16_t)(blk0 * COEF_SLOTS + off);
         }
-        s_off[2 * t] = (uint16_t)(incl - n0 - n1);
-        s_off[2 * t + 1] = (uint16_t)(incl - n1);
+        __builtin_amdgcn_wave_barrier();
+        GAS u32x4_t* dst = (GAS u32x4_t*)(D.coefs + base + (int64_t)blk0 * COEF_SLOTS);
+        for (int p = lane; p < run / 4; p += 64) {
+            const uint4 v = *(const uint4*)&st[4 * p];
+            u32x4_t w;
+            w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+            dst[p] = w;
+        }
+        total += run;
+        __builtin_amdgcn_wave_barrier();
     }
-    __syncthreads();
+    if (lane == 0 && total) atomicAdd(ent, (unsigned long long)total);
+}
+
+// After the barrier that ends emit_lists: lengths and 16-B-unit offsets.
+__device__ __forceinline__ void store_list_meta(const ImgDesc& D, int64_t base, uint32_t bbase, int nblk,
+                                                const uint8_t* s_len, const uint16_t* s_off)
+{
+    const int t = threadIdx.x;
     if (t < nblk) {
         D.ncoef[bbase + t] = s_len[t];
         D.coff[bbase + t] = (uint32_t)((base + s_off[t]) >> 2);
-        if (t == nblk - 1) atomicAdd(ent, (unsigned long long)(s_off[t] + ((s_len[t] + 3) & ~3)));
-    }
-#pragma unroll
-    for (int r = 0; r < (NB * 16 + 255) / 256; r++) {
-        const int blk = (t >> 4) + 16 * r, q = t & 15;
-        if (blk < nblk) {
-            const int len = s_len[blk];
-            if (4 * q < len) {  // entries past len: the row's first non-candidates
-                const uint2 v = *(const uint2*)&oz[blk][4 * q];
-                const uint32_t kk = *(const uint32_t*)&s_k[blk][4 * q];
-                u32x4_t w;
-                w.x = ((uint32_t)(int32_t)(int16_t)v.x << 6) | (kk & 255);
-                w.y = ((uint32_t)((int32_t)v.x >> 16) << 6) | ((kk >> 8) & 255);
-                w.z = ((uint32_t)(int32_t)(int16_t)v.y << 6) | ((kk >> 16) & 255);
-                w.w = ((uint32_t)((int32_t)v.y >> 16) << 6) | (kk >> 24);
-                *(GAS u32x4_t*)(D.coefs + base + s_off[blk] + 4 * q) = w;
-            }
-        }
     }
 }
 
@@ -288,7 +285,7 @@ template <bool BGR>
 __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (&wv)[2][6],
                                              const QNode* __restrict__ nodes, ImgState* states,
                                              uint8_t (*cds)[8][FDC_PX / 2],
-                                             int16_t (*ws)[WSTR], uint8_t (*s_k)[64])
+                                             int16_t (*ws)[WSTR], uint32_t (*stg)[384])
 {
     const ImgDesc& D = *T.D;
     const int tx = T.tx, my = T.my;
@@ -404,9 +401,12 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
     if (t < nblk) D.ncoef[bbase + t] = (uint8_t)oz[t][t & 63];
     if (true) { __syncthreads(); return; }
 #endif
-    emit_lists<FDC_BLK, 6>(D, tile_id * (FDC_BLK * COEF_SLOTS), bbase, nblk, oz, s_k, s_len, s_off, thr,
+    const int64_t base = tile_id * (FDC_BLK * COEF_SLOTS);
+    emit_lists<FDC_BLK, 6>(D, base, nblk, oz, stg, s_len, s_off, thr,
                            (unsigned long long*)&states[T.img].list_entries, fix,
                            [](int a) { return a < 4; });  // one MCU per step: Y0 Y1 Y2 Y3 Cb Cr
+    __syncthreads();
+    store_list_meta(D, base, bbase, nblk, s_len, s_off);
     __syncthreads();  // LDS free for the next tile
 }
 
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
 {
     __shared__ __attribute__((aligned(16))) uint8_t cds[2][8][FDC_PX / 2];  // 2 KB downsampled Cb, Cr
     __shared__ __attribute__((aligned(16))) int16_t ws[FDC_BLK][WSTR];     // 12.75 KB row-pass output
-    __shared__ __attribute__((aligned(16))) uint8_t s_k[FDC_BLK][64];       // 6 KB compacted zig-zag indices
+    __shared__ __attribute__((aligned(16))) uint32_t stg[4][6 * 64];        // 6 KB list staging, one MCU per wave
     const int64_t total = prefix[m];
     const int64_t item0 = (int64_t)blockIdx.x * FDCT_TILES;
     uint32_t cur[2][6], nxt[2][6];
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
             tn = fdct_tile(descs, ids, prefix, m, item0 + k + 1);
             fdct_load(tn, nxt);
         }
-        fdct_compute<BGR>(tc, cur, nodes, states, cds, ws, s_k);
+        fdct_compute<BGR>(tc, cur, nodes, states, cds, ws, stg);
         if (!more) break;
         tc = tn;
 #pragma unroll
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
     __shared__ __attribute__((aligned(16))) int16_t oz[16][64];
     __shared__ uint8_t s_len[16];
     __shared__ uint16_t s_off[128];
-    __shared__ __attribute__((aligned(16))) uint8_t s_k[16][64];
+    __shared__ __attribute__((aligned(16))) uint32_t stg[4][4 * 64];
     const int64_t item = blockIdx.x;
     const int slot = find_slot(prefix, m, item);
     const int img = ids[slot];
@@ -499,9 +499,11 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
     const int nblk = min(16, D.mcux - tx * 16);
     const uint32_t bbase = (uint32_t)by * D.mcux + tx * 16;
     const float thr[2] = {(t & 63) ? nodes[D.cand_node].thr[0][t & 63] : -1.0f, 0.0f};
-    emit_lists<16, 4>(D, (int64_t)tile * (16 * COEF_SLOTS), bbase, nblk, oz, s_k, s_len, s_off, thr,
-                      (unsigned long long*)&states[img].list_entries, [](int, int, int c) { return c; },
-                      [](int) { return true; });
+    const int64_t base = (int64_t)tile * (16 * COEF_SLOTS);
+    emit_lists<16, 4>(D, base, nblk, oz, stg, s_len, s_off, thr, (unsigned long long*)&states[img].list_entries,
+                      [](int, int, int c) { return c; }, [](int) { return true; });
+    __syncthreads();
+    store_list_meta(D, base, bbase, nblk, s_len, s_off);
 }
 
 // =================================================================== Huffman
@@ -814,7 +816,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     // 0xFF-byte count for each alignment k_scan may place it at.  Runs may
     // reach into the following blocks (their first <= 8 bits); nothing
     // follows the chunk's last bit here (k_scan checks the boundary bytes).
-    if (bits > 0) {
+    if (ICX_HUFF_EXP != 5 && bits > 0) {  // EXP 5: timing only, no 0xFF bins
         uint32_t la = 0;  // the <= 8 bits after this block, MSB-aligned
         int have = 0;
         for (int u = t + 1; have < 8 && u < nb; u++) {
@@ -848,7 +850,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
 
     // ---- 4. gather the chunk's words
     GAS uint32_t* dst = gp(D.scratch[cur] + (size_t)chunk * CHUNK_WORDS);
-    for (uint32_t j = (off + 31) >> 5; j * 32 < off + bits; j++) {
+    for (uint32_t j = (off + 31) >> 5; ICX_HUFF_EXP != 6 && j * 32 < off + bits; j++) {  // EXP 6: no gather
         uint32_t outw = 0;
         int have = 0, u = t;
         uint32_t p = j * 32 - off;

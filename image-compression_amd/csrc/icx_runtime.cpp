@@ -431,24 +431,39 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
         if (j.status == ICX_OK && mode != Mode::Search && mode != Mode::Fdct && !j.out) j.status = ICX_E_NULL;
         if (j.status == ICX_OK) order.push_back(i);
     }
+    // ---- device workspace per image (what the sub-batch loop below takes)
+    auto workspace = [&](const icx_fit_job& j) -> size_t {
+        ImgDesc g{};
+        geometry(g, j.img.width, j.img.height, j.img.fmt);
+        const size_t px = (size_t)j.img.width * j.img.height * channels(j.img.fmt);
+        size_t per = coef_bytes(g) + (size_t)g.nchunks * CHUNK_BLOCKS * 5 + (size_t)g.nblocks * BLOCK_WORDS * 4 + 1024 +
+                     2 * ((size_t)g.nchunks * CHUNK_WORDS + 1) * 4 +
+                     (size_t)g.nchunks * (2 * 4 + 2 * 8 + 2 * 4 + 2 * 32 + 8) + 64 + 8 * 256 + 4096;
+        if (!is_device_ptr(j.img.px)) per += px;                   // input staging
+        if (mode == Mode::Fit) per += px;                         // resize buffer
+        if ((mode == Mode::Fit || mode == Mode::Encode) && !is_device_ptr(j.out))
+            per += std::min<uint64_t>(worst_file(g), j.cap);      // output staging
+        return per;
+    };
+    // Sub-batches of about equal size: as few as the budget allows.
+    size_t all_need = 0;
+    for (int i : order) all_need += workspace(jobs[i]);
+    const size_t nsub = std::max<size_t>(1, (all_need + c->budget - 1) / c->budget);
+    const size_t share = (all_need + nsub - 1) / nsub;
     size_t pos = 0;
     while (pos < order.size()) {
         // ---- size a sub-batch against the workspace budget
         std::vector<int> sub;
         size_t need = 1 << 20;
         while (pos < order.size()) {
-            icx_fit_job& j = jobs[order[pos]];
-            ImgDesc g{};
-            geometry(g, j.img.width, j.img.height, j.img.fmt);
-            const int nch = channels(j.img.fmt);
-            size_t per = coef_bytes(g) + (size_t)g.nchunks * CHUNK_BLOCKS * 5 + (size_t)g.nblocks * BLOCK_WORDS * 4 + 1024 +
-                         2 * ((size_t)g.nchunks * CHUNK_WORDS + 1) * 4 +
-                         (size_t)g.nchunks * (2 * 4 + 2 * 8 + 2 * 4 + 2 * 32 + 8) + 64 + 8 * 256;
-            per += (size_t)j.img.width * j.img.height * nch * 2;  // input staging + resize buffer
-            per += std::min<uint64_t>(worst_file(g), j.cap);
-            if (!sub.empty() && need + per > c->budget) break;
+            const size_t per = workspace(jobs[order[pos]]);
+            if (!sub.empty() && (need + per > c->budget || need - (1 << 20) >= share)) break;
             need += per;
             sub.push_back(order[pos++]);
+        }
+        if (c->prof) {  // sub-batches per call and their workspace (reported by bench.py)
+            c->stats["subbatch"].launches++;
+            c->stats["subbatch"].units += (int64_t)(need >> 20);
         }
         hipError_t e = c->dev.reserve(need + ((size_t)sub.size() + 8) * 4096 + (16 << 20));
         if (e != hipSuccess) {
@@ -873,13 +888,13 @@ icx_status icx_create(int device, icx_ctx** out)
         delete c;
         return ICX_E_DEVICE;
     }
-    // Sub-batch workspace: a quarter of the free HBM at creation (a 4K image
-    // needs ~210 MB, so ~80 GB holds a few hundred frames per sub-batch and the
+    // Sub-batch workspace: a third of the free HBM at creation (a 4K image
+    // needs ~200 MB, so ~90 GB holds a few hundred frames per sub-batch and the
     // host synchronises a few times per call, not per handful of images).
     size_t free_b = 0, total_b = 0;
     size_t budget_mb = 16384;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
-        budget_mb = std::max<size_t>(2048, (free_b / 4) >> 20);
+        budget_mb = std::max<size_t>(2048, (free_b / 3) >> 20);
     if (const char* env = getenv("ICX_WORKSPACE_MB")) budget_mb = (size_t)atoll(env);
     c->budget = budget_mb << 20;
     *out = c;
