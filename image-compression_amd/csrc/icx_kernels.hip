@@ -220,9 +220,27 @@ __device__ __forceinline__ void fdct_load(const FdctTile& T, uint32_t (&wv)[2][6
 // own reserved region.  No cross-wave scan: lists are packed per group.
 // Lengths and offsets go to s_len / s_off and, after the caller's barrier,
 // to ncoef / coff (store_list_meta).
-template <int NB, int STEP, class Fix, class Luma>
+// Stage of one wave: STEP blocks' lists, then 64 dwords every lane may write
+// (lanes with nothing to store write there, so the stores need no exec mask).
+template <int STEP> constexpr int STAGE_DW = STEP * 64 + 64;
+
+// v_writelane: lane `a` (0..7, a constant once the caller's loop is unrolled)
+// of v takes the wave-uniform value x - one VALU op, no lane compare.
+#define ICX_WRITELANE(A) \
+    case A: asm volatile("v_writelane_b32 %0, %1, " #A : "+v"(v) : "s"(x)); break;
+__device__ __forceinline__ int writelane(int v, int x, int a)
+{
+    switch (a) {
+        ICX_WRITELANE(0) ICX_WRITELANE(1) ICX_WRITELANE(2) ICX_WRITELANE(3)
+        ICX_WRITELANE(4) ICX_WRITELANE(5) ICX_WRITELANE(6) ICX_WRITELANE(7)
+    }
+    return v;
+}
+#undef ICX_WRITELANE
+
+template <int NB, int STEP, bool FULL, class Fix, class Luma>
 __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int nblk, int16_t (*oz)[WSTR_OF<NB>],
-                                           uint32_t (*stg)[STEP * 64], uint8_t* s_len,
+                                           uint32_t (*stg)[STAGE_DW<STEP>], uint8_t* s_len,
                                            uint16_t* s_off, const float (&thr)[2], unsigned long long* ent,
                                            Fix fix, Luma luma)
 {
@@ -233,22 +251,21 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
     for (int blk0 = wave * STEP; blk0 < nblk; blk0 += 4 * STEP) {
         int c[STEP];
 #pragma unroll
-        for (int a = 0; a < STEP; a++) c[a] = blk0 + a < nblk ? fix(blk0 + a, lane, (int)oz[blk0 + a][lane]) : 0;
+        for (int a = 0; a < STEP; a++)
+            c[a] = FULL || blk0 + a < nblk ? fix(blk0 + a, lane, (int)oz[blk0 + a][lane]) : 0;
         int run = 0, len = 0, off = 0;  // run: padded entries of the group so far (wave-uniform)
 #pragma unroll
         for (int a = 0; a < STEP; a++) {
-            if (blk0 + a >= nblk) break;  // wave-uniform (partial grey tiles)
+            if (!FULL && blk0 + a >= nblk) break;  // wave-uniform (partial grey tiles)
             const bool cand = fabsf((float)c[a]) >= (luma(a) ? thr[0] : thr[1]);
             const uint64_t mask = __ballot(cand);
-            const int cnt = __popcll(mask), r4 = (cnt + 3) & ~3;
+            const int cnt = __builtin_amdgcn_readfirstlane(__popcll(mask)), r4 = (cnt + 3) & ~3;
             const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
             const int slot = cand ? pos : cnt + lane - pos;
-            if (slot < r4) st[run + slot] = ((uint32_t)c[a] << 6) | (uint32_t)lane;
-            if (lane == a) {
-                len = cnt;
-                off = run;
-            }
+            st[slot < r4 ? run + slot : STEP * 64 + lane] = ((uint32_t)c[a] << 6) | (uint32_t)lane;
+            len = writelane(len, cnt, a);
+            off = writelane(off, run, a);
             run += r4;
         }
         if (lane < STEP && blk0 + lane < nblk) {
@@ -285,7 +302,7 @@ template <bool BGR>
 __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (&wv)[2][6],
                                              const QNode* __restrict__ nodes, ImgState* states,
                                              uint8_t (*cds)[8][FDC_PX / 2],
-                                             int16_t (*ws)[WSTR], uint32_t (*stg)[384])
+                                             int16_t (*ws)[WSTR], uint32_t (*stg)[STAGE_DW<6>])
 {
     const ImgDesc& D = *T.D;
     const int tx = T.tx, my = T.my;
@@ -402,9 +419,13 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
     if (true) { __syncthreads(); return; }
 #endif
     const int64_t base = tile_id * (FDC_BLK * COEF_SLOTS);
-    emit_lists<FDC_BLK, 6>(D, base, nblk, oz, stg, s_len, s_off, thr,
-                           (unsigned long long*)&states[T.img].list_entries, fix,
-                           [](int a) { return a < 4; });  // one MCU per step: Y0 Y1 Y2 Y3 Cb Cr
+    unsigned long long* ent = (unsigned long long*)&states[T.img].list_entries;
+    auto luma = [](int a) { return a < 4; };  // one MCU per step: Y0 Y1 Y2 Y3 Cb Cr
+    if (plain)  // interior tile: no dummy blocks
+        emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, stg, s_len, s_off, thr, ent,
+                                     [](int, int, int c) { return c; }, luma);
+    else
+        emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, stg, s_len, s_off, thr, ent, fix, luma);
     __syncthreads();
     store_list_meta(D, base, bbase, nblk, s_len, s_off);
     __syncthreads();  // LDS free for the next tile
@@ -429,7 +450,7 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
 {
     __shared__ __attribute__((aligned(16))) uint8_t cds[2][8][FDC_PX / 2];  // 2 KB downsampled Cb, Cr
     __shared__ __attribute__((aligned(16))) int16_t ws[FDC_BLK][WSTR];     // 12.75 KB row-pass output
-    __shared__ __attribute__((aligned(16))) uint32_t stg[4][6 * 64];        // 6 KB list staging, one MCU per wave
+    __shared__ __attribute__((aligned(16))) uint32_t stg[4][STAGE_DW<6>];   // 7 KB list staging, one MCU per wave
     const int64_t total = prefix[m];
     const int64_t item0 = (int64_t)blockIdx.x * FDCT_TILES;
     uint32_t cur[2][6], nxt[2][6];
@@ -463,7 +484,7 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
     __shared__ __attribute__((aligned(16))) int16_t oz[16][64];
     __shared__ uint8_t s_len[16];
     __shared__ uint16_t s_off[128];
-    __shared__ __attribute__((aligned(16))) uint32_t stg[4][4 * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t stg[4][STAGE_DW<4>];
     const int64_t item = blockIdx.x;
     const int slot = find_slot(prefix, m, item);
     const int img = ids[slot];
@@ -500,7 +521,7 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
     const uint32_t bbase = (uint32_t)by * D.mcux + tx * 16;
     const float thr[2] = {(t & 63) ? nodes[D.cand_node].thr[0][t & 63] : -1.0f, 0.0f};
     const int64_t base = (int64_t)tile * (16 * COEF_SLOTS);
-    emit_lists<16, 4>(D, base, nblk, oz, stg, s_len, s_off, thr, (unsigned long long*)&states[img].list_entries,
+    emit_lists<16, 4, false>(D, base, nblk, oz, stg, s_len, s_off, thr, (unsigned long long*)&states[img].list_entries,
                       [](int, int, int c) { return c; }, [](int) { return true; });
     __syncthreads();
     store_list_meta(D, base, bbase, nblk, s_len, s_off);

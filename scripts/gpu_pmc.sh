@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
 export TMPDIR=/tmp
 TAG=${TAG:-r1}
-ARGS=${PMC_ARGS:-"--images 64 --steps 1 --warmup 0 --no-cpu-baseline --profile 0 --no-cache --target 16000000"}
+ARGS=${PMC_ARGS:-"--images 64 --steps 1 --warmup 0 --no-cpu-baseline --profile 0 --no-cache --target 16000000 --e2e 0"}
 mkdir -p gpurun_out/pmc_${TAG}
 cd /tmp
 for ctr in FETCH_SIZE WRITE_SIZE; do
