@@ -550,6 +550,10 @@ constexpr int SLOT_WORDS = ICX_SLOT_WORDS;
 #endif
 
 constexpr int SLOT_BITS = SLOT_WORDS * 32;
+constexpr int AC_SIZES_ = 11;
+constexpr int TAB_WORDS = 2 * 16 * AC_SIZES_ * 2 + 2 * 64 * 4 + 2 * 16;  // s_ac + s_qf + s_dc
+constexpr int OUT_WORDS = 1024;  // chunk streams up to this many words are assembled in LDS
+static_assert(OUT_WORDS + 8 <= TAB_WORDS, "assembled stream must fit in the table LDS");
 constexpr int AC_SIZES = 11;                // AC magnitude categories 0..10 (8-bit JPEG)
 constexpr int AC_ENTRIES = 16 * AC_SIZES;   // (run, size) slots per table
 
@@ -712,9 +716,13 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
                                                        const int64_t* __restrict__ prefix, int m)
 {
     __shared__ uint32_t slots[CHUNK_BLOCKS * SLOT_WORDS];
-    __shared__ uint2 s_ac[2][AC_ENTRIES];
-    __shared__ uint32_t s_dc[2][16];
-    __shared__ float4 s_qf[2][64];  // (thr, frcp, fbias, -) per zig-zag index
+    // Coding tables during phase 1; afterwards the same LDS holds the chunk's
+    // assembled stream (phase 3, chunks of at most OUT_WORDS words).
+    __shared__ __attribute__((aligned(16))) uint32_t s_tab[TAB_WORDS];
+    uint2 (*s_ac)[AC_ENTRIES] = (uint2 (*)[AC_ENTRIES])s_tab;
+    float4 (*s_qf)[64] = (float4 (*)[64])(s_tab + 2 * AC_ENTRIES * 2);  // (thr, frcp, fbias, -) per zig-zag index
+    uint32_t (*s_dc)[16] = (uint32_t (*)[16])(s_tab + 2 * AC_ENTRIES * 2 + 2 * 64 * 4);
+    uint32_t* const s_out = s_tab;
     __shared__ uint32_t s_off[CHUNK_BLOCKS + 1];
     __shared__ uint32_t s_bits[CHUNK_BLOCKS];
     int32_t* const s_dcq = (int32_t*)s_bits;  // DC exchange; dead before s_bits is written
@@ -831,8 +839,52 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     auto slot_word = [&](int u, uint32_t wi) -> uint32_t {  // word wi of block u's stream
         return s_bits[u] <= SLOT_BITS ? slots[u * SLOT_WORDS + wi] : spill0[(size_t)u * BLOCK_WORDS + wi];
     };
+    GAS uint32_t* dst = gp(D.scratch[cur] + (size_t)chunk * CHUNK_WORDS);
 
-    // ---- 3. 0xFF candidates: every run of eight 1-bits that starts in this
+    if (total <= (uint32_t)OUT_WORDS * 32) {
+        // ---- 3. (common case) assemble the chunk stream in LDS over the dead
+        // tables: every block ORs its words in at its offset; then each word is
+        // stored once (coalesced) and the runs of eight 1-bits starting in it
+        // (with the next word's first 7 bits; zeros past the chunk's last bit,
+        // k_scan checks the boundary bytes) are binned by chunk-local start
+        // position mod 8 (s_ffa): the chunk's 0xFF-byte count for each
+        // alignment k_scan may place it at.
+        const uint32_t nwords = (total + 31) >> 5;
+        for (uint32_t i = t; i < OUT_WORDS + 8; i += CHUNK_BLOCKS) s_out[i] = 0u;
+        __syncthreads();
+        if (bits > 0) {
+            const uint32_t sh = off & 31, nwb = ((uint32_t)bits + 31) >> 5;
+            uint32_t* o = s_out + (off >> 5);
+            for (uint32_t i = 0; i < nwb; i++) {
+                const uint32_t w = slot_word(t, i);
+                atomicOr(o + i, w >> sh);
+                if (sh) atomicOr(o + i + 1, w << (32 - sh));
+            }
+        }
+        __syncthreads();
+        for (uint32_t j = t; j < nwords; j += CHUNK_BLOCKS) {
+            const uint32_t w = s_out[j];
+            dst[j] = w;
+            uint64_t x = ((uint64_t)w << 32) | s_out[j + 1];
+            x &= x << 1;
+            x &= x << 2;
+            x &= x << 4;
+            const uint32_t r = (uint32_t)(x >> 32);  // bit 31-d: a run starts at chunk bit 32j+d
+            if (r) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int n = __popc(r & (0x80808080u >> k));
+                    if (n) atomicAdd(&s_ffa[k], (uint32_t)n);
+                }
+            }
+        }
+        __syncthreads();  // s_ffa complete
+        if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = s_ffa[t];
+        if (t == 0) D.chunk_bits[cur][chunk] = total;
+        return;
+    }
+
+    // ---- 3. (long chunks) 0xFF candidates: every run of eight 1-bits that starts in this
     // block, binned by chunk-local start position mod 8 (s_ffa) - the chunk's
     // 0xFF-byte count for each alignment k_scan may place it at.  Runs may
     // reach into the following blocks (their first <= 8 bits); nothing
@@ -870,7 +922,6 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     }
 
     // ---- 4. gather the chunk's words
-    GAS uint32_t* dst = gp(D.scratch[cur] + (size_t)chunk * CHUNK_WORDS);
     for (uint32_t j = (off + 31) >> 5; ICX_HUFF_EXP != 6 && j * 32 < off + bits; j++) {  // EXP 6: no gather
         uint32_t outw = 0;
         int have = 0, u = t;
