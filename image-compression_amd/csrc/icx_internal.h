@@ -52,10 +52,11 @@ struct QNode {
     int32_t pad;
     // Quantiser of zig-zag coefficient k, table c ([0]=lum [1]=chroma), for the
     // divisor d = q<<3 (jcdctmgr.c: |c| -> (|c| + d/2) / d, truncating):
-    float thr[2][64];      // d - d/2: the quotient is nonzero iff |c| >= thr
-    float frcp[2][64];     // fl(1/d)
-    float fbias[2][64];    // fl((d/2 + 0.5) * frcp): floor(fma(|c|, frcp, fbias)) is
-                           // the quotient exactly for |c| < 2^15 (error << 0.5/d)
+    // per (component, k): x = thr = d - d/2 (the quotient is nonzero iff
+    // |c| >= thr), y = fl(1/d), z = fl((d/2 + 0.5) * y): floor(fma(|c|, y, z))
+    // is the quotient exactly for |c| < 2^15 (error << 0.5/d); w unused.
+    // Interleaved so the trial kernel loads one 16-B entry per index.
+    float4 qf[2][64];
     uint16_t qt[2][64];    // quantisation tables, natural order (DQT payload)
 };
 

@@ -312,7 +312,7 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
     uint8_t* s_len = &cds[0][0][0];                  // phase E list lengths (cds is dead after phase C)
     uint16_t* s_off = (uint16_t*)&cds[0][0][FDC_BLK];  // phase E packed list offsets
     const QNode& CN = nodes[D.cand_node];
-    const float thr[2] = {(t & 63) ? CN.thr[0][t & 63] : -1.0f, (t & 63) ? CN.thr[1][t & 63] : -1.0f};
+    const float thr[2] = {(t & 63) ? CN.qf[0][t & 63].x : -1.0f, (t & 63) ? CN.qf[1][t & 63].x : -1.0f};
 
     // ---- B: YCbCr, two Y row-DCTs, h2v2_downsample of this thread's 2x8 chroma
     {
@@ -519,7 +519,7 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
     __syncthreads();
     const int nblk = min(16, D.mcux - tx * 16);
     const uint32_t bbase = (uint32_t)by * D.mcux + tx * 16;
-    const float thr[2] = {(t & 63) ? nodes[D.cand_node].thr[0][t & 63] : -1.0f, 0.0f};
+    const float thr[2] = {(t & 63) ? nodes[D.cand_node].qf[0][t & 63].x : -1.0f, 0.0f};
     const int64_t base = (int64_t)tile * (16 * COEF_SLOTS);
     emit_lists<16, 4, false>(D, base, nblk, oz, stg, s_len, s_off, thr, (unsigned long long*)&states[img].list_entries,
                       [](int, int, int c) { return c; }, [](int) { return true; });
@@ -746,7 +746,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
 
     if (t < 128) {
         const int c = t >> 6, k = t & 63;
-        s_qf[c][k] = make_float4(N.thr[c][k], N.frcp[c][k], N.fbias[c][k], 0.0f);
+        s_qf[c][k] = N.qf[c][k];
     }
     // AC codes pre-shifted for their (run, size) slot: (code << size, len + size)
     for (int i = t; i < 2 * AC_ENTRIES; i += CHUNK_BLOCKS) (&s_ac[0][0])[i] = (&c_acx[0][0])[i];
@@ -760,7 +760,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     int tb = 0;
     int64_t pb;
     if (D.ncomp == 3) {
-        const uint32_t k6 = (uint32_t)(b % 6);
+        const uint32_t k6 = ((uint32_t)(chunk % 3) * 4u + (uint32_t)t) % 6u;  // b % 6, b0 = 256 chunk
         tb = k6 >= 4;
         if (k6 >= 1 && k6 <= 3) pb = b - 1;
         else if (k6 == 0) pb = b >= 6 ? b - 3 : -1;

@@ -112,9 +112,7 @@ void make_node(float q, QNode& n)
             const uint32_t div = (uint32_t)t[c][kZigzag[k]] << 3;
             volatile float r = 1.0f / (float)div;
             volatile float b = ((float)(div >> 1) + 0.5f) * r;
-            n.thr[c][k] = (float)(div - (div >> 1));
-            n.frcp[c][k] = r;
-            n.fbias[c][k] = b;
+            n.qf[c][k] = make_float4((float)(div - (div >> 1)), r, b, 0.0f);
         }
         for (int i = 0; i < 64; i++) n.qt[c][i] = t[c][i];
     }
@@ -602,7 +600,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                     todo.pop_back();
                     for (int c = 0; c < 2; c++)
                         for (int z = 0; z < 64; z++)
-                            cn.thr[c][z] = first ? B.nodes[n].thr[c][z] : std::min(cn.thr[c][z], B.nodes[n].thr[c][z]);
+                            cn.qf[c][z].x = first ? B.nodes[n].qf[c][z].x : std::min(cn.qf[c][z].x, B.nodes[n].qf[c][z].x);
                     first = false;
                     if (B.nodes[n].child_fit >= 0) todo.push_back(B.nodes[n].child_fit);
                     if (B.nodes[n].child_nofit >= 0) todo.push_back(B.nodes[n].child_nofit);
