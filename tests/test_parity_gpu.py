@@ -204,3 +204,30 @@ def test_invalid_inputs(codec):
     bad = N.Image(img.ctypes.data, 0, 4, 12, N.BGR24)
     assert lib.icx_compress_jpg_to_stream(codec._ctx, ctypes.byref(bad), 0.5, buf.ctypes.data, 10,
                                           ctypes.byref(n)) == N.E_INVALID
+
+
+def test_candidate_lists_mixed_batch(codec, oracle):
+    """One batch whose images reach different quality sets (different cached
+    probes, stale and fresh, none; colour and grey; partial FDCT tiles), so
+    every image gets its own candidate filter: results equal the oracle's."""
+    rng = np.random.default_rng(17)
+    cached_choices = [None, (0.9, 1.0), (0.05, 1.0), (1.0, 1.0), (0.3, 0.85), (0.2, 1.0)]
+    imgs, cached = [], []
+    for i in range(12):
+        h, w = int(rng.integers(9, 360)), int(rng.integers(9, 420))
+        img = smooth(h, w, 100 + i) if i % 3 else noise(h, w, 200 + i)
+        if i % 4 == 3:
+            img = img[:, :, 1].copy()
+        imgs.append(img)
+        cached.append(cached_choices[i % len(cached_choices)])
+    for target, q0 in ((6000, 0.25), (25000, 0.8)):
+        res = codec.fit(imgs, target, q0,
+                        cached=[icx.LearnedParams(*c) if c else None for c in cached])
+        for i, (img, r) in enumerate(zip(imgs, res)):
+            o = oracle.fit(img, target, q0, cached=cached[i])
+            assert r["status"] == N.OK
+            assert (r["success"], r["cache_hit"]) == (o["success"], o["cache_hit"]), (i, target)
+            if o["success"]:
+                assert r["data"] == o["data"], (i, target)
+                assert np.float32(r["learned"].quality) == np.float32(o["quality"])
+                assert r["learned"].scale == o["scale"]
