@@ -230,7 +230,7 @@ inline icx_status upload(icx_ctx* c, void* dst, const void* src, size_t n)
 struct Uploader {
     icx_ctx* c;
     uint8_t *h = nullptr, *d = nullptr;
-    size_t cap = 0, used = 0;
+    size_t cap = 0, used = 0, flushed = 0;
     bool overflow = false;
     Uploader(icx_ctx* ctx, size_t bytes) : c(ctx), cap(bytes)
     {
@@ -263,11 +263,13 @@ struct Uploader {
     // Bytes to reserve for `count` objects of T (with the 64-byte alignment).
     template <class T>
     static size_t need(size_t count) { return align_up(sizeof(T) * count, 64); }
+    // Copies what was put since the last flush (one copy); puts may follow.
     icx_status flush()
     {
         if (overflow) return fail(c, ICX_E_NOMEM, "upload staging exhausted");
-        if (!used) return ICX_OK;
-        hipError_t e = hipMemcpyAsync(d, h, used, hipMemcpyHostToDevice, c->stream);
+        if (used == flushed) return ICX_OK;
+        hipError_t e = hipMemcpyAsync(d + flushed, h + flushed, used - flushed, hipMemcpyHostToDevice, c->stream);
+        flushed = used;
         return e == hipSuccess ? ICX_OK : hip_fail(c, e, "hipMemcpyAsync(H2D)");
     }
 };

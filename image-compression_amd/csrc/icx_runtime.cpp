@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -215,6 +216,9 @@ struct Batch {
     std::vector<ImgDesc> desc;
     std::vector<ImgState> state;
     ImgState* h_state = nullptr;  // pinned mirror for downloads
+    // The stage's small uploads (descriptors, states, launch plans) share one
+    // pinned block and go in one copy per launch group (flush before launches).
+    std::unique_ptr<Uploader> up;
 };
 
 struct DPlan {
@@ -226,20 +230,25 @@ struct DPlan {
 // Build a launch plan over `ids` with per-image work counts.
 icx_status make_plan(Batch& B, const std::vector<int>& ids, const std::vector<int64_t>& counts, DPlan& out)
 {
-    icx_ctx* c = B.c;
     std::vector<int64_t> pre(ids.size() + 1, 0);
     for (size_t i = 0; i < ids.size(); i++) pre[i + 1] = pre[i] + counts[i];
-    int32_t* d_ids = (int32_t*)c->dev.take(ids.size() * sizeof(int32_t) + 4);
-    int64_t* d_pre = (int64_t*)c->dev.take(pre.size() * sizeof(int64_t));
     std::vector<int32_t> ids32(ids.begin(), ids.end());
-    icx_status s;
-    if (!ids32.empty() && (s = upload(c, d_ids, ids32.data(), ids32.size() * 4))) return s;
-    if ((s = upload(c, d_pre, pre.data(), pre.size() * 8))) return s;
-    out.p.ids = d_ids;
-    out.p.prefix = d_pre;
+    ids32.push_back(0);
+    out.p.ids = B.up->put(ids32.data(), ids32.size());
+    out.p.prefix = B.up->put(pre.data(), pre.size());
     out.p.m = (int32_t)ids.size();
     out.total = pre.back();
-    return ICX_OK;
+    return B.up->overflow ? fail(B.c, ICX_E_NOMEM, "upload staging exhausted") : ICX_OK;
+}
+
+// A new stage: descriptors and states go into a fresh upload block (with room
+// for the stage's launch plans); the copy happens at the first launch.
+void new_stage(Batch& B)
+{
+    const size_t m = B.desc.size();
+    const size_t bytes = Uploader::need<ImgDesc>(m) + Uploader::need<ImgState>(m) +
+                         12 * (Uploader::need<int32_t>(m + 1) + Uploader::need<int64_t>(m + 1));
+    B.up.reset(new Uploader(B.c, bytes));
 }
 
 icx_status sync_states(Batch& B)
@@ -257,9 +266,10 @@ icx_status sync_states(Batch& B)
 
 icx_status push_desc_state(Batch& B)
 {
-    icx_status s = upload(B.c, B.d_desc, B.desc.data(), sizeof(ImgDesc) * B.desc.size());
-    if (s) return s;
-    return upload(B.c, B.d_state, B.state.data(), sizeof(ImgState) * B.state.size());
+    new_stage(B);
+    B.d_desc = B.up->put(B.desc.data(), B.desc.size());
+    B.d_state = B.up->put(B.state.data(), B.state.size());
+    return B.up->overflow ? fail(B.c, ICX_E_NOMEM, "upload staging exhausted") : ICX_OK;
 }
 
 // Point image i's descriptor at its pixels for `scale` (resizing on device).
@@ -319,6 +329,7 @@ icx_status run_fdct(Batch& B, const std::vector<int>& ids)
         if (s) return s;
         int64_t px = 0;
         for (int i : sel) px += (int64_t)B.desc[i].w * B.desc[i].h;
+        if ((s = B.up->flush())) return s;
         Timed tm(B.c, "fdct", px);
         launch_fdct(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, kind, B.c->stream);
     }
@@ -362,7 +373,7 @@ icx_status run_trials(Batch& B, const std::vector<int>& ids, int depth)
     for (int i : ids) cnt.push_back(B.desc[i].nchunks);
     DPlan P;
     icx_status s = make_plan(B, ids, cnt, P);
-    if (s) return s;
+    if (s || (s = B.up->flush())) return s;
     icx_ctx* c = B.c;
     for (int t = 0; t < depth; t++) {
         { Timed tm(c, "huff", 0); launch_huff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
@@ -378,7 +389,7 @@ icx_status run_final(Batch& B, const std::vector<int>& ids)
     for (int i : ids) cnt.push_back(B.desc[i].nchunks);
     DPlan P;
     icx_status s = make_plan(B, ids, cnt, P);
-    if (s) return s;
+    if (s || (s = B.up->flush())) return s;
     icx_ctx* c = B.c;
     { Timed tm(c, "ffscan", (int64_t)ids.size()); launch_ffscan(B.d_desc, B.d_state, P.p, c->stream); }
     { Timed tm(c, "stuff", P.total); launch_stuff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
@@ -611,8 +622,6 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             B.desc[k].cand_node = f->second;
             I.orig.cand_node = f->second;
         }
-        B.d_desc = (ImgDesc*)c->dev.take(sizeof(ImgDesc) * m);
-        B.d_state = (ImgState*)c->dev.take(sizeof(ImgState) * m);
         B.d_nodes = (QNode*)c->dev.take(sizeof(QNode) * B.nodes.size());
         B.h_state = (ImgState*)c->host.take(sizeof(ImgState) * m);
         if (!B.h_state) return fail(c, ICX_E_NOMEM, "pinned staging exhausted");
