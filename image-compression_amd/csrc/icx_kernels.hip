@@ -553,7 +553,10 @@ constexpr int SLOT_BITS = SLOT_WORDS * 32;
 constexpr int AC_SIZES_ = 11;
 constexpr int TAB_WORDS = 2 * 16 * AC_SIZES_ * 2 + 2 * 64 * 4 + 2 * 16;  // s_ac + s_qf + s_dc
 constexpr int OUT_WORDS = 1024;  // chunk streams up to this many words are assembled in LDS
-static_assert(OUT_WORDS + 8 <= TAB_WORDS, "assembled stream must fit in the table LDS");
+// 0xFF alignment bins of the assembled path: FF_COPIES copies per bin (lane
+// mod FF_COPIES picks one), so the LDS atomics of a wave rarely collide.
+constexpr int FF_COPIES = 16;
+static_assert(OUT_WORDS + 8 + 8 * FF_COPIES <= TAB_WORDS, "assembled stream must fit in the table LDS");
 constexpr int AC_SIZES = 11;                // AC magnitude categories 0..10 (8-bit JPEG)
 constexpr int AC_ENTRIES = 16 * AC_SIZES;   // (run, size) slots per table
 
@@ -580,6 +583,14 @@ struct LdsSink {
         if (n) *(uint32_t*)((char*)slots + min(wb, wlast)) = (uint32_t)(acc << (32 - n));
     }
 };
+
+#if ICX_HUFF_EXP == 7
+__device__ unsigned long long g_stats[6];
+extern "C" int icx_debug_huff_stats(unsigned long long* out)
+{
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), sizeof(g_stats));
+}
+#endif
 
 struct CountSink {  // timing experiments only (ICX_HUFF_EXP == 2)
     int n;
@@ -740,6 +751,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     const int cur = S.cur;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
 #if ICX_HUFF_EXP == 4  // timing only: launch + descriptor lookup, nothing else
+    if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = 0u;  // sizes stay consistent
     if (t == 0) D.chunk_bits[cur][chunk] = 0u;
     return;
 #endif
@@ -785,6 +797,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     // ---- 1. encode_one_block into the slot (rarely: into the block's HBM spill)
     int bits = 0;
 #if ICX_HUFF_EXP == 3  // timing only: front (tables, list loads, DC exchange), no coding
+    if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = 0u;  // sizes stay consistent
     if (t == 0) D.chunk_bits[cur][chunk] = (uint32_t)(ev[0] + ev[PRE - 1] + qprev) & 1u;
     return;
 #endif
@@ -794,6 +807,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         encode_block(cs, ev, lst, cnt, dq - qprev, s_qf[tb], s_ac[tb], s_dc[tb]);
         bits = cs.n;
     }
+    if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = 0u;  // sizes stay consistent
     if (t == 0) D.chunk_bits[cur][chunk] = (uint32_t)bits;
     return;
 #endif
@@ -812,7 +826,56 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         }
     }
 
+#if ICX_HUFF_EXP == 7  // statistics only: list entries, wave-max lengths, entries that code
+    {
+        int nz = 0;
+        for (int i = 1; i < cnt; i++) {
+            const uint32_t e = lst[i];
+            nz += fabsf((float)((int32_t)e >> 6)) >= s_qf[tb][e & 63].x;
+        }
+        int mx = cnt, sm = cnt, sz = nz, nv = valid;
+        for (int d = 32; d >= 1; d >>= 1) {
+            mx = max(mx, __shfl_xor(mx, d, 64));
+            sm += __shfl_xor(sm, d, 64);
+            sz += __shfl_xor(sz, d, 64);
+            nv += __shfl_xor(nv, d, 64);
+        }
+        __shared__ uint8_t s_c[CHUNK_BLOCKS];
+        __shared__ uint8_t s_l[CHUNK_BLOCKS];
+        s_c[t] = (uint8_t)cnt;
+        s_l[t] = (uint8_t)(tb == 0);
+        __syncthreads();
+        if (t == 0) {
+            int h[65] = {0};
+            for (int i = 0; i < CHUNK_BLOCKS; i++) h[s_c[i]]++;
+            unsigned long long sorted = 0;  // descending: maxima at positions 0, 64, 128, 192
+            int pos = 0;
+            for (int v = 64; v >= 0; v--)
+                for (int k = 0; k < h[v]; k++, pos++)
+                    if ((pos & 63) == 0) sorted += 64ull * v;
+            unsigned long long split = 0;  // luma blocks first, then chroma, in block order
+            int mxw = 0;
+            pos = 0;
+            for (int pass = 1; pass >= 0; pass--)
+                for (int i = 0; i < CHUNK_BLOCKS; i++)
+                    if (s_l[i] == pass) {
+                        mxw = max(mxw, (int)s_c[i]);
+                        if ((++pos & 63) == 0) { split += 64ull * mxw; mxw = 0; }
+                    }
+            split += 64ull * mxw;
+            atomicAdd(&g_stats[4], sorted);
+            atomicAdd(&g_stats[5], split);
+        }
+        if (lane == 0) {
+            atomicAdd(&g_stats[0], (unsigned long long)sm);
+            atomicAdd(&g_stats[1], (unsigned long long)(64 * mx));
+            atomicAdd(&g_stats[2], (unsigned long long)sz);
+            atomicAdd(&g_stats[3], (unsigned long long)nv);
+        }
+    }
+#endif
 #if ICX_HUFF_EXP == 1  // timing only: encode, nothing after
+    if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = 0u;  // sizes stay consistent
     if (t == 0) D.chunk_bits[cur][chunk] = (uint32_t)bits;
     return;
 #endif
@@ -850,7 +913,13 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         // position mod 8 (s_ffa): the chunk's 0xFF-byte count for each
         // alignment k_scan may place it at.
         const uint32_t nwords = (total + 31) >> 5;
-        for (uint32_t i = t; i < OUT_WORDS + 8; i += CHUNK_BLOCKS) s_out[i] = 0u;
+#if ICX_HUFF_EXP == 8  // timing only: up to the scan (sizes stay consistent: no 0xFF)
+        if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = 0u;
+        if (t == 0) D.chunk_bits[cur][chunk] = total;
+        return;
+#endif
+        uint32_t* const s_bin = s_out + OUT_WORDS + 8;  // [8][FF_COPIES] bins, one copy per lane mod 16
+        for (uint32_t i = t; i < OUT_WORDS + 8 + 8 * FF_COPIES; i += CHUNK_BLOCKS) s_out[i] = 0u;
         __syncthreads();
         if (bits > 0) {
             const uint32_t sh = off & 31, nwb = ((uint32_t)bits + 31) >> 5;
@@ -862,9 +931,17 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
             }
         }
         __syncthreads();
+#if ICX_HUFF_EXP == 9  // timing only: up to the LDS assembly (sizes stay consistent)
+        if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = s_out[t] == 0xDEADBEEFu;
+        if (t == 0) D.chunk_bits[cur][chunk] = total;
+        return;
+#endif
         for (uint32_t j = t; j < nwords; j += CHUNK_BLOCKS) {
             const uint32_t w = s_out[j];
             dst[j] = w;
+#if ICX_HUFF_EXP == 10  // timing only: no 0xFF bins
+            continue;
+#endif
             uint64_t x = ((uint64_t)w << 32) | s_out[j + 1];
             x &= x << 1;
             x &= x << 2;
@@ -874,12 +951,17 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
                     const int n = __popc(r & (0x80808080u >> k));
-                    if (n) atomicAdd(&s_ffa[k], (uint32_t)n);
+                    if (n) atomicAdd(&s_bin[k * FF_COPIES + (lane & (FF_COPIES - 1))], (uint32_t)n);
                 }
             }
         }
-        __syncthreads();  // s_ffa complete
-        if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = s_ffa[t];
+        __syncthreads();  // bins complete
+        if (t < 8) {
+            uint32_t n = 0;
+#pragma unroll
+            for (int i = 0; i < FF_COPIES; i++) n += s_bin[t * FF_COPIES + i];
+            D.chunk_ffa[cur][chunk * 8 + t] = n;
+        }
         if (t == 0) D.chunk_bits[cur][chunk] = total;
         return;
     }

@@ -32,5 +32,15 @@ for _ in range(2):
     codec.fit(frames, target, bench.Q0, cached=cached, outputs=outs)
 torch.cuda.synchronize()
 res = {k: codec.profile_query(k) for k in ("fdct", "huff", "scan", "decide", "ffscan", "stuff")}
-print(json.dumps({"lib": os.path.basename(os.environ.get("ICX_LIB", "libicx.so")), "images": n, "kind": kind,
+stats = None
+if os.environ.get("ICX_STATS"):  # ICX_HUFF_EXP=7 build: list statistics over all trials
+    import ctypes
+    lib = ctypes.CDLL(os.environ["ICX_LIB"])
+    buf = (ctypes.c_ulonglong * 6)()
+    lib.icx_debug_huff_stats(buf)
+    ent, wave_slots, nz, blocks, srt, split = list(buf)
+    stats = {"entries_per_block": ent / blocks, "wave_max_per_block": wave_slots / blocks,
+             "lane_efficiency": ent / wave_slots, "coded_ac_per_block": nz / blocks, "block_trials": blocks,
+             "lane_eff_sorted": ent / srt, "lane_eff_luma_chroma_split": ent / split}
+print(json.dumps({"stats": stats, "lib": os.path.basename(os.environ.get("ICX_LIB", "libicx.so")), "images": n, "kind": kind,
                   "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k, v in res.items()}}))
