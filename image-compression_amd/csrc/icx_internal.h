@@ -81,6 +81,8 @@ struct ImgDesc {
     uint64_t cap;
 };
 
+constexpr int ENT_SLOTS = 16;
+
 struct ImgState {
     int32_t node;          // node of the pending trial, -1 = none
     int32_t best_node;     // node of the best fitting trial, -1 = none
@@ -93,7 +95,9 @@ struct ImgState {
     int64_t best_size;
     int64_t out_len;
     uint64_t total_bits[2];
-    uint64_t list_entries; // candidate-list entries the last FDCT wrote (padded; algorithmic bytes)
+    // candidate-list entries the last FDCT wrote (padded; algorithmic bytes),
+    // spread over ENT_SLOTS counters so the FDCT waves' atomics rarely collide
+    uint64_t list_entries[ENT_SLOTS];
     uint32_t ff_total[2];
     float trial_q[MAX_TRIALS + 1];
     int64_t trial_size[MAX_TRIALS + 1];

@@ -283,7 +283,8 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
         total += run;
         __builtin_amdgcn_wave_barrier();
     }
-    if (lane == 0 && total) atomicAdd(ent, (unsigned long long)total);
+    if (ICX_FDCT_EXP != 2 && lane == 0 && total)  // EXP 2: timing only
+        atomicAdd(ent + ((blockIdx.x * 4 + wave) & (ENT_SLOTS - 1)), (unsigned long long)total);
 }
 
 // After the barrier that ends emit_lists: lengths and 16-B-unit offsets.
@@ -419,7 +420,7 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
     if (true) { __syncthreads(); return; }
 #endif
     const int64_t base = tile_id * (FDC_BLK * COEF_SLOTS);
-    unsigned long long* ent = (unsigned long long*)&states[T.img].list_entries;
+    unsigned long long* ent = (unsigned long long*)states[T.img].list_entries;
     auto luma = [](int a) { return a < 4; };  // one MCU per step: Y0 Y1 Y2 Y3 Cb Cr
     if (plain)  // interior tile: no dummy blocks
         emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, stg, s_len, s_off, thr, ent,
@@ -521,7 +522,7 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
     const uint32_t bbase = (uint32_t)by * D.mcux + tx * 16;
     const float thr[2] = {(t & 63) ? nodes[D.cand_node].qf[0][t & 63].x : -1.0f, 0.0f};
     const int64_t base = (int64_t)tile * (16 * COEF_SLOTS);
-    emit_lists<16, 4, false>(D, base, nblk, oz, stg, s_len, s_off, thr, (unsigned long long*)&states[img].list_entries,
+    emit_lists<16, 4, false>(D, base, nblk, oz, stg, s_len, s_off, thr, (unsigned long long*)states[img].list_entries,
                       [](int, int, int c) { return c; }, [](int) { return true; });
     __syncthreads();
     store_list_meta(D, base, bbase, nblk, s_len, s_off);
@@ -738,7 +739,6 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     __shared__ uint32_t s_bits[CHUNK_BLOCKS];
     int32_t* const s_dcq = (int32_t*)s_bits;  // DC exchange; dead before s_bits is written
     __shared__ uint32_t s_wsum[CHUNK_BLOCKS / 64];
-    __shared__ uint32_t s_ffa[8];
 
     const int64_t item = blockIdx.x;
     const int slot = find_slot(prefix, m, item);
@@ -763,7 +763,6 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     // AC codes pre-shifted for their (run, size) slot: (code << size, len + size)
     for (int i = t; i < 2 * AC_ENTRIES; i += CHUNK_BLOCKS) (&s_ac[0][0])[i] = (&c_acx[0][0])[i];
     if (t < 32) s_dc[t >> 4][t & 15] = c_dc[t >> 4][t & 15];
-    if (t < 8) s_ffa[t] = 0;
 
     const int64_t b0 = (int64_t)chunk * CHUNK_BLOCKS;
     const int nb = (int)min((int64_t)CHUNK_BLOCKS, D.nblocks - b0);
@@ -896,6 +895,11 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     }
     s_off[t] = off;
     s_bits[t] = bits;
+    // 0xFF alignment bins, [8][FF_COPIES] over the dead tables (past the
+    // assembled stream): FF_COPIES copies per bin, picked by lane, so that the
+    // LDS atomics of a wave rarely collide on one address
+    uint32_t* const s_bin = s_tab + OUT_WORDS + 8;
+    if (total > (uint32_t)OUT_WORDS * 32 && t < 8 * FF_COPIES) s_bin[t] = 0u;
     __syncthreads();
 
     const GAS uint32_t* spill0 = gp(D.ovf + b0 * BLOCK_WORDS);
@@ -910,7 +914,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         // stored once (coalesced) and the runs of eight 1-bits starting in it
         // (with the next word's first 7 bits; zeros past the chunk's last bit,
         // k_scan checks the boundary bytes) are binned by chunk-local start
-        // position mod 8 (s_ffa): the chunk's 0xFF-byte count for each
+        // position mod 8 (s_bin): the chunk's 0xFF-byte count for each
         // alignment k_scan may place it at.
         const uint32_t nwords = (total + 31) >> 5;
 #if ICX_HUFF_EXP == 8  // timing only: up to the scan (sizes stay consistent: no 0xFF)
@@ -918,7 +922,6 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         if (t == 0) D.chunk_bits[cur][chunk] = total;
         return;
 #endif
-        uint32_t* const s_bin = s_out + OUT_WORDS + 8;  // [8][FF_COPIES] bins, one copy per lane mod 16
         for (uint32_t i = t; i < OUT_WORDS + 8 + 8 * FF_COPIES; i += CHUNK_BLOCKS) s_out[i] = 0u;
         __syncthreads();
         if (bits > 0) {
@@ -967,7 +970,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     }
 
     // ---- 3. (long chunks) 0xFF candidates: every run of eight 1-bits that starts in this
-    // block, binned by chunk-local start position mod 8 (s_ffa) - the chunk's
+    // block, binned by chunk-local start position mod 8 (s_bin) - the chunk's
     // 0xFF-byte count for each alignment k_scan may place it at.  Runs may
     // reach into the following blocks (their first <= 8 bits); nothing
     // follows the chunk's last bit here (k_scan checks the boundary bytes).
@@ -996,7 +999,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
                     const int n = __popc(r & (0x80808080u >> k));
-                    if (n) atomicAdd(&s_ffa[(off + k) & 7], (uint32_t)n);
+                    if (n) atomicAdd(&s_bin[((off + k) & 7) * FF_COPIES + (lane & (FF_COPIES - 1))], (uint32_t)n);
                 }
             }
             cw = nx;
@@ -1022,8 +1025,13 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         }
         dst[j] = outw;
     }
-    __syncthreads();  // s_ffa complete
-    if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = s_ffa[t];
+    __syncthreads();  // bins complete
+    if (t < 8) {
+        uint32_t n = 0;
+#pragma unroll
+        for (int i = 0; i < FF_COPIES; i++) n += s_bin[t * FF_COPIES + i];
+        D.chunk_ffa[cur][chunk * 8 + t] = n;
+    }
     if (t == 0) D.chunk_bits[cur][chunk] = total;
 }
 

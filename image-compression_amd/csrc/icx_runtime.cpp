@@ -344,7 +344,9 @@ void credit_fdct(Batch& B, const std::vector<int>& ids)
     int64_t bytes = 0;
     for (int i : ids) {
         const ImgDesc& d = B.desc[i];
-        B.it[i].entries = (int64_t)B.state[i].list_entries;
+        int64_t e = 0;
+        for (int k = 0; k < ENT_SLOTS; k++) e += (int64_t)B.state[i].list_entries[k];
+        B.it[i].entries = e;
         bytes += (int64_t)d.w * d.h * B.it[i].nch + 4 * B.it[i].entries + 5 * d.nblocks;
     }
     if (B.c->prof) B.c->stats["fdct.bytes"].units += bytes;
