@@ -62,9 +62,22 @@ __device__ __forceinline__ void st8(void* p, int2 v)
     w.y = v.y;
     *(GAS i32x2_t*)p = w;
 }
+// Launch slot of work item `item` (prefix = exclusive item counts per slot,
+// prefix[m] = total).  A proportional guess first - exact when the slots hold
+// equally many items, as for a batch of same-sized frames: two dependent loads
+// instead of log2(m) - then a binary search of what the guess left open.
 __device__ __forceinline__ int find_slot(const int64_t* prefix, int m, int64_t item)
 {
     int lo = 0, hi = m;  // prefix[lo] <= item < prefix[hi]
+#if !ICX_PLAIN_SLOT_SEARCH
+    const int g = min(max((int)(((float)item + 0.5f) * ((float)m / (float)prefix[m])), 0), m - 1);
+    if (prefix[g] <= item) {
+        lo = g;
+        if (item < prefix[g + 1]) return g;
+    } else {
+        hi = g;
+    }
+#endif
     while (hi - lo > 1) {
         int mid = (lo + hi) >> 1;
         if (prefix[mid] <= item) lo = mid; else hi = mid;
