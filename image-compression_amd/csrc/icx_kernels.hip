@@ -1223,6 +1223,8 @@ __global__ __launch_bounds__(1024) void k_ffscan(const ImgDesc* __restrict__ des
 // of the bytes the chunk owns (first bit inside it), EOI (last chunk), written
 // straight into the caller's output buffer: 256 source bytes per step are
 // stuffed into the wave's LDS stage and leave as aligned dwords.
+constexpr int STUFF_BATCH = 8;  // 256-byte pieces whose source loads k_stuff issues together
+
 __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs, const ImgState* __restrict__ states,
                                                const QNode* __restrict__ nodes, const int32_t* __restrict__ ids,
                                                const int64_t* __restrict__ prefix, int m)
@@ -1261,53 +1263,76 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
     }
     const uint64_t bb = (off[c] + 7) >> 3;                 // owned bytes [bb, be)
     const uint64_t be = min((off[c + 1] + 7) >> 3, nbytes);
+    const uint64_t start = off[c], end = off[c + 1];
+    const GAS uint32_t* cs = gp(D.scratch[buf]) + (size_t)c * CHUNK_WORDS;
     uint64_t run = D.chunk_ffoff[c];
     uint32_t* stw = s_stg[threadIdx.x >> 6];                 // this wave's stage
     uint8_t* stb = (uint8_t*)stw;
-    for (uint64_t q0 = bb; q0 < be; q0 += 256) {
-        // 1. four source bytes per lane, each 0xFF followed by a stuffed 0x00,
-        //    laid out back to back in the wave's LDS stage
-        const uint64_t q = q0 + 4 * lane;                    // this lane: bytes q..q+3
-        const int nv = q < be ? (int)min((uint64_t)4, be - q) : 0;
-        uint32_t v = 0;
-        int nout = nv;
-        if (nv) {
-            v = stream_bits(gp(D.scratch[buf]), off, D.nchunks, c, q * 8);
+    for (uint64_t qb = bb; qb < be; qb += 256 * STUFF_BATCH) {
+        // 0. the source words of up to STUFF_BATCH pieces, all loads in flight
+        //    at once (one latency per batch, not per piece)
+        uint32_t w0[STUFF_BATCH], w1[STUFF_BATCH];
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-                if (j < nv && ((v >> (24 - 8 * j)) & 255) == 255) nout++;
-        }
-        int incl = nout;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int y = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += y;
-        }
-        const int len = __shfl(incl, 63, 64);               // stuffed bytes of this piece
-        int p = incl - nout;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (j < nv) {
-                const uint8_t byte = (uint8_t)(v >> (24 - 8 * j));
-                stb[p++] = byte;
-                if (byte == 0xFF) stb[p++] = 0;
+        for (int it = 0; it < STUFF_BATCH; it++) {
+            const uint64_t q = qb + 256 * it + 4 * lane;
+            w0[it] = w1[it] = 0u;
+            if (q < be) {
+                const uint32_t lw = (uint32_t)((q * 8 - start) >> 5);
+                w0[it] = cs[lw];
+                w1[it] = cs[min(lw + 1, (uint32_t)CHUNK_WORDS - 1)];
             }
         }
-        __builtin_amdgcn_wave_barrier();
-        // 2. the piece leaves as aligned dword stores plus at most 3 + 3 byte
-        //    stores at its ends (neighbouring chunks own the bytes around it)
-        const uint64_t g = (uint64_t)hdr + q0 + run;         // output offset of the piece
-        const int head = min((int)((4 - (((uintptr_t)D.out + g) & 3)) & 3), len);  // to a 4-B boundary
-        const int nd = (len - head) >> 2, tail = len - head - 4 * nd;
-        if (lane < head) out[g + lane] = stb[lane];
-        if (lane < tail) out[g + head + 4 * nd + lane] = stb[head + 4 * nd + lane];
-        GAS uint32_t* od = (GAS uint32_t*)(out + g + head);
-        for (int i = lane; i < nd; i += 64) {
-            const int s = head + 4 * i;
-            od[i] = __builtin_amdgcn_alignbyte(stw[(s >> 2) + 1], stw[s >> 2], (uint32_t)(s & 3));
+#pragma unroll
+        for (int it = 0; it < STUFF_BATCH; it++) {
+            const uint64_t q0 = qb + 256 * it;
+            if (q0 >= be) break;  // wave-uniform
+            // 1. four source bytes per lane, each 0xFF followed by a stuffed
+            //    0x00, laid out back to back in the wave's LDS stage
+            const uint64_t q = q0 + 4 * lane;                // this lane: bytes q..q+3
+            const int nv = q < be ? (int)min((uint64_t)4, be - q) : 0;
+            uint32_t v = 0;
+            int nout = nv;
+            if (nv) {
+                const uint32_t sh = (uint32_t)((q * 8 - start) & 31);
+                v = sh ? __builtin_amdgcn_alignbit(w0[it], w1[it], 32 - sh) : w0[it];
+                if (end - q * 8 < 32)  // the chunk's last bits: next chunk / padding
+                    v = stream_bits(gp(D.scratch[buf]), off, D.nchunks, c, q * 8);
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (j < nv && ((v >> (24 - 8 * j)) & 255) == 255) nout++;
+            }
+            int incl = nout;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int y = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += y;
+            }
+            const int len = __shfl(incl, 63, 64);           // stuffed bytes of this piece
+            int p = incl - nout;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (j < nv) {
+                    const uint8_t byte = (uint8_t)(v >> (24 - 8 * j));
+                    stb[p++] = byte;
+                    if (byte == 0xFF) stb[p++] = 0;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            // 2. the piece leaves as aligned dword stores plus at most 3 + 3
+            //    byte stores at its ends (neighbouring chunks own the bytes around it)
+            const uint64_t g = (uint64_t)hdr + q0 + run;     // output offset of the piece
+            const int head = min((int)((4 - (((uintptr_t)D.out + g) & 3)) & 3), len);  // to a 4-B boundary
+            const int nd = (len - head) >> 2, tail = len - head - 4 * nd;
+            if (lane < head) out[g + lane] = stb[lane];
+            if (lane < tail) out[g + head + 4 * nd + lane] = stb[head + 4 * nd + lane];
+            GAS uint32_t* od = (GAS uint32_t*)(out + g + head);
+            for (int i = lane; i < nd; i += 64) {
+                const int s = head + 4 * i;
+                od[i] = __builtin_amdgcn_alignbyte(stw[(s >> 2) + 1], stw[s >> 2], (uint32_t)(s & 3));
+            }
+            __builtin_amdgcn_wave_barrier();
+            run += (uint64_t)(len - (int)min((uint64_t)256, be - q0));  // stuffed zeros so far
         }
-        __builtin_amdgcn_wave_barrier();
-        run += (uint64_t)(len - (int)min((uint64_t)256, be - q0));  // stuffed zeros so far
     }
     if (c == D.nchunks - 1 && lane == 0) {
         out[S.out_len - 2] = 0xFF;
