@@ -633,7 +633,10 @@ struct GlobalSink {
 
 // Candidate-list entries of one block held in registers from the start (four
 // 16-B groups); the rest is read from HBM one group ahead of its use.
-constexpr int PRE = 16;
+#ifndef ICX_PRE
+#define ICX_PRE 24  // list entries loaded up front (24: the most that keeps 64 VGPRs, 8 waves/SIMD)
+#endif
+constexpr int PRE = ICX_PRE;
 
 __device__ __forceinline__ void load_group(uint32_t (&g)[4], const uint32_t* lst, int j, int cnt)
 {
