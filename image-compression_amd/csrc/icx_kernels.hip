@@ -130,14 +130,6 @@ __device__ __forceinline__ void rgb_ycc(int r, int g, int b, int& y, int& cb, in
 }
 
 // =================================================================== FDCT
-// natural (v, u) -> zig-zag position, byte u of kZZRow[v] (v is always a
-// compile-time constant at the call sites, so the table is immediate)
-__device__ __forceinline__ int zz_of(int v, int u)
-{
-    constexpr uint64_t kZZRow[8] = {0x1C1B0F0E06050100ull, 0x2A1D1A100D070402ull, 0x2B291E19110C0803ull, 0x352C281F18120B09ull,
-                                    0x36342D272017130Aull, 0x3C37332E26211614ull, 0x3D3B38322F252215ull, 0x3F3E3A3931302423ull};
-    return (int)((kZZRow[v] >> (8 * u)) & 0xFF);
-}
 
 // Colour: one workgroup = 16 rows x 256 px = 16 MCUs of one MCU row (96 blocks);
 // every phase has 1-3 equal tasks per thread.  LDS 15 KiB -> 8 workgroups/CU.
@@ -155,8 +147,8 @@ __device__ __forceinline__ int zz_of(int v, int u)
 constexpr int FDC_MCU = 16;           // MCUs per colour tile
 constexpr int FDC_PX = FDC_MCU * 16;  // 256 px
 constexpr int FDC_BLK = FDC_MCU * 6;  // 96 blocks
-constexpr int WSTR = 68;              // workspace int16 per block
-template <int NB> constexpr int WSTR_OF = NB == 16 ? 64 : WSTR;  // grey tiles: unpadded rows
+constexpr int WSTR = 72;              // workspace int16 per block (row-pass writes, column reads and
+                                      // the natural-order output of phase D are LDS-bank-conflict-free)
 
 __device__ __forceinline__ void st_row8(int16_t* p, const int (&v)[8])  // 8 int16, 8-B aligned
 {
@@ -219,8 +211,8 @@ __device__ __forceinline__ void fdct_load(const FdctTile& T, uint32_t (&wv)[2][6
 
 // Candidate lists of one FDCT tile (nblk scan blocks from bbase; the tile's
 // list region starts at entry `base`, COEF_SLOTS entries reserved per block).
-// oz[blk] holds block blk's raw coefficients in zig-zag order (fix(blk, lane,
-// c) applies dummy blocks).  The DC and every AC coefficient with |c| >= thr
+// oz[blk] holds block blk's raw coefficients in natural order (fix(blk, lane,
+// c) applies dummy blocks; lane = zig-zag index reads position c_zz_to_nat[lane]).  The DC and every AC coefficient with |c| >= thr
 // (lane 0's thr is negative; the others hold the smallest quantiser
 // threshold of k over the qualities this image may be coded at) form the
 // block's list, entries (c << 6) | k in k order, padded to a multiple of 4
@@ -231,11 +223,18 @@ __device__ __forceinline__ void fdct_load(const FdctTile& T, uint32_t (&wv)[2][6
 // (candidates first, then the rest) into the wave's LDS stage, the group's
 // lists back to back; then the group leaves as 16-B pieces into the group's
 // own reserved region.  No cross-wave scan: lists are packed per group.
-// Lengths and offsets go to s_len / s_off and, after the caller's barrier,
-// to ncoef / coff (store_list_meta).
-// Stage of one wave: STEP blocks' lists, then 64 dwords every lane may write
-// (lanes with nothing to store write there, so the stores need no exec mask).
-template <int STEP> constexpr int STAGE_DW = STEP * 64 + 64;
+// Lengths and offsets go to L.meta and, after the caller's barrier, to
+// ncoef / coff (store_list_meta).
+// Phase-E LDS of a tile: one stage per wave for its group's lists, 64 dwords
+// the lanes with nothing to store write to (never read, shared by the waves,
+// so the stores need no exec mask), and per block (offset in its group << 7)
+// | list length.
+template <int NB, int STEP>
+struct ListStage {
+    uint32_t st[4][STEP * 64];
+    uint32_t dummy[64];
+    uint16_t meta[NB];
+};
 
 // v_writelane: lane `a` (0..7, a constant once the caller's loop is unrolled)
 // of v takes the wave-uniform value x - one VALU op, no lane compare.
@@ -252,20 +251,20 @@ __device__ __forceinline__ int writelane(int v, int x, int a)
 #undef ICX_WRITELANE
 
 template <int NB, int STEP, bool FULL, class Fix, class Luma>
-__device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int nblk, int16_t (*oz)[WSTR_OF<NB>],
-                                           uint32_t (*stg)[STAGE_DW<STEP>], uint8_t* s_len,
-                                           uint16_t* s_off, const float (&thr)[2], unsigned long long* ent,
-                                           Fix fix, Luma luma)
+__device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int nblk, int16_t (*oz)[WSTR],
+                                           ListStage<NB, STEP>& L, const float (&thr)[2],
+                                           unsigned long long* ent, Fix fix, Luma luma)
 {
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    uint32_t* st = stg[wave];
+    uint32_t* st = L.st[wave];
     uint32_t total = 0;
+    const int nat = c_zz_to_nat[lane];  // oz holds natural order; lane = zig-zag index
     for (int blk0 = wave * STEP; blk0 < nblk; blk0 += 4 * STEP) {
         int c[STEP];
 #pragma unroll
         for (int a = 0; a < STEP; a++)
-            c[a] = FULL || blk0 + a < nblk ? fix(blk0 + a, lane, (int)oz[blk0 + a][lane]) : 0;
+            c[a] = FULL || blk0 + a < nblk ? fix(blk0 + a, lane, (int)oz[blk0 + a][nat]) : 0;
         int run = 0, len = 0, off = 0;  // run: padded entries of the group so far (wave-uniform)
 #pragma unroll
         for (int a = 0; a < STEP; a++) {
@@ -276,15 +275,12 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
             const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
             const int slot = cand ? pos : cnt + lane - pos;
-            st[slot < r4 ? run + slot : STEP * 64 + lane] = ((uint32_t)c[a] << 6) | (uint32_t)lane;
+            *(slot < r4 ? st + run + slot : L.dummy + lane) = ((uint32_t)c[a] << 6) | (uint32_t)lane;
             len = writelane(len, cnt, a);
             off = writelane(off, run, a);
             run += r4;
         }
-        if (lane < STEP && blk0 + lane < nblk) {
-            s_len[blk0 + lane] = (uint8_t)len;
-            s_off[blk0 + lane] = (uint16_t)(blk0 * COEF_SLOTS + off);
-        }
+        if (lane < STEP && blk0 + lane < nblk) L.meta[blk0 + lane] = (uint16_t)((off << 7) | len);
         __builtin_amdgcn_wave_barrier();
         GAS u32x4_t* dst = (GAS u32x4_t*)(D.coefs + base + (int64_t)blk0 * COEF_SLOTS);
         for (int p = lane; p < run / 4; p += 64) {
@@ -301,13 +297,15 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
 }
 
 // After the barrier that ends emit_lists: lengths and 16-B-unit offsets.
+template <int NB, int STEP>
 __device__ __forceinline__ void store_list_meta(const ImgDesc& D, int64_t base, uint32_t bbase, int nblk,
-                                                const uint8_t* s_len, const uint16_t* s_off)
+                                                const ListStage<NB, STEP>& L)
 {
     const int t = threadIdx.x;
     if (t < nblk) {
-        D.ncoef[bbase + t] = s_len[t];
-        D.coff[bbase + t] = (uint32_t)((base + s_off[t]) >> 2);
+        const uint32_t m = L.meta[t];
+        D.ncoef[bbase + t] = (uint8_t)(m & 127);
+        D.coff[bbase + t] = (uint32_t)((base + (t / STEP) * (STEP * COEF_SLOTS) + (m >> 7)) >> 2);
     }
 }
 
@@ -315,16 +313,14 @@ __device__ __forceinline__ void store_list_meta(const ImgDesc& D, int64_t base, 
 template <bool BGR>
 __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (&wv)[2][6],
                                              const QNode* __restrict__ nodes, ImgState* states,
-                                             uint8_t (*cds)[8][FDC_PX / 2],
-                                             int16_t (*ws)[WSTR], uint32_t (*stg)[STAGE_DW<6>])
+                                             uint8_t (*cds)[8][FDC_PX / 2], int16_t (*ws)[WSTR],
+                                             ListStage<FDC_BLK, 6>& L)
 {
     const ImgDesc& D = *T.D;
     const int tx = T.tx, my = T.my;
     const int H = D.h;
     const int t = threadIdx.x;
-    int16_t (*oz)[WSTR] = ws;     // zig-zag output (phase D)
-    uint8_t* s_len = &cds[0][0][0];                  // phase E list lengths (cds is dead after phase C)
-    uint16_t* s_off = (uint16_t*)&cds[0][0][FDC_BLK];  // phase E packed list offsets
+    int16_t (*oz)[WSTR] = ws;     // natural-order output (phase D)
     const QNode& CN = nodes[D.cand_node];
     const float thr[2] = {(t & 63) ? CN.qf[0][t & 63].x : -1.0f, (t & 63) ? CN.qf[1][t & 63].x : -1.0f};
 
@@ -377,11 +373,11 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
     }
     __syncthreads();
 
-    // ---- D: column DCT, 3 tasks per thread into registers, then the zig-zag
-    // scatter over the workspace once every column has been read
+    // ---- D: column DCT, 3 tasks per thread, in place: the thread of (block,
+    // column) is the only reader and writer of that column, so the natural-
+    // order output needs no barrier between the reads and the writes
     {
         const int col = t & 7;
-        uint32_t res[3][4];
 #pragma unroll
         for (int rep = 0; rep < 3; rep++) {
             const int blk = (t >> 3) + 32 * rep;
@@ -390,15 +386,7 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
             for (int v = 0; v < 8; v++) d[v] = ws[blk][v * 8 + col];
             fdct8<1>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
 #pragma unroll
-            for (int v = 0; v < 4; v++) res[rep][v] = (d[2 * v] & 0xFFFF) | ((uint32_t)d[2 * v + 1] << 16);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int rep = 0; rep < 3; rep++) {
-            const int blk = (t >> 3) + 32 * rep;
-#pragma unroll
-            for (int v = 0; v < 8; v++)
-                oz[blk][zz_of(v, col)] = (int16_t)(res[rep][v >> 1] >> ((v & 1) * 16));
+            for (int v = 0; v < 8; v++) oz[blk][v * 8 + col] = (int16_t)d[v];
         }
     }
     __syncthreads();
@@ -436,12 +424,11 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
     unsigned long long* ent = (unsigned long long*)states[T.img].list_entries;
     auto luma = [](int a) { return a < 4; };  // one MCU per step: Y0 Y1 Y2 Y3 Cb Cr
     if (plain)  // interior tile: no dummy blocks
-        emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, stg, s_len, s_off, thr, ent,
-                                     [](int, int, int c) { return c; }, luma);
+        emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, L, thr, ent, [](int, int, int c) { return c; }, luma);
     else
-        emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, stg, s_len, s_off, thr, ent, fix, luma);
+        emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, L, thr, ent, fix, luma);
     __syncthreads();
-    store_list_meta(D, base, bbase, nblk, s_len, s_off);
+    store_list_meta(D, base, bbase, nblk, L);
     __syncthreads();  // LDS free for the next tile
 }
 
@@ -462,9 +449,14 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
                                                     const int32_t* __restrict__ ids,
                                                     const int64_t* __restrict__ prefix, int m)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t cds[2][8][FDC_PX / 2];  // 2 KB downsampled Cb, Cr
-    __shared__ __attribute__((aligned(16))) int16_t ws[FDC_BLK][WSTR];     // 12.75 KB row-pass output
-    __shared__ __attribute__((aligned(16))) uint32_t stg[4][STAGE_DW<6>];   // 7 KB list staging, one MCU per wave
+    // 13.5 KiB row-pass output / coefficients + 6.4 KiB shared by the
+    // downsampled chroma (phases B, C) and the list stages (phase E): 20416 B,
+    // eight workgroups per CU
+    __shared__ __attribute__((aligned(16))) int16_t ws[FDC_BLK][WSTR];
+    __shared__ __attribute__((aligned(16))) union {
+        uint8_t cds[2][8][FDC_PX / 2];
+        ListStage<FDC_BLK, 6> ls;
+    } u;
     const int64_t total = prefix[m];
     const int64_t item0 = (int64_t)blockIdx.x * FDCT_TILES;
     uint32_t cur[2][6], nxt[2][6];
@@ -478,7 +470,7 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
             tn = fdct_tile(descs, ids, prefix, m, item0 + k + 1);
             fdct_load(tn, nxt);
         }
-        fdct_compute<BGR>(tc, cur, nodes, states, cds, ws, stg);
+        fdct_compute<BGR>(tc, cur, nodes, states, u.cds, ws, u.ls);
         if (!more) break;
         tc = tn;
 #pragma unroll
@@ -495,10 +487,8 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
                                                    const int64_t* __restrict__ prefix, int m)
 {
     __shared__ __attribute__((aligned(16))) int32_t ws[16][64];
-    __shared__ __attribute__((aligned(16))) int16_t oz[16][64];
-    __shared__ uint8_t s_len[16];
-    __shared__ uint16_t s_off[128];
-    __shared__ __attribute__((aligned(16))) uint32_t stg[4][STAGE_DW<4>];
+    __shared__ __attribute__((aligned(16))) int16_t oz[16][WSTR];
+    __shared__ __attribute__((aligned(16))) ListStage<16, 4> ls;
     const int64_t item = blockIdx.x;
     const int slot = find_slot(prefix, m, item);
     const int img = ids[slot];
@@ -528,17 +518,17 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
         for (int v = 0; v < 8; v++) d[v] = ws[blk][v * 8 + col];
         fdct8<1>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
 #pragma unroll
-        for (int v = 0; v < 8; v++) oz[blk][zz_of(v, col)] = (int16_t)d[v];
+        for (int v = 0; v < 8; v++) oz[blk][v * 8 + col] = (int16_t)d[v];
     }
     __syncthreads();
     const int nblk = min(16, D.mcux - tx * 16);
     const uint32_t bbase = (uint32_t)by * D.mcux + tx * 16;
     const float thr[2] = {(t & 63) ? nodes[D.cand_node].qf[0][t & 63].x : -1.0f, 0.0f};
     const int64_t base = (int64_t)tile * (16 * COEF_SLOTS);
-    emit_lists<16, 4, false>(D, base, nblk, oz, stg, s_len, s_off, thr, (unsigned long long*)states[img].list_entries,
-                      [](int, int, int c) { return c; }, [](int) { return true; });
+    emit_lists<16, 4, false>(D, base, nblk, oz, ls, thr, (unsigned long long*)states[img].list_entries,
+                             [](int, int, int c) { return c; }, [](int) { return true; });
     __syncthreads();
-    store_list_meta(D, base, bbase, nblk, s_len, s_off);
+    store_list_meta(D, base, bbase, nblk, ls);
 }
 
 // =================================================================== Huffman
