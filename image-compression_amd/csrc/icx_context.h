@@ -85,16 +85,41 @@ struct KStat {
 };
 
 
+// Device or host buffer?  hipPointerGetAttributes costs ~0.25 us and the
+// drivers ask per image several times a call, so device allocation ranges
+// (hipMemGetAddressRange of a pointer found to be device memory) are kept in
+// a process-wide map and later pointers inside one are answered without a
+// HIP call.  Device virtual ranges stay reserved by the runtime after a free,
+// so a cached range never holds a host pointer.
 inline bool is_device_ptr(const void* p)
 {
     if (!p) return false;
-    hipPointerAttribute_t a;
-    hipError_t e = hipPointerGetAttributes(&a, p);
+    static std::mutex mu;
+    static std::map<uintptr_t, uintptr_t> ranges;  // base -> end
+    const uintptr_t a = (uintptr_t)p;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = ranges.upper_bound(a);
+        if (it != ranges.begin() && a < (--it)->second) return true;
+    }
+    hipPointerAttribute_t at;
+    hipError_t e = hipPointerGetAttributes(&at, p);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
-    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+    const bool dev = at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+    if (dev) {
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) == hipSuccess && base && size) {
+            std::lock_guard<std::mutex> g(mu);
+            ranges[(uintptr_t)base] = (uintptr_t)base + size;
+        } else {
+            (void)hipGetLastError();
+        }
+    }
+    return dev;
 }
 
 

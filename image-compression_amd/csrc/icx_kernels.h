@@ -15,8 +15,8 @@ void launch_fdct(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, i
                  hipStream_t st);
 void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks,
                  hipStream_t st);
-void launch_scan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st);
-void launch_decide(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, hipStream_t st);
+// k_scan: the trial's offsets, exact file size and one binary-search step (decide)
+void launch_scan(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, hipStream_t st);
 void launch_ffscan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st);
 void launch_stuff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks,
                   hipStream_t st);

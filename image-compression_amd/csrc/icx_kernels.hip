@@ -6,11 +6,11 @@
 //   k_fdct_color / k_fdct_gray  A7+A8+A9: rgb_ycc_convert, edge expansion,
 //                               h2v2_downsample, jpeg_fdct_islow (raw, x8)
 //   k_huff                      A9 quantise + A10 Huffman: per-chunk packed
-//                               bitstream, 16 lanes per 8x8 block
+//                               bitstream, one thread per 8x8 block
 //   k_scan                      exclusive scan of chunk bit counts; 0xFF bytes
 //                               per chunk from the huff kernel's alignment bins
-//                               (exact stuffed size without writing it)
-//   k_decide                    A3 binary-search step (tree walk)
+//                               (exact stuffed size without writing it), then
+//                               the A3 binary-search step (decide_trial)
 //   k_ffscan + k_stuff          final file: header, stuffed bytes, EOI
 //   k_resize                    A12 Java2D bilinear (TransformHelper)
 // No MFMA: integer, byte-oriented work bound by HBM.
@@ -1074,11 +1074,44 @@ __device__ __forceinline__ uint32_t stream_bits(const GAS uint32_t* __restrict__
     return v;
 }
 
+// Exact file size of the pending trial, then one step of
+// findBestQualityByBinarySearch (ImageCompressionJpg.java:176-189); run by
+// thread 0 of the image's k_scan workgroup once the trial's totals are known.
+__device__ __forceinline__ void decide_trial(const ImgDesc& D, ImgState& S, const QNode* __restrict__ nodes,
+                                             uint64_t total_bits, uint32_t ff_total)
+{
+    const int cur = S.cur;
+    S.total_bits[cur] = total_bits;
+    S.ff_total[cur] = ff_total;
+    const int64_t size = (int64_t)D.hdr_len + (int64_t)((total_bits + 7) >> 3) + (int64_t)ff_total + 2;
+    const QNode& N = nodes[S.node];
+    if (S.ntrials <= MAX_TRIALS) {
+        S.trial_q[S.ntrials] = N.mid;
+        S.trial_size[S.ntrials] = size;
+    }
+    S.ntrials++;
+    const bool fits = S.force || size <= D.target;  // currentSize <= targetMaxSizeBytes
+    int next;
+    if (fits) {
+        S.best_node = S.node;
+        S.best_buf = cur;
+        S.best_size = size;
+        S.cur = cur ^ 1;
+        next = N.child_fit;
+    } else {
+        next = N.child_nofit;
+    }
+    if (S.force) next = -1;
+    S.node = next;
+    S.active = next >= 0;
+}
+
 // One workgroup per image: exclusive scan of the chunk bit counts, then each
 // chunk's 0xFF count: its alignment bin chunk_ffa[(8 - off%8) % 8] plus the
 // byte that starts in the chunk and ends in the next one (or in the padding).
 __global__ __launch_bounds__(1024) void k_scan(const ImgDesc* __restrict__ descs, ImgState* states,
-                                               const int32_t* __restrict__ ids, int m)
+                                               const QNode* __restrict__ nodes, const int32_t* __restrict__ ids,
+                                               int m)
 {
     __shared__ uint64_t s_w[16];
     __shared__ uint64_t s_base;
@@ -1130,45 +1163,8 @@ __global__ __launch_bounds__(1024) void k_scan(const ImgDesc* __restrict__ descs
     if (t == 0) {
         uint64_t ff = 0;
         for (int k = 0; k < 16; k++) ff += s_w[k];
-        S.total_bits[cur] = s_base;
-        S.ff_total[cur] = (uint32_t)ff;
+        decide_trial(D, S, nodes, s_base, (uint32_t)ff);
     }
-}
-
-// One thread per image: exact file size of the pending trial, then one step
-// of findBestQualityByBinarySearch (ImageCompressionJpg.java:176-189).
-__global__ void k_decide(const ImgDesc* __restrict__ descs, ImgState* states, const QNode* __restrict__ nodes,
-                         const int32_t* __restrict__ ids, int m)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    const int img = ids[i];
-    ImgState& S = states[img];
-    if (!S.active) return;
-    const ImgDesc& D = descs[img];
-    const int cur = S.cur;
-    const int64_t size = (int64_t)D.hdr_len + (int64_t)((S.total_bits[cur] + 7) >> 3) +
-                         (int64_t)S.ff_total[cur] + 2;
-    const QNode& N = nodes[S.node];
-    if (S.ntrials <= MAX_TRIALS) {
-        S.trial_q[S.ntrials] = N.mid;
-        S.trial_size[S.ntrials] = size;
-    }
-    S.ntrials++;
-    const bool fits = S.force || size <= D.target;  // currentSize <= targetMaxSizeBytes
-    int next;
-    if (fits) {
-        S.best_node = S.node;
-        S.best_buf = cur;
-        S.best_size = size;
-        S.cur = cur ^ 1;
-        next = N.child_fit;
-    } else {
-        next = N.child_nofit;
-    }
-    if (S.force) next = -1;
-    S.node = next;
-    S.active = next >= 0;
 }
 
 // Final pass 1 (one workgroup per image): exclusive scan of the best trial's
@@ -1415,14 +1411,9 @@ void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan
     hipLaunchKernelGGL(k_huff, dim3((unsigned)chunks), dim3(CHUNK_BLOCKS), 0, st, d, s, n, p.ids, p.prefix, p.m);
 }
 
-void launch_scan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st)
+void launch_scan(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_scan, dim3(p.m), dim3(1024), 0, st, d, s, p.ids, p.m);
-}
-
-void launch_decide(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, hipStream_t st)
-{
-    hipLaunchKernelGGL(k_decide, dim3(grid_of(p.m, 64)), dim3(64), 0, st, d, s, n, p.ids, p.m);
+    hipLaunchKernelGGL(k_scan, dim3(p.m), dim3(1024), 0, st, d, s, n, p.ids, p.m);
 }
 
 void launch_ffscan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st)

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -219,6 +220,9 @@ struct Batch {
     // The stage's small uploads (descriptors, states, launch plans) share one
     // pinned block and go in one copy per launch group (flush before launches).
     std::unique_ptr<Uploader> up;
+    // Final passes whose states (file length, status) are read only once the
+    // sub-batch ends: the images and a pinned copy of their stage's states.
+    std::vector<std::pair<std::vector<int>, ImgState*>> finals;
 };
 
 struct DPlan {
@@ -228,6 +232,20 @@ struct DPlan {
 
 
 // Build a launch plan over `ids` with per-image work counts.
+// Host wall time of a region into the profile (name: "host.*"), when profiling.
+struct HostSpan {
+    icx_ctx* c;
+    const char* name;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~HostSpan()
+    {
+        if (!c->prof) return;
+        KStat& k = c->stats[name];
+        k.launches++;
+        k.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+};
+
 icx_status make_plan(Batch& B, const std::vector<int>& ids, const std::vector<int64_t>& counts, DPlan& out)
 {
     std::vector<int64_t> pre(ids.size() + 1, 0);
@@ -253,6 +271,7 @@ void new_stage(Batch& B)
 
 icx_status sync_states(Batch& B)
 {
+    HostSpan hs{B.c, "host.sync"};
     icx_ctx* c = B.c;
     hipError_t e = hipMemcpyAsync(B.h_state, B.d_state, sizeof(ImgState) * B.state.size(), hipMemcpyDeviceToHost,
                                   c->stream);
@@ -379,8 +398,7 @@ icx_status run_trials(Batch& B, const std::vector<int>& ids, int depth)
     icx_ctx* c = B.c;
     for (int t = 0; t < depth; t++) {
         { Timed tm(c, "huff", 0); launch_huff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
-        { Timed tm(c, "scan", (int64_t)ids.size()); launch_scan(B.d_desc, B.d_state, P.p, c->stream); }
-        { Timed tm(c, "decide", (int64_t)ids.size()); launch_decide(B.d_desc, B.d_state, B.d_nodes, P.p, c->stream); }
+        { Timed tm(c, "scan", (int64_t)ids.size()); launch_scan(B.d_desc, B.d_state, B.d_nodes, P.p, c->stream); }
     }
     return ICX_OK;
 }
@@ -462,6 +480,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
     const size_t share = (all_need + nsub - 1) / nsub;
     size_t pos = 0;
     while (pos < order.size()) {
+        std::unique_ptr<HostSpan> prep(new HostSpan{c, "host.prep"});  // until the first launch
         // ---- size a sub-batch against the workspace budget
         std::vector<int> sub;
         size_t need = 1 << 20;
@@ -632,6 +651,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
 
         std::vector<int> all(m);
         for (int k = 0; k < m; k++) all[k] = k;
+        prep.reset();
 
         if (mode == Mode::Fdct) {
             for (int k = 0; k < m; k++) init_state(B.state[k], -1, false);
@@ -655,11 +675,19 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             continue;
         }
 
+        // The final file of each image in ids; no synchronisation: its length
+        // and status come back with a copy of the stage's states read after
+        // the sub-batch's last synchronisation (collect_finals).
         auto finish_found = [&](const std::vector<int>& ids) -> icx_status {
             if (ids.empty()) return ICX_OK;
             icx_status st = run_final(B, ids);
             if (st) return st;
-            return sync_states(B);
+            ImgState* h = (ImgState*)c->host.take(sizeof(ImgState) * m);
+            if (!h) return fail(c, ICX_E_NOMEM, "pinned staging exhausted");
+            hipError_t e2 = hipMemcpyAsync(h, B.d_state, sizeof(ImgState) * m, hipMemcpyDeviceToHost, c->stream);
+            if (e2 != hipSuccess) return hip_fail(c, e2, "state download");
+            B.finals.emplace_back(ids, h);
+            return ICX_OK;
         };
 
         if (mode == Mode::Encode) {  // A4: one forced encode
@@ -754,7 +782,17 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                 pend.swap(rest);
             }
         }
+        // ---- the final passes' file lengths and statuses
+        e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(c, e, "final passes");
+        for (const auto& f : B.finals)
+            for (int k : f.first) {
+                B.state[k].out_len = f.second[k].out_len;
+                B.state[k].status = f.second[k].status;
+            }
         // ---- results + host outputs
+        HostSpan res{c, "host.results"};
         for (int k = 0; k < m; k++) {
             Item& I = B.it[k];
             icx_fit_job& j = *I.job;

@@ -31,7 +31,7 @@ codec.profile_reset()
 for _ in range(2):
     codec.fit(frames, target, bench.Q0, cached=cached, outputs=outs)
 torch.cuda.synchronize()
-res = {k: codec.profile_query(k) for k in ("fdct", "huff", "scan", "decide", "ffscan", "stuff")}
+res = {k: codec.profile_query(k) for k in ("fdct", "huff", "scan", "ffscan", "stuff")}
 stats = None
 if os.environ.get("ICX_STATS"):  # ICX_HUFF_EXP=7 build: list statistics over all trials
     import ctypes
