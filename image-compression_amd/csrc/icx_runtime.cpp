@@ -220,9 +220,6 @@ struct Batch {
     // The stage's small uploads (descriptors, states, launch plans) share one
     // pinned block and go in one copy per launch group (flush before launches).
     std::unique_ptr<Uploader> up;
-    // Final passes whose states (file length, status) are read only once the
-    // sub-batch ends: the images and a pinned copy of their stage's states.
-    std::vector<std::pair<std::vector<int>, ImgState*>> finals;
 };
 
 struct DPlan {
@@ -388,7 +385,11 @@ void credit_huff(Batch& B, const std::vector<int>& ids)
     B.c->stats["huff.bytes"].units += bytes;
 }
 
-icx_status run_trials(Batch& B, const std::vector<int>& ids, int depth)
+// `depth` trials (k_huff + k_scan with its search step) for the images in ids,
+// then - finals - the final file of every image whose search has a best
+// trial (k_ffscan / k_stuff skip the others), all without a host round trip:
+// the stage's one synchronisation then also returns the files' lengths.
+icx_status run_trials(Batch& B, const std::vector<int>& ids, int depth, bool finals)
 {
     std::vector<int64_t> cnt;
     for (int i : ids) cnt.push_back(B.desc[i].nchunks);
@@ -400,19 +401,10 @@ icx_status run_trials(Batch& B, const std::vector<int>& ids, int depth)
         { Timed tm(c, "huff", 0); launch_huff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
         { Timed tm(c, "scan", (int64_t)ids.size()); launch_scan(B.d_desc, B.d_state, B.d_nodes, P.p, c->stream); }
     }
-    return ICX_OK;
-}
-
-icx_status run_final(Batch& B, const std::vector<int>& ids)
-{
-    std::vector<int64_t> cnt;
-    for (int i : ids) cnt.push_back(B.desc[i].nchunks);
-    DPlan P;
-    icx_status s = make_plan(B, ids, cnt, P);
-    if (s || (s = B.up->flush())) return s;
-    icx_ctx* c = B.c;
-    { Timed tm(c, "ffscan", (int64_t)ids.size()); launch_ffscan(B.d_desc, B.d_state, P.p, c->stream); }
-    { Timed tm(c, "stuff", P.total); launch_stuff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
+    if (finals) {
+        { Timed tm(c, "ffscan", (int64_t)ids.size()); launch_ffscan(B.d_desc, B.d_state, P.p, c->stream); }
+        { Timed tm(c, "stuff", P.total); launch_stuff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
+    }
     return ICX_OK;
 }
 
@@ -675,29 +667,13 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             continue;
         }
 
-        // The final file of each image in ids; no synchronisation: its length
-        // and status come back with a copy of the stage's states read after
-        // the sub-batch's last synchronisation (collect_finals).
-        auto finish_found = [&](const std::vector<int>& ids) -> icx_status {
-            if (ids.empty()) return ICX_OK;
-            icx_status st = run_final(B, ids);
-            if (st) return st;
-            ImgState* h = (ImgState*)c->host.take(sizeof(ImgState) * m);
-            if (!h) return fail(c, ICX_E_NOMEM, "pinned staging exhausted");
-            hipError_t e2 = hipMemcpyAsync(h, B.d_state, sizeof(ImgState) * m, hipMemcpyDeviceToHost, c->stream);
-            if (e2 != hipSuccess) return hip_fail(c, e2, "state download");
-            B.finals.emplace_back(ids, h);
-            return ICX_OK;
-        };
-
         if (mode == Mode::Encode) {  // A4: one forced encode
             for (int k = 0; k < m; k++) init_state(B.state[k], B.it[k].cached_node, true);
-            if ((s = push_desc_state(B)) || (s = run_fdct(B, all)) || (s = run_trials(B, all, 1)) ||
+            if ((s = push_desc_state(B)) || (s = run_fdct(B, all)) || (s = run_trials(B, all, 1, true)) ||
                 (s = sync_states(B)))
                 return s;
             credit_fdct(B, all);
             credit_huff(B, all);
-            if ((s = finish_found(all))) return s;
             for (int k = 0; k < m; k++) {
                 B.it[k].found = B.state[k].best_node >= 0;
                 B.it[k].best_q = jobs[sub[k]].quality;
@@ -718,12 +694,11 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                     init_state(B.state[k], B.it[k].cached_node, false);
                     B.it[k].coef_scale = sc < 1.0 ? sc : 1.0;
                 }
-                if ((s = push_desc_state(B)) || (s = run_fdct(B, probe)) || (s = run_trials(B, probe, 1)) ||
+                if ((s = push_desc_state(B)) || (s = run_fdct(B, probe)) || (s = run_trials(B, probe, 1, true)) ||
                     (s = sync_states(B)))
                     return s;
                 credit_fdct(B, probe);
                 credit_huff(B, probe);
-                std::vector<int> hits;
                 for (int k : probe) {
                     B.it[k].encodes += B.state[k].ntrials;
                     if (B.state[k].best_node >= 0) {
@@ -731,10 +706,8 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                         I.found = I.hit = I.done = true;
                         I.best_q = jobs[sub[k]].cached.quality;
                         I.best_scale = jobs[sub[k]].cached.scale;
-                        hits.push_back(k);
                     }
                 }
-                if ((s = finish_found(hits))) return s;
             }
             // ---- scale loop (ImageCompressionJpg.java:91-115)
             std::vector<int> pend;
@@ -753,12 +726,12 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                     init_state(B.state[k], B.it[k].root, false);
                     depth = std::max(depth, B.it[k].depth);
                 }
-                if ((s = push_desc_state(B)) || (s = run_fdct(B, need_fdct)) || (s = run_trials(B, pend, depth)) ||
-                    (s = sync_states(B)))
+                if ((s = push_desc_state(B)) || (s = run_fdct(B, need_fdct)) ||
+                    (s = run_trials(B, pend, depth, mode != Mode::Search)) || (s = sync_states(B)))
                     return s;
                 credit_fdct(B, need_fdct);
                 credit_huff(B, pend);
-                std::vector<int> found, rest;
+                std::vector<int> rest;
                 for (int k : pend) {
                     Item& I = B.it[k];
                     I.encodes += B.state[k].ntrials;
@@ -772,25 +745,14 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                         I.found = I.done = true;
                         I.best_q = B.nodes[B.state[k].best_node].mid;
                         I.best_scale = scale;
-                        found.push_back(k);
                     } else {
                         rest.push_back(k);
                     }
                 }
                 if (mode == Mode::Search) break;
-                if ((s = finish_found(found))) return s;
                 pend.swap(rest);
             }
         }
-        // ---- the final passes' file lengths and statuses
-        e = hipStreamSynchronize(c->stream);
-        if (e == hipSuccess) e = hipGetLastError();
-        if (e != hipSuccess) return hip_fail(c, e, "final passes");
-        for (const auto& f : B.finals)
-            for (int k : f.first) {
-                B.state[k].out_len = f.second[k].out_len;
-                B.state[k].status = f.second[k].status;
-            }
         // ---- results + host outputs
         HostSpan res{c, "host.results"};
         for (int k = 0; k < m; k++) {
