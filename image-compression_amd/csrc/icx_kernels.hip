@@ -746,13 +746,13 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     int32_t* const s_dcq = (int32_t*)s_bits;  // DC exchange; dead before s_bits is written
     __shared__ uint32_t s_wsum[CHUNK_BLOCKS / 64];
 
-    const int64_t item = blockIdx.x;
-    const int slot = find_slot(prefix, m, item);
+    // 2-D launch (every image of the plan has as many chunks): slot = y
+    const int slot = gridDim.y > 1 ? (int)blockIdx.y : find_slot(prefix, m, blockIdx.x);
     const int img = ids[slot];
     const ImgState& S = states[img];
     if (!S.active) return;
     const ImgDesc& D = descs[img];
-    const int chunk = (int)(item - prefix[slot]);
+    const int chunk = gridDim.y > 1 ? (int)blockIdx.x : (int)(blockIdx.x - prefix[slot]);
     const QNode& N = nodes[S.node];
     const int cur = S.cur;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -1220,13 +1220,20 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
 {
     __shared__ uint32_t s_stg[4][132];  // per wave: one stuffed piece (<= 512 B) + read-ahead
     const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (item >= prefix[m]) return;
-    const int slot = find_slot(prefix, m, item);
+    int slot, c;
+    if (gridDim.y > 1) {  // 2-D launch: slot = y, every image has gridDim.x * 4 >= nchunks
+        slot = (int)blockIdx.y;
+        c = (int)item;
+    } else {
+        if (item >= prefix[m]) return;
+        slot = find_slot(prefix, m, item);
+        c = (int)(item - prefix[slot]);
+    }
     const int img = ids[slot];
     const ImgState& S = states[img];
     if (S.best_node < 0 || S.status != 0) return;
     const ImgDesc& D = descs[img];
-    const int c = (int)(item - prefix[slot]);
+    if (c >= D.nchunks) return;
     const int buf = S.best_buf;
     const int lane = threadIdx.x & 63;
     GAS uint8_t* out = gp(D.out);
@@ -1408,7 +1415,8 @@ void launch_fdct(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, i
 void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, hipStream_t st)
 {
     if (chunks <= 0) return;
-    hipLaunchKernelGGL(k_huff, dim3((unsigned)chunks), dim3(CHUNK_BLOCKS), 0, st, d, s, n, p.ids, p.prefix, p.m);
+    const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3((unsigned)p.uniform, (unsigned)p.m) : dim3((unsigned)chunks);
+    hipLaunchKernelGGL(k_huff, grid, dim3(CHUNK_BLOCKS), 0, st, d, s, n, p.ids, p.prefix, p.m);
 }
 
 void launch_scan(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, hipStream_t st)
@@ -1424,7 +1432,9 @@ void launch_ffscan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st)
 void launch_stuff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, hipStream_t st)
 {
     if (chunks <= 0) return;
-    hipLaunchKernelGGL(k_stuff, dim3(grid_of(chunks, 4)), dim3(256), 0, st, d, s, n, p.ids, p.prefix, p.m);
+    const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3((unsigned)grid_of(p.uniform, 4), (unsigned)p.m)
+                                               : dim3((unsigned)grid_of(chunks, 4));
+    hipLaunchKernelGGL(k_stuff, grid, dim3(256), 0, st, d, s, n, p.ids, p.prefix, p.m);
 }
 
 void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int nch, uint8_t* dst, int dw, int dh,

@@ -252,6 +252,10 @@ icx_status make_plan(Batch& B, const std::vector<int>& ids, const std::vector<in
     out.p.ids = B.up->put(ids32.data(), ids32.size());
     out.p.prefix = B.up->put(pre.data(), pre.size());
     out.p.m = (int32_t)ids.size();
+    out.p.uniform = 0;
+    if (!counts.empty() && counts[0] > 0 && counts[0] < (1 << 30) && ids.size() < 65536 &&
+        std::all_of(counts.begin(), counts.end(), [&](int64_t v) { return v == counts[0]; }))
+        out.p.uniform = (int32_t)counts[0];
     out.total = pre.back();
     return B.up->overflow ? fail(B.c, ICX_E_NOMEM, "upload staging exhausted") : ICX_OK;
 }
