@@ -167,10 +167,11 @@ struct FdctTile {
 __device__ __forceinline__ FdctTile fdct_tile(const ImgDesc* __restrict__ descs, const int32_t* __restrict__ ids,
                                               const int64_t* __restrict__ prefix, int m, int64_t item)
 {
-    const int slot = find_slot(prefix, m, item);
+    // 2-D launch (every image of the plan has as many tiles): slot = y, item = tile
+    const int slot = gridDim.y > 1 ? (int)blockIdx.y : find_slot(prefix, m, item);
     const int img = ids[slot];
     const ImgDesc* D = &descs[img];
-    const int tile = (int)(item - prefix[slot]);
+    const int tile = gridDim.y > 1 ? (int)item : (int)(item - prefix[slot]);
     const int tiles_x = (D->mcux + FDC_MCU - 1) / FDC_MCU;
     const int my = tile / tiles_x;
     return FdctTile{D, img, tile - my * tiles_x, my};
@@ -457,7 +458,7 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
         uint8_t cds[2][8][FDC_PX / 2];
         ListStage<FDC_BLK, 6> ls;
     } u;
-    const int64_t total = prefix[m];
+    const int64_t total = gridDim.y > 1 ? prefix[1] - prefix[0] : prefix[m];  // items of this launch row
     const int64_t item0 = (int64_t)blockIdx.x * FDCT_TILES;
     uint32_t cur[2][6], nxt[2][6];
     FdctTile tc = fdct_tile(descs, ids, prefix, m, item0);
@@ -1402,14 +1403,14 @@ void launch_fdct(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, i
                  hipStream_t st)
 {
     if (tiles <= 0) return;
+    const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3(grid_of(p.uniform, FDCT_TILES), (unsigned)p.m)
+                                               : dim3(grid_of(tiles, FDCT_TILES));
     if (kind == 2)
         hipLaunchKernelGGL(k_fdct_gray, dim3((unsigned)tiles), dim3(256), 0, st, d, n, s, p.ids, p.prefix, p.m);
     else if (kind == 0)
-        hipLaunchKernelGGL(k_fdct_color<true>, dim3(grid_of(tiles, FDCT_TILES)), dim3(256), 0, st, d, n, s, p.ids,
-                           p.prefix, p.m);
+        hipLaunchKernelGGL(k_fdct_color<true>, grid, dim3(256), 0, st, d, n, s, p.ids, p.prefix, p.m);
     else
-        hipLaunchKernelGGL(k_fdct_color<false>, dim3(grid_of(tiles, FDCT_TILES)), dim3(256), 0, st, d, n, s, p.ids,
-                           p.prefix, p.m);
+        hipLaunchKernelGGL(k_fdct_color<false>, grid, dim3(256), 0, st, d, n, s, p.ids, p.prefix, p.m);
 }
 
 void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, hipStream_t st)
