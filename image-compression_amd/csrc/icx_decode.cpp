@@ -164,7 +164,7 @@ WPlan plan_of(Uploader& U, const std::vector<int64_t>& counts, const int32_t* d_
 {
     std::vector<int64_t> pre(counts.size() + 1, 0);
     for (size_t i = 0; i < counts.size(); i++) pre[i + 1] = pre[i] + counts[i];
-    WPlan out;
+    WPlan out{};
     out.p.ids = d_ids;
     out.p.prefix = U.put(pre.data(), pre.size());
     out.p.m = (int32_t)counts.size();

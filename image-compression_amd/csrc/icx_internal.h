@@ -110,6 +110,7 @@ struct Plan {
     const int64_t* prefix;  // m + 1 entries
     int32_t m;
     int32_t uniform;        // > 0: every slot holds this many items (2-D launches, no slot search)
+    int32_t identity;       // ids[i] == i for every slot
 };
 
 }  // namespace icx

@@ -169,7 +169,7 @@ __device__ __forceinline__ FdctTile fdct_tile(const ImgDesc* __restrict__ descs,
 {
     // 2-D launch (every image of the plan has as many tiles): slot = y, item = tile
     const int slot = gridDim.y > 1 ? (int)blockIdx.y : find_slot(prefix, m, item);
-    const int img = ids[slot];
+    const int img = ids ? ids[slot] : slot;
     const ImgDesc* D = &descs[img];
     const int tile = gridDim.y > 1 ? (int)item : (int)(item - prefix[slot]);
     const int tiles_x = (D->mcux + FDC_MCU - 1) / FDC_MCU;
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
     __shared__ __attribute__((aligned(16))) ListStage<16, 4> ls;
     const int64_t item = blockIdx.x;
     const int slot = find_slot(prefix, m, item);
-    const int img = ids[slot];
+    const int img = ids ? ids[slot] : slot;
     const ImgDesc& D = descs[img];
     const int tile = (int)(item - prefix[slot]);
     const int tiles_x = (D.mcux + 15) >> 4;
@@ -749,7 +749,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
 
     // 2-D launch (every image of the plan has as many chunks): slot = y
     const int slot = gridDim.y > 1 ? (int)blockIdx.y : find_slot(prefix, m, blockIdx.x);
-    const int img = ids[slot];
+    const int img = ids ? ids[slot] : slot;
     const ImgState& S = states[img];
     if (!S.active) return;
     const ImgDesc& D = descs[img];
@@ -1116,7 +1116,7 @@ __global__ __launch_bounds__(1024) void k_scan(const ImgDesc* __restrict__ descs
 {
     __shared__ uint64_t s_w[16];
     __shared__ uint64_t s_base;
-    const int img = ids[blockIdx.x];
+    const int img = ids ? ids[blockIdx.x] : (int)blockIdx.x;
     ImgState& S = states[img];
     if (!S.active) return;
     const ImgDesc& D = descs[img];
@@ -1175,7 +1175,7 @@ __global__ __launch_bounds__(1024) void k_ffscan(const ImgDesc* __restrict__ des
 {
     __shared__ uint64_t s_w[16];
     __shared__ uint64_t s_base;
-    const int img = ids[blockIdx.x];
+    const int img = ids ? ids[blockIdx.x] : (int)blockIdx.x;
     ImgState& S = states[img];
     if (S.best_node < 0) return;
     const ImgDesc& D = descs[img];
@@ -1230,7 +1230,7 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
         slot = find_slot(prefix, m, item);
         c = (int)(item - prefix[slot]);
     }
-    const int img = ids[slot];
+    const int img = ids ? ids[slot] : slot;
     const ImgState& S = states[img];
     if (S.best_node < 0 || S.status != 0) return;
     const ImgDesc& D = descs[img];
@@ -1398,6 +1398,9 @@ hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat
 }
 
 static inline unsigned grid_of(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+// A plan over images 0..m-1 in order passes no id table: the kernels take
+// slot = image and skip one dependent load at workgroup start.
+static inline const int32_t* plan_ids(const Plan& p) { return p.identity ? nullptr : p.ids; }
 
 void launch_fdct(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, int64_t tiles, int kind,
                  hipStream_t st)
@@ -1406,28 +1409,28 @@ void launch_fdct(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, i
     const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3(grid_of(p.uniform, FDCT_TILES), (unsigned)p.m)
                                                : dim3(grid_of(tiles, FDCT_TILES));
     if (kind == 2)
-        hipLaunchKernelGGL(k_fdct_gray, dim3((unsigned)tiles), dim3(256), 0, st, d, n, s, p.ids, p.prefix, p.m);
+        hipLaunchKernelGGL(k_fdct_gray, dim3((unsigned)tiles), dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
     else if (kind == 0)
-        hipLaunchKernelGGL(k_fdct_color<true>, grid, dim3(256), 0, st, d, n, s, p.ids, p.prefix, p.m);
+        hipLaunchKernelGGL(k_fdct_color<true>, grid, dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
     else
-        hipLaunchKernelGGL(k_fdct_color<false>, grid, dim3(256), 0, st, d, n, s, p.ids, p.prefix, p.m);
+        hipLaunchKernelGGL(k_fdct_color<false>, grid, dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
 }
 
 void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, hipStream_t st)
 {
     if (chunks <= 0) return;
     const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3((unsigned)p.uniform, (unsigned)p.m) : dim3((unsigned)chunks);
-    hipLaunchKernelGGL(k_huff, grid, dim3(CHUNK_BLOCKS), 0, st, d, s, n, p.ids, p.prefix, p.m);
+    hipLaunchKernelGGL(k_huff, grid, dim3(CHUNK_BLOCKS), 0, st, d, s, n, plan_ids(p), p.prefix, p.m);
 }
 
 void launch_scan(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_scan, dim3(p.m), dim3(1024), 0, st, d, s, n, p.ids, p.m);
+    hipLaunchKernelGGL(k_scan, dim3(p.m), dim3(1024), 0, st, d, s, n, plan_ids(p), p.m);
 }
 
 void launch_ffscan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_ffscan, dim3(p.m), dim3(1024), 0, st, d, s, p.ids, p.m);
+    hipLaunchKernelGGL(k_ffscan, dim3(p.m), dim3(1024), 0, st, d, s, plan_ids(p), p.m);
 }
 
 void launch_stuff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, hipStream_t st)
@@ -1435,7 +1438,7 @@ void launch_stuff(const ImgDesc* d, const ImgState* s, const QNode* n, const Pla
     if (chunks <= 0) return;
     const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3((unsigned)grid_of(p.uniform, 4), (unsigned)p.m)
                                                : dim3((unsigned)grid_of(chunks, 4));
-    hipLaunchKernelGGL(k_stuff, grid, dim3(256), 0, st, d, s, n, p.ids, p.prefix, p.m);
+    hipLaunchKernelGGL(k_stuff, grid, dim3(256), 0, st, d, s, n, plan_ids(p), p.prefix, p.m);
 }
 
 void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int nch, uint8_t* dst, int dw, int dh,

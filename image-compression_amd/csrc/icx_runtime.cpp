@@ -253,6 +253,8 @@ icx_status make_plan(Batch& B, const std::vector<int>& ids, const std::vector<in
     out.p.prefix = B.up->put(pre.data(), pre.size());
     out.p.m = (int32_t)ids.size();
     out.p.uniform = 0;
+    out.p.identity = 1;
+    for (size_t i = 0; i < ids.size(); i++) out.p.identity &= ids[i] == (int)i;
     if (!counts.empty() && counts[0] > 0 && counts[0] < (1 << 30) && ids.size() < 65536 &&
         std::all_of(counts.begin(), counts.end(), [&](int64_t v) { return v == counts[0]; }))
         out.p.uniform = (int32_t)counts[0];
