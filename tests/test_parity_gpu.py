@@ -231,3 +231,22 @@ def test_candidate_lists_mixed_batch(codec, oracle):
                 assert r["data"] == o["data"], (i, target)
                 assert np.float32(r["learned"].quality) == np.float32(o["quality"])
                 assert r["learned"].scale == o["scale"]
+
+
+def test_same_size_batch_matches_oracle(codec, oracle):
+    """Same-sized frames: the launches take the 2-D grid (image = y, no slot
+    search) in every stage - the probe over all images (identity plan) and
+    the search over the misses (a subset, with its id table) - and partial
+    FDCT tiles (width 600 = 2 tiles + 88 px)."""
+    imgs = [smooth(136, 600, 300 + i) if i % 2 else noise(136, 600, 400 + i) for i in range(6)]
+    cached = [icx.LearnedParams(0.25, 1.0)] * len(imgs)
+    for target in (12000, 40000):
+        res = codec.fit(imgs, target, 0.25, cached=cached)
+        for i, (img, r) in enumerate(zip(imgs, res)):
+            o = oracle.fit(img, target, 0.25, cached=(0.25, 1.0))
+            assert r["status"] == N.OK
+            assert (r["success"], r["cache_hit"]) == (o["success"], o["cache_hit"]), (i, target)
+            if o["success"]:
+                assert r["data"] == o["data"], (i, target)
+                assert np.float32(r["learned"].quality) == np.float32(o["quality"])
+                assert r["learned"].scale == o["scale"]
