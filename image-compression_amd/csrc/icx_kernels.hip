@@ -66,6 +66,21 @@ __device__ __forceinline__ void st8(void* p, int2 v)
 // prefix[m] = total).  A proportional guess first - exact when the slots hold
 // equally many items, as for a batch of same-sized frames: two dependent loads
 // instead of log2(m) - then a binary search of what the guess left open.
+// Inclusive prefix sum over the 64 lanes of a wave with DPP moves (row
+// shifts within 16-lane rows, then row broadcasts 15 and 31): a few cycles per
+// step instead of an LDS-crossbar round trip per __shfl_up.  Every lane must
+// be active.
+__device__ __forceinline__ int wave_incl_scan(int x)
+{
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
 __device__ __forceinline__ int find_slot(const int64_t* prefix, int m, int64_t item)
 {
     int lo = 0, hi = m;  // prefix[lo] <= item < prefix[hi]
@@ -886,12 +901,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     return;
 #endif
     // ---- 2. exclusive scan of block bits
-    int incl = bits;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-    }
+    const int incl = wave_incl_scan(bits);
     if (lane == 63) s_wsum[wv] = incl;
     __syncthreads();
     uint32_t off = incl - bits, total = 0;
@@ -1298,13 +1308,8 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
                 for (int j = 0; j < 4; j++)
                     if (j < nv && ((v >> (24 - 8 * j)) & 255) == 255) nout++;
             }
-            int incl = nout;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const int y = __shfl_up(incl, d, 64);
-                if (lane >= d) incl += y;
-            }
-            const int len = __shfl(incl, 63, 64);           // stuffed bytes of this piece
+            const int incl = wave_incl_scan(nout);
+            const int len = __builtin_amdgcn_readlane(incl, 63);  // stuffed bytes of this piece
             int p = incl - nout;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
