@@ -1136,13 +1136,9 @@ __global__ __launch_bounds__(1024) void k_scan(const ImgDesc* __restrict__ descs
     __syncthreads();
     for (int base = 0; base < D.nchunks; base += 1024) {
         const int i = base + t;
-        uint64_t v = i < D.nchunks ? D.chunk_bits[cur][i] : 0;
-        uint64_t x = v;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            uint64_t y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
+        // a chunk holds < 2^19 bits, 64 of them < 2^32: the wave scan is 32-bit
+        const uint64_t v = i < D.nchunks ? D.chunk_bits[cur][i] : 0;
+        const uint64_t x = (uint32_t)wave_incl_scan((int)v);
         if (lane == 63) s_w[wv] = x;
         __syncthreads();
         uint64_t wbase = s_base;
@@ -1195,13 +1191,8 @@ __global__ __launch_bounds__(1024) void k_ffscan(const ImgDesc* __restrict__ des
     __syncthreads();
     for (int base = 0; base < D.nchunks; base += 1024) {
         const int i = base + t;
-        uint64_t v = i < D.nchunks ? D.chunk_ff[buf][i] : 0;
-        uint64_t x = v;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            uint64_t y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
+        const uint64_t v = i < D.nchunks ? D.chunk_ff[buf][i] : 0;  // < 2^16 per chunk
+        const uint64_t x = (uint32_t)wave_incl_scan((int)v);
         if (lane == 63) s_w[wv] = x;
         __syncthreads();
         uint64_t wbase = s_base;
