@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/icx.h"
+#include "icx_internal.h"
 
 namespace icx {
 
@@ -203,24 +204,41 @@ inline hipEvent_t get_event(icx_ctx* c)
     return e;
 }
 
-struct Timed {  // brackets one launch with events when profiling is on
+// Times one launch when profiling is on: its events go to the launch
+// wrapper (g_launch_timing), which records them in the dispatch itself; a
+// region whose wrapper launched nothing returns them unused
+// (ext).  Without ext, events are recorded on the stream around the region.
+struct Timed {
     icx_ctx* c;
     Pending p;
-    bool on;
-    Timed(icx_ctx* ctx, const char* name, int64_t units) : c(ctx), on(ctx->prof)
+    bool on, ext;
+    Timed(icx_ctx* ctx, const char* name, int64_t units, bool ext_launch = false)
+        : c(ctx), on(ctx->prof), ext(ext_launch)
     {
         if (!on) return;
         p.name = name;
         p.units = units;
         p.a = get_event(c);
         p.b = get_event(c);
-        hipEventRecord(p.a, c->stream);
+        if (ext) g_launch_timing = LaunchTiming{p.a, p.b, false};
+        else hipEventRecord(p.a, c->stream);
     }
     ~Timed()
     {
         if (!on) return;
-        hipEventRecord(p.b, c->stream);
-        c->pending.push_back(p);
+        if (!ext) {
+            hipEventRecord(p.b, c->stream);
+            c->pending.push_back(p);
+            return;
+        }
+        const bool used = g_launch_timing.used;
+        g_launch_timing = LaunchTiming{};
+        if (used) {
+            c->pending.push_back(p);
+        } else {
+            c->evpool.push_back(p.a);
+            c->evpool.push_back(p.b);
+        }
     }
 };
 

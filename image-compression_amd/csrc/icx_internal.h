@@ -105,6 +105,15 @@ struct ImgState {
 
 // A launch plan: the images taking part (ids into desc/state arrays) and
 // the exclusive prefix of work items (tiles or chunks) per image.
+// Profiling: events a launch wrapper (icx_kernels.hip) hands to
+// hipExtLaunchKernelGGL, which timestamps the dispatch itself - no marker
+// packets between the kernels.  Set by Timed (icx_context.h) for one launch.
+struct LaunchTiming {
+    hipEvent_t a = nullptr, b = nullptr;
+    bool used = false;
+};
+extern thread_local LaunchTiming g_launch_timing;
+
 struct Plan {
     const int32_t* ids;
     const int64_t* prefix;  // m + 1 entries

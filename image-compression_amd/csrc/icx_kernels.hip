@@ -14,6 +14,7 @@
 //   k_ffscan + k_stuff          final file: header, stuffed bytes, EOI
 //   k_resize                    A12 Java2D bilinear (TransformHelper)
 // No MFMA: integer, byte-oriented work bound by HBM.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1393,6 +1394,22 @@ hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat
     return hipMemcpyToSymbol(HIP_SYMBOL(c_hdr), hdr, 2 * HDR_COLOR);
 }
 
+thread_local LaunchTiming g_launch_timing;
+
+// hipLaunchKernelGGL, or - when a Timed region handed over events - the
+// extended launch that records them at the dispatch's start and end.
+#define ICX_LAUNCH(K, GRID, BLOCK, SHM, ST, ...)                                                          \
+    do {                                                                                                  \
+        LaunchTiming& lt_ = g_launch_timing;                                                              \
+        if (lt_.a) {                                                                                      \
+            hipExtLaunchKernelGGL(K, GRID, BLOCK, SHM, ST, lt_.a, lt_.b, 0, __VA_ARGS__);                 \
+            lt_.a = lt_.b = nullptr;                                                                      \
+            lt_.used = true;                                                                              \
+        } else {                                                                                          \
+            hipLaunchKernelGGL(K, GRID, BLOCK, SHM, ST, __VA_ARGS__);                                     \
+        }                                                                                                 \
+    } while (0)
+
 static inline unsigned grid_of(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 // A plan over images 0..m-1 in order passes no id table: the kernels take
 // slot = image and skip one dependent load at workgroup start.
@@ -1405,28 +1422,28 @@ void launch_fdct(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, i
     const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3(grid_of(p.uniform, FDCT_TILES), (unsigned)p.m)
                                                : dim3(grid_of(tiles, FDCT_TILES));
     if (kind == 2)
-        hipLaunchKernelGGL(k_fdct_gray, dim3((unsigned)tiles), dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
+        ICX_LAUNCH(k_fdct_gray, dim3((unsigned)tiles), dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
     else if (kind == 0)
-        hipLaunchKernelGGL(k_fdct_color<true>, grid, dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
+        ICX_LAUNCH(k_fdct_color<true>, grid, dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
     else
-        hipLaunchKernelGGL(k_fdct_color<false>, grid, dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
+        ICX_LAUNCH(k_fdct_color<false>, grid, dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
 }
 
 void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, hipStream_t st)
 {
     if (chunks <= 0) return;
     const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3((unsigned)p.uniform, (unsigned)p.m) : dim3((unsigned)chunks);
-    hipLaunchKernelGGL(k_huff, grid, dim3(CHUNK_BLOCKS), 0, st, d, s, n, plan_ids(p), p.prefix, p.m);
+    ICX_LAUNCH(k_huff, grid, dim3(CHUNK_BLOCKS), 0, st, d, s, n, plan_ids(p), p.prefix, p.m);
 }
 
 void launch_scan(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_scan, dim3(p.m), dim3(1024), 0, st, d, s, n, plan_ids(p), p.m);
+    ICX_LAUNCH(k_scan, dim3(p.m), dim3(1024), 0, st, d, s, n, plan_ids(p), p.m);
 }
 
 void launch_ffscan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_ffscan, dim3(p.m), dim3(1024), 0, st, d, s, plan_ids(p), p.m);
+    ICX_LAUNCH(k_ffscan, dim3(p.m), dim3(1024), 0, st, d, s, plan_ids(p), p.m);
 }
 
 void launch_stuff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, hipStream_t st)
@@ -1434,7 +1451,7 @@ void launch_stuff(const ImgDesc* d, const ImgState* s, const QNode* n, const Pla
     if (chunks <= 0) return;
     const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3((unsigned)grid_of(p.uniform, 4), (unsigned)p.m)
                                                : dim3((unsigned)grid_of(chunks, 4));
-    hipLaunchKernelGGL(k_stuff, grid, dim3(256), 0, st, d, s, n, plan_ids(p), p.prefix, p.m);
+    ICX_LAUNCH(k_stuff, grid, dim3(256), 0, st, d, s, n, plan_ids(p), p.prefix, p.m);
 }
 
 void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int nch, uint8_t* dst, int dw, int dh,
@@ -1450,7 +1467,7 @@ void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int nch, uin
     a.dyl = (int64_t)(iy * 4294967296.0);
     a.x0l = (int64_t)(0.5 * ix * 4294967296.0);  // transform of the first pixel centre (0.5)
     a.y0l = (int64_t)(0.5 * iy * 4294967296.0);
-    hipLaunchKernelGGL(k_resize, dim3(grid_of(dw, 64), grid_of(dh, 4)), dim3(256), 0, st, a);
+    ICX_LAUNCH(k_resize, dim3(grid_of(dw, 64), grid_of(dh, 4)), dim3(256), 0, st, a);
 }
 
 }  // namespace icx

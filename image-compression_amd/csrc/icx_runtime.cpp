@@ -352,7 +352,7 @@ icx_status run_fdct(Batch& B, const std::vector<int>& ids)
         int64_t px = 0;
         for (int i : sel) px += (int64_t)B.desc[i].w * B.desc[i].h;
         if ((s = B.up->flush())) return s;
-        Timed tm(B.c, "fdct", px);
+        Timed tm(B.c, "fdct", px, true);
         launch_fdct(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, kind, B.c->stream);
     }
     return ICX_OK;
@@ -404,12 +404,12 @@ icx_status run_trials(Batch& B, const std::vector<int>& ids, int depth, bool fin
     if (s || (s = B.up->flush())) return s;
     icx_ctx* c = B.c;
     for (int t = 0; t < depth; t++) {
-        { Timed tm(c, "huff", 0); launch_huff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
-        { Timed tm(c, "scan", (int64_t)ids.size()); launch_scan(B.d_desc, B.d_state, B.d_nodes, P.p, c->stream); }
+        { Timed tm(c, "huff", 0, true); launch_huff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
+        { Timed tm(c, "scan", (int64_t)ids.size(), true); launch_scan(B.d_desc, B.d_state, B.d_nodes, P.p, c->stream); }
     }
     if (finals) {
-        { Timed tm(c, "ffscan", (int64_t)ids.size()); launch_ffscan(B.d_desc, B.d_state, P.p, c->stream); }
-        { Timed tm(c, "stuff", P.total); launch_stuff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
+        { Timed tm(c, "ffscan", (int64_t)ids.size(), true); launch_ffscan(B.d_desc, B.d_state, P.p, c->stream); }
+        { Timed tm(c, "stuff", P.total, true); launch_stuff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
     }
     return ICX_OK;
 }
