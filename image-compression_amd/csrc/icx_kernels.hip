@@ -1215,7 +1215,10 @@ __global__ __launch_bounds__(1024) void k_ffscan(const ImgDesc* __restrict__ des
 // of the bytes the chunk owns (first bit inside it), EOI (last chunk), written
 // straight into the caller's output buffer: 256 source bytes per step are
 // stuffed into the wave's LDS stage and leave as aligned dwords.
-constexpr int STUFF_BATCH = 8;  // 256-byte pieces whose source loads k_stuff issues together
+#ifndef ICX_STUFF_BATCH
+#define ICX_STUFF_BATCH 3  // measured: 3 beats 2, 4, 6, 8, 16 (fewer VGPRs, more waves in flight)
+#endif
+constexpr int STUFF_BATCH = ICX_STUFF_BATCH;  // 256-byte pieces whose source loads k_stuff issues together
 
 __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs, const ImgState* __restrict__ states,
                                                const QNode* __restrict__ nodes, const int32_t* __restrict__ ids,
