@@ -272,13 +272,26 @@ void new_stage(Batch& B)
     B.up.reset(new Uploader(B.c, bytes));
 }
 
+// Wait for the stream by polling it: the stage decisions sit on the critical
+// path between two device stages, and a blocking wait's wake-up latency
+// (scheduler-dependent, 20 us to several hundred on a busy host) is idle
+// device time.
+hipError_t stream_wait(hipStream_t st)
+{
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipErrorNotReady) return e;
+        __builtin_ia32_pause();
+    }
+}
+
 icx_status sync_states(Batch& B)
 {
     HostSpan hs{B.c, "host.sync"};
     icx_ctx* c = B.c;
     hipError_t e = hipMemcpyAsync(B.h_state, B.d_state, sizeof(ImgState) * B.state.size(), hipMemcpyDeviceToHost,
                                   c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = stream_wait(c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "state download");
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
