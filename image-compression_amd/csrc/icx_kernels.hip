@@ -506,11 +506,11 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
     __shared__ __attribute__((aligned(16))) int32_t ws[16][64];
     __shared__ __attribute__((aligned(16))) int16_t oz[16][WSTR];
     __shared__ __attribute__((aligned(16))) ListStage<16, 4> ls;
-    const int64_t item = blockIdx.x;
-    const int slot = find_slot(prefix, m, item);
+    // 2-D launch (every image of the plan has as many tiles): slot = y
+    const int slot = gridDim.y > 1 ? (int)blockIdx.y : find_slot(prefix, m, blockIdx.x);
     const int img = ids ? ids[slot] : slot;
     const ImgDesc& D = descs[img];
-    const int tile = (int)(item - prefix[slot]);
+    const int tile = gridDim.y > 1 ? (int)blockIdx.x : (int)(blockIdx.x - prefix[slot]);
     const int tiles_x = (D.mcux + 15) >> 4;
     const int by = tile / tiles_x, tx = tile - by * tiles_x;
     const int W = D.w, H = D.h, x0 = tx * 128;
@@ -1425,7 +1425,8 @@ void launch_fdct(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, i
     const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3(grid_of(p.uniform, FDCT_TILES), (unsigned)p.m)
                                                : dim3(grid_of(tiles, FDCT_TILES));
     if (kind == 2)
-        ICX_LAUNCH(k_fdct_gray, dim3((unsigned)tiles), dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
+        ICX_LAUNCH(k_fdct_gray, p.uniform > 0 && p.m > 1 ? dim3((unsigned)p.uniform, (unsigned)p.m) : dim3((unsigned)tiles),
+                   dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
     else if (kind == 0)
         ICX_LAUNCH(k_fdct_color<true>, grid, dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
     else

@@ -238,9 +238,10 @@ def test_same_size_batch_matches_oracle(codec, oracle):
     search) in every stage - the probe over all images (identity plan) and
     the search over the misses (a subset, with its id table) - and partial
     FDCT tiles (width 600 = 2 tiles + 88 px)."""
-    imgs = [smooth(136, 600, 300 + i) if i % 2 else noise(136, 600, 400 + i) for i in range(6)]
-    cached = [icx.LearnedParams(0.25, 1.0)] * len(imgs)
-    for target in (12000, 40000):
+    colour = [smooth(136, 600, 300 + i) if i % 2 else noise(136, 600, 400 + i) for i in range(6)]
+    grey = [im[:, :, 1].copy() for im in colour]  # grey FDCT: 2-D launch too
+    cached = [icx.LearnedParams(0.25, 1.0)] * len(colour)
+    for imgs, target in ((colour, 12000), (colour, 40000), (grey, 8000)):
         res = codec.fit(imgs, target, 0.25, cached=cached)
         for i, (img, r) in enumerate(zip(imgs, res)):
             o = oracle.fit(img, target, 0.25, cached=(0.25, 1.0))
