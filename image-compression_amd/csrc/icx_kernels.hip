@@ -803,9 +803,16 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         pb = b - 1;
     }
     const int cnt = valid ? (int)D.ncoef[b] : 0;
+    // a DC predictor in the previous chunk (the chunk's first blocks): its
+    // list offset and DC entry are fetched alongside this block's own, not
+    // after the DC exchange (they would stall the first wave, and through the
+    // scan barrier the workgroup)
+    const bool ext_prev = pb >= 0 && pb < b0;
+    const uint32_t prev_off = ext_prev ? D.coff[pb] : 0u;
     const uint32_t* lst = (const uint32_t*)D.coefs + 4 * (size_t)D.coff[valid ? b : b0];
     uint32_t ev[PRE];
     load_list(ev, lst, cnt);
+    const int32_t prev_dc = ext_prev ? gp(D.coefs)[4 * (size_t)prev_off] : 0;
     __syncthreads();  // tables ready
 
     const float4 q0t = s_qf[tb][0];
@@ -814,7 +821,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     __syncthreads();
     int qprev = 0;
     if (pb >= b0) qprev = s_dcq[pb - b0];
-    else if (pb >= 0) qprev = quant(gp(D.coefs)[4 * (size_t)gp(D.coff)[pb]] >> 6, q0t.y, q0t.z);
+    else if (ext_prev) qprev = quant(prev_dc >> 6, q0t.y, q0t.z);
 
     // ---- 1. encode_one_block into the slot (rarely: into the block's HBM spill)
     int bits = 0;
