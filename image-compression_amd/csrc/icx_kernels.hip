@@ -924,7 +924,11 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     // assembled stream): FF_COPIES copies per bin, picked by lane, so that the
     // LDS atomics of a wave rarely collide on one address
     uint32_t* const s_bin = s_tab + OUT_WORDS + 8;
-    if (total > (uint32_t)OUT_WORDS * 32 && t < 8 * FF_COPIES) s_bin[t] = 0u;
+    if (total > (uint32_t)OUT_WORDS * 32) {
+        if (t < 8 * FF_COPIES) s_bin[t] = 0u;
+    } else {  // the assembled stream and its bins start zeroed (tables are dead)
+        for (uint32_t i = t; i < OUT_WORDS + 8 + 8 * FF_COPIES; i += CHUNK_BLOCKS) s_tab[i] = 0u;
+    }
     __syncthreads();
 
     const GAS uint32_t* spill0 = gp(D.ovf + b0 * BLOCK_WORDS);
@@ -947,8 +951,6 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         if (t == 0) D.chunk_bits[cur][chunk] = total;
         return;
 #endif
-        for (uint32_t i = t; i < OUT_WORDS + 8 + 8 * FF_COPIES; i += CHUNK_BLOCKS) s_out[i] = 0u;
-        __syncthreads();
         if (bits > 0) {
             const uint32_t sh = off & 31, nwb = ((uint32_t)bits + 31) >> 5;
             uint32_t* o = s_out + (off >> 5);
