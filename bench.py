@@ -12,7 +12,8 @@ MP counted once per image (decoded W x H).
 
 Multi-GPU: one process per GPU (torchrun); each rank owns its own frames
 (file-list sharding, no data-path collective) -> weak scaling.  The barrier
-and the max-over-ranks reduction of the step time are the only collectives.
+and the max-over-ranks reduction of the step time are the only collectives,
+on a gloo (host) process group: no RCCL anywhere on the path.
 """
 import argparse
 import json
@@ -221,7 +222,7 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("gloo")  # host group: no device exchange on the path (no RCCL)
 
     frames = make_frames(args.images, 1000003 * rank, dev)
     if args.host_io:
@@ -262,7 +263,7 @@ def main():
     codec.profile(False)
     validate()
     if dist:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
 

@@ -144,6 +144,11 @@ bool build_dec_huff(const uint8_t* bits, const uint8_t* vals, int n, DecHuff& t,
     int code = 0, k = 0, nsub = 0;
     for (int l = 1; l <= 16; l++) {
         const int cnt = bits[l - 1];
+        // jdhuff.c jpeg_make_d_derived_tbl rejects a length whose codes run
+        // into the all-ones code or past it; checked BEFORE any entry of the
+        // length is written, so an over-subscribed DHT never indexes past lut
+        // (every code written below is < 2^l, its prefix < 2^DEC_LUT_BITS)
+        if (code + cnt >= (1 << l) || k + cnt > n) return false;
         slow.valoff[l] = k - code;
         for (int i = 0; i < cnt; i++, code++, k++) {
             const uint16_t e = (uint16_t)((l << 8) | vals[k]);
@@ -161,7 +166,6 @@ bool build_dec_huff(const uint8_t* bits, const uint8_t* vals, int n, DecHuff& t,
             }
         }
         slow.maxcode[l] = cnt ? code - 1 : -1;
-        if (code >= (1 << l)) return false;  // all-ones code or over-subscribed (jdhuff.c)
         code <<= 1;
     }
     if (k != n) return false;

@@ -9,6 +9,7 @@
 // state kept in HBM (no host round trip between trials), then one host
 // synchronisation to decide which images move on to the next 0.85x scale.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -272,16 +273,29 @@ void new_stage(Batch& B)
     B.up.reset(new Uploader(B.c, bytes));
 }
 
-// Wait for the stream by polling it: the stage decisions sit on the critical
-// path between two device stages, and a blocking wait's wake-up latency
-// (scheduler-dependent, 20 us to several hundred on a busy host) is idle
-// device time.
+// Wait for the stream: the stage decisions sit on the critical path between
+// two device stages, and a blocking wait's wake-up latency (scheduler-
+// dependent, 20 us to several hundred on a busy host) is idle device time.
+// So poll - tightly for the first 50 us, then yielding the core to the
+// decode / writer pools between polls - and block only once the stage has
+// run for 2 ms, where a wake-up is small against the stage itself.
 hipError_t stream_wait(hipStream_t st)
 {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     for (;;) {
         const hipError_t e = hipStreamQuery(st);
         if (e != hipErrorNotReady) return e;
-        __builtin_ia32_pause();
+        const auto dt = clk::now() - t0;
+        if (dt < std::chrono::microseconds(50)) {
+#if defined(__x86_64__) || defined(__i386__)
+            __builtin_ia32_pause();
+#endif
+        } else if (dt < std::chrono::milliseconds(2)) {
+            sched_yield();
+        } else {
+            return hipStreamSynchronize(st);
+        }
     }
 }
 

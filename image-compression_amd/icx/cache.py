@@ -6,11 +6,15 @@ stdlib) stands in with the same schema and the same semantics:
 
   * table LEARNED_PARAMS_CACHE(WIDTH_BUCKET INT, HEIGHT_BUCKET INT,
     SIZE_BUCKET BIGINT, QUALITY FLOAT, SCALE DOUBLE, PK(w, h, s))  (:48-55)
-  * the configured path has a trailing ".mv.db" stripped (:32); the file is
+  * the configured path is made absolute and every ".mv.db" in it removed
+    (`toAbsolutePath().toString().replace(".mv.db", "")`, :32); the file is
     "<path>.icx.sqlite"
-  * load_all_to_map reads every row into the in-memory L1 map (:68-93)
+  * load_all_to_map reads every row into the in-memory L1 map (:68-93); a
+    database error is logged and the rows read so far are returned, so a
+    corrupt or locked cache file means a cold cache, not an aborted batch
   * save_all_from_map upserts (MERGE) every entry in batches of 1000 inside
-    one transaction (:100-155)
+    one transaction (:100-155); on a database error the transaction is rolled
+    back and the error logged (:139-152)
   * the L1 map itself is a plain dict guarded by the caller (the reference's
     ConcurrentHashMap, :69); quality values stay float32-exact.
 """
@@ -35,10 +39,7 @@ SCHEMA = """CREATE TABLE IF NOT EXISTS LEARNED_PARAMS_CACHE (
 
 
 def db_file(path) -> str:
-    p = str(path)
-    if p.endswith(".mv.db"):
-        p = p[: -len(".mv.db")]
-    return p + ".icx.sqlite"
+    return os.path.abspath(str(path)).replace(".mv.db", "") + ".icx.sqlite"
 
 
 class LockedDict(dict):
@@ -63,9 +64,12 @@ class CacheManager:
 
     def load_all_to_map(self) -> LockedDict:
         m = LockedDict()
-        for wb, hb, sb, q, s in self.conn.execute(
-                "SELECT WIDTH_BUCKET, HEIGHT_BUCKET, SIZE_BUCKET, QUALITY, SCALE FROM LEARNED_PARAMS_CACHE"):
-            m[SimilarityKey(int(wb), int(hb), int(sb))] = LearnedParams(float(np.float32(q)), float(s))
+        try:
+            for wb, hb, sb, q, s in self.conn.execute(
+                    "SELECT WIDTH_BUCKET, HEIGHT_BUCKET, SIZE_BUCKET, QUALITY, SCALE FROM LEARNED_PARAMS_CACHE"):
+                m[SimilarityKey(int(wb), int(hb), int(sb))] = LearnedParams(float(np.float32(q)), float(s))
+        except sqlite3.Error:
+            log.exception("從 L2 快取載入時發生錯誤")  # the reference continues with what it has
         log.info("從 L2 快取載入 %d 筆學習參數到 L1", len(m))
         return m
 
@@ -74,12 +78,16 @@ class CacheManager:
                 for k, v in list(m.items())]
         if not rows:
             return 0
-        with self.conn:  # one transaction
-            for i in range(0, len(rows), batch_size):
-                self.conn.executemany(
-                    "INSERT OR REPLACE INTO LEARNED_PARAMS_CACHE "
-                    "(WIDTH_BUCKET, HEIGHT_BUCKET, SIZE_BUCKET, QUALITY, SCALE) VALUES (?, ?, ?, ?, ?)",
-                    rows[i:i + batch_size])
+        try:
+            with self.conn:  # one transaction; rolled back if any batch fails
+                for i in range(0, len(rows), batch_size):
+                    self.conn.executemany(
+                        "INSERT OR REPLACE INTO LEARNED_PARAMS_CACHE "
+                        "(WIDTH_BUCKET, HEIGHT_BUCKET, SIZE_BUCKET, QUALITY, SCALE) VALUES (?, ?, ?, ?, ?)",
+                        rows[i:i + batch_size])
+        except sqlite3.Error:
+            log.exception("儲存 L1 快取至 L2 時發生錯誤，交易已回滾")
+            return 0
         log.info("成功將 %d 筆 L1 快取資料寫回 L2", len(rows))
         return len(rows)
 

@@ -27,6 +27,7 @@ import concurrent.futures as cf
 import logging
 import os
 import queue
+import sqlite3
 import threading
 import time
 from dataclasses import dataclass, field
@@ -244,12 +245,21 @@ def decode_group(codec, items: List[_Item]):
         return
     res = codec.decode_jpg_batch([it.decoded.data for it in todo], subsampling=0, device_out=True)
     for it, (st, img) in zip(todo, res):
+        it.decoded.data = None
         if st == N.OK:
             it.decoded.image = img
-        else:
-            log.warning("%s - GPU 解碼失敗 (icx status %d)，改用主機解碼", it.path, st)
+            continue
+        log.warning("%s - GPU 解碼失敗 (icx status %d)，改用主機解碼", it.path, st)
+        try:  # a corrupt file fails alone, as its own processImage task would
             it.decoded.image = _host_decode(it.path, it.decoded.subsampling)
-        it.decoded.data = None
+        except MemoryError as e:
+            _fail(it, e)
+        except OSError:  # ImageCompression.java:101-103 (IOException from reader.read)
+            log.warning("%s - 處理圖片時發生 I/O 錯誤 (可能非支援格式或檔案損毀)", it.path)
+            it.report = CompressionReport(CompressionResult.FAILED_IO_ERROR, it.original_size, 0)
+            it.decoded = None
+        except Exception as e:
+            _fail(it, e)
 
 
 def _jpeg_write(it: _Item, data: bytes, success: bool):
@@ -269,6 +279,9 @@ def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, ca
     except Exception as e:  # context-level failure: every image of the group fails alike
         for it in items:
             _fail(it, e)
+        return
+    items = [it for it in items if it.report is None]  # files whose decode failed are done
+    if not items:
         return
     keys = [create_key(it.decoded.image, it.original_size) for it in items]
     with cache.lock:
@@ -446,14 +459,15 @@ class CompressionBatch:
         mgr = None
         if cache is None:
             mgr = CacheManager(self.h2_cache_path)
-            mgr.init_schema()
-            cache = mgr.load_all_to_map()
-            log.info("初始化 H2 二級快取，並載入至記憶體 L1 快取。")
         elif not hasattr(cache, "lock"):
             cache = LockedDict(cache)
         rep = BatchReport()
         t0 = time.perf_counter()
         try:
+            if mgr is not None:  # CompressionBatch.java:49-52 (inside the try: a schema error ends the batch)
+                mgr.init_schema()
+                cache = mgr.load_all_to_map()
+                log.info("初始化 H2 二級快取，並載入至記憶體 L1 快取。")
             lines = read_file_list(self.file_list_path)
             mine = shard(lines, self.rank, self.world)
             rep.total = len(mine)
@@ -463,13 +477,16 @@ class CompressionBatch:
                 if it.report is not None:
                     rep.add(it.report)
             rep.megapixels = sum(getattr(it, "mp", 0.0) for it in items)
+        except sqlite3.Error:  # CompressionBatch.java:134-139: logged, the batch ends
+            log.exception("執行批次壓縮時發生未預期錯誤")
         finally:
             rep.seconds = time.perf_counter() - t0
-            rep.cache_size = len(cache)
+            rep.cache_size = len(cache) if cache is not None else 0
             if mgr is not None:
-                log.info("記憶體中 L1 快取最終大小: %d", len(cache))
-                if save_cache:
-                    mgr.save_all_from_map(cache)
+                if cache is not None:
+                    log.info("記憶體中 L1 快取最終大小: %d", len(cache))
+                    if save_cache:
+                        mgr.save_all_from_map(cache)
                 mgr.close()
         return rep
 

@@ -184,3 +184,57 @@ def test_png_writer_adaptive_filters_round_trip():
         assert np.array_equal(back, img if img.ndim == 2 else img[:, :, ::-1])
     types = set(filter_rows(grad.reshape(64, -1), 3)[:, 0].tolist())
     assert len(types) >= 2  # the smooth gradient picks predictive filters, not only "None"
+
+
+def test_corrupt_jpeg_fails_alone_in_its_group(tmp_path):
+    """A file the device decoder rejects and the host decoder cannot read either
+    fails by itself (FAILED_IO_ERROR, as reader.read's IOException does in
+    ImageCompression.java:101-103); the valid files of its device group still
+    compress (one bad file used to fail the whole group)."""
+    good = []
+    for i in range(3):
+        f = tmp_path / f"g{i}.jpg"
+        write_jpeg(f, noise(70 + i, 110, 20 + i))
+        good.append(str(f))
+    bad = tmp_path / "bad.jpg"
+    data = (tmp_path / "g0.jpg").read_bytes()
+    bad.write_bytes(data[: len(data) * 3 // 5])  # header intact, scan truncated
+    bad_bytes = bad.read_bytes()
+
+    class RejectingCodec(OracleCodec):
+        def decode_jpg_batch(self, datas, subsampling=0, device_out=False):
+            out = super().decode_jpg_batch(datas, subsampling, device_out)
+            return [(icx.core.N.E_CORRUPT, None) if bytes(d) == bad_bytes else r for d, r in zip(datas, out)]
+
+    lst = tmp_path / "list.txt"
+    lst.write_text("\n".join([good[0], str(bad), good[1], good[2]]) + "\n")
+    b = pipeline.CompressionBatch(lst, tmp_path / "out", CompressionParams(0.25, 1000, 60, 60, 20000), 1,
+                                  tmp_path / "cache", codecs=[RejectingCodec()], group_size=4)
+    rep = b.execute(cache=LockedDict())
+    assert rep.total == 4 and rep.success == 3, rep.counts
+    assert rep.counts[CompressionResult.FAILED_IO_ERROR] == 1
+    for g in good:
+        assert (tmp_path / "out" / os.path.basename(g)).exists()
+    assert not (tmp_path / "out" / "bad.jpg").exists()
+
+
+def test_cache_errors_do_not_abort(tmp_path, caplog):
+    """H2CacheManager.loadAllToMap / saveAllFromMap catch SQLException, log it
+    and carry on (cache/H2CacheManager.java:89-92, 148-152); the JDBC path has
+    every '.mv.db' removed (:32)."""
+    import sqlite3
+    assert db_file(tmp_path / "a.mv.db" / "c.mv.db").endswith("a/c.icx.sqlite")
+    m = CacheManager(tmp_path / "c")
+    m.init_schema()
+    m.save_all_from_map({SimilarityKey(1, 2, 3): LearnedParams(0.5, 1.0)})
+    m.conn.execute("DROP TABLE LEARNED_PARAMS_CACHE")
+    assert len(m.load_all_to_map()) == 0  # logged, empty map
+    assert m.save_all_from_map({SimilarityKey(1, 2, 3): LearnedParams(0.5, 1.0)}) == 0  # rolled back
+    m.close()
+    # a file that is not a database: the batch logs the error and ends, no exception
+    bad = tmp_path / "junk"
+    (tmp_path / "junk.icx.sqlite").write_bytes(b"not a database" * 100)
+    lst = tmp_path / "list.txt"
+    lst.write_text("missing.jpg\n")
+    rep = pipeline.CompressionBatch(lst, tmp_path / "out", P, 1, bad, codecs=[OracleCodec()]).execute()
+    assert rep.total == 0
