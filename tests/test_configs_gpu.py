@@ -23,6 +23,13 @@ pytestmark = pytest.mark.gpu
 MIB = 1 << 20
 
 
+def _trials(o):
+    """The oracle's encode count without saveCompressedImage's re-encode
+    (ImageCompressionJpg.java:255-260): the device keeps the best trial's
+    stream instead, so it runs exactly the search trials."""
+    return o["encodes"] - (1 if o["success"] and not o["cache_hit"] else 0)
+
+
 def _fit_equal(codec, oracle, imgs, target, q0):
     res = codec.fit(imgs, target, q0)
     out = []
@@ -30,7 +37,7 @@ def _fit_equal(codec, oracle, imgs, target, q0):
         o = oracle.fit(img, target, q0)
         assert r["status"] == N.OK, (i, r["status"])
         assert r["success"] == o["success"] and r["cache_hit"] == o["cache_hit"] is False, i
-        assert r["encodes"] == o["encodes"], (i, r["encodes"], o["encodes"])
+        assert r["encodes"] == _trials(o), (i, r["encodes"], o["encodes"])
         if o["success"]:
             assert r["data"] == o["data"], i
             assert np.float32(r["learned"].quality) == np.float32(o["quality"]), i
@@ -76,7 +83,7 @@ def test_8192_source_subsampled_decode_then_fit(codec, oracle, kind):
     res = codec.fit([st_dev[0][1]], MIB, 0.25)[0]
     o = oracle.fit(ref, MIB, 0.25)
     assert res["status"] == N.OK and res["success"] == o["success"] and o["success"]
-    assert res["data"] == o["data"] and res["encodes"] == o["encodes"]
+    assert res["data"] == o["data"] and res["encodes"] == _trials(o)
     assert np.float32(res["learned"].quality) == np.float32(o["quality"])
     assert res["learned"].scale == o["scale"]
     # the learned-cache key uses the decoded dims and the source file size (CacheTools.java:14-21)
