@@ -24,10 +24,6 @@
 
 namespace icx {
 
-#ifndef ICX_FDCT_EXP
-#define ICX_FDCT_EXP 0  // timing-only FDCT variants (scripts/huff_phases.py); 0 = the product
-#endif
-
 __constant__ uint8_t c_nat_to_zz[64];
 __constant__ uint8_t c_zz_to_nat[64];
 __constant__ uint32_t c_dc[2][16];    // (code << 8) | length, by category
@@ -309,7 +305,7 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
         total += run;
         __builtin_amdgcn_wave_barrier();
     }
-    if (ICX_FDCT_EXP != 2 && lane == 0 && total)  // EXP 2: timing only
+    if (lane == 0 && total)
         atomicAdd(ent + ((blockIdx.x * 4 + wave) & (ENT_SLOTS - 1)), (unsigned long long)total);
 }
 
@@ -433,10 +429,6 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
         return c;
     };
     const int64_t tile_id = (int64_t)my * ((D.mcux + FDC_MCU - 1) / FDC_MCU) + tx;
-#if ICX_FDCT_EXP == 1  // timing only: no list emission
-    if (t < nblk) D.ncoef[bbase + t] = (uint8_t)oz[t][t & 63];
-    if (true) { __syncthreads(); return; }
-#endif
     const int64_t base = tile_id * (FDC_BLK * COEF_SLOTS);
     unsigned long long* ent = (unsigned long long*)states[T.img].list_entries;
     auto luma = [](int a) { return a < 4; };  // one MCU per step: Y0 Y1 Y2 Y3 Cb Cr
@@ -566,9 +558,6 @@ __device__ __forceinline__ int nbits(int a) { return a ? 32 - __clz(a) : 0; }
 #define ICX_SLOT_WORDS 13
 #endif
 constexpr int SLOT_WORDS = ICX_SLOT_WORDS;
-#ifndef ICX_HUFF_EXP
-#define ICX_HUFF_EXP 0  // timing-only variants (scripts/huff_phases.sh); 0 = the product
-#endif
 
 constexpr int SLOT_BITS = SLOT_WORDS * 32;
 constexpr int AC_SIZES_ = 11;
@@ -605,19 +594,6 @@ struct LdsSink {
     }
 };
 
-#if ICX_HUFF_EXP == 7
-__device__ unsigned long long g_stats[6];
-extern "C" int icx_debug_huff_stats(unsigned long long* out)
-{
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), sizeof(g_stats));
-}
-#endif
-
-struct CountSink {  // timing experiments only (ICX_HUFF_EXP == 2)
-    int n;
-    __device__ __forceinline__ void put(uint32_t, int len) { n += len; }
-    __device__ __forceinline__ void finish() {}
-};
 
 struct GlobalSink {
     uint64_t acc;
@@ -773,11 +749,6 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     const QNode& N = nodes[S.node];
     const int cur = S.cur;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-#if ICX_HUFF_EXP == 4  // timing only: launch + descriptor lookup, nothing else
-    if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = 0u;  // sizes stay consistent
-    if (t == 0) D.chunk_bits[cur][chunk] = 0u;
-    return;
-#endif
 
     if (t < 128) {
         const int c = t >> 6, k = t & 63;
@@ -825,21 +796,6 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
 
     // ---- 1. encode_one_block into the slot (rarely: into the block's HBM spill)
     int bits = 0;
-#if ICX_HUFF_EXP == 3  // timing only: front (tables, list loads, DC exchange), no coding
-    if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = 0u;  // sizes stay consistent
-    if (t == 0) D.chunk_bits[cur][chunk] = (uint32_t)(ev[0] + ev[PRE - 1] + qprev) & 1u;
-    return;
-#endif
-#if ICX_HUFF_EXP == 2  // timing only: code lengths counted, no bit packing, nothing after
-    if (valid) {
-        CountSink cs{0};
-        encode_block(cs, ev, lst, cnt, dq - qprev, s_qf[tb], s_ac[tb], s_dc[tb]);
-        bits = cs.n;
-    }
-    if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = 0u;  // sizes stay consistent
-    if (t == 0) D.chunk_bits[cur][chunk] = (uint32_t)bits;
-    return;
-#endif
     if (valid) {
         const uint32_t sb = (uint32_t)(t * SLOT_WORDS * 4);
         LdsSink sink{0, 0, sb, sb + (SLOT_WORDS - 1) * 4, slots};
@@ -855,59 +811,6 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         }
     }
 
-#if ICX_HUFF_EXP == 7  // statistics only: list entries, wave-max lengths, entries that code
-    {
-        int nz = 0;
-        for (int i = 1; i < cnt; i++) {
-            const uint32_t e = lst[i];
-            nz += fabsf((float)((int32_t)e >> 6)) >= s_qf[tb][e & 63].x;
-        }
-        int mx = cnt, sm = cnt, sz = nz, nv = valid;
-        for (int d = 32; d >= 1; d >>= 1) {
-            mx = max(mx, __shfl_xor(mx, d, 64));
-            sm += __shfl_xor(sm, d, 64);
-            sz += __shfl_xor(sz, d, 64);
-            nv += __shfl_xor(nv, d, 64);
-        }
-        __shared__ uint8_t s_c[CHUNK_BLOCKS];
-        __shared__ uint8_t s_l[CHUNK_BLOCKS];
-        s_c[t] = (uint8_t)cnt;
-        s_l[t] = (uint8_t)(tb == 0);
-        __syncthreads();
-        if (t == 0) {
-            int h[65] = {0};
-            for (int i = 0; i < CHUNK_BLOCKS; i++) h[s_c[i]]++;
-            unsigned long long sorted = 0;  // descending: maxima at positions 0, 64, 128, 192
-            int pos = 0;
-            for (int v = 64; v >= 0; v--)
-                for (int k = 0; k < h[v]; k++, pos++)
-                    if ((pos & 63) == 0) sorted += 64ull * v;
-            unsigned long long split = 0;  // luma blocks first, then chroma, in block order
-            int mxw = 0;
-            pos = 0;
-            for (int pass = 1; pass >= 0; pass--)
-                for (int i = 0; i < CHUNK_BLOCKS; i++)
-                    if (s_l[i] == pass) {
-                        mxw = max(mxw, (int)s_c[i]);
-                        if ((++pos & 63) == 0) { split += 64ull * mxw; mxw = 0; }
-                    }
-            split += 64ull * mxw;
-            atomicAdd(&g_stats[4], sorted);
-            atomicAdd(&g_stats[5], split);
-        }
-        if (lane == 0) {
-            atomicAdd(&g_stats[0], (unsigned long long)sm);
-            atomicAdd(&g_stats[1], (unsigned long long)(64 * mx));
-            atomicAdd(&g_stats[2], (unsigned long long)sz);
-            atomicAdd(&g_stats[3], (unsigned long long)nv);
-        }
-    }
-#endif
-#if ICX_HUFF_EXP == 1  // timing only: encode, nothing after
-    if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = 0u;  // sizes stay consistent
-    if (t == 0) D.chunk_bits[cur][chunk] = (uint32_t)bits;
-    return;
-#endif
     // ---- 2. exclusive scan of block bits
     const int incl = wave_incl_scan(bits);
     if (lane == 63) s_wsum[wv] = incl;
@@ -946,11 +849,6 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         // position mod 8 (s_bin): the chunk's 0xFF-byte count for each
         // alignment k_scan may place it at.
         const uint32_t nwords = (total + 31) >> 5;
-#if ICX_HUFF_EXP == 8  // timing only: up to the scan (sizes stay consistent: no 0xFF)
-        if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = 0u;
-        if (t == 0) D.chunk_bits[cur][chunk] = total;
-        return;
-#endif
         if (bits > 0) {
             const uint32_t sh = off & 31, nwb = ((uint32_t)bits + 31) >> 5;
             uint32_t* o = s_out + (off >> 5);
@@ -961,17 +859,9 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
             }
         }
         __syncthreads();
-#if ICX_HUFF_EXP == 9  // timing only: up to the LDS assembly (sizes stay consistent)
-        if (t < 8) D.chunk_ffa[cur][chunk * 8 + t] = s_out[t] == 0xDEADBEEFu;
-        if (t == 0) D.chunk_bits[cur][chunk] = total;
-        return;
-#endif
         for (uint32_t j = t; j < nwords; j += CHUNK_BLOCKS) {
             const uint32_t w = s_out[j];
             dst[j] = w;
-#if ICX_HUFF_EXP == 10  // timing only: no 0xFF bins
-            continue;
-#endif
             uint64_t x = ((uint64_t)w << 32) | s_out[j + 1];
             x &= x << 1;
             x &= x << 2;
@@ -1001,7 +891,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     // 0xFF-byte count for each alignment k_scan may place it at.  Runs may
     // reach into the following blocks (their first <= 8 bits); nothing
     // follows the chunk's last bit here (k_scan checks the boundary bytes).
-    if (ICX_HUFF_EXP != 5 && bits > 0) {  // EXP 5: timing only, no 0xFF bins
+    if (bits > 0) {
         uint32_t la = 0;  // the <= 8 bits after this block, MSB-aligned
         int have = 0;
         for (int u = t + 1; have < 8 && u < nb; u++) {
@@ -1034,7 +924,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     }
 
     // ---- 4. gather the chunk's words
-    for (uint32_t j = (off + 31) >> 5; ICX_HUFF_EXP != 6 && j * 32 < off + bits; j++) {  // EXP 6: no gather
+    for (uint32_t j = (off + 31) >> 5; j * 32 < off + bits; j++) {
         uint32_t outw = 0;
         int have = 0, u = t;
         uint32_t p = j * 32 - off;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build an experimental libicx variant: build_variant.sh NAME "-DFLAG=..." -> image-compression_amd/lib/libicx_NAME.so
+# Build a libicx variant with tuning macros (ICX_PRE, ICX_SLOT_WORDS, ICX_FDCT_TILES): build_variant.sh NAME "-DFLAG=..." -> image-compression_amd/lib/libicx_NAME.so
 set -e
 cd "$(dirname "$0")/../image-compression_amd"
 mkdir -p build/var lib
