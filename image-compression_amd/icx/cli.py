@@ -7,7 +7,8 @@ defaults, plus GPU placement flags.
 
 Multi-GPU: either one process driving several devices (--devices, one worker
 thread per GPU sharing one L1 cache), or one process per GPU under torchrun
-(RANK/WORLD_SIZE/LOCAL_RANK): the file list is sharded by line index, result
+(RANK/WORLD_SIZE/LOCAL_RANK): the file list is sharded by file size
+(longest-processing-time first, pipeline.shard), result
 counters are summed and the learned-cache entries merged on rank 0, which
 writes the L2 cache (H2 AUTO_SERVER's multi-process role,
 H2CacheManager.java:34-35).

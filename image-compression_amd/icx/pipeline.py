@@ -420,9 +420,35 @@ def read_file_list(path) -> List[str]:
         return [ln.strip() for ln in f if ln.strip()]
 
 
-def shard(lines, rank: int, world: int):
-    """File-list sharding across ranks: line i goes to rank i % world."""
-    return [(i, p) for i, p in enumerate(lines) if i % world == rank]
+def _file_cost(path) -> int:
+    try:
+        return os.path.getsize(path)
+    except OSError:
+        return 0  # a missing file costs a stat (SKIPPED_NOT_FOUND)
+
+
+def shard(lines, rank: int, world: int, cost=_file_cost):
+    """File-list sharding across ranks, balanced by cost (longest processing
+    time first): files in decreasing cost (the file size: decode bytes, and
+    the pixels and trials that come with them — an 8K or a noise frame costs
+    about twice a smooth 4K one), each to the rank with the least cost so far
+    (ties: the lower rank, then the lower line index).  Every rank computes
+    the same assignment from the same list, so no exchange is needed.
+    Returns this rank's (line index, path) pairs in list order."""
+    if world <= 1:
+        return list(enumerate(lines))
+    import heapq
+    costs = [cost(p) for p in lines]
+    order = sorted(range(len(lines)), key=lambda i: (-costs[i], i))
+    heap = [(0, r) for r in range(world)]
+    mine = []
+    for i in order:
+        load, r = heapq.heappop(heap)
+        if r == rank:
+            mine.append(i)
+        heapq.heappush(heap, (load + costs[i] + 1, r))  # +1: empty files still cost a task
+    mine.sort()
+    return [(i, lines[i]) for i in mine]
 
 
 class CompressionBatch:

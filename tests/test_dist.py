@@ -20,7 +20,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, lst, out, cache, q):
+def _worker(rank, world, port, lst, out, cache, q, report_shard=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "image-compression_amd"))
@@ -35,7 +35,11 @@ def _worker(rank, world, port, lst, out, cache, q):
     b = pipeline.CompressionBatch(lst, out, CompressionParams(0.25, 1000, 100, 60, 20000), 1, cache,
                                   codecs=[OracleCodec()], group_size=2, rank=rank, world=world)
     rep, merged = run_distributed(b, dist)
-    q.put((rank, rep.total, rep.success, rep.failed, rep.original_size, len(merged)))
+    if report_shard:  # this rank's own shard (before the reduction): line indices and bytes
+        mine = pipeline.shard(pipeline.read_file_list(lst), rank, world)
+        q.put((rank, [i for i, _ in mine], sum(os.path.getsize(p) for _, p in mine), rep.total, rep.success))
+    else:
+        q.put((rank, rep.total, rep.success, rep.failed, rep.original_size, len(merged)))
     dist.destroy_process_group()
 
 
@@ -67,3 +71,32 @@ def test_two_rank_sharded_batch(tmp_path):
     assert sorted(os.listdir(out)) == sorted(os.path.basename(f) for f in files)
     from icx.cache import CacheManager
     assert len(CacheManager(tmp_path / "c").load_all_to_map()) == ncache >= 1
+
+
+def test_two_rank_shards_balance_skewed_sizes(tmp_path):
+    """gloo world_size 2 over a skewed list (two large files among small
+    ones, both large ones early in the list): each rank's shard holds within
+    10 % of the bytes, every file is compressed once."""
+    files = []
+    for i in range(12):
+        f = tmp_path / f"img{i}.jpg"
+        h, w = (300, 400) if i in (0, 2) else (60 + 3 * i, 110 + 10 * i)
+        Image.fromarray(noise(h, w, i)).save(f, "JPEG", quality=95)
+        files.append(str(f))
+    lst = tmp_path / "list.txt"
+    lst.write_text("\n".join(files))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, str(lst), str(tmp_path / "out"), str(tmp_path / "c"), q,
+                                            True)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(2))
+    assert sorted(res[0][1] + res[1][1]) == list(range(12))
+    b0, b1 = res[0][2], res[1][2]
+    assert max(b0, b1) <= 1.10 * min(b0, b1), (b0, b1)
+    assert res[0][3:] == res[1][3:] == (12, 12)

@@ -166,6 +166,64 @@ def test_shard_partition():
     assert [len(p) for p in parts] == [4, 4, 3]
 
 
+def test_shard_balances_skewed_costs():
+    """Cost-balanced sharding (8K and noise files cost ~2x a
+    smooth 4K one): a skewed mix of file costs splits within 10 % across 8
+    ranks, where the old i % world split is off by far more; every line goes
+    to exactly one rank and each shard keeps list order."""
+    rng = np.random.default_rng(5)
+    costs = {}
+    lines = []
+    for i in range(400):  # 4K smooth ~2.5 MB, 4K noise ~7.7 MB, a few 8K ~30 MB, in runs
+        c = [2_500_000, 7_700_000, 30_000_000][0 if i % 50 < 30 else 1 if i % 50 < 47 else 2]
+        c += int(rng.integers(0, 200_000))
+        lines.append(f"f{i}.jpg")
+        costs[lines[-1]] = c
+    world = 8
+    parts = [pipeline.shard(lines, r, world, cost=costs.__getitem__) for r in range(world)]
+    idx = [i for p in parts for i, _ in p]
+    assert sorted(idx) == list(range(len(lines)))
+    assert all([i for i, _ in p] == sorted(i for i, _ in p) for p in parts)
+    loads = [sum(costs[f] for _, f in p) for p in parts]
+    assert max(loads) <= 1.10 * min(loads)
+    rr = [sum(costs[f] for i, f in enumerate(lines) if i % world == r) for r in range(world)]
+    assert max(rr) > 1.10 * min(rr)  # the skew is real: round robin would not balance it
+
+
+def test_two_codecs_share_the_work_queue(tmp_path):
+    """In-process --devices: one worker thread per codec pulls device groups
+    from one queue and they share one L1 cache; every output equals the
+    single-codec oracle run."""
+    import time
+
+    class SlowCodec(OracleCodec):
+        def fit(self, *a, **k):
+            time.sleep(0.05)  # long enough that the other worker takes the next group
+            return super().fit(*a, **k)
+
+    files = []
+    for i in range(8):
+        f = tmp_path / f"img{i}.jpg"
+        # distinct cache keys (w // 100 differs): outputs do not depend on completion order
+        write_jpeg(f, (smooth if i % 2 else noise)(70 + 4 * i, 150 + 100 * i, i))
+        files.append(str(f))
+    lst = tmp_path / "list.txt"
+    lst.write_text("\n".join(files))
+    codecs = [SlowCodec(), SlowCodec()]
+    out = tmp_path / "out"
+    b = pipeline.CompressionBatch(str(lst), str(out), P, 1, str(tmp_path / "c"), codecs=codecs, group_size=1)
+    rep = b.execute()
+    assert rep.total == 8 and rep.success == 8
+    assert all(c.calls >= 1 for c in codecs) and sum(c.calls for c in codecs) == 8
+    ref_out = tmp_path / "ref"
+    ref = pipeline.CompressionBatch(str(lst), str(ref_out), P, 1, str(tmp_path / "c2"), codecs=[OracleCodec()],
+                                    group_size=1)
+    assert ref.execute().success == 8
+    for f in files:
+        n = os.path.basename(f)
+        assert (out / n).read_bytes() == (ref_out / n).read_bytes()
+
+
 def test_png_writer_adaptive_filters_round_trip():
     """icx.pngio: every row filter the adaptive choice can pick decodes back to
     the exact pixels (PNG parity is on pixels)."""
