@@ -174,6 +174,51 @@ def e2e_leg(codec, dev, n_frames, steps, distinct=8, cpu_sample=0, threads=16):
     return line
 
 
+def link_rates(dev, nbytes=1 << 30, reps=5):
+    """PCIe link rates of this box: one pinned host buffer <-> HBM, GB/s."""
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    rates = {}
+    for name, (dst, src) in (("h2d", (d, h)), ("d2h", (h, d))):
+        dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        rates[name] = nbytes * reps / (time.perf_counter() - t0) / 1e9
+    return rates
+
+
+def host_io_leg(codec, frames, n, steps, warmup, cached):
+    """SURVEY §8(d)'s headline definition, PCIe included: decoded BGR frames
+    in pinned host memory -> final JPEG bytes in pinned host memory.  The
+    library uploads sub-batch s+1 and downloads s-1 on their own streams while
+    s computes (icx_runtime.cpp run_batch, prefetch)."""
+    dev = frames[0].device
+    link = link_rates(dev)
+    hf = [f.cpu().pin_memory() for f in frames[:n]]
+    outs = torch.empty((n, TARGET + 1), dtype=torch.uint8).pin_memory()
+    b = codec.prepare(hf, TARGET, Q0, cached=cached[:n] if cached else None, outputs=[outs[i] for i in range(n)])
+    for _ in range(max(1, warmup)):
+        b.run()
+    res = b.results()
+    assert all(r["success"] and r["status"] == 0 for r in res), "host-io leg: frames failed"
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        b.run()
+    dt = (time.perf_counter() - t0) / steps
+    up = sum(f.numel() for f in hf)
+    down = sum(r["out_len"] for r in res)
+    h2d = up / dt / 1e9
+    return {"metric": "megapixels/sec JPEG encode, pinned host BGR in -> host JPEG bytes out (PCIe included)",
+            "value": round(n * W * H / 1e6 / dt, 1), "unit": "MP/s", "frames": n, "steps": steps,
+            "ms_per_step": round(dt * 1e3, 3),
+            "h2d_GBps": round(h2d, 2), "d2h_GBps": round(down / dt / 1e9, 2),
+            "link_h2d_GBps": round(link["h2d"], 2), "link_d2h_GBps": round(link["d2h"], 2),
+            "h2d_frac_of_link": round(h2d / link["h2d"], 4)}
+
+
 def e2e_cpu_baseline(srcs, n_sample, threads):
     """The same per-image loop on host cores with the oracle (test
     infrastructure): IJG-6b decode restatement + compressJpgWithTargetSize
@@ -206,6 +251,8 @@ def main():
     ap.add_argument("--images", type=int, default=1000, help="4K frames per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=320, help="4K frames for the CPU baseline (~10 s on 16 cores)")
     ap.add_argument("--e2e", type=int, default=200, help="frames of the decode+encode leg (0 = skip)")
+    ap.add_argument("--host-io-frames", type=int, default=200,
+                    help="frames of the PCIe-inclusive leg (pinned host in/out; 0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
     ap.add_argument("--target", type=int, default=TARGET, help="-t bytes (default 1 MiB)")
@@ -312,6 +359,10 @@ def main():
         "stages": stages,
         "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k, v in kstats.items()},
     }
+    if rank == 0 and world == 1 and args.host_io_frames and not args.host_io:
+        batch = None
+        line["host_io"] = host_io_leg(codec, frames, min(args.host_io_frames, args.images), args.steps,
+                                      args.warmup, cached)
     if rank == 0 and world == 1 and args.e2e and not args.host_io:
         batch = None
         line["e2e"] = e2e_leg(codec, dev, args.e2e, args.steps,

@@ -175,6 +175,12 @@ struct icx_ctx {
     size_t budget = 0;  // device workspace budget per sub-batch
     DevPool pool;
     DevPool hpool;  // pinned host buffers (hpool.host = true)
+    // Host-buffer batches: inputs are uploaded (io_up) into one of two staging
+    // arenas while the previous sub-batch computes, outputs leave (io_down)
+    // while the next one computes; created on first use.
+    hipStream_t io_up = nullptr, io_down = nullptr;
+    icx::DevArena stage[2];
+    hipEvent_t ev_up[2] = {nullptr, nullptr}, ev_down[2] = {nullptr, nullptr}, ev_done = nullptr;
 };
 
 namespace icx {

@@ -484,7 +484,19 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
         if (j.status == ICX_OK && mode != Mode::Search && mode != Mode::Fdct && !j.out) j.status = ICX_E_NULL;
         if (j.status == ICX_OK) order.push_back(i);
     }
-    // ---- device workspace per image (what the sub-batch loop below takes)
+    // ---- device workspace per image (what the sub-batch loop below takes);
+    // host inputs and outputs are staged separately (stage_bytes), in one of
+    // two arenas that alternate between sub-batches
+    auto out_staging = [&](const icx_fit_job& j) -> size_t {
+        if (!(mode == Mode::Fit || mode == Mode::Encode) || is_device_ptr(j.out)) return 0;
+        ImgDesc g{};
+        geometry(g, j.img.width, j.img.height, j.img.fmt);
+        return std::min<uint64_t>(worst_file(g), j.cap);
+    };
+    auto stage_bytes = [&](const icx_fit_job& j) -> size_t {
+        const size_t px = (size_t)j.img.width * j.img.height * channels(j.img.fmt);
+        return (is_device_ptr(j.img.px) ? 0 : align_up(px, 256)) + align_up(out_staging(j), 256);
+    };
     auto workspace = [&](const icx_fit_job& j) -> size_t {
         ImgDesc g{};
         geometry(g, j.img.width, j.img.height, j.img.fmt);
@@ -492,29 +504,113 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
         size_t per = coef_bytes(g) + (size_t)g.nchunks * CHUNK_BLOCKS * 5 + (size_t)g.nblocks * BLOCK_WORDS * 4 + 1024 +
                      2 * ((size_t)g.nchunks * CHUNK_WORDS + 1) * 4 +
                      (size_t)g.nchunks * (2 * 4 + 2 * 8 + 2 * 4 + 2 * 32 + 8) + 64 + 8 * 256 + 4096;
-        if (!is_device_ptr(j.img.px)) per += px;                   // input staging
-        if (mode == Mode::Fit) per += px;                         // resize buffer
-        if ((mode == Mode::Fit || mode == Mode::Encode) && !is_device_ptr(j.out))
-            per += std::min<uint64_t>(worst_file(g), j.cap);      // output staging
+        if (mode == Mode::Fit) per += px;  // resize buffer
         return per;
     };
-    // Sub-batches of about equal size: as few as the budget allows.
-    size_t all_need = 0;
-    for (int i : order) all_need += workspace(jobs[i]);
-    const size_t nsub = std::max<size_t>(1, (all_need + c->budget - 1) / c->budget);
+    // Sub-batches of about equal size: as few as the budget allows (the two
+    // staging arenas count against it).
+    size_t all_need = 0, all_stage = 0;
+    for (int i : order) {
+        all_need += workspace(jobs[i]) + 2 * stage_bytes(jobs[i]);
+        all_stage += stage_bytes(jobs[i]);
+    }
+    size_t nsub = std::max<size_t>(1, (all_need + c->budget - 1) / c->budget);
+    // Host buffers: sub-batches of ~512 MB of uploads (up to 16), so that all
+    // but the first upload and the last sub-batch's kernels and downloads
+    // overlap (the link moves ~57 GB/s, the kernels ~30x that)
+    if (all_stage > 0)
+        nsub = std::max(nsub, std::min<size_t>({16, order.size(), (all_stage + (512u << 20) - 1) / (512u << 20)}));
     const size_t share = (all_need + nsub - 1) / nsub;
-    size_t pos = 0;
-    while (pos < order.size()) {
-        std::unique_ptr<HostSpan> prep(new HostSpan{c, "host.prep"});  // until the first launch
-        // ---- size a sub-batch against the workspace budget
+    std::vector<std::vector<int>> subs;
+    std::vector<size_t> sub_need;
+    size_t stage_max = 0;
+    for (size_t pos = 0; pos < order.size();) {
         std::vector<int> sub;
-        size_t need = 1 << 20;
+        size_t need = 1 << 20, acct = 1 << 20, st = 0;
         while (pos < order.size()) {
-            const size_t per = workspace(jobs[order[pos]]);
-            if (!sub.empty() && (need + per > c->budget || need - (1 << 20) >= share)) break;
+            const icx_fit_job& j = jobs[order[pos]];
+            const size_t per = workspace(j), sb = stage_bytes(j);
+            if (!sub.empty() && (acct + per + 2 * sb > c->budget || acct - (1 << 20) >= share)) break;
             need += per;
+            acct += per + 2 * sb;
+            st += sb;
             sub.push_back(order[pos++]);
         }
+        stage_max = std::max(stage_max, st);
+        subs.push_back(std::move(sub));
+        sub_need.push_back(need);
+    }
+    // ---- host staging: uploads of sub-batch s+1 (io_up) run while s
+    // computes; downloads of s (io_down) while s+1 computes
+    struct HostIO {
+        std::vector<uint8_t*> px, out;
+        bool up = false, down = false;
+    };
+    std::vector<HostIO> hio(subs.size());
+    struct IoDrain {  // every exit waits for the copies that touch the caller's buffers
+        icx_ctx* c;
+        ~IoDrain()
+        {
+            if (c->io_up) hipStreamSynchronize(c->io_up);
+            if (c->io_down) hipStreamSynchronize(c->io_down);
+        }
+    } io_drain{c};
+    if (stage_max > 0) {
+        if (!c->io_up) {
+            hipError_t e = hipStreamCreateWithFlags(&c->io_up, hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->io_down, hipStreamNonBlocking);
+            for (int b = 0; b < 2 && e == hipSuccess; b++) {
+                e = hipEventCreateWithFlags(&c->ev_up[b], hipEventDisableTiming);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_down[b], hipEventDisableTiming);
+            }
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming);
+            if (e != hipSuccess) return hip_fail(c, e, "host I/O streams");
+        }
+        // both arenas reserved before any work: a re-allocation (hipFree)
+        // would synchronise the device in the middle of the pipeline
+        for (int b = 0; b < 2 && b < (int)subs.size(); b++) {
+            hipError_t e = c->stage[b].reserve(stage_max + 4096);
+            if (e != hipSuccess) {
+                for (int i : order) jobs[i].status = ICX_E_NOMEM;
+                (void)hipGetLastError();
+                return fail(c, ICX_E_NOMEM, "host staging allocation failed");
+            }
+        }
+    }
+    auto prefetch = [&](size_t si) -> icx_status {
+        if (si >= subs.size() || stage_max == 0) return ICX_OK;
+        const std::vector<int>& sub = subs[si];
+        HostIO& H = hio[si];
+        DevArena& A = c->stage[si & 1];
+        A.used = 0;
+        H.px.assign(sub.size(), nullptr);
+        H.out.assign(sub.size(), nullptr);
+        // the arena's last reader (sub-batch si-2's downloads) must be done
+        hipError_t e = hipStreamWaitEvent(c->io_up, c->ev_down[si & 1], 0);
+        for (size_t k = 0; k < sub.size() && e == hipSuccess; k++) {
+            const icx_fit_job& j = jobs[sub[k]];
+            if (!is_device_ptr(j.img.px)) {
+                const size_t row = (size_t)j.img.width * channels(j.img.fmt);
+                H.px[k] = (uint8_t*)A.take(row * j.img.height);
+                e = (size_t)j.img.stride == row  // packed rows: one linear copy
+                        ? hipMemcpyAsync(H.px[k], j.img.px, row * j.img.height, hipMemcpyHostToDevice, c->io_up)
+                        : hipMemcpy2DAsync(H.px[k], row, j.img.px, j.img.stride, row, j.img.height,
+                                           hipMemcpyHostToDevice, c->io_up);
+                H.up = true;
+            }
+            if (out_staging(j)) {
+                H.out[k] = (uint8_t*)A.take(out_staging(j));
+                H.down = true;
+            }
+        }
+        if (e == hipSuccess && H.up) e = hipEventRecord(c->ev_up[si & 1], c->io_up);
+        return e == hipSuccess ? ICX_OK : hip_fail(c, e, "input upload");
+    };
+    if (icx_status ps = prefetch(0)) return ps;
+    for (size_t si = 0; si < subs.size(); si++) {
+        std::unique_ptr<HostSpan> prep(new HostSpan{c, "host.prep"});  // until the first launch
+        const std::vector<int>& sub = subs[si];
+        const size_t need = sub_need[si];
         if (c->prof) {  // sub-batches per call and their workspace (reported by bench.py)
             c->stats["subbatch"].launches++;
             c->stats["subbatch"].units += (int64_t)(need >> 20);
@@ -524,6 +620,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             for (int i : sub) jobs[i].status = ICX_E_NOMEM;
             (void)hipGetLastError();
             c->err = "device workspace allocation failed";
+            if (icx_status ps = prefetch(si + 1)) return ps;  // the next sub-batch still needs its inputs
             continue;
         }
         c->dev.used = 0;
@@ -582,17 +679,12 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                 d.chunk_ffa[b] = (uint32_t*)c->dev.take((size_t)d.nchunks * 32);
             }
             d.chunk_ffoff = (uint64_t*)c->dev.take((size_t)d.nchunks * 8);
-            // input pixels
-            if (is_device_ptr(j.img.px)) {
+            // input pixels (host rows: uploaded into the staging arena by prefetch)
+            if (hio[si].px.empty() || !hio[si].px[k]) {
                 I.dpx = j.img.px;
             } else {
-                const size_t row = (size_t)j.img.width * I.nch;
-                uint8_t* st = (uint8_t*)c->dev.take(row * j.img.height);
-                e = hipMemcpy2DAsync(st, row, j.img.px, j.img.stride, row, j.img.height, hipMemcpyHostToDevice,
-                                     c->stream);
-                if (e != hipSuccess) return hip_fail(c, e, "input upload");
-                I.dpx = st;
-                d.stride = (int32_t)row;
+                I.dpx = hio[si].px[k];
+                d.stride = (int32_t)((size_t)j.img.width * I.nch);
             }
             d.px = I.dpx;
             I.orig = d;
@@ -602,15 +694,13 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             I.host_out = false;
             I.dout = nullptr;
             if (mode == Mode::Fit || mode == Mode::Encode) {
-                if (is_device_ptr(j.out)) {
+                if (hio[si].out.empty() || !hio[si].out[k]) {
                     I.dout = j.out;
                     d.cap = j.cap;
-                } else {
-                    const uint64_t cap = std::min<uint64_t>(worst_file(d), j.cap);
-                    I.dout = (uint8_t*)c->dev.take(cap);
+                } else {  // staging bound >= any file we can produce
+                    I.dout = hio[si].out[k];
                     I.host_out = true;
-                    d.cap = cap;
-                    if (cap < j.cap) d.cap = cap;  // staging bound >= any file we can produce
+                    d.cap = std::min<uint64_t>(worst_file(d), j.cap);
                 }
             }
             d.out = I.dout;
@@ -673,6 +763,11 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
         if (!B.h_state) return fail(c, ICX_E_NOMEM, "pinned staging exhausted");
         icx_status s = upload(c, B.d_nodes, B.nodes.data(), sizeof(QNode) * B.nodes.size());
         if (s) return s;
+        // this sub-batch's pixels have landed before its first kernel; the
+        // next sub-batch's upload starts behind them on io_up
+        if (hio[si].up && (e = hipStreamWaitEvent(c->stream, c->ev_up[si & 1], 0)) != hipSuccess)
+            return hip_fail(c, e, "hipStreamWaitEvent");
+        if ((s = prefetch(si + 1))) return s;
 
         std::vector<int> all(m);
         for (int k = 0; k < m; k++) all[k] = k;
@@ -786,8 +881,14 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                 pend.swap(rest);
             }
         }
-        // ---- results + host outputs
+        // ---- results + host outputs (downloads on io_down, behind this
+        // sub-batch's kernels; they overlap the next sub-batch)
         HostSpan res{c, "host.results"};
+        if (hio[si].down) {
+            if ((e = hipEventRecord(c->ev_done, c->stream)) != hipSuccess ||
+                (e = hipStreamWaitEvent(c->io_down, c->ev_done, 0)) != hipSuccess)
+                return hip_fail(c, e, "output download");
+        }
         for (int k = 0; k < m; k++) {
             Item& I = B.it[k];
             icx_fit_job& j = *I.job;
@@ -814,10 +915,12 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             }
             j.status = ICX_OK;
             if (I.host_out) {
-                e = hipMemcpyAsync(j.out, I.dout, j.out_len, hipMemcpyDeviceToHost, c->stream);
+                e = hipMemcpyAsync(j.out, I.dout, j.out_len, hipMemcpyDeviceToHost, c->io_down);
                 if (e != hipSuccess) return hip_fail(c, e, "output download");
             }
         }
+        if (hio[si].down && (e = hipEventRecord(c->ev_down[si & 1], c->io_down)) != hipSuccess)
+            return hip_fail(c, e, "output download");
         e = hipStreamSynchronize(c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "hipStreamSynchronize");
         if (search_out && m > 0 && sub[0] == 0) *search_out = B.state[0];  // trial record of job 0
@@ -950,6 +1053,17 @@ void icx_destroy(icx_ctx* ctx)
     for (auto& p : ctx->pending) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
     for (auto e : ctx->evpool) hipEventDestroy(e);
     hipStreamDestroy(ctx->stream);
+    if (ctx->io_up) {
+        hipStreamSynchronize(ctx->io_up);
+        hipStreamSynchronize(ctx->io_down);
+        hipStreamDestroy(ctx->io_up);
+        hipStreamDestroy(ctx->io_down);
+        for (int b = 0; b < 2; b++) {
+            if (ctx->ev_up[b]) hipEventDestroy(ctx->ev_up[b]);
+            if (ctx->ev_down[b]) hipEventDestroy(ctx->ev_down[b]);
+        }
+        if (ctx->ev_done) hipEventDestroy(ctx->ev_done);
+    }
     delete ctx;
 }
 

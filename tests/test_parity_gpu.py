@@ -251,3 +251,35 @@ def test_same_size_batch_matches_oracle(codec, oracle):
                 assert r["data"] == o["data"], (i, target)
                 assert np.float32(r["learned"].quality) == np.float32(o["quality"])
                 assert r["learned"].scale == o["scale"]
+
+
+def test_host_buffers_pipelined_over_subbatches(oracle, monkeypatch):
+    """Host inputs and outputs (pageable numpy and pinned torch) through the
+    pipelined host I/O of run_batch: a small workspace budget forces several
+    sub-batches, so uploads of sub-batch s+1 and downloads of s-1 overlap the
+    kernels of s on their own streams.  Every file equals the oracle's."""
+    import torch
+    monkeypatch.setenv("ICX_WORKSPACE_MB", "24")
+    c = icx.Codec(0)
+    try:
+        imgs, targets = [], []
+        for i in range(9):
+            h, w = 360 + 24 * i, 520 + 40 * i
+            im = (smooth if i % 2 else noise)(h, w, 40 + i)
+            imgs.append(torch.from_numpy(im).pin_memory() if i % 3 == 0 else im)
+            targets.append(h * w // 5)
+        c.profile(True)
+        c.profile_reset()
+        for target in (min(targets), max(targets)):
+            res = c.fit(imgs, target, 0.25)
+            for i, r in enumerate(res):
+                im = imgs[i].numpy() if hasattr(imgs[i], "numpy") else imgs[i]
+                o = oracle.fit(im, target, 0.25)
+                assert r["status"] == 0 and r["success"] == o["success"], (i, target)
+                if o["success"]:
+                    assert r["data"] == o["data"], (i, target)
+                    assert np.float32(r["learned"].quality) == np.float32(o["quality"])
+                    assert r["learned"].scale == o["scale"]
+        assert c.profile_query("subbatch")["launches"] >= 6  # >= 3 sub-batches per call
+    finally:
+        c.close()
