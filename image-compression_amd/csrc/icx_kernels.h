@@ -20,7 +20,7 @@ void launch_scan(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, h
 void launch_ffscan(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st);
 void launch_stuff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks,
                   hipStream_t st);
-void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int nch, uint8_t* dst, int dw,
+void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int fmt, uint8_t* dst, int dw,
                    int dh, int dstride, hipStream_t st);
 
 }  // namespace icx

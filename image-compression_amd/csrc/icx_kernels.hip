@@ -19,6 +19,7 @@
 
 #include <algorithm>
 
+#include "../../include/icx.h"
 #include "icx_internal.h"
 #include "icx_kernels.h"
 
@@ -1275,6 +1276,69 @@ __global__ __launch_bounds__(256) void k_resize(ResizeArgs a)
     }
 }
 
+// Four-byte pixels (ImageTools.java:12-15 keeps the source type): Java2D's
+// TransformHelper fetches the four neighbours as IntArgbPre (colours times
+// alpha through AlphaMath's mul8table; an opaque type's alpha is 0xff),
+// interpolates the four channels like k_resize, and the SrcOver mask blit onto
+// the new all-zero image stores alpha 0 as a zero pixel, alpha 0xff as is,
+// else un-premultiplies through div8table.  XRGB (TYPE_INT_RGB) stores 0 in
+// its unused byte.  AB = alpha byte (0: ABGR, 3: BGRA / RGBA).
+__device__ __forceinline__ uint32_t mul8(uint32_t a, uint32_t c)  // AlphaMath.c mul8table[a][c]
+{
+    return ((c * (a * 0x010101u) + (1u << 23)) >> 24) & 0xffu;
+}
+
+template <int AB, bool OPAQUE>
+__global__ __launch_bounds__(256) void k_resize4(ResizeArgs a)
+{
+    const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (dx >= a.dw || dy >= a.dh) return;
+    const int64_t half = (int64_t)1 << 31;
+    const int64_t yl = a.y0l + (int64_t)dy * a.dyl - half;
+    const int64_t xl = a.x0l + (int64_t)dx * a.dxl - half;
+    const int yw = (int)(yl >> 32), xw = (int)(xl >> 32);
+    const int yf = (int)((uint32_t)yl >> 24), xf = (int)((uint32_t)xl >> 24);
+    int ya, yb, xa, xb;
+    if (yw < 0) ya = yb = 0; else if (yw + 1 >= a.sh) ya = yb = yw; else { ya = yw; yb = yw + 1; }
+    if (xw < 0) xa = xb = 0; else if (xw + 1 >= a.sw) xa = xb = xw; else { xa = xw; xb = xw + 1; }
+    const GAS uint32_t* ra = (const GAS uint32_t*)(a.src + (size_t)ya * a.sstride);
+    const GAS uint32_t* rb = (const GAS uint32_t*)(a.src + (size_t)yb * a.sstride);
+    const uint32_t p[4] = {ra[xa], ra[xb], rb[xa], rb[xb]};
+    uint32_t pre[4][4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        const uint32_t al = OPAQUE ? 255u : (p[s] >> (8 * AB)) & 255u;
+#pragma unroll
+        for (int b = 0; b < 4; b++) pre[s][b] = b == AB ? al : mul8(al, (p[s] >> (8 * b)) & 255u);
+    }
+    int v[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        const int top = ((int)pre[0][b] << 8) + ((int)pre[1][b] - (int)pre[0][b]) * xf;
+        const int bot = ((int)pre[2][b] << 8) + ((int)pre[3][b] - (int)pre[2][b]) * xf;
+        v[b] = (((top << 8) + (bot - top) * yf) + (1 << 15)) >> 16;
+    }
+    const uint32_t al = (uint32_t)v[AB];
+    uint32_t out = 0;
+    if (OPAQUE) {
+#pragma unroll
+        for (int b = 0; b < 4; b++) out |= b == AB ? 0u : (uint32_t)v[b] << (8 * b);
+    } else if (al == 255u) {
+#pragma unroll
+        for (int b = 0; b < 4; b++) out |= (uint32_t)v[b] << (8 * b);
+    } else if (al != 0u) {  // div8table[al][c]: c >= al gives 255
+        const uint32_t inc = ((0xffu << 24) + al / 2) / al;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const uint32_t c = (uint32_t)v[b];
+            const uint32_t d = b == AB ? al : c >= al ? 255u : ((1u << 23) + c * inc) >> 24;
+            out |= d << (8 * b);
+        }
+    }
+    *(GAS uint32_t*)(a.dst + (size_t)dy * a.dstride + (size_t)dx * 4) = out;
+}
+
 // =================================================================== host side
 hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat[64],
                             const uint32_t dc[2][16], const uint32_t ac[2][256],
@@ -1357,12 +1421,12 @@ void launch_stuff(const ImgDesc* d, const ImgState* s, const QNode* n, const Pla
     ICX_LAUNCH(k_stuff, grid, dim3(256), 0, st, d, s, n, plan_ids(p), p.prefix, p.m);
 }
 
-void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int nch, uint8_t* dst, int dw, int dh,
+void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int fmt, uint8_t* dst, int dw, int dh,
                    int dstride, hipStream_t st)
 {
     ResizeArgs a;
     a.src = src; a.dst = dst;
-    a.sw = sw; a.sh = sh; a.sstride = sstride; a.nch = nch;
+    a.sw = sw; a.sh = sh; a.sstride = sstride; a.nch = fmt == ICX_GRAY8 ? 1 : fmt <= ICX_RGB24 ? 3 : 4;
     a.dw = dw; a.dh = dh; a.dstride = dstride; a.pad = 0;
     // AffineTransform.scale(dw/sw, dh/sh).createInverse(): m00 = 1.0 / (dw/sw)
     const double ix = 1.0 / ((double)dw / sw), iy = 1.0 / ((double)dh / sh);
@@ -1370,7 +1434,14 @@ void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int nch, uin
     a.dyl = (int64_t)(iy * 4294967296.0);
     a.x0l = (int64_t)(0.5 * ix * 4294967296.0);  // transform of the first pixel centre (0.5)
     a.y0l = (int64_t)(0.5 * iy * 4294967296.0);
-    ICX_LAUNCH(k_resize, dim3(grid_of(dw, 64), grid_of(dh, 4)), dim3(256), 0, st, a);
+    const dim3 grid(grid_of(dw, 64), grid_of(dh, 4));
+    switch (fmt) {
+    case ICX_XRGB32: ICX_LAUNCH((k_resize4<3, true>), grid, dim3(256), 0, st, a); break;
+    case ICX_ARGB32:
+    case ICX_RGBA32: ICX_LAUNCH((k_resize4<3, false>), grid, dim3(256), 0, st, a); break;
+    case ICX_ABGR32: ICX_LAUNCH((k_resize4<0, false>), grid, dim3(256), 0, st, a); break;
+    default: ICX_LAUNCH(k_resize, grid, dim3(256), 0, st, a);
+    }
 }
 
 }  // namespace icx

@@ -142,7 +142,7 @@ int build_tree(float lo, float hi, int iter, std::vector<QNode>& nodes, int& dep
     return idx;
 }
 
-int channels(int fmt) { return fmt == ICX_GRAY8 ? 1 : 3; }
+int channels(int fmt) { return fmt == ICX_GRAY8 ? 1 : fmt <= ICX_RGB24 ? 3 : 4; }
 
 void geometry(ImgDesc& d, int w, int h, int fmt)
 {
@@ -333,7 +333,8 @@ void stage_pixels(Batch& B, int i, double scale)
         icx_scaled_dims(I.orig.w, I.orig.h, scale, &dw, &dh);
         {
             Timed tm(c, "resize", (int64_t)dw * dh);
-            launch_resize(I.dpx, I.orig.w, I.orig.h, I.orig.stride, I.nch, I.dresize, dw, dh, dw * I.nch, c->stream);
+            launch_resize(I.dpx, I.orig.w, I.orig.h, I.orig.stride, I.orig.fmt, I.dresize, dw, dh, dw * I.nch,
+                          c->stream);
         }
         geometry(d, dw, dh, I.orig.fmt);
         d.px = I.dresize;
@@ -458,8 +459,9 @@ icx_status validate(const icx_image* img)
 {
     if (!img || !img->px) return ICX_E_NULL;
     if (img->width <= 0 || img->height <= 0 || img->width > 65535 || img->height > 65535) return ICX_E_INVALID;
-    if (img->fmt < ICX_BGR24 || img->fmt > ICX_GRAY8) return ICX_E_INVALID;
+    if (img->fmt < ICX_BGR24 || img->fmt > ICX_RGBA32) return ICX_E_INVALID;
     if (img->stride < img->width * channels(img->fmt)) return ICX_E_INVALID;
+    if (channels(img->fmt) == 4 && (((uintptr_t)img->px | (uintptr_t)img->stride) & 3)) return ICX_E_INVALID;
     return ICX_OK;
 }
 
@@ -481,6 +483,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
         j.learned.scale = 0.0;
         j.encodes = 0;
         j.status = validate(&j.img);
+        if (j.status == ICX_OK && j.img.fmt > ICX_GRAY8) j.status = ICX_E_UNSUPPORTED;  // JPEG: no alpha rasters
         if (j.status == ICX_OK && mode != Mode::Search && mode != Mode::Fdct && !j.out) j.status = ICX_E_NULL;
         if (j.status == ICX_OK) order.push_back(i);
     }
@@ -1206,7 +1209,7 @@ icx_status icx_resize_bilinear(icx_ctx* ctx, const icx_image* src, uint8_t* dst,
     uint8_t* d = dout ? dst : (uint8_t*)ctx->dev.take((size_t)dst_stride * dst_h);
     {
         Timed tm(ctx, "resize", (int64_t)dst_w * dst_h);
-        launch_resize(s, src->width, src->height, sstride, nch, d, dst_w, dst_h, dst_stride, ctx->stream);
+        launch_resize(s, src->width, src->height, sstride, src->fmt, d, dst_w, dst_h, dst_stride, ctx->stream);
     }
     if (!dout) {
         e = hipMemcpyAsync(dst, d, (size_t)dst_stride * dst_h, hipMemcpyDeviceToHost, ctx->stream);

@@ -12,8 +12,9 @@ LIB_PATH = os.environ.get("ICX_LIB") or os.path.join(os.path.dirname(_HERE), "li
 
 # icx_status
 OK, E_INVALID, E_NOMEM, E_DEVICE, E_BUFFER, E_UNSUPPORTED, E_CORRUPT, E_NULL = range(8)
-# icx_fmt
-BGR24, RGB24, GRAY8 = 0, 1, 2
+# icx_fmt (XRGB32/ARGB32: TYPE_INT_RGB/ARGB int rasters, ABGR32: TYPE_4BYTE_ABGR, RGBA32: PNG order)
+BGR24, RGB24, GRAY8, XRGB32, ARGB32, ABGR32, RGBA32 = range(7)
+CHANNELS = {BGR24: 3, RGB24: 3, GRAY8: 1, XRGB32: 4, ARGB32: 4, ABGR32: 4, RGBA32: 4}
 
 EXPORTS = [
     "icx_abi_version", "icx_create", "icx_destroy", "icx_status_string", "icx_last_error",
@@ -24,6 +25,7 @@ EXPORTS = [
     "icx_profile_enable", "icx_profile_reset", "icx_profile_query",
     "icx_jpeg_info", "icx_decode_jpg", "icx_decode_jpg_batch", "icx_debug_decode_coefs",
     "icx_device_alloc", "icx_device_free", "icx_memcpy", "icx_host_alloc", "icx_host_free",
+    "icx_png_bound", "icx_png_encode",
 ]
 
 
@@ -120,12 +122,14 @@ def load():
         "icx_memcpy": (c.c_int, [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]),
         "icx_host_alloc": (c.c_int, [c.c_void_p, c.c_size_t, P(c.c_void_p)]),
         "icx_host_free": (c.c_int, [c.c_void_p, c.c_void_p]),
+        "icx_png_bound": (c.c_size_t, [P(Image)]),
+        "icx_png_encode": (c.c_int, [P(Image), c.c_int32, c.c_void_p, c.c_size_t, P(c.c_size_t)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
-    if lib.icx_abi_version() != 1:
+    if lib.icx_abi_version() != 2:
         raise NativeLibraryError("libicx ABI version mismatch")
     _lib = lib
     return lib

@@ -92,11 +92,21 @@ def create_key(image, file_size) -> SimilarityKey:
 
 
 def _fmt_of(img):
+    """The BufferedImage type of an array: (H, W) grey = TYPE_BYTE_GRAY,
+    (H, W, 3) = TYPE_3BYTE_BGR, (H, W, 4) = TYPE_4BYTE_ABGR (bytes A, B, G, R:
+    how ImageIO reads an RGBA PNG).  Other layouts: pass fmt explicitly."""
     if img.ndim == 2 or (img.ndim == 3 and img.shape[2] == 1):
         return N.GRAY8
     if img.ndim == 3 and img.shape[2] == 3:
         return N.BGR24
+    if img.ndim == 3 and img.shape[2] == 4:
+        return N.ABGR32
     raise ValueError(f"unsupported image shape {tuple(img.shape)}")
+
+
+def _out_shape(h, w, fmt):
+    nch = N.CHANNELS[fmt]
+    return (h, w) if nch == 1 else (h, w, nch)
 
 
 class DeviceImage:
@@ -205,11 +215,13 @@ def _image_struct(img, fmt=None):
         fmt = _fmt_of(img)
     h, w = int(img.shape[0]), int(img.shape[1])
     if getattr(img, "icx_device", False):
-        return N.Image(img.data_ptr(), w, h, w * (1 if fmt == N.GRAY8 else 3), fmt), img
+        return N.Image(img.data_ptr(), w, h, w * N.CHANNELS[fmt], fmt), img
     if isinstance(img, np.ndarray):
         if img.dtype != np.uint8:
             raise ValueError("image must be uint8")
-        if not (img.flags["C_CONTIGUOUS"] or (img.strides[-1] == 1 and (img.ndim == 2 or img.strides[1] == 3))):
+        nch = N.CHANNELS[fmt]
+        if not (img.flags["C_CONTIGUOUS"] or (img.strides[-1] == 1 and (img.ndim == 2 or img.strides[1] == nch)
+                                              and (nch != 4 or img.strides[0] % 4 == 0))):
             img = np.ascontiguousarray(img)
         ptr, stride = img.ctypes.data, img.strides[0]
     else:  # torch tensor (CUDA or CPU)
@@ -254,25 +266,24 @@ class Codec:
                                  f"({self._lib.icx_last_error(self._ctx).decode()})")
 
     # -------------------------------------------------------------- A12
-    def resize_image(self, original_image, scale: float) -> np.ndarray:
-        """ImageTools.resizeImage(BufferedImage, double): Java2D bilinear."""
-        img, keep = _image_struct(original_image)
+    def resize_image(self, original_image, scale: float, fmt=None) -> np.ndarray:
+        """ImageTools.resizeImage(BufferedImage, double): Java2D bilinear; the
+        result keeps the source type (ImageTools.java:12-15)."""
+        img, keep = _image_struct(original_image, fmt)
         w = ctypes.c_int32()
         h = ctypes.c_int32()
         self._lib.icx_scaled_dims(img.width, img.height, float(scale), ctypes.byref(w), ctypes.byref(h))
-        nch = 1 if img.fmt == N.GRAY8 else 3
-        out = np.empty((h.value, w.value, nch) if nch == 3 else (h.value, w.value), np.uint8)
+        out = np.empty(_out_shape(h.value, w.value, img.fmt), np.uint8)
         st = self._lib.icx_resize_image(self._ctx, ctypes.byref(img), float(scale), out.ctypes.data, out.nbytes,
                                         ctypes.byref(w), ctypes.byref(h))
         self._check(st, "icx_resize_image")
         return out
 
-    def resize_to(self, original_image, width: int, height: int) -> np.ndarray:
-        img, keep = _image_struct(original_image)
-        nch = 1 if img.fmt == N.GRAY8 else 3
-        out = np.empty((height, width, nch) if nch == 3 else (height, width), np.uint8)
+    def resize_to(self, original_image, width: int, height: int, fmt=None) -> np.ndarray:
+        img, keep = _image_struct(original_image, fmt)
+        out = np.empty(_out_shape(height, width, img.fmt), np.uint8)
         st = self._lib.icx_resize_bilinear(self._ctx, ctypes.byref(img), out.ctypes.data, width, height,
-                                           width * nch)
+                                           width * N.CHANNELS[img.fmt])
         self._check(st, "icx_resize_bilinear")
         return out
 

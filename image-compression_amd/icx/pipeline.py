@@ -77,14 +77,23 @@ def format_file_size(size: int) -> str:
 
 
 def _to_array(im):
-    """Decoded raster as the BufferedImage type the JDK reader returns."""
+    """Decoded raster as the BufferedImage type the JDK reader returns:
+    TYPE_BYTE_GRAY (H, W), TYPE_3BYTE_BGR (H, W, 3) or, with an alpha channel,
+    TYPE_4BYTE_ABGR (H, W, 4) - ImageTools.resizeImage keeps that type and
+    the PNG is written back with its alpha (ImageTools.java:12-15)."""
     mode = im.mode
     if mode == "L":
         return np.asarray(im, dtype=np.uint8)
     if mode in ("I;16", "I;16B", "I", "F", "1"):
         return np.asarray(im.convert("L"), dtype=np.uint8)
+    if mode in ("LA", "PA") or (mode == "P" and "transparency" in im.info):
+        # grey+alpha is TYPE_CUSTOM there, drawn into TYPE_INT_ARGB: RGBA out
+        # (the JDK's linear-grey -> sRGB conversion of that case is not restated)
+        mode, im = "RGBA", im.convert("RGBA")
+    if mode == "RGBA":
+        return np.ascontiguousarray(np.asarray(im, dtype=np.uint8)[:, :, ::-1])  # TYPE_4BYTE_ABGR
     if mode != "RGB":
-        im = im.convert("RGB")  # CMYK/P/RGBA/LA: approximate (DESIGN.md §9)
+        im = im.convert("RGB")  # CMYK / palette without transparency: approximate (DESIGN.md §9)
     rgb = np.asarray(im, dtype=np.uint8)
     return np.ascontiguousarray(rgb[:, :, ::-1])  # TYPE_3BYTE_BGR
 

@@ -1,69 +1,37 @@
-"""PNG writer for the PNG path's output (host side; deflate releases the GIL,
-so the batch driver runs it on a writer thread pool).
+"""PNG writer of the PNG path: libicx's icx_png_encode (C++ on the calling
+host thread; ctypes releases the GIL, so the batch driver's writer pool
+encodes one image per thread).
 
-The reference writes PNG through the JDK's PNGImageWriter
-(ImageCompressionPng.java:70): per row it picks the filter (None, Sub, Up,
-Average, Paeth) with the smallest sum of |filtered byte as signed|, then
-deflates.  This writer uses the same row-filter heuristic (vectorised over the
-whole image) and zlib; the deflate bytes themselves are not pinned (no JDK
-here) — parity for PNG is on decoded pixels and dimensions.
+Reference: ImageCompressionPng.java:70, ImageIO.write(img, "png", file).
+The JDK writer's filter heuristic and deflate bytes are not pinnable here (no
+JDK): parity is on decoded pixels, dimensions and colour type,
+and the per-row filter choice is checked against tests/png_ref.py.
 """
-import struct
-import zlib
+import ctypes
 
 import numpy as np
 
-
-def _chunk(tag, data):
-    c = struct.pack(">I", len(data)) + tag + data
-    return c + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+from . import _native as N
 
 
-def filter_rows(raw: np.ndarray, bpp: int) -> np.ndarray:
-    """raw (h, rowbytes) u8 -> (h, 1 + rowbytes) u8 with the per-row filter of
-    minimum sum of absolute signed residuals (ties: the lower filter type)."""
-    h, n = raw.shape
-    x = raw.astype(np.int16)
-    a = np.zeros_like(x)
-    a[:, bpp:] = x[:, :-bpp]                  # left
-    b = np.zeros_like(x)
-    b[1:] = x[:-1]                            # up
-    c = np.zeros_like(x)
-    c[1:, bpp:] = x[:-1, :-bpp]               # up-left
-    p = a + b - c
-    pa, pb, pc = np.abs(p - a), np.abs(p - b), np.abs(p - c)
-    paeth = np.where((pa <= pb) & (pa <= pc), a, np.where(pb <= pc, b, c))
-    best_cost = None
-    out = np.empty((h, n + 1), np.uint8)
-    for ftype, pred in enumerate((None, a, b, (a + b) >> 1, paeth)):
-        res = (x if pred is None else x - pred).astype(np.uint8)  # mod 256
-        cost = np.abs(res.view(np.int8).astype(np.int32)).sum(axis=1)
-        if best_cost is None:
-            best_cost = cost
-            out[:, 1:] = res
-            out[:, 0] = 0
-            continue
-        take = cost < best_cost
-        if take.any():
-            out[take, 1:] = res[take]
-            out[take, 0] = ftype
-            best_cost = np.where(take, cost, best_cost)
-    return out
+def encode_png(img, fmt=None, level: int = 6) -> bytes:
+    """img: host (H, W) grey, (H, W, 3) BGR or (H, W, 4) ABGR uint8 array (or
+    another icx_fmt given explicitly) -> PNG file bytes (grey, RGB or RGBA)."""
+    from .core import _image_struct
+    lib = N.load()
+    im, keep = _image_struct(np.ascontiguousarray(img), fmt)
+    cap = lib.icx_png_bound(ctypes.byref(im))
+    if cap == 0:
+        raise N.IcxError(N.E_UNSUPPORTED, "image too large for one IDAT chunk")
+    out = np.empty(cap, np.uint8)
+    n = ctypes.c_size_t()
+    st = lib.icx_png_encode(ctypes.byref(im), int(level), out.ctypes.data, cap, ctypes.byref(n))
+    if st != N.OK:
+        raise N.IcxError(st, f"icx_png_encode: {lib.icx_status_string(st).decode()}")
+    return out[:n.value].tobytes()
 
 
-def encode_png(img: np.ndarray, level: int = 6) -> bytes:
-    """img: (H, W, 3) BGR or (H, W) grey uint8."""
-    if img.ndim == 2:
-        rgb, ctype, bpp = img, 0, 1
-    else:
-        rgb, ctype, bpp = np.ascontiguousarray(img[:, :, ::-1]), 2, 3
-    h, w = rgb.shape[:2]
-    raw = filter_rows(rgb.reshape(h, -1), bpp)
-    ihdr = struct.pack(">IIBBBBB", w, h, 8, ctype, 0, 0, 0)
-    return (b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", ihdr) +
-            _chunk(b"IDAT", zlib.compress(raw.tobytes(), level)) + _chunk(b"IEND", b""))
-
-
-def write_png(path, img: np.ndarray) -> None:
+def write_png(path, img, fmt=None) -> None:
+    data = encode_png(img, fmt)
     with open(path, "wb") as f:
-        f.write(encode_png(img))
+        f.write(data)

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ICX_ABI_VERSION 1
+#define ICX_ABI_VERSION 2  /* 2: four-byte pixel formats, icx_png_encode */
 
 typedef struct icx_ctx icx_ctx;
 
@@ -50,8 +50,25 @@ typedef enum icx_status {
 
 /* Pixel layouts.  ICX_BGR24 is java.awt.image.BufferedImage.TYPE_3BYTE_BGR,
  * the type the JDK JPEG reader returns for YCbCr JPEGs; ICX_GRAY8 is
- * TYPE_BYTE_GRAY (1-component JPEG). */
-typedef enum icx_fmt { ICX_BGR24 = 0, ICX_RGB24 = 1, ICX_GRAY8 = 2 } icx_fmt;
+ * TYPE_BYTE_GRAY (1-component JPEG).
+ * Four-byte pixels (the PNG path: ImageTools.java:12-15 keeps the source
+ * type, TYPE_CUSTOM -> TYPE_INT_ARGB / TYPE_INT_RGB) are accepted by the
+ * resize / PNG entry points only; rows and px must be 4-byte aligned.  The
+ * JPEG entry points return ICX_E_UNSUPPORTED for them (the JDK JPEG writer
+ * refuses alpha rasters).  Byte order in memory (little-endian ints):
+ *   ICX_XRGB32  TYPE_INT_RGB    int 0x00RRGGBB: B, G, R, 0 (alpha ignored, written 0)
+ *   ICX_ARGB32  TYPE_INT_ARGB   int 0xAARRGGBB: B, G, R, A
+ *   ICX_ABGR32  TYPE_4BYTE_ABGR bytes A, B, G, R (ImageIO's reading of an RGBA PNG)
+ *   ICX_RGBA32  bytes R, G, B, A (PNG colour type 6 row order) */
+typedef enum icx_fmt {
+    ICX_BGR24 = 0,
+    ICX_RGB24 = 1,
+    ICX_GRAY8 = 2,
+    ICX_XRGB32 = 3,
+    ICX_ARGB32 = 4,
+    ICX_ABGR32 = 5,
+    ICX_RGBA32 = 6
+} icx_fmt;
 
 /* A decoded image (BufferedImage).  stride in bytes. */
 typedef struct icx_image {
@@ -152,7 +169,9 @@ icx_status icx_compress_jpg_batch(icx_ctx* ctx, icx_fit_job* jobs, int32_t n);
 
 /* A12  ImageTools.resizeImage (ImageTools.java:7-26): Java2D bilinear resize
  * to (max(1,(int)(w*scale)), max(1,(int)(h*scale))).  dst gets the same fmt,
- * tightly packed (stride = w*channels). */
+ * tightly packed (stride = w*channels).  Alpha formats are interpolated in
+ * premultiplied form and composited SrcOver onto the new (transparent)
+ * image, as Java2D's TransformHelper + IntArgbPre mask blit do. */
 icx_status icx_resize_image(icx_ctx* ctx, const icx_image* src, double scale, uint8_t* dst,
                             size_t cap, int32_t* out_w, int32_t* out_h);
 
@@ -167,6 +186,15 @@ icx_status icx_resize_bilinear(icx_ctx* ctx, const icx_image* src, uint8_t* dst,
 icx_status icx_png_fit(icx_ctx* ctx, const icx_image* src, int32_t min_width, int32_t min_height,
                        uint8_t* dst, size_t cap, int32_t* out_w, int32_t* out_h,
                        int32_t* resized);
+
+/* The PNG write of ImageCompressionPng (ImageCompressionPng.java:70,
+ * ImageIO.write(img, "png", file)) for host pixels: 8-bit grey (GRAY8), RGB
+ * (BGR24/RGB24/XRGB32) or RGBA (ARGB32/ABGR32/RGBA32); per row the filter
+ * (None, Sub, Up, Average, Paeth) with the least sum of |residual byte as
+ * signed| (ties: the lower type), one zlib stream at `level` (0-9, -1 = 6)
+ * in one IDAT.  Needs cap >= icx_png_bound(img); *out_len = file bytes. */
+size_t icx_png_bound(const icx_image* img);
+icx_status icx_png_encode(const icx_image* img, int32_t level, uint8_t* out, size_t cap, size_t* out_len);
 
 /* ------------------------------------------------------------- decode (A11) */
 /* ImageCompression.decodeImageWithSubsampling (ImageCompression.java:107-165)

@@ -678,10 +678,81 @@ void oracle_scaled_dims(int w, int h, double scale, int* dw, int* dh)
 
 static inline int64_t dbl_to_long(double d) { return (int64_t)(d * 4294967296.0); }
 
+/* Java2D AlphaMath.c initAlphaTables: mul8table[a][c] ~ a*c/255 and
+ * div8table[a][c] ~ c*255/a (c < a; 255 from c = a on), both in 8.24 fixed
+ * point with the tables' own rounding.  Row/column 0 of mul8table is 0. */
+static inline int mul8(int a, int c)
+{
+    const uint32_t inc = (uint32_t)a * 0x010101u;
+    return (int)((c * inc + (1u << 23)) >> 24) & 0xff;
+}
+
+static inline int div8(int a, int c)
+{
+    if (c >= a) return 255;
+    const uint32_t inc = ((0xffu << 24) + (uint32_t)a / 2) / (uint32_t)a;
+    return (int)(((1u << 23) + (uint32_t)c * inc) >> 24);
+}
+
+/* Four-byte pixels (ImageTools.java:12-15 keeps the type; TYPE_CUSTOM with
+ * alpha becomes TYPE_INT_ARGB): TransformHelper fetches the four neighbours
+ * as IntArgbPre (colours premultiplied by mul8table, an opaque type's alpha
+ * 0xff), interpolates all four channels as above, and the SrcOver mask blit
+ * onto the new all-zero image stores alpha 0 as untouched zero pixels,
+ * alpha 0xff as is, and otherwise un-premultiplies with div8table.  An
+ * XRGB (TYPE_INT_RGB) destination stores 0 in its unused byte. */
+static int resize4(const uint8_t* src, int sw, int sh, int sstride, int fmt, uint8_t* dst, int dw, int dh,
+                   int dstride)
+{
+    const int ab = fmt == OR_ABGR32 ? 0 : 3;  /* alpha byte */
+    const int opaque = fmt == OR_XRGB32;
+    double ix = 1.0 / ((double)dw / sw), iy = 1.0 / ((double)dh / sh);
+    int64_t dxl = dbl_to_long(ix), dyl = dbl_to_long(iy);
+    int64_t x0l = dbl_to_long(0.5 * ix), y0l = dbl_to_long(0.5 * iy);
+    const int64_t half = (int64_t)1 << 31;
+    for (int dy = 0; dy < dh; dy++) {
+        int64_t yl = y0l + (int64_t)dy * dyl - half;
+        int yw = (int)(yl >> 32), yf = (int)((uint32_t)yl >> 24), ya, yb;
+        if (yw < 0) ya = yb = 0;
+        else if (yw + 1 >= sh) ya = yb = yw;
+        else { ya = yw; yb = yw + 1; }
+        for (int dx = 0; dx < dw; dx++) {
+            int64_t xl = x0l + (int64_t)dx * dxl - half;
+            int xw = (int)(xl >> 32), xf = (int)((uint32_t)xl >> 24), xa, xb;
+            if (xw < 0) xa = xb = 0;
+            else if (xw + 1 >= sw) xa = xb = xw;
+            else { xa = xw; xb = xw + 1; }
+            const uint8_t* q[4] = {src + (size_t)ya * sstride + 4 * xa, src + (size_t)ya * sstride + 4 * xb,
+                                   src + (size_t)yb * sstride + 4 * xa, src + (size_t)yb * sstride + 4 * xb};
+            int pre[4][4];
+            for (int s = 0; s < 4; s++) {
+                const int a = opaque ? 255 : q[s][ab];
+                for (int b = 0; b < 4; b++) pre[s][b] = b == ab ? a : mul8(a, q[s][b]);
+            }
+            int v[4];
+            for (int b = 0; b < 4; b++) {
+                int top = (pre[0][b] << 8) + (pre[1][b] - pre[0][b]) * xf;
+                int bot = (pre[2][b] << 8) + (pre[3][b] - pre[2][b]) * xf;
+                v[b] = (((top << 8) + (bot - top) * yf) + (1 << 15)) >> 16;
+            }
+            uint8_t* o = dst + (size_t)dy * dstride + 4 * dx;
+            const int a = v[ab];
+            for (int b = 0; b < 4; b++) {
+                if (opaque) o[b] = b == ab ? 0 : (uint8_t)v[b];
+                else if (a == 0) o[b] = 0;
+                else if (b == ab || a == 255) o[b] = (uint8_t)v[b];
+                else o[b] = (uint8_t)div8(a, v[b]);
+            }
+        }
+    }
+    return 0;
+}
+
 int oracle_resize(const uint8_t* src, int sw, int sh, int sstride, int fmt, uint8_t* dst, int dw,
                   int dh, int dstride)
 {
     if (sw <= 0 || sh <= 0 || dw <= 0 || dh <= 0 || !src || !dst) return 1;
+    if (fmt >= OR_XRGB32) return resize4(src, sw, sh, sstride, fmt, dst, dw, dh, dstride);
     int nch = (fmt == OR_GRAY8) ? 1 : 3;
     double ix = 1.0 / ((double)dw / sw), iy = 1.0 / ((double)dh / sh);
     int64_t dxl = dbl_to_long(ix), dyl = dbl_to_long(iy);

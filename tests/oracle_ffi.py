@@ -100,13 +100,15 @@ class Oracle:
         self.L.oracle_scaled_dims(w, h, float(s), ctypes.byref(a), ctypes.byref(b))
         return a.value, b.value
 
-    def resize(self, img, dw, dh):
+    def resize(self, img, dw, dh, fmt=None):
+        """fmt: icx_fmt numbering; default grey / BGR24 / ABGR32 by channels."""
         img = np.ascontiguousarray(img)
         h, w = img.shape[:2]
-        nch = 1 if img.ndim == 2 else 3
-        out = np.empty((dh, dw, nch) if nch == 3 else (dh, dw), np.uint8)
-        self.L.oracle_resize(img.ctypes.data, w, h, img.strides[0], fmt_of(img), out.ctypes.data, dw, dh,
-                             dw * nch)
+        nch = 1 if img.ndim == 2 else img.shape[2]
+        if fmt is None:
+            fmt = 2 if nch == 1 else 0 if nch == 3 else 5
+        out = np.empty((dh, dw, nch) if nch > 1 else (dh, dw), np.uint8)
+        self.L.oracle_resize(img.ctypes.data, w, h, img.strides[0], fmt, out.ctypes.data, dw, dh, dw * nch)
         return out
 
     def fit(self, img, target, q0, cached=None):

@@ -42,7 +42,7 @@ class OracleCodec:
             return None
         s = min(params.min_width / w, params.min_height / h)
         dw, dh = self.o.scaled_dims(w, h, s)
-        return self.o.resize(img, dw, dh)
+        return self.o.resize(img, dw, dh)  # (H, W, 4) = ABGR, as icx.core._fmt_of
 
     def compress_png_with_target_size(self, img, output_file, params):
         r = self.png_resize(img, params)

@@ -148,6 +148,48 @@ def test_resize_matches_restatement(codec, oracle):
         assert np.array_equal(codec.resize_image(g, 0.5), oracle.resize(g, dw, dh))
 
 
+@pytest.mark.parametrize("fmt", [N.XRGB32, N.ARGB32, N.ABGR32, N.RGBA32])
+def test_resize_four_byte_formats_match_restatement(codec, oracle, fmt):
+    """ImageTools.java:12-15 keeps the type: four-byte rasters through
+    k_resize4 (premultiplied bilinear, SrcOver onto a zero image) equal the
+    oracle's restatement bit for bit - transparent, opaque and partial alpha
+    regions, down- and up-scaling, odd sizes, 4K."""
+    rng = np.random.default_rng(fmt)
+    ab = 0 if fmt == N.ABGR32 else 3
+    for h, w, dw, dh in [(90, 120, 76, 51), (1, 7, 3, 1), (37, 29, 80, 61), (2160, 3840, 1920, 1080)]:
+        img = rng.integers(0, 256, (h, w, 4), dtype=np.uint8)
+        img[: h // 3, :, ab] = 0
+        img[h // 3: 2 * h // 3, :, ab] = 255
+        got = codec.resize_to(img, dw, dh, fmt=fmt)
+        assert np.array_equal(got, oracle.resize(img, dw, dh, fmt=fmt)), (fmt, h, w)
+        if fmt == N.XRGB32:
+            assert (got[:, :, 3] == 0).all()
+
+
+def test_png_fit_keeps_alpha(codec, oracle, tmp_path):
+    """compressPngWithTargetSize on a TYPE_4BYTE_ABGR raster: the resized PNG
+    is RGBA, its pixels equal the restatement's, transparent areas stay
+    transparent."""
+    from PIL import Image
+    rng = np.random.default_rng(4)
+    abgr = rng.integers(0, 256, (600, 800, 4), dtype=np.uint8)
+    abgr[:200, :, 0] = 0
+    out = tmp_path / "alpha.png"
+    assert codec.compress_png_with_target_size(abgr, out, icx.CompressionParams(0, 0, 100, 100, 0)) is True
+    im = Image.open(out)
+    assert im.mode == "RGBA" and im.size == (100, 75)
+    assert np.array_equal(np.asarray(im)[:, :, ::-1], oracle.resize(abgr, 100, 75))
+    assert (np.asarray(im)[:20, :, 3] == 0).all()
+
+
+def test_jpeg_rejects_alpha_rasters(codec):
+    """The JDK JPEG writer refuses alpha rasters: the JPEG entry points return
+    ICX_E_UNSUPPORTED for four-byte formats."""
+    img = np.zeros((16, 16, 4), np.uint8)
+    r = codec.fit([img], 10 ** 6, 0.25)[0]
+    assert r["status"] == N.E_UNSUPPORTED and not r["success"]
+
+
 def test_png_fit(codec, tmp_path):
     """ImageCompressionPngTest.java:38-88 restated."""
     small = np.zeros((100, 100, 3), np.uint8)

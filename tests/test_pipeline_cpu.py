@@ -224,24 +224,104 @@ def test_two_codecs_share_the_work_queue(tmp_path):
         assert (out / n).read_bytes() == (ref_out / n).read_bytes()
 
 
+def _png_idat_rows(data, h):
+    """Inflated IDAT of a single-IDAT PNG, as (h, 1 + rowbytes) filtered rows."""
+    import struct
+    import zlib
+    pos, idat = 8, b""
+    while pos < len(data):
+        n, = struct.unpack(">I", data[pos:pos + 4])
+        if data[pos + 4:pos + 8] == b"IDAT":
+            idat += data[pos + 8:pos + 8 + n]
+        pos += 12 + n
+    raw = np.frombuffer(zlib.decompress(idat), np.uint8)
+    return raw.reshape(h, -1)
+
+
 def test_png_writer_adaptive_filters_round_trip():
-    """icx.pngio: every row filter the adaptive choice can pick decodes back to
-    the exact pixels (PNG parity is on pixels)."""
+    """icx_png_encode (native, libicx): every row filter the adaptive choice
+    can pick decodes back to the exact pixels (PNG parity is on pixels,
+    SURVEY.md §8c), and the filtered rows - filter type and residuals - equal
+    the numpy reference writer's (tests/png_ref.py) for grey, BGR and ABGR."""
     import io
 
     from PIL import Image
 
-    from icx.pngio import encode_png, filter_rows
+    from icx.pngio import encode_png
+    from tests.png_ref import filter_rows
     rng = np.random.default_rng(5)
     y = np.arange(64)[:, None]
     x = np.arange(97)[None, :]
     grad = np.stack(np.broadcast_arrays((x + y) % 256, (3 * x) % 256, (5 * y) % 256), -1).astype(np.uint8)
+    alpha = np.concatenate([np.broadcast_to((x * y) % 256, (64, 97))[:, :, None].astype(np.uint8), grad], -1)
     for img in [grad, rng.integers(0, 256, (31, 17, 3), dtype=np.uint8), grad[:, :, 1].copy(),
-                np.zeros((1, 1, 3), np.uint8), rng.integers(0, 256, (5, 2), dtype=np.uint8)]:
-        back = np.asarray(Image.open(io.BytesIO(encode_png(img))))
-        assert np.array_equal(back, img if img.ndim == 2 else img[:, :, ::-1])
+                np.zeros((1, 1, 3), np.uint8), rng.integers(0, 256, (5, 2), dtype=np.uint8), alpha,
+                rng.integers(0, 256, (9, 13, 4), dtype=np.uint8)]:
+        data = encode_png(img)
+        back = np.asarray(Image.open(io.BytesIO(data)))
+        assert np.array_equal(back, img if img.ndim == 2 else img[:, :, ::-1])  # BGR/ABGR -> RGB/RGBA
+        rows = img if img.ndim == 2 else np.ascontiguousarray(img[:, :, ::-1])
+        bpp = 1 if img.ndim == 2 else img.shape[2]
+        ref = filter_rows(rows.reshape(img.shape[0], -1), bpp)
+        assert np.array_equal(_png_idat_rows(data, img.shape[0]), ref)
     types = set(filter_rows(grad.reshape(64, -1), 3)[:, 0].tolist())
     assert len(types) >= 2  # the smooth gradient picks predictive filters, not only "None"
+
+
+def test_png_alpha_kept_through_the_pipeline(tmp_path):
+    """ImageTools.java:12-15 keeps the alpha channel: an RGBA PNG is resized
+    as TYPE_4BYTE_ABGR (premultiplied bilinear, icx_resize restatement) and
+    written back as an RGBA PNG with its alpha; a grey+alpha PNG (TYPE_CUSTOM
+    -> TYPE_INT_ARGB) comes back as RGBA too; opaque RGB stays RGB."""
+    from PIL import Image
+
+    from tests.oracle_ffi import Oracle
+    rng = np.random.default_rng(9)
+    h, w = 90, 160
+    rgba = rng.integers(0, 256, (h, w, 4), dtype=np.uint8)
+    rgba[:30, :, 3] = 0      # transparent band
+    rgba[30:60, :, 3] = 255  # opaque band
+    Image.fromarray(rgba, "RGBA").save(tmp_path / "a.png")
+    la = rng.integers(0, 256, (h, w, 2), dtype=np.uint8)
+    Image.fromarray(la, "LA").save(tmp_path / "b.png")
+    Image.fromarray(rgba[:, :, :3].copy(), "RGB").save(tmp_path / "c.png")
+    out = tmp_path / "out"
+    out.mkdir()
+    params = CompressionParams(0.25, 10, 100, 60, 20000)
+    o = Oracle()
+    for name in ("a.png", "b.png", "c.png"):
+        r = pipeline.process_image(tmp_path / name, out, params, {}, OracleCodec())
+        assert r.result == CompressionResult.COMPRESSED_SUCCESS, name
+    a = Image.open(out / "a.png")
+    assert a.mode == "RGBA" and a.size == (100, 56)
+    exp = o.resize(np.ascontiguousarray(rgba[:, :, ::-1]), 100, 56)[:, :, ::-1]  # ABGR restatement -> RGBA
+    assert np.array_equal(np.asarray(a), exp)
+    assert (np.asarray(a)[:15, :, 3] == 0).all() and (np.asarray(a)[:15] == 0).all()
+    assert Image.open(out / "b.png").mode == "RGBA"
+    assert Image.open(out / "c.png").mode == "RGB"
+
+
+def test_alpha_resize_restatement_rules():
+    """The oracle's four-byte resize (Java2D TransformHelper + IntArgbPre
+    SrcOver blit): opaque pixels give the three-byte result, XRGB writes 0 in
+    its spare byte, fully transparent output pixels are zero, and each
+    channel stays within its alpha bound (C <= A when premultiplied)."""
+    from tests.oracle_ffi import Oracle
+    o = Oracle()
+    rng = np.random.default_rng(2)
+    bgr = rng.integers(0, 256, (23, 37, 3), dtype=np.uint8)
+    ref = o.resize(bgr, 15, 11)
+    opaque = np.concatenate([np.full((23, 37, 1), 255, np.uint8), bgr], -1)  # ABGR, A = 255
+    assert np.array_equal(o.resize(opaque, 15, 11)[:, :, 1:], ref)
+    xrgb = np.concatenate([bgr, rng.integers(0, 256, (23, 37, 1), dtype=np.uint8)], -1)  # B G R X
+    r = o.resize(xrgb, 15, 11, fmt=3)
+    assert np.array_equal(r[:, :, :3], ref) and (r[:, :, 3] == 0).all()
+    clear = opaque.copy()
+    clear[:, :, 0] = 0
+    assert (o.resize(clear, 15, 11) == 0).all()
+    mixed = np.concatenate([rng.integers(0, 256, (23, 37, 1), dtype=np.uint8), bgr], -1)
+    r = o.resize(mixed, 40, 30)
+    assert ((r[:, :, 0] == 0) <= (r[:, :, 1:] == 0).all(-1)).all()  # alpha 0 -> zero pixel
 
 
 def test_corrupt_jpeg_fails_alone_in_its_group(tmp_path):
