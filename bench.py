@@ -357,7 +357,9 @@ def main():
                    "workspace_mb_per_subbatch": int(sb["units"] / max(1, sb["launches"]))},
         "roofline": roof,
         "stages": stages,
-        "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k, v in kstats.items()},
+        "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3), "units": v["units"],
+                        **({"algo_bytes": int(bytes_of[k])} if k in bytes_of else {})}
+                    for k, v in kstats.items()},
     }
     if rank == 0 and world == 1 and args.host_io_frames and not args.host_io:
         batch = None

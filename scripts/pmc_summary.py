@@ -1,15 +1,26 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 PMC passes into HBM bytes per kernel dispatch.
+"""Summarise rocprofv3 PMC passes of one bench.py run into HBM bytes per unit
+of work, next to the algorithmic bytes the library counted in the same run.
 
-gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) reports half
-of the bytes of a wide coalesced streaming read -> doubled; WRITE_SIZE (KiB) is
-exact for 16-B-per-lane stores (other widths uncalibrated)."""
+  pmc_summary.py DIR BENCH_JSON
+
+DIR holds one rocprofv3 output per counter (DIR/FETCH_SIZE, DIR/WRITE_SIZE);
+BENCH_JSON is the JSON line of the same command (run with --warmup 0 --steps 1
+so that every icx:: dispatch of the process is a timed one; the line's
+"kernels" give units and algorithmic bytes).  gfx950 corrections
+(MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) counts half the bytes of a wide
+coalesced read -> doubled; profiles/r2/calib_fetch_summary.json shows the
+same factor for k_huff's 16-B list gathers.  WRITE_SIZE is exact for 16-B
+stores (k_huff's and k_fdct's)."""
 import csv
 import glob
 import json
 import os
 import sys
 from collections import defaultdict
+
+SHORT = {"k_fdct_color": "fdct", "k_fdct_gray": "fdct", "k_huff": "huff", "k_scan": "scan",
+         "k_ffscan": "ffscan", "k_stuff": "stuff", "k_resize": "resize"}
 
 
 def load(d, ctr):
@@ -23,30 +34,37 @@ def load(d, ctr):
     return vals
 
 
-def main(d, units):
+def main(d, bench_json):
+    line = json.loads([l for l in open(bench_json) if l.startswith("{")][-1])
+    kern = line["kernels"]
     fetch, write = load(d, "FETCH_SIZE"), load(d, "WRITE_SIZE")
     out = {}
     for k in sorted(set(fetch) | set(write)):
         if not k.startswith("icx::"):
             continue
-        f = fetch.get(k, [])
-        w = write.get(k, [])
-        fb = 2 * 1024 * sum(f) / max(1, len(f))
-        wb = 1024 * sum(w) / max(1, len(w))
-        out[k] = {"dispatches": len(f), "fetch_bytes_per_dispatch_x2": fb, "write_bytes_per_dispatch": wb,
-                  "hbm_bytes_per_dispatch": fb + wb}
-    short = {k.split("::")[-1].split("<")[0].replace("k_", "").replace("_color", "").replace("_gray", ""): v
-             for k, v in out.items()}
-    per_unit = {}
-    for name, u in units.items():
-        if name in short and u > 0:
-            per_unit[name] = short[name]["hbm_bytes_per_dispatch"] / u
-    res = {"kernels": out, "units_per_dispatch": units, "bytes_per_unit": per_unit}
+        short = SHORT.get(k.split("::")[-1].split("<")[0])
+        f, w = fetch.get(k, []), write.get(k, [])
+        fb, wb = 2 * 1024 * sum(f), 1024 * sum(w)
+        e = {"dispatches": len(f), "fetch_bytes_x2": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
+             "fetch_x2_per_dispatch": [round(2 * 1024 * v) for v in f]}
+        if short in kern and kern[short].get("units"):
+            ku = kern[short]
+            e["units"] = ku["units"]
+            e["bench_launches"] = ku["launches"]
+            e["hbm_bytes_per_unit"] = (fb + wb) / ku["units"]
+            if "algo_bytes" in ku:
+                e["algo_bytes"] = ku["algo_bytes"]
+                e["algo_bytes_per_unit"] = ku["algo_bytes"] / ku["units"]
+                e["traffic_over_algo"] = (fb + wb) / ku["algo_bytes"]
+        out[k] = e
+    per_unit = {SHORT[k.split("::")[-1].split("<")[0]]: v["hbm_bytes_per_unit"]
+                for k, v in out.items() if "hbm_bytes_per_unit" in v}
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of: bench.py " +
+                     " ".join(sys.argv[3:]), "kernels": out, "bytes_per_unit": per_unit}
     json.dump(res, open(os.path.join(d, "pmc_summary.json"), "w"), indent=1)
-    print(json.dumps(res, indent=1))
+    print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "fetch_x2_per_dispatch"} for k, v in out.items()},
+                     indent=1))
 
 
 if __name__ == "__main__":
-    # units: work per dispatch in the PMC config (fdct = pixels, huff = scan blocks)
-    units = dict(kv.split("=") for kv in sys.argv[2:])
-    main(sys.argv[1], {k: float(v) for k, v in units.items()})
+    main(sys.argv[1], sys.argv[2])
