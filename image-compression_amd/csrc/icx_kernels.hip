@@ -274,7 +274,14 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
     uint32_t* st = L.st[wave];
     uint32_t total = 0;
     const int nat = c_zz_to_nat[lane];  // oz holds natural order; lane = zig-zag index
-    for (int blk0 = wave * STEP; blk0 < nblk; blk0 += 4 * STEP) {
+    // wave w takes groups NB/(4 STEP) * w .. (consecutive blocks) and packs their
+    // lists back to back in its own region: one partly used cache line per wave
+    // region instead of one per group (k_huff's gathers fetch whole lines)
+    constexpr int GPW = NB / (4 * STEP);  // groups per wave
+    GAS u32x4_t* const region = (GAS u32x4_t*)(D.coefs + base + (int64_t)wave * GPW * STEP * COEF_SLOTS);
+    for (int g = 0; g < GPW; g++) {
+        const int blk0 = (wave * GPW + g) * STEP;
+        if (blk0 >= nblk) break;
         int c[STEP];
 #pragma unroll
         for (int a = 0; a < STEP; a++)
@@ -294,9 +301,10 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
             off = writelane(off, run, a);
             run += r4;
         }
-        if (lane < STEP && blk0 + lane < nblk) L.meta[blk0 + lane] = (uint16_t)((off << 7) | len);
+        // meta: (offset in the wave region, 16-B units) << 7 | length
+        if (lane < STEP && blk0 + lane < nblk) L.meta[blk0 + lane] = (uint16_t)((((int)total + off) >> 2 << 7) | len);
         __builtin_amdgcn_wave_barrier();
-        GAS u32x4_t* dst = (GAS u32x4_t*)(D.coefs + base + (int64_t)blk0 * COEF_SLOTS);
+        GAS u32x4_t* dst = region + total / 4;
         for (int p = lane; p < run / 4; p += 64) {
             const uint4 v = *(const uint4*)&st[4 * p];
             u32x4_t w;
@@ -316,10 +324,11 @@ __device__ __forceinline__ void store_list_meta(const ImgDesc& D, int64_t base, 
                                                 const ListStage<NB, STEP>& L)
 {
     const int t = threadIdx.x;
+    constexpr int GPW = NB / (4 * STEP);
     if (t < nblk) {
         const uint32_t m = L.meta[t];
         D.ncoef[bbase + t] = (uint8_t)(m & 127);
-        D.coff[bbase + t] = (uint32_t)((base + (t / STEP) * (STEP * COEF_SLOTS) + (m >> 7)) >> 2);
+        D.coff[bbase + t] = (uint32_t)((base + (t / (GPW * STEP)) * (GPW * STEP * COEF_SLOTS)) >> 2) + (m >> 7);
     }
 }
 
