@@ -38,7 +38,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s
 # content-dependent amounts (candidate lists), so the library counts them per
 # launch ("<kernel>.bytes" profile entries): fdct = pixels read + lists, list
 # offsets and lengths written; huff = per trial, every block's padded list +
-# offset + length read.  resize: a fixed 6 B per destination pixel.
+# offset + length read, and the trial's bitstream (>= bits / 8) + per-chunk
+# bit counts and 0xFF bins written.  resize: a fixed 6 B per destination pixel.
 ALGO_BYTES_FIXED = {"resize": 6.0}
 UNIT_NAME = {"fdct": "pixel", "huff": "scan block (per trial)", "resize": "destination pixel"}
 

@@ -99,6 +99,9 @@ struct ImgState {
     // spread over ENT_SLOTS counters so the FDCT waves' atomics rarely collide
     uint64_t list_entries[ENT_SLOTS];
     uint32_t ff_total[2];
+    // bytes k_huff wrote for this state's trials: each trial's stream words
+    // (at least total_bits / 8) and its per-chunk bit counts and 0xFF bins
+    uint64_t huff_wbytes;
     float trial_q[MAX_TRIALS + 1];
     int64_t trial_size[MAX_TRIALS + 1];
 };

@@ -1004,6 +1004,7 @@ __device__ __forceinline__ void decide_trial(const ImgDesc& D, ImgState& S, cons
     const int cur = S.cur;
     S.total_bits[cur] = total_bits;
     S.ff_total[cur] = ff_total;
+    S.huff_wbytes += (total_bits + 7) / 8 + (uint64_t)D.nchunks * 36;
     const int64_t size = (int64_t)D.hdr_len + (int64_t)((total_bits + 7) >> 3) + (int64_t)ff_total + 2;
     const QNode& N = nodes[S.node];
     if (S.ntrials <= MAX_TRIALS) {

@@ -405,15 +405,17 @@ void credit_fdct(Batch& B, const std::vector<int>& ids)
 // Blocks actually quantised+coded by the trials of `ids` since their state
 // was initialised (inactive images exit k_huff at once): the huff kernel's
 // algorithmic work - and bytes: every trial reads each block's list (padded
-// entries), its offset and its length - credited after the stage's
-// synchronisation.
+// entries), its offset and its length, and writes its bitstream (the trial
+// that fits is the file: no re-encode) with the chunks' bit counts and 0xFF
+// bins - credited after the stage's synchronisation.
 void credit_huff(Batch& B, const std::vector<int>& ids)
 {
     if (!B.c->prof) return;
     int64_t blocks = 0, bytes = 0;
     for (int i : ids) {
         blocks += (int64_t)B.state[i].ntrials * B.desc[i].nblocks;
-        bytes += (int64_t)B.state[i].ntrials * (4 * B.it[i].entries + 5 * B.desc[i].nblocks);
+        bytes += (int64_t)B.state[i].ntrials * (4 * B.it[i].entries + 5 * B.desc[i].nblocks) +
+                 (int64_t)B.state[i].huff_wbytes;
     }
     B.c->stats["huff"].units += blocks;
     B.c->stats["huff.bytes"].units += bytes;
