@@ -22,7 +22,7 @@ cat gpurun_out/bench_${TAG}.json
 if [ -z "$SKIP_PROF" ]; then
   cd /tmp
   timeout -k 10 ${T_PROF:-400} rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_${TAG}" -o run \
-      -- python3 "$R/bench.py" ${PROF_ARGS:---steps 20 --warmup 5 --e2e 0 --no-cpu-baseline} \
+      -- python3 "$R/bench.py" ${PROF_ARGS:---steps 20 --warmup 5 --e2e 0 --no-cpu-baseline --host-io-frames 0} \
       > "$R/gpurun_out/prof_${TAG}.out" 2>&1 || { echo "rocprof failed rc=$?"; tail -20 "$R/gpurun_out/prof_${TAG}.out"; exit 1; }
   cd "$R"
   find gpurun_out/prof_${TAG} -name '*kernel_stats.csv' -exec cat {} \;
