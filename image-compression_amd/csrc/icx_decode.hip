@@ -4,9 +4,10 @@
 // oracle/icx_oracle_decode.c for the CPU statement of the same algorithm).
 //
 // Kernel map (per sub-batch of images, all launched on the context's stream):
-//   k_unstuff_end      first terminating marker of each entropy segment
-//   k_unstuff_count    per 4 KiB tile: unstuffed bytes (RSTn -> DEC_PAD bytes)
-//   k_unstuff_scan     per image: tile offsets, stream length, tail pad
+//   k_unstuff_count    per 4 KiB tile: unstuffed bytes (RSTn -> DEC_PAD bytes),
+//                      and the first terminating marker of each entropy segment
+//   k_unstuff_scan     per image: tile offsets (the marker's tile recounted),
+//                      stream length, tail pad
 //   k_unstuff_scatter  compact the stream, record restart-interval starts
 //   k_dec_init         guessed entry state of every subsequence
 //   k_dec_sync         one relaxation step of E[j+1] = walk(E[j]) (icx_decode.h)
@@ -119,23 +120,18 @@ __global__ void __launch_bounds__(256) k_stage(const StageJob* J, Plan p)
 }
 
 // ------------------------------------------------------------------ unstuff
-__global__ void __launch_bounds__(256) k_unstuff_end(const DecDesc* D, DecState* S, Plan p)
+// True when one of the 16 bytes or the byte before them is 0xFF: only then can
+// a byte of this thread be a stuffed zero, a marker or an RSTn code.
+__device__ __forceinline__ bool any_ff(const uint4& v, int prev)
 {
-    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
-    const int img = p.ids[slot];
-    const DecDesc& d = D[img];
-    const int64_t base = (blockIdx.x - p.prefix[slot]) * (int64_t)DEC_TILE + threadIdx.x * 16;
-    if (base >= d.scan_len) return;
-    Bytes16 B;
-    load16(d, base, B);
-    for (int k = 0; k < 16; k++) {
-        const int64_t i = base + k;
-        const int nx = k < 15 ? B.b[k + 1] : B.next;
-        if (i + 1 < d.scan_len && B.b[k] == 0xFF && nx != 0x00 && nx != 0xFF && !is_rst(nx)) {
-            atomicMin((unsigned long long*)&S[img].end, (unsigned long long)i);
-            return;
-        }
+    uint32_t m = 0;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t x = ~w[k];  // 0xFF bytes -> zero bytes
+        m |= (x - 0x01010101u) & ~x & 0x80808080u;
     }
+    return m != 0 || prev == 0xFF;
 }
 
 // Output bytes / RSTn markers of thread t's 16 stuffed bytes below `end`.
@@ -151,26 +147,55 @@ __device__ __forceinline__ void unstuff_counts(const Bytes16& B, int64_t base, i
     }
 }
 
-__global__ void __launch_bounds__(256) k_unstuff_count(const DecDesc* D, const DecState* S, Plan p)
+// Per 4 KiB tile: output bytes and RSTn markers of its bytes below scan_len,
+// and (atomicMin into S.end) the first terminating marker - a 0xFF followed by
+// neither 0x00, 0xFF nor an RSTn code.  Bytes from that marker on are dropped
+// by k_unstuff_scan (it recounts the marker's tile and zeroes the tiles after
+// it), so one pass over the stuffed stream finds both.  A thread whose bytes
+// hold no 0xFF (nor follow one) counts them without the per-byte rule.
+__global__ void __launch_bounds__(256) k_unstuff_count(const DecDesc* D, DecState* S, Plan p)
 {
-    __shared__ uint32_t sh[8];
+    __shared__ uint32_t sh[2][4];
     const int slot = slot_of(p.prefix, p.m, blockIdx.x);
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
     const int64_t tile = blockIdx.x - p.prefix[slot];
     const int64_t base = tile * DEC_TILE + threadIdx.x * 16;
     uint32_t nb = 0, nr = 0;
-    if (base < S[img].end) {
-        Bytes16 B;
-        load16(d, base, B);
-        unstuff_counts(B, base, S[img].end, nb, nr);
+    if (base < d.scan_len) {
+        const uint4 v = *(const uint4*)(d.scan + base);  // scan copy is 16-B aligned and padded
+        const int prev = base > 0 ? d.scan[base - 1] : 0;
+        if (!any_ff(v, prev)) {
+            nb = (uint32_t)min((int64_t)16, d.scan_len - base);
+        } else {
+            Bytes16 B;
+            load16(d, base, B);
+            unstuff_counts(B, base, d.scan_len, nb, nr);
+            for (int k = 0; k < 16; k++) {
+                const int64_t i = base + k;
+                const int nx = k < 15 ? B.b[k + 1] : B.next;
+                if (i + 1 < d.scan_len && B.b[k] == 0xFF && nx != 0x00 && nx != 0xFF && !is_rst(nx)) {
+                    atomicMin((unsigned long long*)&S[img].end, (unsigned long long)i);
+                    break;
+                }
+            }
+        }
     }
-    uint32_t tb, tr;
-    block_exscan<256>(nb, sh, tb);
-    block_exscan<256>(nr, sh, tr);
+    // workgroup sums: wave reduction, then the four wave totals
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        nb += __shfl_xor(nb, o, 64);
+        nr += __shfl_xor(nr, o, 64);
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) {
+        sh[0][w] = nb;
+        sh[1][w] = nr;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        d.tile_cnt[tile] = tb;
-        d.tile_rst[tile] = tr;
+        d.tile_cnt[tile] = sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3];
+        d.tile_rst[tile] = sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3];
     }
 }
 
@@ -179,13 +204,45 @@ __global__ void __launch_bounds__(1024) k_unstuff_scan(const DecDesc* D, DecStat
                                                        uint32_t sub_bits)
 {
     __shared__ uint32_t sh[24];
+    __shared__ uint32_t te_cnt[2];
     const int img = ids[blockIdx.x];
     const DecDesc& d = D[img];
     DecState& st = S[img];
+    // k_unstuff_count counted every tile up to scan_len: the tile holding the
+    // terminating marker is recounted below it (4 bytes per thread), the
+    // tiles after it count nothing
+    const int64_t end = st.end;
+    const int64_t te = end / DEC_TILE;
+    if (te < d.ntiles) {
+        uint32_t nb = 0, nr = 0;
+#pragma unroll
+        for (int k = 0; k < DEC_TILE / 1024; k++) {
+            const int64_t i = te * DEC_TILE + threadIdx.x * (DEC_TILE / 1024) + k;
+            if (i < end) {
+                int rst;
+                nb += (uint32_t)dec_unstuff_rule(i > 0 ? d.scan[i - 1] : 0, d.scan[i], d.scan[i + 1], &rst);
+                nr += (uint32_t)rst;
+            }
+        }
+        uint32_t tb, tr;
+        block_exscan<1024>(nb, sh, tb);
+        block_exscan<1024>(nr, sh, tr);
+        if (threadIdx.x == 0) {
+            te_cnt[0] = tb;
+            te_cnt[1] = tr;
+        }
+        __syncthreads();
+    }
     uint32_t carry_b = 0, carry_r = 0;
     for (int t0 = 0; t0 < d.ntiles; t0 += 1024) {
         const int t = t0 + threadIdx.x;
-        const uint32_t b = t < d.ntiles ? d.tile_cnt[t] : 0, r = t < d.ntiles ? d.tile_rst[t] : 0;
+        uint32_t b = t < d.ntiles ? d.tile_cnt[t] : 0, r = t < d.ntiles ? d.tile_rst[t] : 0;
+        if (t == te) {
+            b = te_cnt[0];
+            r = te_cnt[1];
+        } else if (t > te) {
+            b = r = 0;
+        }
         uint32_t sb, sr;
         const uint32_t eb = block_exscan<1024>(b, sh, sb);
         const uint32_t er = block_exscan<1024>(r, sh, sr);
@@ -216,54 +273,99 @@ __global__ void __launch_bounds__(1024) k_unstuff_scan(const DecDesc* D, DecStat
 }
 
 // Compact one tile: each thread applies the unstuffing rule to its 16 bytes
-// (fully unrolled, no dynamic register indexing), writes its output bytes at
-// its workgroup-local offset in LDS, and the workgroup then copies the tile's
-// contiguous output to HBM with consecutive lanes on consecutive bytes.
+// (fully unrolled, no dynamic register indexing) and places its output bytes
+// at its workgroup-local offset in a zeroed LDS copy of the tile's output - a
+// thread without 0xFF bytes as four shifted dwords (the two partial ones ORed
+// in), the others byte by byte - and the workgroup then stores the tile's
+// output as aligned dwords (funnel-shifted out of LDS), the unaligned head and
+// tail bytes by single lanes.
 __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const DecState* S, Plan p)
 {
     __shared__ uint32_t sh[8];
-    __shared__ uint8_t buf[DEC_TILE / 2 * DEC_PAD + 64];  // worst case: an RSTn marker every 2 bytes
+    __shared__ uint32_t bufw[(DEC_TILE / 2 * DEC_PAD + 64) / 4];  // worst case: an RSTn marker every 2 bytes
+    uint8_t* const buf = (uint8_t*)bufw;
     const int slot = slot_of(p.prefix, p.m, blockIdx.x);
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
     const int64_t tile = blockIdx.x - p.prefix[slot];
     const int64_t base = tile * DEC_TILE + threadIdx.x * 16;
     const int64_t end = S[img].end;
+    if (tile * DEC_TILE >= end) return;  // workgroup-uniform: nothing of this tile is data
     Bytes16 B;
     for (int k = 0; k < 16; k++) B.b[k] = 0;
     B.prev = B.next = 0;
-    if (base < end) load16(d, base, B);
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    bool plain = false;  // 16 data bytes, no 0xFF among them or before them
+    if (base < end) {
+        v = *(const uint4*)(d.scan + base);
+        plain = base + 16 <= end && !any_ff(v, base > 0 ? d.scan[base - 1] : 0);
+        if (!plain) load16(d, base, B);
+    }
     int out[16], rsts[16];
     uint32_t nb = 0, nr = 0;
+    if (plain) {
+        nb = 16;
+    } else {
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        int rst = 0;
-        const int c = base + k < end
-                          ? dec_unstuff_rule(k ? B.b[k - 1] : B.prev, B.b[k], k < 15 ? B.b[k + 1] : B.next, &rst)
-                          : 0;
-        out[k] = c;
-        rsts[k] = rst;
-        nb += (uint32_t)c;
-        nr += (uint32_t)rst;
+        for (int k = 0; k < 16; k++) {
+            int rst = 0;
+            const int c = base + k < end ? dec_unstuff_rule(k ? B.b[k - 1] : B.prev, B.b[k],
+                                                            k < 15 ? B.b[k + 1] : B.next, &rst)
+                                         : 0;
+            out[k] = c;
+            rsts[k] = rst;
+            nb += (uint32_t)c;
+            nr += (uint32_t)rst;
+        }
     }
     uint32_t tb, tr;
     uint32_t ob = block_exscan<256>(nb, sh, tb);
     uint32_t orr = block_exscan<256>(nr, sh, tr) + d.tile_rst[tile];
     const uint32_t tile_off = d.tile_cnt[tile];
+    for (uint32_t k = threadIdx.x; k < (tb + 7) / 4; k += 256) bufw[k] = 0;
+    __syncthreads();
+    if (plain) {
+        const uint32_t s8 = (ob & 3) * 8;
+        uint32_t* wp = bufw + (ob >> 2);
+        if (s8 == 0) {
+            wp[0] = v.x; wp[1] = v.y; wp[2] = v.z; wp[3] = v.w;
+        } else {
+            atomicOr(wp, v.x << s8);
+            wp[1] = (v.x >> (32 - s8)) | (v.y << s8);
+            wp[2] = (v.y >> (32 - s8)) | (v.z << s8);
+            wp[3] = (v.z >> (32 - s8)) | (v.w << s8);
+            atomicOr(wp + 4, v.w >> (32 - s8));
+        }
+    } else {
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        if (rsts[k]) {
-            for (int q = 0; q < DEC_PAD; q++) buf[ob + q] = 0xFF;
-            ob += DEC_PAD;
-            if (orr + 1 < (uint32_t)d.nseg_max) d.seg[orr + 1] = tile_off + ob;
-            orr++;
-        } else if (out[k]) {
-            buf[ob++] = B.b[k];
+        for (int k = 0; k < 16; k++) {
+            if (rsts[k]) {
+                for (int q = 0; q < DEC_PAD; q++) buf[ob + q] = 0xFF;
+                ob += DEC_PAD;
+                if (orr + 1 < (uint32_t)d.nseg_max) d.seg[orr + 1] = tile_off + ob;
+                orr++;
+            } else if (out[k]) {
+                buf[ob++] = B.b[k];
+            }
         }
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < tb; k += 256)
-        if ((int64_t)(tile_off + k) < d.ent_cap) d.ent[tile_off + k] = buf[k];
+    // tile output = global bytes [tile_off, tile_off + tb)
+    const uint32_t head = min((4u - (tile_off & 3u)) & 3u, tb);
+    if (threadIdx.x < head && (int64_t)(tile_off + threadIdx.x) < d.ent_cap)
+        d.ent[tile_off + threadIdx.x] = buf[threadIdx.x];
+    const uint32_t nw = (tb - head) >> 2;         // whole aligned dwords
+    const uint32_t sh8 = head;                    // local byte of the first dword: head + 4k
+    uint32_t* const dstw = (uint32_t*)(d.ent + tile_off + head);  // 4-byte aligned
+    const int64_t cap_w = (d.ent_cap - (int64_t)(tile_off + head)) >> 2;
+    for (uint32_t k = threadIdx.x; k < nw; k += 256) {
+        const uint32_t lb = head + 4 * k;
+        const uint32_t val = __builtin_amdgcn_alignbyte(bufw[(lb >> 2) + 1], bufw[lb >> 2], sh8);
+        if ((int64_t)k < cap_w) dstw[k] = val;
+    }
+    const uint32_t t0 = head + 4 * nw;
+    if (threadIdx.x < tb - t0 && (int64_t)(tile_off + t0 + threadIdx.x) < d.ent_cap)
+        d.ent[tile_off + t0 + threadIdx.x] = buf[t0 + threadIdx.x];
 }
 
 // ------------------------------------------------------------ entropy decode
@@ -844,7 +946,6 @@ void launch_unstuff(const DecDesc* d, DecState* s, const Plan& tiles, int64_t nt
                     uint32_t sub_bits, hipStream_t st)
 {
     if (ntiles <= 0 || m <= 0) return;
-    hipLaunchKernelGGL(k_unstuff_end, dim3((unsigned)ntiles), dim3(256), 0, st, d, s, tiles);
     hipLaunchKernelGGL(k_unstuff_count, dim3((unsigned)ntiles), dim3(256), 0, st, d, s, tiles);
     hipLaunchKernelGGL(k_unstuff_scan, dim3((unsigned)m), dim3(1024), 0, st, d, s, ids, sub_bits);
     hipLaunchKernelGGL(k_unstuff_scatter, dim3((unsigned)ntiles), dim3(256), 0, st, d, s, tiles);
