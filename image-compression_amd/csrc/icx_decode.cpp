@@ -386,9 +386,11 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         }
         // ---- settle the subsequence entry states
         int it = 0;
+        static const char* const sync_names[] = {"dec_sync", "dec_sync_r1", "dec_sync_r2", "dec_sync_r3",
+                                                 "dec_sync_r4", "dec_sync_r5", "dec_sync_r6", "dec_sync_r7+"};
         for (;;) {
             for (int k = 0; k < 4 && it < max_it; k++, it++) {
-                Timed tm(c, "dec_sync", 0);
+                Timed tm(c, sync_names[std::min(it, 7)], 0);
                 launch_dec_sync(d_desc, d_state, Ps.p, Ps.total, S, it, max_it, d_changed + it, c->stream);
             }
             e = hipMemcpyAsync(h_changed, d_changed + it - 1, 4, hipMemcpyDeviceToHost, c->stream);
@@ -398,6 +400,16 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             if (it >= max_it) return fail(c, ICX_E_DEVICE, "entropy decode did not settle");
         }
         c->stats["dec_sync_iters"].launches += it;
+        if (c->prof) {  // profiling: subsequences re-walked by each later launch (worklist sizes)
+            std::vector<uint32_t> wl((size_t)m * max_it);
+            e = hipMemcpy(wl.data(), d_wlcnt, wl.size() * 4, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return hip_fail(c, e, "worklist counters");
+            int64_t subs = 0;
+            for (int k = 0; k < m; k++) subs += desc[k].nsub_max;
+            c->stats["dec_sync_walks"].units += subs;
+            for (int r = 0; r + 1 < it; r++)
+                for (int k = 0; k < m; k++) c->stats["dec_sync_walks"].units += wl[(size_t)k * max_it + r];
+        }
         launch_dec_offsets(d_desc, d_state, d_ids, m, c->stream);
         {
             Timed tm(c, "dec_write", stuffed);

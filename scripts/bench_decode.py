@@ -59,8 +59,14 @@ def main():
         P.run()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
-    kern = {k: codec.profile_query(k) for k in ("dec_unstuff", "dec_init", "dec_sync", "dec_write", "dec_dc", "dec_idct",
-                                                 "dec_color", "dec_sync_iters")}
+    names = ("dec_unstuff", "dec_init", "dec_sync", "dec_write", "dec_dc", "dec_idct", "dec_color", "dec_sync_iters")
+    rel = ("dec_sync_r1", "dec_sync_r2", "dec_sync_r3", "dec_sync_r4", "dec_sync_r5", "dec_sync_r6", "dec_sync_r7+")
+    kern = {k: codec.profile_query(k) for k in names}
+    relaunch = {k[9:]: codec.profile_query(k) for k in rel}
+    walks = codec.profile_query("dec_sync_walks")["units"]
+    kern["dec_sync0"] = dict(kern["dec_sync"])
+    kern["dec_sync"] = dict(kern["dec_sync"])
+    kern["dec_sync"]["ms"] += sum(v["ms"] for v in relaunch.values())
     mp = a.frames * a.height * a.width / 1e6
     stuffed = sum(len(srcs[i % len(srcs)]) for i in range(a.frames))
     print(json.dumps({"metric": "megapixels/sec JPEG decode (4K q95 4:2:0, HBM-resident)", "value": round(mp / dt, 1),
@@ -68,7 +74,9 @@ def main():
                       "mean_jpeg_bytes": stuffed // a.frames,
                       "kernels_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in kern.items()
                                               if k != "dec_sync_iters"},
-                      "sync_launches_per_step": kern["dec_sync_iters"]["launches"] / a.steps}))
+                      "sync_launches_per_step": kern["dec_sync_iters"]["launches"] / a.steps,
+                      "sync_relaunch_ms": {k: round(v["ms"] / a.steps, 3) for k, v in relaunch.items() if v["launches"]},
+                      "sync_walks_per_step": walks / a.steps}))
     codec.close()
 
 
