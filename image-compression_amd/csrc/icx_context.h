@@ -179,6 +179,10 @@ struct icx_ctx {
     // arenas while the previous sub-batch computes, outputs leave (io_down)
     // while the next one computes; created on first use.
     hipStream_t io_up = nullptr, io_down = nullptr;
+    // decoder: images whose entry states settled early finish on dec_aux while
+    // the others keep relaxing on `stream` (created at the first decode)
+    hipStream_t dec_aux = nullptr;
+    hipEvent_t ev_dec_split = nullptr, ev_dec_aux = nullptr;
     icx::DevArena stage[2];
     hipEvent_t ev_up[2] = {nullptr, nullptr}, ev_down[2] = {nullptr, nullptr}, ev_done = nullptr;
 };
@@ -218,8 +222,9 @@ struct Timed {
     icx_ctx* c;
     Pending p;
     bool on, ext;
-    Timed(icx_ctx* ctx, const char* name, int64_t units, bool ext_launch = false)
-        : c(ctx), on(ctx->prof), ext(ext_launch)
+    hipStream_t st;  // the stream the region's launches go to (default: the context's)
+    Timed(icx_ctx* ctx, const char* name, int64_t units, bool ext_launch = false, hipStream_t stream = nullptr)
+        : c(ctx), on(ctx->prof), ext(ext_launch), st(stream ? stream : ctx->stream)
     {
         if (!on) return;
         p.name = name;
@@ -227,13 +232,13 @@ struct Timed {
         p.a = get_event(c);
         p.b = get_event(c);
         if (ext) g_launch_timing = LaunchTiming{p.a, p.b, false};
-        else hipEventRecord(p.a, c->stream);
+        else hipEventRecord(p.a, st);
     }
     ~Timed()
     {
         if (!on) return;
         if (!ext) {
-            hipEventRecord(p.b, c->stream);
+            hipEventRecord(p.b, st);
             c->pending.push_back(p);
             return;
         }

@@ -260,7 +260,10 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         // every small argument array of the sub-batch travels in one packed upload
         const size_t up = Uploader::need<DecTab>(m) + Uploader::need<DecDesc>(m) + Uploader::need<DecState>(m) +
                           Uploader::need<int32_t>(m) + Uploader::need<StageJob>(m) +
-                          6 * Uploader::need<int64_t>(m + 1);
+                          3 * Uploader::need<int64_t>(m + 1) +
+                          // the decode tails (subsets settled at one check): ids and 4 plans each; each
+                          // image is in one tail, so at most m + 1 tails of 36 B per image + alignment
+                          36 * (size_t)m + (size_t)(m + 1) * (64 + 4 * 72);
         hipError_t e = c->dev.reserve(need + up + (size_t)m * 64 * 1024 + (16 << 20));
         if (e != hipSuccess) {
             for (DecItem* it : sub) it->job->status = ICX_E_NOMEM;
@@ -367,9 +370,9 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             cnt_rows[k] = q.fuse420 ? (int64_t)q.mcuy * ((q.mcux + 7) / 8) : 0;
             stuffed += desc[k].scan_len;
         }
+        // plans of the whole sub-batch; the pixel stages get theirs per tail
         const WPlan Pg = plan_of(U, cnt_stage, d_ids), Pt = plan_of(U, cnt_tiles, d_ids),
-                    Ps = plan_of(U, cnt_subs, d_ids), Pb = plan_of(U, cnt_blk, d_ids),
-                    Pp = plan_of(U, cnt_px, d_ids), Pr = plan_of(U, cnt_rows, d_ids);
+                    Ps = plan_of(U, cnt_subs, d_ids);
         icx_status st = U.flush();
         if (st) return st;
         e = hipMemsetAsync(d_changed, 0, (size_t)max_it * 4, c->stream);
@@ -384,53 +387,113 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             Timed tm(c, "dec_init", stuffed);
             launch_dec_init(d_desc, d_state, Ps.p, Ps.total, S, warm_bits(S), c->stream);
         }
-        // ---- settle the subsequence entry states
+        // ---- settle the subsequence entry states.  An image whose last sync
+        // launch appended nothing to its worklist has settled (its worklists
+        // stay empty); at each check the images that settled since the last one
+        // run the rest of their decode on the aux stream while the others keep
+        // relaxing here.  The relaxation's later launches re-walk the few long
+        // chains of unsynchronised subsequences one link per launch and leave
+        // most of the chip idle, so the settled images' write, DC, IDCT and
+        // colour passes fill it.
+        auto tail = [&](const std::vector<int>& ks, hipStream_t s) -> icx_status {
+            std::vector<int32_t> sid(ks.begin(), ks.end());
+            std::vector<int64_t> a, b, r, q;
+            int64_t stf = 0, tpx = 0;
+            for (int k : ks) {
+                a.push_back(cnt_subs[k]);
+                b.push_back(cnt_blk[k]);
+                r.push_back(cnt_rows[k]);
+                q.push_back(cnt_px[k]);
+                stf += desc[k].scan_len;
+                tpx += (int64_t)desc[k].w * desc[k].h;
+            }
+            const int n = (int)ks.size();
+            const int32_t* d_sid = U.put(sid.data(), sid.size());
+            const WPlan Ws = plan_of(U, a, d_sid), Wb = plan_of(U, b, d_sid), Wr = plan_of(U, r, d_sid),
+                        Wp = plan_of(U, q, d_sid);
+            if (icx_status st = U.flush()) return st;  // on c->stream, behind the launches that settled them
+            if (s != c->stream) {
+                hipError_t he2 = hipEventRecord(c->ev_dec_split, c->stream);
+                if (he2 == hipSuccess) he2 = hipStreamWaitEvent(s, c->ev_dec_split, 0);
+                if (he2 != hipSuccess) return hip_fail(c, he2, "decode stream split");
+            }
+            launch_dec_offsets(d_desc, d_state, d_sid, n, s);
+            {
+                Timed tm(c, "dec_write", stf, false, s);
+                launch_dec_write(d_desc, d_state, Ws.p, Ws.total, S, s);
+            }
+            {
+                Timed tm(c, "dec_dc", n, false, s);
+                launch_dec_dc(d_desc, d_state, d_sid, n, s);
+            }
+            if (!coef_out) {
+                {
+                    Timed tm(c, "dec_idct", tpx, false, s);
+                    launch_dec_idct(d_desc, d_state, Wb.p, Wb.total, s);
+                }
+                {
+                    Timed tm(c, "dec_color", tpx, false, s);
+                    launch_dec_luma_color_420(d_desc, d_state, Wr.p, Wr.total, s);
+                    launch_dec_color(d_desc, d_state, Wp.p, Wp.total, s);
+                }
+            }
+            return ICX_OK;
+        };
+        if (!c->dec_aux) {
+            hipError_t he2 = hipStreamCreateWithFlags(&c->dec_aux, hipStreamNonBlocking);
+            if (he2 == hipSuccess) he2 = hipEventCreateWithFlags(&c->ev_dec_split, hipEventDisableTiming);
+            if (he2 == hipSuccess) he2 = hipEventCreateWithFlags(&c->ev_dec_aux, hipEventDisableTiming);
+            if (he2 != hipSuccess) return hip_fail(c, he2, "decode aux stream");
+        }
+        uint32_t* h_wl = (uint32_t*)c->host.take((size_t)m * 4);
+        if (!h_wl) return fail(c, ICX_E_NOMEM, "pinned staging exhausted");
+        std::vector<char> tailed(m, 0);
+        bool aux_used = false;
         int it = 0;
         static const char* const sync_names[] = {"dec_sync", "dec_sync_r1", "dec_sync_r2", "dec_sync_r3",
                                                  "dec_sync_r4", "dec_sync_r5", "dec_sync_r6", "dec_sync_r7+"};
+        static const int SYNC_PER_CHECK = getenv("ICX_DEC_CHECK") ? atoi(getenv("ICX_DEC_CHECK")) : 2;
         for (;;) {
-            for (int k = 0; k < 4 && it < max_it; k++, it++) {
+            for (int k = 0; k < SYNC_PER_CHECK && it < max_it; k++, it++) {
                 Timed tm(c, sync_names[std::min(it, 7)], 0);
-                launch_dec_sync(d_desc, d_state, Ps.p, Ps.total, S, it, max_it, d_changed + it, c->stream);
+                launch_dec_sync(d_desc, d_state, Ps.p, Ps.total, S, it, m, d_changed + it, c->stream);
             }
             e = hipMemcpyAsync(h_changed, d_changed + it - 1, 4, hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(h_wl, d_wlcnt + (size_t)(it - 1) * m, (size_t)m * 4, hipMemcpyDeviceToHost,
+                                   c->stream);
             if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
             if (e != hipSuccess) return hip_fail(c, e, "sync counter");
             if (*h_changed == 0) break;
             if (it >= max_it) return fail(c, ICX_E_DEVICE, "entropy decode did not settle");
+            std::vector<int> early;
+            for (int k = 0; k < m; k++)
+                if (!tailed[k] && h_wl[k] == 0) early.push_back(k);
+            if (!early.empty()) {
+                for (int k : early) tailed[k] = 1;
+                if (icx_status st = tail(early, c->dec_aux)) return st;
+                aux_used = true;
+            }
         }
         c->stats["dec_sync_iters"].launches += it;
         if (c->prof) {  // profiling: subsequences re-walked by each later launch (worklist sizes)
-            std::vector<uint32_t> wl((size_t)m * max_it);
+            std::vector<uint32_t> wl((size_t)m * it);
             e = hipMemcpy(wl.data(), d_wlcnt, wl.size() * 4, hipMemcpyDeviceToHost);
             if (e != hipSuccess) return hip_fail(c, e, "worklist counters");
             int64_t subs = 0;
             for (int k = 0; k < m; k++) subs += desc[k].nsub_max;
             c->stats["dec_sync_walks"].units += subs;
-            for (int r = 0; r + 1 < it; r++)
-                for (int k = 0; k < m; k++) c->stats["dec_sync_walks"].units += wl[(size_t)k * max_it + r];
+            for (size_t i = 0; i < (size_t)m * (it - 1); i++) c->stats["dec_sync_walks"].units += wl[i];  // launches 1..it-1
         }
-        launch_dec_offsets(d_desc, d_state, d_ids, m, c->stream);
-        {
-            Timed tm(c, "dec_write", stuffed);
-            launch_dec_write(d_desc, d_state, Ps.p, Ps.total, S, c->stream);
-        }
-        {
-            Timed tm(c, "dec_dc", m);
-            launch_dec_dc(d_desc, d_state, d_ids, m, c->stream);
-        }
-        int64_t px = 0;
-        for (int k = 0; k < m; k++) px += (int64_t)desc[k].w * desc[k].h;
-        if (!coef_out) {
-            {
-                Timed tm(c, "dec_idct", px);
-                launch_dec_idct(d_desc, d_state, Pb.p, Pb.total, c->stream);
-            }
-            {
-                Timed tm(c, "dec_color", px);
-                launch_dec_luma_color_420(d_desc, d_state, Pr.p, Pr.total, c->stream);
-                launch_dec_color(d_desc, d_state, Pp.p, Pp.total, c->stream);
-            }
+        std::vector<int> rest;
+        for (int k = 0; k < m; k++)
+            if (!tailed[k]) rest.push_back(k);
+        if (!rest.empty())
+            if (icx_status st = tail(rest, c->stream)) return st;
+        if (aux_used) {  // the final download waits for the aux stream's images too
+            e = hipEventRecord(c->ev_dec_aux, c->dec_aux);
+            if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_dec_aux, 0);
+            if (e != hipSuccess) return hip_fail(c, e, "decode stream join");
         }
         DecState* h_state = (DecState*)c->host.take(sizeof(DecState) * m);
         if (!h_state) return fail(c, ICX_E_NOMEM, "pinned staging exhausted");

@@ -89,7 +89,7 @@ struct DecDesc {
     uint64_t* est;         // entry state per subsequence (nsub_max + 1)
     uint64_t* ck;          // sync-walk checkpoints, DEC_CK_MAX per subsequence (dec_sync_walk)
     uint32_t* wl[2];       // subsequences to re-walk in the next sync launch (ping-pong)
-    uint32_t* wl_cnt;      // entries appended to the worklist by sync launch r: wl_cnt[r]
+    uint32_t* wl_cnt;      // entries appended to image i's worklist by sync launch r: wl_cnt[r * images + i]
     uint32_t* ncnt;        // blocks completed inside each subsequence
     uint32_t* boff;        // blocks completed before each subsequence
     int16_t* coefs;        // nblocks x 64, natural order, quantised; [0] = DC difference

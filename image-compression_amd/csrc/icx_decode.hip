@@ -428,7 +428,7 @@ __device__ __forceinline__ uint32_t selector(const DecTab* T)
 // (staged in LDS) and stops where it meets its previous walk (dec_sync_walk).
 template <bool FIRST>
 __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
-                                                  int iter, int max_it, uint32_t* changed)
+                                                  int iter, int nimg, uint32_t* changed)
 {
     __shared__ __attribute__((aligned(16))) DecHuff L[4];
     __shared__ uint64_t ckl[FIRST ? 1 : 256][DEC_CK_MAX];
@@ -438,7 +438,7 @@ __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecSta
     const DecState& st = S[img];
     if (st.status) return;
     const int64_t k = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
-    const uint32_t n = FIRST ? st.nsub : d.wl_cnt[(int64_t)img * max_it + iter - 1];
+    const uint32_t n = FIRST ? st.nsub : d.wl_cnt[(int64_t)(iter - 1) * nimg + img];
     if ((blockIdx.x - p.prefix[slot]) * 256 >= (int64_t)n) return;
     load_tables(d.tab, L);
     if (k >= n) return;
@@ -467,7 +467,7 @@ __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecSta
     if (x != old) {
         __hip_atomic_store(&d.est[j + 1], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (j + 1 < st.nsub) {
-            const uint32_t pos = atomicAdd(&d.wl_cnt[(int64_t)img * max_it + iter], 1u);
+            const uint32_t pos = atomicAdd(&d.wl_cnt[(int64_t)iter * nimg + img], 1u);
             d.wl[(iter + 1) & 1][pos] = j + 1;
         }
         atomicAdd(changed, 1u);
@@ -586,9 +586,59 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
     if (w.bad) atomicOr(&S[img].status, 6);
 }
 
+// DC prediction of MCUs [m0, m1) of one image, NB blocks per MCU (the first
+// NY luma): pass 1 (WRITE false) sums the differences since the range's last
+// restart into acc; pass 2 (WRITE true) turns them into values from pred.
+// The restart test walks a running boundary instead of dividing per MCU.
+// NB == 0: any layout (nb blocks per MCU at run time).
+template <int NB, bool WRITE>
+__device__ __forceinline__ void dc_range(ICX_GLOBAL int32_t* dc, int nb, int64_t m0, int64_t m1, int ri, int ny,
+                                         int32_t (&acc)[3], int& reset)
+{
+    int64_t next = ri ? (m0 + ri - 1) / ri * ri : INT64_MAX;  // first restart boundary >= m0
+    for (int64_t m = m0; m < m1; m++) {
+        if (m == next) {
+            acc[0] = acc[1] = acc[2] = 0;
+            reset = 1;
+            next += ri;
+        }
+        if (NB > 0) {
+            int32_t v[NB > 0 ? NB : 1];
+#pragma unroll
+            for (int k = 0; k < NB; k++) v[k] = dc[m * NB + k];
+#pragma unroll
+            for (int k = 0; k < NB; k++) {
+                const int c = k < ny ? 0 : k - ny + 1;
+                acc[c] += v[k];
+                if (WRITE) dc[m * NB + k] = (int32_t)(int16_t)acc[c];
+            }
+        } else {
+            for (int k = 0; k < nb; k++) {
+                const int c = k < ny ? 0 : k - ny + 1;
+                acc[c] += dc[m * nb + k];
+                if (WRITE) dc[m * nb + k] = (int32_t)(int16_t)acc[c];
+            }
+        }
+    }
+}
+
+template <bool WRITE>
+__device__ __forceinline__ void dc_range_any(ICX_GLOBAL int32_t* dc, int nb, int64_t m0, int64_t m1, int ri, int ny,
+                                             int32_t (&acc)[3], int& reset)
+{
+    switch (nb) {  // 4:2:0, 4:2:2, 4:4:4, grey; anything else at run time
+        case 6: dc_range<6, WRITE>(dc, nb, m0, m1, ri, ny, acc, reset); break;
+        case 4: dc_range<4, WRITE>(dc, nb, m0, m1, ri, ny, acc, reset); break;
+        case 3: dc_range<3, WRITE>(dc, nb, m0, m1, ri, ny, acc, reset); break;
+        case 1: dc_range<1, WRITE>(dc, nb, m0, m1, ri, ny, acc, reset); break;
+        default: dc_range<0, WRITE>(dc, nb, m0, m1, ri, ny, acc, reset); break;
+    }
+}
+
 // One workgroup per image: DC values from the differences the write pass left
 // in d.dc, in place, per component, the predictor reset at every restart
-// interval (jdhuff.c process_restart).
+// interval (jdhuff.c process_restart).  Each thread takes a contiguous range
+// of MCUs; a segmented scan over the threads carries the predictors.
 __global__ void __launch_bounds__(1024) k_dec_dc(const DecDesc* D, const DecState* S, const int32_t* ids)
 {
     __shared__ int32_t sv[3][1024];
@@ -598,17 +648,13 @@ __global__ void __launch_bounds__(1024) k_dec_dc(const DecDesc* D, const DecStat
     if (S[img].status) return;
     const int64_t nmcu = (int64_t)d.mcux * d.mcuy;
     const int64_t per = (nmcu + 1023) / 1024;
-    const int64_t m0 = threadIdx.x * per, m1 = m0 + per < nmcu ? m0 + per : nmcu;
+    const int64_t m0 = min((int64_t)threadIdx.x * per, nmcu), m1 = min(m0 + per, nmcu);
+    ICX_GLOBAL int32_t* dc = (ICX_GLOBAL int32_t*)d.dc;
+    const int nb = d.nbmcu, ri = d.ri, ny = d.nby;
     // pass 1: this thread's sums since its last reset
     int32_t acc[3] = {0, 0, 0};
     int reset = 0;
-    for (int64_t m = m0; m < m1; m++) {
-        if (d.ri && m % d.ri == 0) {
-            acc[0] = acc[1] = acc[2] = 0;
-            reset = 1;
-        }
-        for (int k = 0; k < d.nbmcu; k++) acc[k < d.nby ? 0 : k - d.nby + 1] += d.dc[m * d.nbmcu + k];
-    }
+    dc_range_any<false>(dc, nb, m0, m1, ri, ny, acc, reset);
     for (int c = 0; c < 3; c++) sv[c][threadIdx.x] = acc[c];
     sf[threadIdx.x] = reset;
     __syncthreads();
@@ -634,14 +680,7 @@ __global__ void __launch_bounds__(1024) k_dec_dc(const DecDesc* D, const DecStat
     if (threadIdx.x > 0)
         for (int c = 0; c < 3; c++) pred[c] = sv[c][threadIdx.x - 1];
     // pass 2: write DC values
-    for (int64_t m = m0; m < m1; m++) {
-        if (d.ri && m % d.ri == 0) pred[0] = pred[1] = pred[2] = 0;
-        for (int k = 0; k < d.nbmcu; k++) {
-            const int c = k < d.nby ? 0 : k - d.nby + 1;
-            pred[c] += d.dc[m * d.nbmcu + k];
-            d.dc[m * d.nbmcu + k] = (int32_t)(int16_t)pred[c];
-        }
-    }
+    dc_range_any<true>(dc, nb, m0, m1, ri, ny, pred, reset);
 }
 
 // ------------------------------------------------------------------- IDCT
@@ -958,11 +997,11 @@ void launch_dec_init(const DecDesc* d, const DecState* s, const Plan& subs, int6
 }
 
 void launch_dec_sync(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
-                     int iter, int max_it, uint32_t* changed, hipStream_t st)
+                     int iter, int nimg, uint32_t* changed, hipStream_t st)
 {
     if (nwg > 0)
         hipLaunchKernelGGL(iter == 0 ? k_dec_sync<true> : k_dec_sync<false>, dim3((unsigned)nwg), dim3(256), 0, st,
-                           d, s, subs, sub_bits, iter, max_it, changed);
+                           d, s, subs, sub_bits, iter, nimg, changed);
 }
 
 void launch_dec_offsets(const DecDesc* d, DecState* s, const int32_t* ids, int m, hipStream_t st)

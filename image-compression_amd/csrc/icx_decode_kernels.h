@@ -17,9 +17,9 @@ void launch_unstuff(const DecDesc* d, DecState* s, const Plan& tiles, int64_t nt
 void launch_dec_init(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
                      uint32_t warm, hipStream_t st);
 // iter 0 walks every subsequence, iter r > 0 the worklist built by iter r-1;
-// wl_cnt holds max_it counters per image (zeroed before iter 0)
+// wl_cnt holds nimg counters per launch (wl_cnt[r * nimg + image], zeroed before iter 0)
 void launch_dec_sync(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
-                     int iter, int max_it, uint32_t* changed, hipStream_t st);
+                     int iter, int nimg, uint32_t* changed, hipStream_t st);
 void launch_dec_offsets(const DecDesc* d, DecState* s, const int32_t* ids, int m, hipStream_t st);
 void launch_dec_write(const DecDesc* d, DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
                       hipStream_t st);

@@ -1058,6 +1058,12 @@ void icx_destroy(icx_ctx* ctx)
     for (auto& p : ctx->pending) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
     for (auto e : ctx->evpool) hipEventDestroy(e);
     hipStreamDestroy(ctx->stream);
+    if (ctx->dec_aux) {
+        hipStreamSynchronize(ctx->dec_aux);
+        hipStreamDestroy(ctx->dec_aux);
+        hipEventDestroy(ctx->ev_dec_split);
+        hipEventDestroy(ctx->ev_dec_aux);
+    }
     if (ctx->io_up) {
         hipStreamSynchronize(ctx->io_up);
         hipStreamSynchronize(ctx->io_down);
