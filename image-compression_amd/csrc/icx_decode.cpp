@@ -171,6 +171,13 @@ WPlan plan_of(Uploader& U, const std::vector<int64_t>& counts, const int32_t* d_
     out.p.prefix = U.put(pre.data(), pre.size());
     out.p.m = (int32_t)counts.size();
     out.total = pre.back();
+    // 2-D launch (no slot search at workgroup start: a binary search of the
+    // prefix array is a chain of dependent loads, which short workgroups such
+    // as a 4 KiB unstuff tile would mostly wait on) unless more than a third
+    // of its workgroups would find nothing to do
+    const int64_t maxc = counts.empty() ? 0 : *std::max_element(counts.begin(), counts.end());
+    if (out.p.m > 1 && out.p.m <= 65535 && maxc > 0 && maxc < (1ll << 31) && maxc * out.p.m * 2 <= out.total * 3)
+        out.p.width = (int32_t)maxc;
     return out;
 }
 

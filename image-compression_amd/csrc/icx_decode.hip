@@ -40,6 +40,21 @@ __device__ __forceinline__ int slot_of(const int64_t* prefix, int m, int64_t ite
     return lo;
 }
 
+// Slot and item of this workgroup: 2-D launches (Plan.width > 0: x = item,
+// y = slot) need no search and drop the items past a slot's count; 1-D
+// launches search the prefix array.
+__device__ __forceinline__ bool plan_slot(const Plan& p, int& slot, int64_t& item)
+{
+    if (gridDim.y > 1) {
+        slot = (int)blockIdx.y;
+        item = blockIdx.x;
+        return item < p.prefix[slot + 1] - p.prefix[slot];
+    }
+    slot = slot_of(p.prefix, p.m, blockIdx.x);
+    item = blockIdx.x - p.prefix[slot];
+    return true;
+}
+
 // Block-wide exclusive scan of one uint32 per thread (blockDim.x == NT).
 template <int NT>
 __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint32_t& total)
@@ -69,8 +84,6 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint3
     return r;
 }
 
-__device__ __forceinline__ bool is_rst(int c) { return c >= 0xD0 && c <= 0xD7; }
-
 // 16 stuffed bytes of thread t of tile `tile` (zero beyond scan_len) plus neighbours.
 struct Bytes16 {
     uint8_t b[16];
@@ -95,9 +108,11 @@ __device__ __forceinline__ void load16(const DecDesc& d, int64_t base, Bytes16& 
 // funnel shift; a dword is read only if it holds a byte of the source.
 __global__ void __launch_bounds__(256) k_stage(const StageJob* J, Plan p)
 {
-    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    int slot;
+    int64_t item;
+    if (!plan_slot(p, slot, item)) return;
     const StageJob j = J[slot];
-    const int64_t o = (blockIdx.x - p.prefix[slot]) * (int64_t)STAGE_TILE + threadIdx.x * 16;
+    const int64_t o = item * (int64_t)STAGE_TILE + threadIdx.x * 16;
     if (o >= j.dst_len) return;
     uint32_t w[4] = {0, 0, 0, 0};
     if (o < j.len) {
@@ -134,17 +149,51 @@ __device__ __forceinline__ bool any_ff(const uint4& v, int prev)
     return m != 0 || prev == 0xFF;
 }
 
-// Output bytes / RSTn markers of thread t's 16 stuffed bytes below `end`.
-__device__ __forceinline__ void unstuff_counts(const Bytes16& B, int64_t base, int64_t end, uint32_t& nb, uint32_t& nr)
+// Byte classes of 16 stuffed bytes as 16-bit masks (bit k = byte k), SWAR on
+// the four dwords: 0xFF bytes, 0x00 bytes, RSTn codes (0xD0..0xD7).
+__device__ __forceinline__ uint32_t zero_bytes4(uint32_t x)  // bit j: byte j of x is 0
 {
-    nb = nr = 0;
+    const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;  // exact per byte
+    uint32_t m = (~nz & 0x80808080u) >> 7;  // bits 0, 8, 16, 24
+    m |= m >> 7;
+    m |= m >> 14;
+    return m & 0xFu;
+}
+struct ByteClass {
+    uint32_t ff, z, r;
+};
+__device__ __forceinline__ ByteClass classify16(const uint4& v)
+{
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    ByteClass c{0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        if (base + k >= end) break;
-        int rst;
-        nb += (uint32_t)dec_unstuff_rule(k ? B.b[k - 1] : B.prev, B.b[k], k < 15 ? B.b[k + 1] : B.next, &rst);
-        nr += (uint32_t)rst;
+    for (int k = 0; k < 4; k++) {
+        c.ff |= zero_bytes4(~w[k]) << (4 * k);
+        c.z |= zero_bytes4(w[k]) << (4 * k);
+        c.r |= zero_bytes4((w[k] ^ 0xD0D0D0D0u) & 0xF8F8F8F8u) << (4 * k);
     }
+    return c;
+}
+
+// The unstuffing rule (dec_unstuff_rule) over 16 bytes at once, given the byte
+// before them (prev) and after them (next): keep = bytes contributing one
+// output byte, rst = RSTn codes (DEC_PAD bytes each), mark = 0xFF bytes that
+// start a terminating marker (followed by neither 0x00, 0xFF nor an RSTn code).
+struct Unstuff16 {
+    uint32_t keep, rst, mark;
+};
+__device__ __forceinline__ Unstuff16 unstuff16(const ByteClass& c, int prev, int next)
+{
+    const uint32_t pff = ((c.ff << 1) | (prev == 0xFF ? 1u : 0u)) & 0xFFFFu;  // byte k follows a 0xFF
+    const uint32_t nz = (c.z >> 1) | (next == 0x00 ? 0x8000u : 0u);           // byte k precedes a 0x00
+    const uint32_t nff = (c.ff >> 1) | (next == 0xFF ? 0x8000u : 0u);
+    const uint32_t nr = (c.r >> 1) | (next >= 0xD0 && next <= 0xD7 ? 0x8000u : 0u);
+    const uint32_t stuffed = pff & c.z, rst = pff & c.r & ~c.ff;
+    Unstuff16 u;
+    u.keep = (~c.ff & ~stuffed & ~rst & 0xFFFFu) | (c.ff & nz);
+    u.rst = rst;
+    u.mark = c.ff & ~nz & ~nff & ~nr;
+    return u;
 }
 
 // Per 4 KiB tile: output bytes and RSTn markers of its bytes below scan_len,
@@ -156,10 +205,11 @@ __device__ __forceinline__ void unstuff_counts(const Bytes16& B, int64_t base, i
 __global__ void __launch_bounds__(256) k_unstuff_count(const DecDesc* D, DecState* S, Plan p)
 {
     __shared__ uint32_t sh[2][4];
-    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    int slot;
+    int64_t tile;
+    if (!plan_slot(p, slot, tile)) return;
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
-    const int64_t tile = blockIdx.x - p.prefix[slot];
     const int64_t base = tile * DEC_TILE + threadIdx.x * 16;
     uint32_t nb = 0, nr = 0;
     if (base < d.scan_len) {
@@ -167,18 +217,15 @@ __global__ void __launch_bounds__(256) k_unstuff_count(const DecDesc* D, DecStat
         const int prev = base > 0 ? d.scan[base - 1] : 0;
         if (!any_ff(v, prev)) {
             nb = (uint32_t)min((int64_t)16, d.scan_len - base);
-        } else {
-            Bytes16 B;
-            load16(d, base, B);
-            unstuff_counts(B, base, d.scan_len, nb, nr);
-            for (int k = 0; k < 16; k++) {
-                const int64_t i = base + k;
-                const int nx = k < 15 ? B.b[k + 1] : B.next;
-                if (i + 1 < d.scan_len && B.b[k] == 0xFF && nx != 0x00 && nx != 0xFF && !is_rst(nx)) {
-                    atomicMin((unsigned long long*)&S[img].end, (unsigned long long)i);
-                    break;
-                }
-            }
+        } else {  // branch-free rule over the 16 bytes (SWAR masks)
+            const Unstuff16 u = unstuff16(classify16(v), prev, d.scan[base + 16]);
+            const int64_t rem = d.scan_len - base;  // bytes of this thread below scan_len
+            const uint32_t valid = rem >= 16 ? 0xFFFFu : (1u << rem) - 1;
+            nb = (uint32_t)__popc(u.keep & valid) + DEC_PAD * (uint32_t)__popc(u.rst & valid);
+            nr = (uint32_t)__popc(u.rst & valid);
+            // a marker needs its next byte below scan_len
+            const uint32_t mk = u.mark & (rem - 1 >= 16 ? 0xFFFFu : (1u << (rem - 1)) - 1);
+            if (mk) atomicMin((unsigned long long*)&S[img].end, (unsigned long long)(base + __builtin_ctz(mk)));
         }
     }
     // workgroup sums: wave reduction, then the four wave totals
@@ -284,40 +331,31 @@ __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const
     __shared__ uint32_t sh[8];
     __shared__ uint32_t bufw[(DEC_TILE / 2 * DEC_PAD + 64) / 4];  // worst case: an RSTn marker every 2 bytes
     uint8_t* const buf = (uint8_t*)bufw;
-    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    int slot;
+    int64_t tile;
+    if (!plan_slot(p, slot, tile)) return;
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
-    const int64_t tile = blockIdx.x - p.prefix[slot];
     const int64_t base = tile * DEC_TILE + threadIdx.x * 16;
     const int64_t end = S[img].end;
     if (tile * DEC_TILE >= end) return;  // workgroup-uniform: nothing of this tile is data
-    Bytes16 B;
-    for (int k = 0; k < 16; k++) B.b[k] = 0;
-    B.prev = B.next = 0;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     bool plain = false;  // 16 data bytes, no 0xFF among them or before them
+    uint32_t keep = 0, rstm = 0;
     if (base < end) {
         v = *(const uint4*)(d.scan + base);
-        plain = base + 16 <= end && !any_ff(v, base > 0 ? d.scan[base - 1] : 0);
-        if (!plain) load16(d, base, B);
-    }
-    int out[16], rsts[16];
-    uint32_t nb = 0, nr = 0;
-    if (plain) {
-        nb = 16;
-    } else {
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            int rst = 0;
-            const int c = base + k < end ? dec_unstuff_rule(k ? B.b[k - 1] : B.prev, B.b[k],
-                                                            k < 15 ? B.b[k + 1] : B.next, &rst)
-                                         : 0;
-            out[k] = c;
-            rsts[k] = rst;
-            nb += (uint32_t)c;
-            nr += (uint32_t)rst;
+        const int prev = base > 0 ? d.scan[base - 1] : 0;
+        plain = base + 16 <= end && !any_ff(v, prev);
+        if (!plain) {  // the rule over the 16 bytes as masks (bytes from `end` on drop out)
+            const Unstuff16 u = unstuff16(classify16(v), prev, d.scan[base + 16]);
+            const int64_t rem = end - base;
+            const uint32_t valid = rem >= 16 ? 0xFFFFu : (1u << rem) - 1;
+            keep = u.keep & valid;
+            rstm = u.rst & valid;
         }
     }
+    const uint32_t nr = (uint32_t)__popc(rstm);
+    const uint32_t nb = plain ? 16u : (uint32_t)__popc(keep) + DEC_PAD * nr;
     uint32_t tb, tr;
     uint32_t ob = block_exscan<256>(nb, sh, tb);
     uint32_t orr = block_exscan<256>(nr, sh, tr) + d.tile_rst[tile];
@@ -336,15 +374,40 @@ __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const
             wp[3] = (v.z >> (32 - s8)) | (v.w << s8);
             atomicOr(wp + 4, v.w >> (32 - s8));
         }
-    } else {
+    } else if (nr == 0 && nb > 0) {
+        // drop the bytes outside `keep` (highest first, so lower positions stay
+        // put: usually one stuffed zero), then OR the nb bytes in at ob
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t drop = ~keep & 0xFFFFu;
+        while (drop) {
+            const int k = 31 - __builtin_clz(drop);
+            drop &= ~(1u << k);
+            const int q = k >> 2;
+            const uint32_t low = (1u << (8 * (k & 3))) - 1u;  // bytes of dword q below k
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t up = j < 3 ? w[j + 1] << 24 : 0u;
+                if (j > q) w[j] = (w[j] >> 8) | up;
+                else if (j == q) w[j] = (w[j] & low) | ((w[j] >> 8) & ~low) | up;
+            }
+        }
+        const uint32_t s8 = (ob & 3) * 8;
+        uint32_t* wp = bufw + (ob >> 2);
+        atomicOr(wp, w[0] << s8);
+#pragma unroll
+        for (int j = 1; j < 4; j++) atomicOr(wp + j, (w[j] << s8) | (s8 ? w[j - 1] >> (32 - s8) : 0u));
+        if (s8) atomicOr(wp + 4, w[3] >> (32 - s8));
+    } else if (nr > 0) {  // RSTn codes (restart intervals): byte by byte
+        Bytes16 B;
+        load16(d, base, B);
 #pragma unroll
         for (int k = 0; k < 16; k++) {
-            if (rsts[k]) {
+            if ((rstm >> k) & 1) {
                 for (int q = 0; q < DEC_PAD; q++) buf[ob + q] = 0xFF;
                 ob += DEC_PAD;
                 if (orr + 1 < (uint32_t)d.nseg_max) d.seg[orr + 1] = tile_off + ob;
                 orr++;
-            } else if (out[k]) {
+            } else if ((keep >> k) & 1) {
                 buf[ob++] = B.b[k];
             }
         }
@@ -382,12 +445,14 @@ __global__ void __launch_bounds__(256) k_dec_init(const DecDesc* D, const DecSta
                                                   uint32_t warm)
 {
     __shared__ __attribute__((aligned(16))) DecHuff L[4];
-    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    int slot;
+    int64_t wg;
+    if (!plan_slot(p, slot, wg)) return;
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
     const DecState& st = S[img];
-    const int64_t j = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
-    const bool live = st.status == 0 && (blockIdx.x - p.prefix[slot]) * 256 < (int64_t)st.nsub;
+    const int64_t j = wg * 256 + threadIdx.x;
+    const bool live = st.status == 0 && wg * 256 < (int64_t)st.nsub;
     if (live) load_tables(d.tab, L);
     if (j > d.nsub_max) return;
     const uint32_t start = (uint32_t)j * sub_bits;
@@ -432,14 +497,16 @@ __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecSta
 {
     __shared__ __attribute__((aligned(16))) DecHuff L[4];
     __shared__ uint64_t ckl[FIRST ? 1 : 256][DEC_CK_MAX];
-    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    int slot;
+    int64_t wg;
+    if (!plan_slot(p, slot, wg)) return;
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
     const DecState& st = S[img];
     if (st.status) return;
-    const int64_t k = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
+    const int64_t k = wg * 256 + threadIdx.x;
     const uint32_t n = FIRST ? st.nsub : d.wl_cnt[(int64_t)(iter - 1) * nimg + img];
-    if ((blockIdx.x - p.prefix[slot]) * 256 >= (int64_t)n) return;
+    if (wg * 256 >= (int64_t)n) return;
     load_tables(d.tab, L);
     if (k >= n) return;
     const uint32_t j = FIRST ? (uint32_t)k : d.wl[iter & 1][k];
@@ -526,13 +593,15 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
 {
     __shared__ __attribute__((aligned(16))) DecHuff L[4];
     __shared__ uint32_t slots[256 * SLOT_DW];
-    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    int slot;
+    int64_t wg;
+    if (!plan_slot(p, slot, wg)) return;
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
     const DecState& st = S[img];
     if (st.status) return;
-    const int64_t j = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
-    if ((blockIdx.x - p.prefix[slot]) * 256 >= (int64_t)st.nsub) return;
+    const int64_t j = wg * 256 + threadIdx.x;
+    if (wg * 256 >= (int64_t)st.nsub) return;
     const int lane = threadIdx.x & 63;
     uint32_t* wave_slots = slots + (threadIdx.x - lane) * SLOT_DW;
     uint32_t* mys = slots + threadIdx.x * SLOT_DW;
@@ -770,12 +839,14 @@ __device__ __forceinline__ uint2 idct_block_row(const DecDesc& d, int64_t b, int
 __global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecState* S, Plan p)
 {
     __shared__ int32_t ws[32][8 * 9];
-    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    int slot;
+    int64_t wg;
+    if (!plan_slot(p, slot, wg)) return;
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
     if (S[img].status) return;
     const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;
-    const int i = (int)(blockIdx.x - p.prefix[slot]) * 32 + lb;  // < 2^31: at most 65535^2 * 3 / 64 blocks
+    const int i = (int)wg * 32 + lb;  // < 2^31: at most 65535^2 * 3 / 64 blocks
     int m, k;
     if (d.fuse420) {
         m = i >> 1;
@@ -833,11 +904,13 @@ __device__ __forceinline__ uint8_t clamp255(int v) { return (uint8_t)(v < 0 ? 0 
 // Thread per 4 output pixels of one output row; one image per workgroup.
 __global__ void __launch_bounds__(256) k_dec_color(const DecDesc* D, const DecState* S, Plan p)
 {
-    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    int slot;
+    int64_t wg;
+    if (!plan_slot(p, slot, wg)) return;
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
     if (S[img].status) return;
-    const int64_t item = (blockIdx.x - p.prefix[slot]) * 256 + threadIdx.x;
+    const int64_t item = wg * 256 + threadIdx.x;
     const int gpr = (d.ow + 3) >> 2;
     const int y = (int)(item / gpr), x0 = (int)(item % gpr) * 4;
     if (y >= d.oh) return;
@@ -887,12 +960,14 @@ __global__ void __launch_bounds__(256) k_dec_luma_color_420(const DecDesc* D, co
     __shared__ int32_t ws[32][8 * 9];
     __shared__ __attribute__((aligned(16))) uint32_t ly[16][LC_W / 4];
     __shared__ uint32_t lc[2][10][LC_CD];  // [cb|cr][chroma row cy0-1+j][dword]; byte q <-> column cx0-4+q
-    const int slot = slot_of(p.prefix, p.m, blockIdx.x);
+    int slot;
+    int64_t wg;
+    if (!plan_slot(p, slot, wg)) return;
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
     if (S[img].status) return;
     const int tpr = (d.mcux + LC_NM - 1) / LC_NM;
-    const int item = (int)(blockIdx.x - p.prefix[slot]);
+    const int item = (int)wg;
     const int my = item / tpr, mx0 = (item - my * tpr) * LC_NM;
     const int t = threadIdx.x;
     // chroma staging first: its loads overlap the luma IDCT
@@ -976,31 +1051,37 @@ __global__ void __launch_bounds__(256) k_dec_luma_color_420(const DecDesc* D, co
 }
 
 // ---------------------------------------------------------------- launchers
+// 2-D grid (x = item, y = slot) when the plan asks for one, else one row of nwg
+static dim3 grid_of(const Plan& p, int64_t nwg)
+{
+    return p.width > 0 ? dim3((unsigned)p.width, (unsigned)p.m) : dim3((unsigned)nwg);
+}
+
 void launch_stage(const StageJob* jobs, const Plan& tiles, int64_t nwg, hipStream_t st)
 {
-    if (nwg > 0) hipLaunchKernelGGL(k_stage, dim3((unsigned)nwg), dim3(256), 0, st, jobs, tiles);
+    if (nwg > 0) hipLaunchKernelGGL(k_stage, grid_of(tiles, nwg), dim3(256), 0, st, jobs, tiles);
 }
 
 void launch_unstuff(const DecDesc* d, DecState* s, const Plan& tiles, int64_t ntiles, const int32_t* ids, int m,
                     uint32_t sub_bits, hipStream_t st)
 {
     if (ntiles <= 0 || m <= 0) return;
-    hipLaunchKernelGGL(k_unstuff_count, dim3((unsigned)ntiles), dim3(256), 0, st, d, s, tiles);
+    hipLaunchKernelGGL(k_unstuff_count, grid_of(tiles, ntiles), dim3(256), 0, st, d, s, tiles);
     hipLaunchKernelGGL(k_unstuff_scan, dim3((unsigned)m), dim3(1024), 0, st, d, s, ids, sub_bits);
-    hipLaunchKernelGGL(k_unstuff_scatter, dim3((unsigned)ntiles), dim3(256), 0, st, d, s, tiles);
+    hipLaunchKernelGGL(k_unstuff_scatter, grid_of(tiles, ntiles), dim3(256), 0, st, d, s, tiles);
 }
 
 void launch_dec_init(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
                      uint32_t warm, hipStream_t st)
 {
-    if (nwg > 0) hipLaunchKernelGGL(k_dec_init, dim3((unsigned)nwg), dim3(256), 0, st, d, s, subs, sub_bits, warm);
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_init, grid_of(subs, nwg), dim3(256), 0, st, d, s, subs, sub_bits, warm);
 }
 
 void launch_dec_sync(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
                      int iter, int nimg, uint32_t* changed, hipStream_t st)
 {
     if (nwg > 0)
-        hipLaunchKernelGGL(iter == 0 ? k_dec_sync<true> : k_dec_sync<false>, dim3((unsigned)nwg), dim3(256), 0, st,
+        hipLaunchKernelGGL(iter == 0 ? k_dec_sync<true> : k_dec_sync<false>, grid_of(subs, nwg), dim3(256), 0, st,
                            d, s, subs, sub_bits, iter, nimg, changed);
 }
 
@@ -1012,7 +1093,7 @@ void launch_dec_offsets(const DecDesc* d, DecState* s, const int32_t* ids, int m
 void launch_dec_write(const DecDesc* d, DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
                       hipStream_t st)
 {
-    if (nwg > 0) hipLaunchKernelGGL(k_dec_write, dim3((unsigned)nwg), dim3(256), 0, st, d, s, subs, sub_bits);
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_write, grid_of(subs, nwg), dim3(256), 0, st, d, s, subs, sub_bits);
 }
 
 void launch_dec_dc(const DecDesc* d, const DecState* s, const int32_t* ids, int m, hipStream_t st)
@@ -1022,17 +1103,17 @@ void launch_dec_dc(const DecDesc* d, const DecState* s, const int32_t* ids, int 
 
 void launch_dec_idct(const DecDesc* d, const DecState* s, const Plan& blocks, int64_t nwg, hipStream_t st)
 {
-    if (nwg > 0) hipLaunchKernelGGL(k_dec_idct, dim3((unsigned)nwg), dim3(256), 0, st, d, s, blocks);
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_idct, grid_of(blocks, nwg), dim3(256), 0, st, d, s, blocks);
 }
 
 void launch_dec_color(const DecDesc* d, const DecState* s, const Plan& px, int64_t nwg, hipStream_t st)
 {
-    if (nwg > 0) hipLaunchKernelGGL(k_dec_color, dim3((unsigned)nwg), dim3(256), 0, st, d, s, px);
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_color, grid_of(px, nwg), dim3(256), 0, st, d, s, px);
 }
 
 void launch_dec_luma_color_420(const DecDesc* d, const DecState* s, const Plan& tiles, int64_t nwg, hipStream_t st)
 {
-    if (nwg > 0) hipLaunchKernelGGL(k_dec_luma_color_420, dim3((unsigned)nwg), dim3(256), 0, st, d, s, tiles);
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_luma_color_420, grid_of(tiles, nwg), dim3(256), 0, st, d, s, tiles);
 }
 
 }  // namespace icx

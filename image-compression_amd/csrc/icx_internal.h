@@ -123,6 +123,7 @@ struct Plan {
     int32_t m;
     int32_t uniform;        // > 0: every slot holds this many items (2-D launches, no slot search)
     int32_t identity;       // ids[i] == i for every slot
+    int32_t width = 0;      // decoder: > 0 = 2-D launch (x < width items, y = slot; items past a slot's count exit)
 };
 
 }  // namespace icx
