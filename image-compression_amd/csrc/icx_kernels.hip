@@ -631,25 +631,25 @@ struct GlobalSink {
 #endif
 constexpr int PRE = ICX_PRE;
 
-__device__ __forceinline__ void load_group(uint32_t (&g)[4], const uint32_t* lst, int j, int cnt)
+// List groups are loaded whether or not they hold entries of the block: a
+// load under an exec mask is merged with its default by a copy, and the copy
+// waits for the load at once - the group loads would run one after another.
+// Entries past the block's length (the following blocks' lists) are never
+// coded (encode_block checks the index against the length).  A block's list
+// starts at most 64 entries before the end of its FDCT wave's reserved
+// region, so every load stays inside that region.
+__device__ __forceinline__ void load_group(uint32_t (&g)[4], const uint32_t* lst, int j)
 {
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (j < cnt) v = ld16(lst + j);
+    const uint4 v = ld16(lst + j);
     g[0] = v.x; g[1] = v.y; g[2] = v.z; g[3] = v.w;
 }
 
-__device__ __forceinline__ void load_list(uint32_t (&ev)[PRE], const uint32_t* lst, int cnt)
+__device__ __forceinline__ void load_list(uint32_t (&ev)[PRE], const uint32_t* lst)
 {
-    // group 0 is always written (DC + padding), the others only up to cnt
 #pragma unroll
     for (int g = 0; g < PRE / 4; g++) {
         uint32_t w[4];
-        if (g == 0) {
-            const uint4 v = ld16(lst);
-            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-        } else {
-            load_group(w, lst, 4 * g, cnt);
-        }
+        load_group(w, lst, 4 * g);
 #pragma unroll
         for (int j = 0; j < 4; j++) ev[4 * g + j] = w[j];
     }
@@ -676,7 +676,7 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
     const uint2 zrl = ac[15 * AC_SIZES];
     uint32_t last = 0;  // zig-zag index of the last nonzero coefficient
     uint32_t g0[4] = {0u, 0u, 0u, 0u}, g1[4];
-    load_group(g1, lst, PRE, cnt);
+    load_group(g1, lst, PRE);
     uint32_t en = ev[1];
     float4 qn = qf[en & 63];
 #pragma unroll
@@ -692,14 +692,14 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
                 if ((j & 3) == 0) {
 #pragma unroll
                     for (int q = 0; q < 4; q++) g0[q] = g1[q];
-                    if (j + 4 < 64) load_group(g1, lst, j + 4, cnt);
+                    if (j + 4 < 64) load_group(g1, lst, j + 4);
                 }
                 en = g0[j & 3];
             }
             qn = qf[en & 63];
         }
         const float f = (float)((int32_t)e >> 6);
-        if (fabsf(f) >= qk.x) {  // quotient != 0
+        if (i < cnt && fabsf(f) >= qk.x) {  // quotient != 0
             const uint32_t k = e & 63;
             uint32_t run = k - last - 1;
             while (run >= 16) {
@@ -730,7 +730,7 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
 //   4. gather: every 32-bit word of the chunk stream is assembled by the
 //      thread whose block holds the word's first bit (reading the following
 //      blocks' slots as needed) and stored once to scratch[cur].
-__global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict__ descs,
+__global__ __launch_bounds__(CHUNK_BLOCKS, 8) void k_huff(const ImgDesc* __restrict__ descs,
                                                        const ImgState* __restrict__ states,
                                                        const QNode* __restrict__ nodes,
                                                        const int32_t* __restrict__ ids,
@@ -753,20 +753,9 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     const int slot = gridDim.y > 1 ? (int)blockIdx.y : find_slot(prefix, m, blockIdx.x);
     const int img = ids ? ids[slot] : slot;
     const ImgState& S = states[img];
-    if (!S.active) return;
     const ImgDesc& D = descs[img];
     const int chunk = gridDim.y > 1 ? (int)blockIdx.x : (int)(blockIdx.x - prefix[slot]);
-    const QNode& N = nodes[S.node];
-    const int cur = S.cur;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-
-    if (t < 128) {
-        const int c = t >> 6, k = t & 63;
-        s_qf[c][k] = N.qf[c][k];
-    }
-    // AC codes pre-shifted for their (run, size) slot: (code << size, len + size)
-    for (int i = t; i < 2 * AC_ENTRIES; i += CHUNK_BLOCKS) (&s_ac[0][0])[i] = (&c_acx[0][0])[i];
-    if (t < 32) s_dc[t >> 4][t & 15] = c_dc[t >> 4][t & 15];
 
     const int64_t b0 = (int64_t)chunk * CHUNK_BLOCKS;
     const int nb = (int)min((int64_t)CHUNK_BLOCKS, D.nblocks - b0);
@@ -783,17 +772,40 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     } else {
         pb = b - 1;
     }
-    const int cnt = valid ? (int)D.ncoef[b] : 0;
-    // a DC predictor in the previous chunk (the chunk's first blocks): its
-    // list offset and DC entry are fetched alongside this block's own, not
-    // after the DC exchange (they would stall the first wave, and through the
-    // scan barrier the workgroup)
+    // The prologue's loads go out in two rounds with one wait between them
+    // (issued one after another with a wait each, they were a chain of about
+    // eight memory latencies in front of every chunk): first the block's
+    // list length and offset, the DC predictor's list offset and the coding
+    // tables (the list meta depends only on the descriptor, so it goes out
+    // even before the image's state says whether it is still searching);
+    // then, once the tables are in LDS, the list itself and the predictor's
+    // DC entry (the list groups are loaded unconditionally, see load_group).
+    // A DC predictor in the previous chunk (the chunk's first blocks): its
+    // list offset and DC entry are fetched alongside this block's own.
     const bool ext_prev = pb >= 0 && pb < b0;
-    const uint32_t prev_off = ext_prev ? D.coff[pb] : 0u;
-    const uint32_t* lst = (const uint32_t*)D.coefs + 4 * (size_t)D.coff[valid ? b : b0];
+    const GAS uint32_t* coff = gp(D.coff);
+    const int cnt = valid ? (int)gp(D.ncoef)[b] : 0;
+    const uint32_t my_off = coff[valid ? b : b0];
+    const uint32_t prev_off = coff[ext_prev ? pb : b0];
+    if (!S.active) return;
+    const QNode& N = nodes[S.node];
+    const int cur = S.cur;
+    const float4 qv = N.qf[(t >> 6) & 1][t & 63];  // used by t < 128
+    // AC codes pre-shifted for their (run, size) slot: (code << size, len + size)
+    static_assert(2 * AC_ENTRIES <= 2 * CHUNK_BLOCKS, "two AC entries per thread");
+    const uint2 ac0 = (&c_acx[0][0])[t];
+    const bool has_ac1 = t + CHUNK_BLOCKS < 2 * AC_ENTRIES;
+    const uint2 ac1 = (&c_acx[0][0])[has_ac1 ? t + CHUNK_BLOCKS : t];
+    const uint32_t dcv = c_dc[(t >> 4) & 1][t & 15];  // used by t < 32
+    if (t < 128) s_qf[t >> 6][t & 63] = qv;
+    (&s_ac[0][0])[t] = ac0;
+    if (has_ac1) (&s_ac[0][0])[t + CHUNK_BLOCKS] = ac1;
+    if (t < 32) s_dc[t >> 4][t & 15] = dcv;
+    __builtin_amdgcn_sched_barrier(0);  // the table registers die before the list arrives
+    const uint32_t* lst = (const uint32_t*)D.coefs + 4 * (size_t)my_off;
     uint32_t ev[PRE];
-    load_list(ev, lst, cnt);
-    const int32_t prev_dc = ext_prev ? gp(D.coefs)[4 * (size_t)prev_off] : 0;
+    load_list(ev, lst);
+    const int32_t prev_dc_raw = gp(D.coefs)[4 * (size_t)prev_off];
     __syncthreads();  // tables ready
 
     const float4 q0t = s_qf[tb][0];
@@ -802,7 +814,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
     __syncthreads();
     int qprev = 0;
     if (pb >= b0) qprev = s_dcq[pb - b0];
-    else if (ext_prev) qprev = quant(prev_dc >> 6, q0t.y, q0t.z);
+    else if (ext_prev) qprev = quant(prev_dc_raw >> 6, q0t.y, q0t.z);
 
     // ---- 1. encode_one_block into the slot (rarely: into the block's HBM spill)
     int bits = 0;
@@ -814,7 +826,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS) void k_huff(const ImgDesc* __restrict
         sink.finish();
         if (bits > SLOT_BITS) {  // rare: reload the list (ev[] is dead by now)
             uint32_t e2[PRE];
-            load_list(e2, lst, cnt);
+            load_list(e2, lst);
             GlobalSink g{0, 0, 0, gp(D.ovf + b * BLOCK_WORDS)};
             encode_block(g, e2, lst, cnt, dq - qprev, s_qf[tb], s_ac[tb], s_dc[tb]);
             g.finish();
