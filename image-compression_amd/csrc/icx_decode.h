@@ -232,11 +232,11 @@ struct DecReader {
 // HUFF_EXTEND (jdhuff.c)
 ICX_HD int dec_extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
-// Decode one symbol: (length << 8) | symbol, 0 if no valid code.
+// Decode one symbol: (length << 8) | symbol, 0 if no valid code.  e = the
+// first-level entry of pk (dec_symbol looks it up itself).
 template <class HuffPtr>
-ICX_HD uint32_t dec_symbol(HuffPtr t, const ICX_GLOBAL DecSlow* slow, uint32_t pk)
+ICX_HD uint32_t dec_symbol_from(HuffPtr t, const ICX_GLOBAL DecSlow* slow, uint32_t pk, uint32_t e)
 {
-    uint32_t e = t->lut[pk >> (16 - DEC_LUT_BITS)];
     if (e & DEC_SUB) e = t->lut2[e & (DEC_NSUB - 1)][pk & ((1u << (16 - DEC_LUT_BITS)) - 1)];
     if (e & DEC_SLOW) {
         e = 0;
@@ -249,6 +249,32 @@ ICX_HD uint32_t dec_symbol(HuffPtr t, const ICX_GLOBAL DecSlow* slow, uint32_t p
         }
     }
     return e;
+}
+
+template <class HuffPtr>
+ICX_HD uint32_t dec_symbol(HuffPtr t, const ICX_GLOBAL DecSlow* slow, uint32_t pk)
+{
+    return dec_symbol_from(t, slow, pk, t->lut[pk >> (16 - DEC_LUT_BITS)]);
+}
+
+// Huffman tables with the first level in one place (LDS) and the whole table
+// (second level, slow path) in global memory: k_dec_write keeps only the
+// 10-bit first levels in LDS to leave room for its block slots.
+struct SplitHuff {
+    const uint16_t (*lut)[1 << DEC_LUT_BITS];
+    const ICX_GLOBAL DecHuff* full;
+};
+
+template <class HuffPtr>
+ICX_HD uint32_t dec_lookup(HuffPtr H, int ti, const ICX_GLOBAL DecSlow* slow, uint32_t pk)
+{
+    return dec_symbol(&H[ti], &slow[ti], pk);
+}
+
+ICX_HD uint32_t dec_lookup(const SplitHuff& H, int ti, const ICX_GLOBAL DecSlow* slow, uint32_t pk)
+{
+    const uint32_t e = H.lut[ti][pk >> (16 - DEC_LUT_BITS)];
+    return (e & (DEC_SUB | DEC_SLOW)) ? dec_symbol_from(&H.full[ti], &slow[ti], pk, e) : e;
 }
 
 // zig-zag index -> natural index with jpeg_natural_order's tail (k > 63 -> 63)
@@ -297,7 +323,11 @@ ICX_HD int dec_zz(int n)
 ICX_HD int dec_sel(uint32_t selp, int comp, int ac) { return (int)((selp >> (4 * (2 * comp + ac))) & 3); }
 
 // Sink of an owned walk: put(zig-zag index, value) per symbol (index 0 = the
-// DC difference, 64 = nothing), flush_if(block complete and owned, index).
+// DC difference), flush_if(block complete and owned, index).  Every symbol
+// stores exactly one value at an index below 64: a ZRL or EOB stores 0 at the
+// current index (still zero in the block being assembled), and the symbols of
+// the partial block a walk starts in (owned by the previous subsequence) store
+// at index 0, which the walk's first owned block overwrites with its DC.
 struct NoSink {
     ICX_HD void put(int, int) {}
     ICX_HD void flush_if(bool, int64_t) {}
@@ -348,7 +378,7 @@ struct DecWalker {
         R.refill();
         const bool ac = z != 0;
         const int ti = dec_sel(selp, comp, ac ? 1 : 0);
-        const uint32_t e = dec_symbol(&H[ti], &slow[ti], R.peek16());
+        const uint32_t e = dec_lookup(H, ti, slow, R.peek16());
         const int len = (int)(e >> 8), sym = (int)(e & 255);
         if (len == 0 || (!ac && sym > 11)) {  // no valid code here
             invalid();
@@ -361,7 +391,7 @@ struct DecWalker {
         pos += (uint32_t)(len + sz);
         const int x = sz ? dec_extend(v, sz) : 0;
         const int zc = z + run;                 // zig-zag index of an AC coefficient
-        if (OWNED) sink.put(!own ? 64 : !ac ? 0 : sz ? (zc > 63 ? 63 : zc) : 64, x);
+        if (OWNED) sink.put(!own ? 0 : !ac ? 0 : sz ? (zc > 63 ? 63 : zc) : z, x);
         z = !ac ? 1 : sz ? zc + 1 : (run == 15 ? z + 16 : 64);
         const bool end = z >= 64;
         if (OWNED) {

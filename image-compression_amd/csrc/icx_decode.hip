@@ -563,19 +563,22 @@ __global__ void __launch_bounds__(1024) k_dec_offsets(const DecDesc* D, DecState
     }
 }
 
-// Per-thread block assembly slot in LDS: 64 int16 at a stride of 33 dwords, so
-// the 64 lanes' slots start on 64 distinct banks and lanes storing the same
-// zig-zag position (they walk in near lockstep) do not collide.
-constexpr int SLOT_DW = 33;
+// Per-thread block assembly slot in LDS: 64 int16 (32 dwords) in zig-zag
+// order, the DC difference at [0].  Int16 z of lane l's slot sits at
+// (z ^ (l & 62)): lanes storing the same zig-zag position (they walk in near
+// lockstep) and the 32 lanes copying one slot hit 64 (32) distinct banks
+// without a pad dword, so 256 slots take 32 KiB and, with the 8 KiB of
+// first-level Huffman tables, a workgroup 40 KiB: four per CU.
+constexpr int SLOT_DW = 32;
 
-// Slots hold a block in zig-zag order (no index table per coefficient), the
-// DC difference at [0]; a lane that finishes an owned block only records its
-// index, and the wave then copies every finished slot together (below),
-// permuting to natural order on the way.
+// A lane that finishes an owned block only records its index, and the wave
+// then copies every finished slot together (below), permuting to natural
+// order on the way.
 struct PendSink {
-    int16_t* slot;  // 64 int16 + the pad dword, which takes put(64, .)
+    uint8_t* slot;  // this lane's slot
+    uint32_t sw;    // lane & 62
     int64_t pend;   // block waiting for the wave flush, -1 = none
-    __device__ __forceinline__ void put(int z, int v) { slot[z] = (int16_t)v; }
+    __device__ __forceinline__ void put(int z, int v) { *(int16_t*)(slot + ((z ^ sw) << 1)) = (int16_t)v; }
     __device__ __forceinline__ void flush_if(bool c, int64_t bi) { pend = c ? bi : pend; }
 };
 
@@ -588,11 +591,13 @@ struct PendSink {
 // block stores are the only vector-memory traffic between top-ups, so no
 // symbol waits for them.  A per-lane flush would cost
 // every lane of the wave ~70 instructions whenever any lane finishes a block,
-// which on q95 content is most iterations.
+// which on q95 content is most iterations.  Only the first levels of the
+// Huffman tables are in LDS (SplitHuff): the second levels of the few codes
+// longer than 10 bits are read from the image's tables in global memory.
 __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S, Plan p, uint32_t sub_bits)
 {
-    __shared__ __attribute__((aligned(16))) DecHuff L[4];
-    __shared__ uint32_t slots[256 * SLOT_DW];
+    __shared__ __attribute__((aligned(16))) uint16_t L1[4][1 << DEC_LUT_BITS];
+    __shared__ __attribute__((aligned(16))) uint32_t slots[256 * SLOT_DW];
     int slot;
     int64_t wg;
     if (!plan_slot(p, slot, wg)) return;
@@ -606,11 +611,19 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
     uint32_t* wave_slots = slots + (threadIdx.x - lane) * SLOT_DW;
     uint32_t* mys = slots + threadIdx.x * SLOT_DW;
     for (int k = 0; k < 32; k++) mys[k] = 0;
-    load_tables(d.tab, L);
+    {  // first levels of the image's distinct tables
+        const int n = (int)(d.tab->ntab * sizeof(L1[0]) / 16);
+        for (int k = threadIdx.x; k < n; k += blockDim.x) {
+            const int t = k / (int)(sizeof(L1[0]) / 16), o = k % (int)(sizeof(L1[0]) / 16);
+            ((uint4*)L1[t])[o] = ((const uint4*)d.tab->h[t].lut)[o];
+        }
+        __syncthreads();
+    }
     const uint32_t stop = (uint32_t)(j + 1) * sub_bits;
-    DecWalker<true, DecHuff*> w = dec_walker<true>(d, (DecHuff*)L, d.tab->slow, selector(d.tab),
-                                                   (const uint32_t*)d.ent, d.seg, st.nseg, st.ent_len * 8,
-                                                   j < st.nsub ? (int64_t)d.boff[j] : 0);
+    const SplitHuff H{(const uint16_t (*)[1 << DEC_LUT_BITS])L1, (const ICX_GLOBAL DecHuff*)d.tab->h};
+    DecWalker<true, SplitHuff> w = dec_walker<true>(d, H, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent,
+                                                    d.seg, st.nseg, st.ent_len * 8,
+                                                    j < st.nsub ? (int64_t)d.boff[j] : 0);
     bool run = false;
     if (j < st.nsub) {
         const uint64_t e = d.est[j];
@@ -620,7 +633,7 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
             run = w.running(stop);
         }
     }
-    PendSink sk{(int16_t*)mys, -1};
+    PendSink sk{(uint8_t*)mys, (uint32_t)(lane & 62), -1};
     ICX_GLOBAL uint32_t* coefs32 = (ICX_GLOBAL uint32_t*)d.coefs;  // global_store: vmcnt only, not lgkmcnt
     ICX_GLOBAL int32_t* dcs = (ICX_GLOBAL int32_t*)d.dc;
     const int zl = dec_zz((2 * lane) & 63), zh = dec_zz((2 * lane + 1) & 63);  // this lane's flush pair
@@ -640,7 +653,8 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
             uint32_t* src = wave_slots + l * SLOT_DW;
             if (lane < 32) {
                 const uint16_t* s16 = (const uint16_t*)src;
-                const uint32_t v = s16[zl] | ((uint32_t)s16[zh] << 16);
+                const int lsw = l & 62;
+                const uint32_t v = s16[zl ^ lsw] | ((uint32_t)s16[zh ^ lsw] << 16);
                 __builtin_amdgcn_wave_barrier();  // every lane's reads before the zeroing
                 src[lane] = 0;
                 coefs32[bi * 32 + lane] = v;

@@ -90,6 +90,22 @@ def test_decode_4k_q95_matches_oracle(codec, oracle, kind):
     assert np.array_equal(got, ref)
 
 
+def test_decode_batch_settling_at_different_launches(codec, oracle, dgolden):
+    """One batch whose images settle their entry states at different sync
+    launches (smooth frames early, uniform noise late, small files at once):
+    the settled ones finish on the aux stream while the rest keep relaxing
+    (icx_decode.cpp); every image must still equal the oracle."""
+    meta, jpgs, _ = dgolden
+    datas = [_jpeg((smooth if i % 2 == 0 else noise)(h, w, 40 + i)[:, :, ::-1].copy(), quality=95, subsampling=2)
+             for i, (h, w) in enumerate([(2160, 3840), (2160, 3840), (1080, 1920), (1080, 1920), (720, 1280)])]
+    datas += [jpgs["c130x250_s2_q95"], jpgs["rst7_130x250_444"]]
+    res = codec.decode_jpg_batch(datas, subsampling=1)
+    for i, (data, (st, img)) in enumerate(zip(datas, res)):
+        rc, ref = oracle.jpeg_decode(data)
+        assert rc == 0 and st == N.OK, (i, st)
+        assert np.array_equal(img, ref), i
+
+
 def test_decode_8k_reference_subsampling_rule(codec, oracle):
     """decodeImageWithSubsampling's rule (ImageCompression.java:140-153):
     s = 2 for an 8192-wide image, 1 below."""
