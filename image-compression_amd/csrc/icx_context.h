@@ -4,6 +4,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+
 #include <algorithm>
 #include <cstring>
 #include <map>
@@ -250,6 +252,20 @@ struct Timed {
             c->evpool.push_back(p.a);
             c->evpool.push_back(p.b);
         }
+    }
+};
+
+// Host wall time of a region into the profile (name: "host.*"), when profiling.
+struct HostSpan {
+    icx_ctx* c;
+    const char* name;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~HostSpan()
+    {
+        if (!c->prof) return;
+        KStat& k = c->stats[name];
+        k.launches++;
+        k.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
 };
 

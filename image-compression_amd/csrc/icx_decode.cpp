@@ -157,6 +157,16 @@ uint32_t warm_bits(uint32_t sub_bits)
     return std::min<uint32_t>(8192, sub_bits / 2);
 }
 
+// The header tables build_dec_tab reads are equal (so are the DecTabs).
+bool same_tables(const JpegHeader& a, const JpegHeader& b)
+{
+    return a.ncomp == b.ncomp && !memcmp(a.td, b.td, sizeof(a.td)) && !memcmp(a.ta, b.ta, sizeof(a.ta)) &&
+           !memcmp(a.tq, b.tq, sizeof(a.tq)) && !memcmp(a.qt, b.qt, sizeof(a.qt)) &&
+           !memcmp(a.qt_ok, b.qt_ok, sizeof(a.qt_ok)) && !memcmp(a.hn, b.hn, sizeof(a.hn)) &&
+           !memcmp(a.h_ok, b.h_ok, sizeof(a.h_ok)) && !memcmp(a.hbits, b.hbits, sizeof(a.hbits)) &&
+           !memcmp(a.hvals, b.hvals, sizeof(a.hvals));
+}
+
 struct WPlan {
     Plan p;
     int64_t total;
@@ -193,7 +203,10 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
     for (int i = 0; i < n; i++) dev_in[i] = jobs[i].data && is_device_ptr(jobs[i].data);
     std::vector<JpegHeader> hdr(n);
     std::vector<icx_status> hst(n, ICX_OK);
-    if (icx_status s = fetch_headers(c, jobs, n, dev_in, hdr, hst)) return s;
+    {
+        HostSpan hs{c, "host.dec_headers"};
+        if (icx_status s = fetch_headers(c, jobs, n, dev_in, hdr, hst)) return s;
+    }
     for (int i = 0; i < n; i++) {
         icx_decode_job& j = jobs[i];
         j.width = j.height = j.src_width = j.src_height = 0;
@@ -287,19 +300,41 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         c->host.used = 0;
         Uploader U(c, up);
 
+        // Decode tables once per distinct header tables (a batch of files from
+        // one encoder shares them): images point at their table set.
+        std::vector<int> tab_of(m);
+        std::vector<int> uniq;  // first image of each distinct set
+        for (int k = 0; k < m; k++) {
+            int u = -1;
+            for (int q = (int)uniq.size() - 1; q >= 0 && q >= (int)uniq.size() - 4; q--)
+                if (same_tables(sub[k]->J, sub[uniq[q]]->J)) {
+                    u = q;
+                    break;
+                }
+            if (u < 0) {
+                u = (int)uniq.size();
+                uniq.push_back(k);
+            }
+            tab_of[k] = u;
+        }
         DecTab* h_tab;
-        DecTab* d_tab = U.alloc<DecTab>(m, &h_tab);
+        DecTab* d_tab = U.alloc<DecTab>(uniq.size(), &h_tab);
         StageJob* h_stage;
         const StageJob* d_stage = U.alloc<StageJob>(m, &h_stage);
         if (U.overflow) return fail(c, ICX_E_NOMEM, "upload staging exhausted");
         std::vector<DecState> states(m);
         std::vector<int64_t> cnt_stage(m);
+        std::vector<char> tab_ok(uniq.size(), 0);
         int64_t max_nsub = 0;
         for (int k = 0; k < m; k++) {
+            HostSpan hs_tab{c, "host.dec_setup"};
             DecItem& it = *sub[k];
             DecDesc& d = desc[k];
-            h_tab[k] = DecTab{};
-            if (!build_dec_tab(it.J, h_tab[k])) {
+            if (uniq[tab_of[k]] == k) {
+                h_tab[tab_of[k]] = DecTab{};
+                tab_ok[tab_of[k]] = build_dec_tab(it.J, h_tab[tab_of[k]]);
+            }
+            if (!tab_ok[tab_of[k]]) {
                 it.job->status = ICX_E_CORRUPT;
                 states[k].status = 6;
             }
@@ -349,7 +384,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
                 d.out = it.host_out ? (uint8_t*)c->dev.take(it.job->out_len) : it.job->out;
                 d.ostride = d.ow * it.nch;
             }
-            d.tab = d_tab + k;
+            d.tab = d_tab + tab_of[k];
             states[k].end = scan_len;  // coefficients need no clearing: the write pass stores whole blocks
         }
         const int max_it = (int)max_nsub + 8;  // each launch settles at least one more subsequence

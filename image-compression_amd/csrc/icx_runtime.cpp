@@ -230,20 +230,6 @@ struct DPlan {
 
 
 // Build a launch plan over `ids` with per-image work counts.
-// Host wall time of a region into the profile (name: "host.*"), when profiling.
-struct HostSpan {
-    icx_ctx* c;
-    const char* name;
-    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-    ~HostSpan()
-    {
-        if (!c->prof) return;
-        KStat& k = c->stats[name];
-        k.launches++;
-        k.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    }
-};
-
 icx_status make_plan(Batch& B, const std::vector<int>& ids, const std::vector<int64_t>& counts, DPlan& out)
 {
     std::vector<int64_t> pre(ids.size() + 1, 0);

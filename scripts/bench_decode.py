@@ -76,7 +76,9 @@ def main():
                                               if k != "dec_sync_iters"},
                       "sync_launches_per_step": kern["dec_sync_iters"]["launches"] / a.steps,
                       "sync_relaunch_ms": {k: round(v["ms"] / a.steps, 3) for k, v in relaunch.items() if v["launches"]},
-                      "sync_walks_per_step": walks / a.steps}))
+                      "sync_walks_per_step": walks / a.steps,
+                      "host_ms_per_step": {k: round(codec.profile_query(k)["ms"] / a.steps, 3)
+                                           for k in ("host.dec_headers", "host.dec_setup")}}))
     codec.close()
 
 
