@@ -1147,7 +1147,9 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
                                                const int64_t* __restrict__ prefix, int m)
 {
     __shared__ uint32_t s_stg[4][132];  // per wave: one stuffed piece (<= 512 B) + read-ahead
-    const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    // wave-uniform (readfirstlane: the chunk's state and descriptor fields then
+    // come in scalar loads)
+    const int64_t item = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int slot, c;
     if (gridDim.y > 1) {  // 2-D launch: slot = y, every image has gridDim.x * 4 >= nchunks
         slot = (int)blockIdx.y;
@@ -1159,14 +1161,20 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
     }
     const int img = ids ? ids[slot] : slot;
     const ImgState& S = states[img];
-    if (S.best_node < 0 || S.status != 0) return;
     const ImgDesc& D = descs[img];
-    if (c >= D.nchunks) return;
-    const int buf = S.best_buf;
+    // The prologue's loads in three rounds (state and descriptor fields; the
+    // chunk's offsets; its stream words), each issued whole before the early
+    // exits - one after another, with the exits between them, they were a
+    // chain of about ten memory latencies in front of a chunk's few hundred
+    // bytes of work.  Indices are clamped so every load is in bounds.
+    const int best = S.best_node, status = S.status, buf = S.best_buf & 1, nch = D.nchunks;
+    const GAS uint64_t* off = gp(buf ? D.chunk_off[1] : D.chunk_off[0]);
+    const int cc = min(c, nch - 1);
+    const uint64_t total = off[nch], start = off[cc], end = off[cc + 1];
+    uint64_t run = gp(D.chunk_ffoff)[cc];
+    if (best < 0 || status != 0 || c >= nch) return;
     const int lane = threadIdx.x & 63;
     GAS uint8_t* out = gp(D.out);
-    const GAS uint64_t* off = gp(D.chunk_off[buf]);
-    const uint64_t total = off[D.nchunks];
     const uint64_t nbytes = (total + 7) >> 3;
     const int hdr = D.hdr_len;
 
@@ -1185,11 +1193,9 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
             out[i] = v;
         }
     }
-    const uint64_t bb = (off[c] + 7) >> 3;                 // owned bytes [bb, be)
-    const uint64_t be = min((off[c + 1] + 7) >> 3, nbytes);
-    const uint64_t start = off[c], end = off[c + 1];
-    const GAS uint32_t* cs = gp(D.scratch[buf]) + (size_t)c * CHUNK_WORDS;
-    uint64_t run = D.chunk_ffoff[c];
+    const uint64_t bb = (start + 7) >> 3;                  // owned bytes [bb, be)
+    const uint64_t be = min((end + 7) >> 3, nbytes);
+    const GAS uint32_t* cs = gp(buf ? D.scratch[1] : D.scratch[0]) + (size_t)c * CHUNK_WORDS;
     uint32_t* stw = s_stg[threadIdx.x >> 6];                 // this wave's stage
     uint8_t* stb = (uint8_t*)stw;
     for (uint64_t qb = bb; qb < be; qb += 256 * STUFF_BATCH) {
@@ -1197,14 +1203,11 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
         //    at once (one latency per batch, not per piece)
         uint32_t w0[STUFF_BATCH], w1[STUFF_BATCH];
 #pragma unroll
-        for (int it = 0; it < STUFF_BATCH; it++) {
-            const uint64_t q = qb + 256 * it + 4 * lane;
-            w0[it] = w1[it] = 0u;
-            if (q < be) {
-                const uint32_t lw = (uint32_t)((q * 8 - start) >> 5);
-                w0[it] = cs[lw];
-                w1[it] = cs[min(lw + 1, (uint32_t)CHUNK_WORDS - 1)];
-            }
+        for (int it = 0; it < STUFF_BATCH; it++) {  // unconditional (clamped): see load_group
+            const uint64_t q = min(qb + 256 * it + 4 * lane, be);
+            const uint32_t lw = min((uint32_t)((q * 8 - start) >> 5), (uint32_t)CHUNK_WORDS - 1);
+            w0[it] = cs[lw];
+            w1[it] = cs[min(lw + 1, (uint32_t)CHUNK_WORDS - 1)];
         }
 #pragma unroll
         for (int it = 0; it < STUFF_BATCH; it++) {
