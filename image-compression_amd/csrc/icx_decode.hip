@@ -976,17 +976,24 @@ __global__ void __launch_bounds__(256) k_dec_luma_color_420(const DecDesc* D, co
     __shared__ uint32_t lc[2][10][LC_CD];  // [cb|cr][chroma row cy0-1+j][dword]; byte q <-> column cx0-4+q
     int slot;
     int64_t wg;
-    if (!plan_slot(p, slot, wg)) return;
+    // the image's state and descriptor fields are read before the exits, so
+    // their loads go out together with the plan's (a chain of dependent loads
+    // otherwise, long against a workgroup's few microseconds of work)
+    const bool in = plan_slot(p, slot, wg);
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
-    if (S[img].status) return;
-    const int tpr = (d.mcux + LC_NM - 1) / LC_NM;
+    const int status = S[img].status, mcux = d.mcux, cw = d.cw[1], ch = d.ch[1], pwd = d.pw[1] >> 2;
+    const int pw0 = d.pw[0], ph0 = d.ph[0], nbmcu = d.nbmcu, ow = d.ow, oh = d.oh;
+    const uint8_t* plane1 = d.plane[1];
+    const uint8_t* plane2 = d.plane[2];
+    const int pitch1 = d.pw[1], pitch2 = d.pw[2];
+    if (!in || status) return;
+    const int tpr = (mcux + LC_NM - 1) / LC_NM;
     const int item = (int)wg;
     const int my = item / tpr, mx0 = (item - my * tpr) * LC_NM;
     const int t = threadIdx.x;
     // chroma staging first: its loads overlap the luma IDCT
-    const int cw = d.cw[1], ch = d.ch[1], cx0 = mx0 * 8, cy0 = my * 8;
-    const int pwd = d.pw[1] >> 2;
+    const int cx0 = mx0 * 8, cy0 = my * 8;
     for (int e = t; e < 2 * 10 * LC_CD; e += 256) {
         const int comp = e / (10 * LC_CD), rem = e - comp * (10 * LC_CD);
         const int j = rem / LC_CD, q = rem - j * LC_CD;
@@ -994,22 +1001,22 @@ __global__ void __launch_bounds__(256) k_dec_luma_color_420(const DecDesc* D, co
         rr = rr < 0 ? 0 : rr > ch - 1 ? ch - 1 : rr;
         int dw = (cx0 >> 2) - 1 + q;
         dw = dw < 0 ? 0 : dw > pwd - 1 ? pwd - 1 : dw;  // clamped dwords hold only unused columns
-        lc[comp][j][q] = ((const uint32_t*)(d.plane[1 + comp] + (int64_t)rr * d.pw[1 + comp]))[dw];
+        lc[comp][j][q] = ((const uint32_t*)((comp ? plane2 : plane1) + (int64_t)rr * (comp ? pitch2 : pitch1)))[dw];
     }
     {  // luma: block lb = MCU lb / 4, block k = lb % 4 of it
         const int lb = t >> 3, r = t & 7, mx = mx0 + (lb >> 2), k = lb & 3;
         const int bx = mx * 2 + (k & 1), by = my * 2 + (k >> 1);
-        const bool real = mx < d.mcux && bx * 8 < d.pw[0] && by * 8 < d.ph[0];
-        const int64_t b = ((int64_t)my * d.mcux + mx) * d.nbmcu + k;
+        const bool real = mx < mcux && bx * 8 < pw0 && by * 8 < ph0;
+        const int64_t b = ((int64_t)my * mcux + mx) * nbmcu + k;
         const uint2 row = idct_block_row(d, b, 0, r, real, ws[lb]);
         *(uint2*)&ly[(k >> 1) * 8 + r][(lb >> 2) * 4 + (k & 1) * 2] = row;
     }
     __syncthreads();
     const int rp = t >> 5, xt = 4 * (t & 31);  // chroma row cy0 + rp -> output rows 2rp, 2rp+1; columns xt..xt+3
     const int x0 = mx0 * 16;
-    const int n = d.ow - x0 - xt;
+    const int n = ow - x0 - xt;
     const int y0 = my * 16 + 2 * rp;
-    if (n <= 0 || y0 >= d.oh) return;
+    if (n <= 0 || y0 >= oh) return;
     const int i0 = (x0 + xt) >> 1;       // chroma columns i0, i0 + 1
     const int li = (xt >> 1) + 4;        // local byte of i0
     int cv[2][2][4];                     // [comp][top|bottom row][column]
@@ -1037,7 +1044,7 @@ __global__ void __launch_bounds__(256) k_dec_luma_color_420(const DecDesc* D, co
         }
     }
     const int m = n < 4 ? n : 4;
-    const int rows = d.oh - y0 < 2 ? 1 : 2;
+    const int rows = oh - y0 < 2 ? 1 : 2;
 #pragma unroll
     for (int h = 0; h < 2; h++) {  // unrolled: cv stays in registers
         if (h >= rows) break;
