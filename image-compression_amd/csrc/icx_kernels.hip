@@ -681,7 +681,10 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
     float4 qn = qf[en & 63];
 #pragma unroll
     for (int i = 1; i < 64; i++) {
-        if ((i & 3) == 1 && !__any(i < cnt)) break;  // every list of the wave is done
+        // every list of the wave is done (checked at every entry: the lists'
+        // padding to whole 16-B groups is never coded, and the test is a
+        // scalar compare against the wave's lane mask)
+        if (!__any(i < cnt)) break;
         const uint32_t e = en;
         const float4 qk = qn;
         if (i + 1 < 64) {
