@@ -13,7 +13,7 @@ hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat
 // kind: 0 = BGR24, 1 = RGB24, 2 = GRAY8
 void launch_fdct(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, int64_t tiles, int kind,
                  hipStream_t st);
-void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks,
+void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, bool rev,
                  hipStream_t st);
 // k_scan: the trial's offsets, exact file size and one binary-search step (decide)
 void launch_scan(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, hipStream_t st);

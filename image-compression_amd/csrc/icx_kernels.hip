@@ -737,7 +737,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS, 8) void k_huff(const ImgDesc* __restr
                                                        const ImgState* __restrict__ states,
                                                        const QNode* __restrict__ nodes,
                                                        const int32_t* __restrict__ ids,
-                                                       const int64_t* __restrict__ prefix, int m)
+                                                       const int64_t* __restrict__ prefix, int m, int rev)
 {
     __shared__ uint32_t slots[CHUNK_BLOCKS * SLOT_WORDS];
     // Coding tables during phase 1; afterwards the same LDS holds the chunk's
@@ -752,8 +752,11 @@ __global__ __launch_bounds__(CHUNK_BLOCKS, 8) void k_huff(const ImgDesc* __restr
     int32_t* const s_dcq = (int32_t*)s_bits;  // DC exchange; dead before s_bits is written
     __shared__ uint32_t s_wsum[CHUNK_BLOCKS / 64];
 
-    // 2-D launch (every image of the plan has as many chunks): slot = y
-    const int slot = gridDim.y > 1 ? (int)blockIdx.y : find_slot(prefix, m, blockIdx.x);
+    // 2-D launch (every image of the plan has as many chunks): slot = y, in
+    // reverse order on every other trial (rev), so a trial starts with the
+    // images whose lists the previous one read last - still in the Infinity Cache
+    const int slot = gridDim.y > 1 ? (int)(rev ? gridDim.y - 1 - blockIdx.y : blockIdx.y)
+                                   : find_slot(prefix, m, blockIdx.x);
     const int img = ids ? ids[slot] : slot;
     const ImgState& S = states[img];
     const ImgDesc& D = descs[img];
@@ -1424,11 +1427,12 @@ void launch_fdct(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, i
         ICX_LAUNCH(k_fdct_color<false>, grid, dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
 }
 
-void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, hipStream_t st)
+void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, bool rev,
+                 hipStream_t st)
 {
     if (chunks <= 0) return;
     const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3((unsigned)p.uniform, (unsigned)p.m) : dim3((unsigned)chunks);
-    ICX_LAUNCH(k_huff, grid, dim3(CHUNK_BLOCKS), 0, st, d, s, n, plan_ids(p), p.prefix, p.m);
+    ICX_LAUNCH(k_huff, grid, dim3(CHUNK_BLOCKS), 0, st, d, s, n, plan_ids(p), p.prefix, p.m, rev ? 1 : 0);
 }
 
 void launch_scan(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, hipStream_t st)

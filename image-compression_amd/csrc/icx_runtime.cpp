@@ -218,6 +218,7 @@ struct Batch {
     std::vector<ImgDesc> desc;
     std::vector<ImgState> state;
     ImgState* h_state = nullptr;  // pinned mirror for downloads
+    int huff_launches = 0;        // trial launches so far: odd ones walk the images in reverse (launch_huff)
     // The stage's small uploads (descriptors, states, launch plans) share one
     // pinned block and go in one copy per launch group (flush before launches).
     std::unique_ptr<Uploader> up;
@@ -420,7 +421,7 @@ icx_status run_trials(Batch& B, const std::vector<int>& ids, int depth, bool fin
     if (s || (s = B.up->flush())) return s;
     icx_ctx* c = B.c;
     for (int t = 0; t < depth; t++) {
-        { Timed tm(c, "huff", 0, true); launch_huff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, c->stream); }
+        { Timed tm(c, "huff", 0, true); launch_huff(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, (B.huff_launches++) & 1, c->stream); }
         { Timed tm(c, "scan", (int64_t)ids.size(), true); launch_scan(B.d_desc, B.d_state, B.d_nodes, P.p, c->stream); }
     }
     if (finals) {
