@@ -10,7 +10,18 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
 export TMPDIR=/tmp
 TAG=${TAG:-final}
-TAG=$TAG bash scripts/gpu_round.sh || exit 1
+# traces and per-dispatch counter rows are reduced to what the summaries read
+# (the merged gpurun_out/ must stay under 64 MiB)
+slim() {
+  find "$1" -name '*kernel_trace.csv' -delete
+  for f in $(find "$1" -name '*counter_collection.csv'); do
+    { head -1 "$f"; grep 'icx::' "$f" || true; } > "$f.tmp" && mv "$f.tmp" "$f"
+  done
+}
+if [ -z "$SKIP_ROUND" ]; then
+  TAG=$TAG bash scripts/gpu_round.sh || exit 1
+  slim gpurun_out/prof_${TAG}
+fi
 ONE="--steps 1 --warmup 0 --no-cpu-baseline --e2e 0 --host-io-frames 0"
 O=$R/gpurun_out/pmc_${TAG}
 mkdir -p $O
@@ -19,6 +30,9 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$O/$ctr" -o run \
       -- python3 "$R/bench.py" $ONE > "$O/$ctr.out" 2>&1 || { echo "pmc $ctr failed rc=$?"; tail -20 "$O/$ctr.out"; exit 1; }
 done
+slim "$O"
 cd "$R"
 TAG=sq_${TAG} SQ_ARGS="$ONE" bash scripts/gpu_sq.sh > gpurun_out/sq_${TAG}.txt 2>&1 || { echo "sq failed"; tail -20 gpurun_out/sq_${TAG}.txt; exit 1; }
+slim gpurun_out/sq_${TAG}
+du -sh gpurun_out
 echo done
