@@ -571,12 +571,12 @@ constexpr int SLOT_WORDS = ICX_SLOT_WORDS;
 
 constexpr int SLOT_BITS = SLOT_WORDS * 32;
 constexpr int AC_SIZES_ = 11;
-constexpr int TAB_WORDS = 2 * 16 * AC_SIZES_ * 2 + 2 * 64 * 4 + 2 * 16;  // s_ac + s_qf + s_dc
+constexpr int TAB_WORDS = 2 * 16 * AC_SIZES_ * 2 + 2 * 64 * 2 + 2 * 16;  // s_ac + s_qf + s_dc
 constexpr int OUT_WORDS = 1024;  // chunk streams up to this many words are assembled in LDS
 // 0xFF alignment bins of the assembled path: FF_COPIES copies per bin (lane
 // mod FF_COPIES picks one), so the LDS atomics of a wave rarely collide.
 constexpr int FF_COPIES = 16;
-static_assert(OUT_WORDS + 8 + 8 * FF_COPIES <= TAB_WORDS, "assembled stream must fit in the table LDS");
+constexpr int TABLE_LDS_WORDS = TAB_WORDS > OUT_WORDS + 8 + 8 * FF_COPIES ? TAB_WORDS : OUT_WORDS + 8 + 8 * FF_COPIES;
 constexpr int AC_SIZES = 11;                // AC magnitude categories 0..10 (8-bit JPEG)
 constexpr int AC_ENTRIES = 16 * AC_SIZES;   // (run, size) slots per table
 
@@ -665,7 +665,7 @@ __device__ __forceinline__ void load_list(uint32_t (&ev)[PRE], const uint32_t* l
 // constants are read while the current one is coded.
 template <class Sink>
 __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PRE], const uint32_t* lst, int cnt,
-                                             int diff, const float4* qf, const uint2* ac, const uint32_t* dc)
+                                             int diff, const float2* qf, const uint2* ac, const uint32_t* dc)
 {
     {
         const int ds = nbits(diff < 0 ? -diff : diff);
@@ -678,7 +678,7 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
     uint32_t g0[4] = {0u, 0u, 0u, 0u}, g1[4];
     load_group(g1, lst, PRE);
     uint32_t en = ev[1];
-    float4 qn = qf[en & 63];
+    float2 qn = qf[en & 63];
 #pragma unroll
     for (int i = 1; i < 64; i++) {
         // every list of the wave is done (checked at every entry: the lists'
@@ -686,7 +686,7 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
         // scalar compare against the wave's lane mask)
         if (!__any(i < cnt)) break;
         const uint32_t e = en;
-        const float4 qk = qn;
+        const float2 qk = qn;
         if (i + 1 < 64) {
             const int j = i + 1;
             if (j < PRE) {
@@ -707,14 +707,16 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
             qn = qf[en & 63];
         }
         const float f = (float)((int32_t)e >> 6);
-        if (i < cnt && fabsf(f) >= qk.x) {  // quotient != 0
+        // the quotient (exact for every |c| and divisor: tests/test_quant_exact.py),
+        // nonzero iff y >= 1 - no threshold table: 8-B quantiser reads
+        const float y = fmaf(fabsf(f), qk.x, qk.y);
+        if (i < cnt && y >= 1.0f) {
             const uint32_t k = e & 63;
             uint32_t run = k - last - 1;
             while (run >= 16) {
                 sink.put(zrl.x, (int)zrl.y);
                 run -= 16;
             }
-            const float y = fmaf(fabsf(f), qk.y, qk.z);
             const uint32_t u = (uint32_t)y;                    // |q| >= 1
             const int sz = __builtin_amdgcn_frexp_expf(y);     // bit length of |q|
             const uint2 c2 = ac[run * AC_SIZES + sz];
@@ -747,10 +749,10 @@ __global__ __launch_bounds__(CHUNK_BLOCKS, 8) void k_huff(const ImgDesc* __restr
     __shared__ uint32_t slots[CHUNK_BLOCKS * SLOT_WORDS];
     // Coding tables during phase 1; afterwards the same LDS holds the chunk's
     // assembled stream (phase 3, chunks of at most OUT_WORDS words).
-    __shared__ __attribute__((aligned(16))) uint32_t s_tab[TAB_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t s_tab[TABLE_LDS_WORDS];
     uint2 (*s_ac)[AC_ENTRIES] = (uint2 (*)[AC_ENTRIES])s_tab;
-    float4 (*s_qf)[64] = (float4 (*)[64])(s_tab + 2 * AC_ENTRIES * 2);  // (thr, frcp, fbias, -) per zig-zag index
-    uint32_t (*s_dc)[16] = (uint32_t (*)[16])(s_tab + 2 * AC_ENTRIES * 2 + 2 * 64 * 4);
+    float2 (*s_qf)[64] = (float2 (*)[64])(s_tab + 2 * AC_ENTRIES * 2);  // (frcp, fbias) per zig-zag index
+    uint32_t (*s_dc)[16] = (uint32_t (*)[16])(s_tab + 2 * AC_ENTRIES * 2 + 2 * 64 * 2);
     uint32_t* const s_out = s_tab;
     __shared__ uint32_t s_off[CHUNK_BLOCKS + 1];
     __shared__ uint32_t s_bits[CHUNK_BLOCKS];
@@ -808,7 +810,7 @@ __global__ __launch_bounds__(CHUNK_BLOCKS, 8) void k_huff(const ImgDesc* __restr
     const bool has_ac1 = t + CHUNK_BLOCKS < 2 * AC_ENTRIES;
     const uint2 ac1 = (&c_acx[0][0])[has_ac1 ? t + CHUNK_BLOCKS : t];
     const uint32_t dcv = c_dc[(t >> 4) & 1][t & 15];  // used by t < 32
-    if (t < 128) s_qf[t >> 6][t & 63] = qv;
+    if (t < 128) s_qf[t >> 6][t & 63] = make_float2(qv.y, qv.z);
     (&s_ac[0][0])[t] = ac0;
     if (has_ac1) (&s_ac[0][0])[t + CHUNK_BLOCKS] = ac1;
     if (t < 32) s_dc[t >> 4][t & 15] = dcv;
@@ -819,13 +821,13 @@ __global__ __launch_bounds__(CHUNK_BLOCKS, 8) void k_huff(const ImgDesc* __restr
     const int32_t prev_dc_raw = gp(D.coefs)[4 * (size_t)prev_off];
     __syncthreads();  // tables ready
 
-    const float4 q0t = s_qf[tb][0];
-    const int dq = quant((int32_t)ev[0] >> 6, q0t.y, q0t.z);
+    const float2 q0t = s_qf[tb][0];
+    const int dq = quant((int32_t)ev[0] >> 6, q0t.x, q0t.y);
     s_dcq[t] = dq;
     __syncthreads();
     int qprev = 0;
     if (pb >= b0) qprev = s_dcq[pb - b0];
-    else if (ext_prev) qprev = quant(prev_dc_raw >> 6, q0t.y, q0t.z);
+    else if (ext_prev) qprev = quant(prev_dc_raw >> 6, q0t.x, q0t.y);
 
     // ---- 1. encode_one_block into the slot (rarely: into the block's HBM spill)
     int bits = 0;
