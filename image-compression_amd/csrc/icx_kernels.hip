@@ -229,7 +229,7 @@ __device__ __forceinline__ void fdct_load(const FdctTile& T, uint32_t (&wv)[2][6
 // c) applies dummy blocks; lane = zig-zag index reads position c_zz_to_nat[lane]).  The DC and every AC coefficient with |c| >= thr
 // (lane 0's thr is negative; the others hold the smallest quantiser
 // threshold of k over the qualities this image may be coded at) form the
-// block's list, entries (c << 6) | k in k order, padded to a multiple of 4
+// block's list, entries float_bits(c) | (k << 3) in k order, padded to a multiple of 4
 // entries (k_huff reads 16-B groups) with the block's first non-candidates,
 // which cannot quantise to nonzero in any trial.
 // One wave per group of STEP blocks (one MCU for colour; luma(a): block
@@ -296,7 +296,7 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
             const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
             const int slot = cand ? pos : cnt + lane - pos;
-            *(slot < r4 ? st + run + slot : L.dummy + lane) = ((uint32_t)c[a] << 6) | (uint32_t)lane;
+            *(slot < r4 ? st + run + slot : L.dummy + lane) = __float_as_uint((float)c[a]) | ((uint32_t)lane << 3);
             len = writelane(len, cnt, a);
             off = writelane(off, run, a);
             run += r4;
@@ -656,13 +656,20 @@ __device__ __forceinline__ void load_list(uint32_t (&ev)[PRE], const uint32_t* l
 }
 
 // encode_one_block (jchuff.c) of one 8x8 block from its candidate list
-// (entries (c << 6) | k, zig-zag order, entry 0 = DC, zero entries past the
+// (entries float_bits(c) | (k << 3), zig-zag order, entry 0 = DC, zero entries past the
 // end): DC difference, then the AC run/size codes of the entries that
 // quantise to nonzero — zero runs are index gaps, since every coefficient
 // missing from the list quantises to zero at this trial's quality.  qf/ac/dc
 // are the LDS tables of the block's component (ac entries: (code << size,
 // len + size) at [run * AC_SIZES + size]).  The next entry's quantiser
 // constants are read while the current one is coded.
+// Quantiser constants of an entry's zig-zag index: entry & 0x1F8 is their
+// byte offset (one VALU op for the LDS address).
+__device__ __forceinline__ float2 qent(const float2* qf, uint32_t e)
+{
+    return *(const float2*)((const char*)qf + (e & 0x1F8u));
+}
+
 template <class Sink>
 __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PRE], const uint32_t* lst, int cnt,
                                              int diff, const float2* qf, const uint2* ac, const uint32_t* dc)
@@ -678,7 +685,7 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
     uint32_t g0[4] = {0u, 0u, 0u, 0u}, g1[4];
     load_group(g1, lst, PRE);
     uint32_t en = ev[1];
-    float2 qn = qf[en & 63];
+    float2 qn = qent(qf, en);
 #pragma unroll
     for (int i = 1; i < 64; i++) {
         // every list of the wave is done (checked at every entry: the lists'
@@ -704,14 +711,14 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
                 }
                 en = g0[j & 3];
             }
-            qn = qf[en & 63];
+            qn = qent(qf, en);
         }
-        const float f = (float)((int32_t)e >> 6);
+        const float f = __uint_as_float(e & ~0x1FFu);  // the coefficient (exact: integer, |c| <= 2^15)
         // the quotient (exact for every |c| and divisor: tests/test_quant_exact.py),
         // nonzero iff y >= 1 - no threshold table: 8-B quantiser reads
         const float y = fmaf(fabsf(f), qk.x, qk.y);
         if (i < cnt && y >= 1.0f) {
-            const uint32_t k = e & 63;
+            const uint32_t k = (e >> 3) & 63;
             uint32_t run = k - last - 1;
             while (run >= 16) {
                 sink.put(zrl.x, (int)zrl.y);
@@ -822,12 +829,12 @@ __global__ __launch_bounds__(CHUNK_BLOCKS, 8) void k_huff(const ImgDesc* __restr
     __syncthreads();  // tables ready
 
     const float2 q0t = s_qf[tb][0];
-    const int dq = quant((int32_t)ev[0] >> 6, q0t.x, q0t.y);
+    const int dq = quant((int)__uint_as_float(ev[0] & ~0x1FFu), q0t.x, q0t.y);
     s_dcq[t] = dq;
     __syncthreads();
     int qprev = 0;
     if (pb >= b0) qprev = s_dcq[pb - b0];
-    else if (ext_prev) qprev = quant(prev_dc_raw >> 6, q0t.x, q0t.y);
+    else if (ext_prev) qprev = quant((int)__uint_as_float((uint32_t)prev_dc_raw & ~0x1FFu), q0t.x, q0t.y);
 
     // ---- 1. encode_one_block into the slot (rarely: into the block's HBM spill)
     int bits = 0;
