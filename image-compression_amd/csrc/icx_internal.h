@@ -10,7 +10,7 @@
 //               quantiser entry in k_huff) — entry 0 is the DC, then every
 //               AC coefficient that can quantise to nonzero in ANY trial this
 //               image may run (|c| >= the smallest threshold over the image's
-//               reachable quality nodes, `cand_node`), zero-padded to a
+//               reachable quality nodes, `cand_node`), padded (any bits) to a
 //               multiple of 4.  The lists of one FDCT tile are packed back to
 //               back inside the tile's region (room for 64 entries per block);
 //               block b's list starts at entry 4 * coff[b] and holds ncoef[b]

@@ -229,9 +229,9 @@ __device__ __forceinline__ void fdct_load(const FdctTile& T, uint32_t (&wv)[2][6
 // c) applies dummy blocks; lane = zig-zag index reads position c_zz_to_nat[lane]).  The DC and every AC coefficient with |c| >= thr
 // (lane 0's thr is negative; the others hold the smallest quantiser
 // threshold of k over the qualities this image may be coded at) form the
-// block's list, entries float_bits(c) | (k << 3) in k order, padded to a multiple of 4
-// entries (k_huff reads 16-B groups) with the block's first non-candidates,
-// which cannot quantise to nonzero in any trial.
+// block's list, entries float_bits(c) | (k << 3) in k order, padded to a
+// multiple of 4 entries (k_huff reads 16-B groups; the padding holds whatever
+// the stage held - k_huff codes only the first `length` entries).
 // One wave per group of STEP blocks (one MCU for colour; luma(a): block
 // blk0 + a is luma), lane = k: per block a ballot/mbcnt partition
 // (candidates first, then the rest) into the wave's LDS stage, the group's
@@ -290,13 +290,16 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
 #pragma unroll
         for (int a = 0; a < STEP; a++) {
             if (!FULL && blk0 + a >= nblk) break;  // wave-uniform (partial grey tiles)
-            const bool cand = fabsf((float)c[a]) >= (luma(a) ? thr[0] : thr[1]);
+            const float cf = (float)c[a];
+            const bool cand = fabsf(cf) >= (luma(a) ? thr[0] : thr[1]);
             const uint64_t mask = __ballot(cand);
             const int cnt = __builtin_amdgcn_readfirstlane(__popcll(mask)), r4 = (cnt + 3) & ~3;
             const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-            const int slot = cand ? pos : cnt + lane - pos;
-            *(slot < r4 ? st + run + slot : L.dummy + lane) = __float_as_uint((float)c[a]) | ((uint32_t)lane << 3);
+            // the padding to a whole 16-B group is left as it is in the stage:
+            // k_huff never codes an entry past the list's length (writing the
+            // block's first non-candidates there cost 4 VALU per block: FDCT +9 %)
+            *(cand ? st + run + pos : L.dummy + lane) = __float_as_uint(cf) | ((uint32_t)lane << 3);
             len = writelane(len, cnt, a);
             off = writelane(off, run, a);
             run += r4;
