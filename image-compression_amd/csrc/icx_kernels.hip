@@ -134,12 +134,21 @@ __device__ __forceinline__ void fdct8(int32_t& d0, int32_t& d1, int32_t& d2, int
     d1 = DESCALE(t7 + z1 + z4, SH);
 }
 
-// rgb_ycc_convert (jccolor.c): 16-bit fixed point, FIX(x) = (int)(x*65536+0.5)
-__device__ __forceinline__ void rgb_ycc(int r, int g, int b, int& y, int& cb, int& cr)
+// rgb_ycc_convert (jccolor.c): 16-bit fixed point, FIX(x) = (int)(x*65536+0.5):
+//   y  = (19595 r + 38470 g + 7471 b + 32768) >> 16
+//   cb = (-11059 r - 21709 g + 32768 b + (128 << 16) + 32767) >> 16
+//   cr = (32768 r - 27439 g - 5329 b + (128 << 16) + 32767) >> 16
+// Each output's weights sum to a power of two (19595 + 38470 + 7471 = 65536,
+// 11059 + 21709 = 27439 + 5329 = 32768), so over e = r - g and d = b - g the
+// same integers need two products each and y - 128 (the level-shifted
+// sample the DCT takes) one add - exact for every (r, g, b): the multiple of
+// 2^16 leaves the floor division unchanged.
+__device__ __forceinline__ void rgb_ycc(int r, int g, int b, int& y128, int& cb, int& cr)
 {
-    y = (19595 * r + 38470 * g + 7471 * b + 32768) >> 16;
-    cb = (-11059 * r - 21709 * g + 32768 * b + (128 << 16) + 32767) >> 16;
-    cr = (32768 * r - 27439 * g - 5329 * b + (128 << 16) + 32767) >> 16;
+    const int e = r - g, d = b - g;
+    y128 = g + ((19595 * e + 7471 * d + 32768 - (128 << 16)) >> 16);
+    cb = ((d << 15) - 11059 * e + (128 << 16) + 32767) >> 16;
+    cr = ((e << 15) - 5329 * d + (128 << 16) + 32767) >> 16;
 }
 
 // =================================================================== FDCT
@@ -364,9 +373,8 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
                 const int c1 = (wv[h][o1 >> 2] >> ((o1 & 3) * 8)) & 255;
                 const int c2 = (wv[h][o2 >> 2] >> ((o2 & 3) * 8)) & 255;
                 const int R = BGR ? c2 : c0, G = c1, B = BGR ? c0 : c2;
-                int yy, cb, cr;
-                rgb_ycc(R, G, B, yy, cb, cr);
-                yv[k] = yy - 128;
+                int cb, cr;
+                rgb_ycc(R, G, B, yv[k], cb, cr);
                 csum[0][k >> 1] += cb;
                 csum[1][k >> 1] += cr;
             }
