@@ -295,7 +295,9 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
 #pragma unroll
         for (int a = 0; a < STEP; a++)
             c[a] = FULL || blk0 + a < nblk ? fix(blk0 + a, lane, (int)oz[blk0 + a][nat]) : 0;
-        int run = 0, len = 0, off = 0;  // run: padded entries of the group so far (wave-uniform)
+        // run: padded entries of the group so far (wave-uniform); lane a < STEP of
+        // meta: block a's (offset in the wave region, 16-B units) << 7 | length
+        int run = 0, meta = 0;
 #pragma unroll
         for (int a = 0; a < STEP; a++) {
             if (!FULL && blk0 + a >= nblk) break;  // wave-uniform (partial grey tiles)
@@ -309,12 +311,10 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
             // k_huff never codes an entry past the list's length (writing the
             // block's first non-candidates there cost 4 VALU per block: FDCT +9 %)
             *(cand ? st + run + pos : L.dummy + lane) = __float_as_uint(cf) | ((uint32_t)lane << 3);
-            len = writelane(len, cnt, a);
-            off = writelane(off, run, a);
+            meta = writelane(meta, (((int)total + run) >> 2 << 7) | cnt, a);  // scalar arithmetic, one VALU op
             run += r4;
         }
-        // meta: (offset in the wave region, 16-B units) << 7 | length
-        if (lane < STEP && blk0 + lane < nblk) L.meta[blk0 + lane] = (uint16_t)((((int)total + off) >> 2 << 7) | len);
+        if (lane < STEP && blk0 + lane < nblk) L.meta[blk0 + lane] = (uint16_t)meta;
         __builtin_amdgcn_wave_barrier();
         GAS u32x4_t* dst = region + total / 4;
         for (int p = lane; p < run / 4; p += 64) {
