@@ -340,6 +340,10 @@ def main():
                   "avg_launch_ms": round(kstats[k]["ms"] / kstats[k]["launches"], 4),
                   "algo_bytes_per_unit": round(b / kstats[k]["units"], 2), "unit": UNIT_NAME[k]}
               for k, b in bytes_of.items()}
+    if "fdct" in stages:  # launch-size independent forms (sub-batch sizes follow the HBM budget)
+        px, ms = kstats["fdct"]["units"], kstats["fdct"]["ms"]
+        stages["fdct"]["ms_per_333_frames"] = round(ms / px * 333.3 * W * H, 4)
+        stages["fdct"]["frac_at_6B_per_px"] = round(6 * px / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
     res = batch.results()
     line = {
         "metric": "megapixels/sec JPEG encode (4K, -t 1MiB, q=0.25 cached)",
