@@ -4,10 +4,11 @@
 //   px          u8 BGR/RGB/grey rows (caller's buffer, or the resize buffer)
 //   coefs       sparse jpeg_fdct_islow output (raw, x8): per scan block
 //               (MCU order Y0 Y1 Y2 Y3 Cb Cr) a list of 32-bit entries
-//               float_bits(c) | (k << 3) in zig-zag order k (|c| <= 2^15, so
-//               the float's low 9 mantissa bits are free; entry & ~0x1FF is c
-//               as a float, entry & 0x1F8 the byte offset of k's 8-B
-//               quantiser entry in k_huff) — entry 0 is the DC, then every
+//               float_bits(c) | (chroma << 9) | (k << 3) in zig-zag order k
+//               (|c| <= 8192 < 2^14 for 8-bit samples, so the float's low 10
+//               mantissa bits are free; entry & ~0x3FF is c as a float,
+//               entry & 0x3F8 the byte offset of the block's 8-B quantiser
+//               entry in k_huff's [component][k] table) — entry 0 is the DC, then every
 //               AC coefficient that can quantise to nonzero in ANY trial this
 //               image may run (|c| >= the smallest threshold over the image's
 //               reachable quality nodes, `cand_node`), padded (any bits) to a

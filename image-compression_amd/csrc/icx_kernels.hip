@@ -238,7 +238,7 @@ __device__ __forceinline__ void fdct_load(const FdctTile& T, uint32_t (&wv)[2][6
 // c) applies dummy blocks; lane = zig-zag index reads position c_zz_to_nat[lane]).  The DC and every AC coefficient with |c| >= thr
 // (lane 0's thr is negative; the others hold the smallest quantiser
 // threshold of k over the qualities this image may be coded at) form the
-// block's list, entries float_bits(c) | (k << 3) in k order, padded to a
+// block's list, entries float_bits(c) | (chroma << 9) | (k << 3) in k order, padded to a
 // multiple of 4 entries (k_huff reads 16-B groups; the padding holds whatever
 // the stage held - k_huff codes only the first `length` entries).
 // One wave per group of STEP blocks (one MCU for colour; luma(a): block
@@ -310,7 +310,8 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
             // the padding to a whole 16-B group is left as it is in the stage:
             // k_huff never codes an entry past the list's length (writing the
             // block's first non-candidates there cost 4 VALU per block: FDCT +9 %)
-            *(cand ? st + run + pos : L.dummy + lane) = __float_as_uint(cf) | ((uint32_t)lane << 3);
+            *(cand ? st + run + pos : L.dummy + lane) =
+                __float_as_uint(cf) | ((uint32_t)lane << 3) | (luma(a) ? 0u : 0x200u);
             meta = writelane(meta, (((int)total + run) >> 2 << 7) | cnt, a);  // scalar arithmetic, one VALU op
             run += r4;
         }
@@ -674,11 +675,12 @@ __device__ __forceinline__ void load_list(uint32_t (&ev)[PRE], const uint32_t* l
 // are the LDS tables of the block's component (ac entries: (code << size,
 // len + size) at [run * AC_SIZES + size]).  The next entry's quantiser
 // constants are read while the current one is coded.
-// Quantiser constants of an entry's zig-zag index: entry & 0x1F8 is their
-// byte offset (one VALU op for the LDS address).
+// Quantiser constants of an entry's component and zig-zag index: entry &
+// 0x3F8 is their byte offset in the [2][64] table (one VALU op for the LDS
+// address, no per-lane table base).
 __device__ __forceinline__ float2 qent(const float2* qf, uint32_t e)
 {
-    return *(const float2*)((const char*)qf + (e & 0x1F8u));
+    return *(const float2*)((const char*)qf + (e & 0x3F8u));
 }
 
 template <class Sink>
@@ -724,7 +726,7 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
             }
             qn = qent(qf, en);
         }
-        const float f = __uint_as_float(e & ~0x1FFu);  // the coefficient (exact: integer, |c| <= 2^15)
+        const float f = __uint_as_float(e & ~0x3FFu);  // the coefficient (exact: integer, |c| < 2^14)
         // the quotient (exact for every |c| and divisor: tests/test_quant_exact.py),
         // nonzero iff y >= 1 - no threshold table: 8-B quantiser reads
         const float y = fmaf(fabsf(f), qk.x, qk.y);
@@ -840,26 +842,26 @@ __global__ __launch_bounds__(CHUNK_BLOCKS, 8) void k_huff(const ImgDesc* __restr
     __syncthreads();  // tables ready
 
     const float2 q0t = s_qf[tb][0];
-    const int dq = quant((int)__uint_as_float(ev[0] & ~0x1FFu), q0t.x, q0t.y);
+    const int dq = quant((int)__uint_as_float(ev[0] & ~0x3FFu), q0t.x, q0t.y);
     s_dcq[t] = dq;
     __syncthreads();
     int qprev = 0;
     if (pb >= b0) qprev = s_dcq[pb - b0];
-    else if (ext_prev) qprev = quant((int)__uint_as_float((uint32_t)prev_dc_raw & ~0x1FFu), q0t.x, q0t.y);
+    else if (ext_prev) qprev = quant((int)__uint_as_float((uint32_t)prev_dc_raw & ~0x3FFu), q0t.x, q0t.y);
 
     // ---- 1. encode_one_block into the slot (rarely: into the block's HBM spill)
     int bits = 0;
     if (valid) {
         const uint32_t sb = (uint32_t)(t * SLOT_WORDS * 4);
         LdsSink sink{0, 0, sb, sb + (SLOT_WORDS - 1) * 4, slots};
-        encode_block(sink, ev, lst, cnt, dq - qprev, s_qf[tb], s_ac[tb], s_dc[tb]);
+        encode_block(sink, ev, lst, cnt, dq - qprev, &s_qf[0][0], s_ac[tb], s_dc[tb]);
         bits = (int)(sink.wb - sb) * 8 + sink.n;
         sink.finish();
         if (bits > SLOT_BITS) {  // rare: reload the list (ev[] is dead by now)
             uint32_t e2[PRE];
             load_list(e2, lst);
             GlobalSink g{0, 0, 0, gp(D.ovf + b * BLOCK_WORDS)};
-            encode_block(g, e2, lst, cnt, dq - qprev, s_qf[tb], s_ac[tb], s_dc[tb]);
+            encode_block(g, e2, lst, cnt, dq - qprev, &s_qf[0][0], s_ac[tb], s_dc[tb]);
             g.finish();
         }
     }

@@ -780,7 +780,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                 if (cnt[blk] != 64 || (size_t)off[blk] * 4 + 64 > raw.size())
                     return fail(c, ICX_E_DEVICE, "debug FDCT list is not complete");
                 for (int i = 0; i < 64; i++) {
-                    const uint32_t v = (uint32_t)raw[(size_t)off[blk] * 4 + i], cb = v & ~0x1FFu;
+                    const uint32_t v = (uint32_t)raw[(size_t)off[blk] * 4 + i], cb = v & ~0x3FFu;
                     float cf;
                     std::memcpy(&cf, &cb, 4);
                     fdct_out[blk * 64 + ((v >> 3) & 63)] = (int16_t)cf;
