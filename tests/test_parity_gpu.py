@@ -325,3 +325,36 @@ def test_host_buffers_pipelined_over_subbatches(oracle, monkeypatch):
         assert c.profile_query("subbatch")["launches"] >= 6  # >= 3 sub-batches per call
     finally:
         c.close()
+
+
+def test_bench_headline_frames_match_oracle(codec, oracle):
+    """The headline workload itself (bench.py: frames from make_frames, -t 1 MiB,
+    cached LearnedParams(0.25, 1.0), outputs in HBM, one prepared batch run
+    twice as in the timed loop): every frame's file, quality and encode count
+    equal the oracle's compressJpgWithTargetSize on the same pixels."""
+    import torch
+
+    import bench
+    dev = torch.device("cuda", 0)
+    n = 4  # two smooth (cache hit at q = 0.25), two noise (search)
+    frames = bench.make_frames(n, 1000003 * 3, dev)
+    outs = torch.empty((n, bench.TARGET + 1), dtype=torch.uint8, device=dev)
+    batch = codec.prepare(frames, bench.TARGET, bench.Q0, cached=[icx.LearnedParams(bench.Q0, 1.0)] * n,
+                          outputs=[outs[i] for i in range(n)])
+    for _ in range(2):
+        batch.run()
+    torch.cuda.synchronize()
+    res = batch.results()
+    for i in range(n):
+        img = frames[i].cpu().numpy()
+        ref = oracle.fit(img, bench.TARGET, bench.Q0, cached=(bench.Q0, 1.0))
+        r = res[i]
+        assert r["success"] and ref["success"], i
+        assert outs[i, :r["out_len"]].cpu().numpy().tobytes() == ref["data"], i
+        assert np.float32(r["learned"].quality) == np.float32(ref["quality"]), i
+        # the oracle counts saveCompressedImage's re-encode after a search
+        # (ImageCompressionJpg.java:255-260); the device stuffs the best trial instead
+        trials = ref["encodes"] - (0 if ref["cache_hit"] else 1)
+        assert r["learned"].scale == ref["scale"] and r["encodes"] == trials, (i, r["encodes"], ref["encodes"])
+        assert r["cache_hit"] == ref["cache_hit"], i
+    assert [r["cache_hit"] for r in res] == [True, False, True, False]
