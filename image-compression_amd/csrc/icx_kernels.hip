@@ -102,36 +102,75 @@ __device__ __forceinline__ int find_slot(const int64_t* prefix, int m, int64_t i
 #define PASS1_BITS 2
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
 
+// Two int16 lanes (lo, hi) of one dword, and lo * c0 + hi * c1 + acc in one
+// VOP3P v_dot2_i32_i16 (exact: products and sums stay far inside int32).  The
+// builtin compiles to the two-address v_dot2c form, which needs a v_mov of
+// the accumulator in front of every chain; the three-address form reads the
+// coefficient pair from an SGPR and the accumulator from any VGPR.
+__device__ __forceinline__ uint32_t pack16(int lo, int hi)
+{
+    return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
+}
+template <int C0, int C1>
+__device__ __forceinline__ int dot2(uint32_t p, int acc)
+{
+    static_assert(C0 >= -32768 && C0 < 32768 && C1 >= -32768 && C1 < 32768, "int16 weights");
+    int d;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(p), "s"(((uint32_t)C0 & 0xFFFFu) | ((uint32_t)C1 << 16)), "v"(acc));
+    return d;
+}
+
 // One 1-D pass of jpeg_fdct_islow (jfdctint.c, IJG 6b).  pass 0 = rows
 // (outputs scaled up by PASS1_BITS), pass 1 = columns.
-template <int PASS>
+// The rotations are IJG's products expanded per input: e.g. the odd part's
+// d7 = t4*2446 + z1*-7373 + z3*-16069 + z5 (z1 = t4+t7, z3 = t4+t6, z5 =
+// (t4+t5+t6+t7)*9633) is t4*-11363 + t5*9633 + t6*-6436 + t7*2260 - the same
+// integer, so the same DESCALE - i.e. two dot2 ops over (t4, t5), (t6, t7)
+// with the rounding constant as the accumulator.  Every t* fits int16 (rows:
+// |t| <= 510 from 8-bit samples; columns: row outputs lie in [-4096, 4080],
+// so |t| <= 16352), checked exhaustively over the extreme inputs on the host.
+// 34 instead of ~48 VALU per pass.
+// HI (columns only): every output is left in the high 16 bits of its int32
+// (low bits undefined) for a ds_write_b16_d16_hi store - no shift: doubled
+// weights (all still int16: the largest is 11363) and rounding constant give
+// 2x + 2^15, whose bits 16.. are DESCALE(x, 15); d0 / d4 are shifted left
+// instead of right.
+template <int PASS, bool HI = false>
 __device__ __forceinline__ void fdct8(int32_t& d0, int32_t& d1, int32_t& d2, int32_t& d3,
                                       int32_t& d4, int32_t& d5, int32_t& d6, int32_t& d7)
 {
+    static_assert(!HI || PASS == 1, "high-half outputs for the column pass");
     int32_t t0 = d0 + d7, t7 = d0 - d7, t1 = d1 + d6, t6 = d1 - d6;
     int32_t t2 = d2 + d5, t5 = d2 - d5, t3 = d3 + d4, t4 = d3 - d4;
     int32_t t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
     constexpr int SH = PASS == 0 ? CONST_BITS - PASS1_BITS : CONST_BITS + PASS1_BITS;
+    constexpr int K = HI ? 2 : 1;          // weight scale
+    constexpr int OS = HI ? 0 : SH;        // output shift
+    constexpr int R = 1 << (SH - 1 + (HI ? 1 : 0));
     if (PASS == 0) {
         d0 = (t10 + t11) << PASS1_BITS;
         d4 = (t10 - t11) << PASS1_BITS;
+    } else if (HI) {
+        d0 = (t10 + t11 + (1 << (PASS1_BITS - 1))) << (16 - PASS1_BITS);
+        d4 = (t10 - t11 + (1 << (PASS1_BITS - 1))) << (16 - PASS1_BITS);
     } else {
         d0 = DESCALE(t10 + t11, PASS1_BITS);
         d4 = DESCALE(t10 - t11, PASS1_BITS);
     }
-    int32_t z1 = (t12 + t13) * 4433;                  // FIX_0_541196100
-    d2 = DESCALE(z1 + t13 * 6270, SH);                // FIX_0_765366865
-    d6 = DESCALE(z1 - t12 * 15137, SH);               // FIX_1_847759065
-    z1 = t4 + t7;
-    int32_t z2 = t5 + t6, z3 = t4 + t6, z4 = t5 + t7;
-    int32_t z5 = (z3 + z4) * 9633;                    // FIX_1_175875602
-    t4 *= 2446; t5 *= 16819; t6 *= 25172; t7 *= 12299;
-    z1 *= -7373; z2 *= -20995; z3 *= -16069; z4 *= -3196;
-    z3 += z5; z4 += z5;
-    d7 = DESCALE(t4 + z1 + z3, SH);
-    d5 = DESCALE(t5 + z2 + z4, SH);
-    d3 = DESCALE(t6 + z2 + z3, SH);
-    d1 = DESCALE(t7 + z1 + z4, SH);
+    int r = R;  // the rounding constant, once in a VGPR for all six chains
+    asm("" : "+v"(r));
+    // even: z1 = (t12 + t13) * FIX_0_541196100, + t13 * FIX_0_765366865, - t12 * FIX_1_847759065
+    const uint32_t e = pack16(t12, t13);
+    d2 = dot2<K * 4433, K * 10703>(e, r) >> OS;
+    d6 = dot2<K * -10704, K * 4433>(e, r) >> OS;
+    // odd: FIX_0_298631336 2446, FIX_2_053119869 16819, FIX_3_072711026 25172,
+    // FIX_1_501321110 12299, FIX_0_899976223 7373, FIX_2_562915447 20995,
+    // FIX_1_961570560 16069, FIX_0_390180644 3196, FIX_1_175875602 9633
+    const uint32_t a = pack16(t4, t5), b = pack16(t6, t7);
+    d7 = dot2<K * -6436, K * 2260>(b, dot2<K * -11363, K * 9633>(a, r)) >> OS;
+    d5 = dot2<K * -11362, K * 6437>(b, dot2<K * 9633, K * 2261>(a, r)) >> OS;
+    d3 = dot2<K * -2259, K * 9633>(b, dot2<K * -6436, K * -11362>(a, r)) >> OS;
+    d1 = dot2<K * 9633, K * 11363>(b, dot2<K * 2260, K * 6437>(a, r)) >> OS;
 }
 
 // rgb_ycc_convert (jccolor.c): 16-bit fixed point, FIX(x) = (int)(x*65536+0.5):
@@ -142,13 +181,17 @@ __device__ __forceinline__ void fdct8(int32_t& d0, int32_t& d1, int32_t& d2, int
 // 11059 + 21709 = 27439 + 5329 = 32768), so over e = r - g and d = b - g the
 // same integers need two products each and y - 128 (the level-shifted
 // sample the DCT takes) one add - exact for every (r, g, b): the multiple of
-// 2^16 leaves the floor division unchanged.
-__device__ __forceinline__ void rgb_ycc(int r, int g, int b, int& y128, int& cb, int& cr)
+// 2^16 leaves the floor division unchanged.  Over the negated differences
+// (g - r, g - b), packed as int16 pairs, every weight fits int16 (32768 d =
+// -32768 * (g - b)): one dot2 per output, the rounding constants (ky, kc,
+// held in VGPRs by the caller) as accumulators.
+constexpr int YCC_KY = 32768 - (128 << 16), YCC_KC = (128 << 16) + 32767;
+__device__ __forceinline__ void rgb_ycc(int r, int g, int b, int ky, int kc, int& y128, int& cb, int& cr)
 {
-    const int e = r - g, d = b - g;
-    y128 = g + ((19595 * e + 7471 * d + 32768 - (128 << 16)) >> 16);
-    cb = ((d << 15) - 11059 * e + (128 << 16) + 32767) >> 16;
-    cr = ((e << 15) - 5329 * d + (128 << 16) + 32767) >> 16;
+    const uint32_t n = pack16(g - r, g - b);
+    y128 = g + (dot2<-19595, -7471>(n, ky) >> 16);
+    cb = dot2<11059, -32768>(n, kc) >> 16;
+    cr = dot2<-32768, 5329>(n, kc) >> 16;
 }
 
 // =================================================================== FDCT
@@ -174,8 +217,8 @@ constexpr int WSTR = 72;              // workspace int16 per block (row-pass wri
 
 __device__ __forceinline__ void st_row8(int16_t* p, const int (&v)[8])  // 8 int16, 8-B aligned
 {
-    *(uint2*)p = make_uint2((v[0] & 0xFFFF) | (v[1] << 16), (v[2] & 0xFFFF) | (v[3] << 16));
-    *(uint2*)(p + 4) = make_uint2((v[4] & 0xFFFF) | (v[5] << 16), (v[6] & 0xFFFF) | (v[7] << 16));
+    *(uint2*)p = make_uint2(pack16(v[0], v[1]), pack16(v[2], v[3]));  // one v_perm per pair
+    *(uint2*)(p + 4) = make_uint2(pack16(v[4], v[5]), pack16(v[6], v[7]));
 }
 
 // Phase B loads: this thread's rows 2i, 2i+1 of the tile, pixels 8sg..8sg+7
@@ -364,6 +407,8 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
     {
         const int i = t >> 5, sg = t & 31;
         int csum[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};  // 2x2 sums of Cb, Cr
+        int ky = YCC_KY, kc = YCC_KC;
+        asm("" : "+v"(ky), "+v"(kc));
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             int yv[8];
@@ -375,7 +420,7 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
                 const int c2 = (wv[h][o2 >> 2] >> ((o2 & 3) * 8)) & 255;
                 const int R = BGR ? c2 : c0, G = c1, B = BGR ? c0 : c2;
                 int cb, cr;
-                rgb_ycc(R, G, B, yv[k], cb, cr);
+                rgb_ycc(R, G, B, ky, kc, yv[k], cb, cr);
                 csum[0][k >> 1] += cb;
                 csum[1][k >> 1] += cr;
             }
@@ -419,9 +464,9 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
             int32_t d[8];
 #pragma unroll
             for (int v = 0; v < 8; v++) d[v] = ws[blk][v * 8 + col];
-            fdct8<1>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+            fdct8<1, true>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
 #pragma unroll
-            for (int v = 0; v < 8; v++) oz[blk][v * 8 + col] = (int16_t)d[v];
+            for (int v = 0; v < 8; v++) oz[blk][v * 8 + col] = (int16_t)(d[v] >> 16);  // ds_write_b16_d16_hi
         }
     }
     __syncthreads();
@@ -547,9 +592,9 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
         int32_t d[8];
 #pragma unroll
         for (int v = 0; v < 8; v++) d[v] = ws[blk][v * 8 + col];
-        fdct8<1>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+        fdct8<1, true>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
 #pragma unroll
-        for (int v = 0; v < 8; v++) oz[blk][v * 8 + col] = (int16_t)d[v];
+        for (int v = 0; v < 8; v++) oz[blk][v * 8 + col] = (int16_t)(d[v] >> 16);  // ds_write_b16_d16_hi
     }
     __syncthreads();
     const int nblk = min(16, D.mcux - tx * 16);
