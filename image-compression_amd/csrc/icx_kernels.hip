@@ -728,6 +728,21 @@ __device__ __forceinline__ float2 qent(const float2* qf, uint32_t e)
     return *(const float2*)((const char*)qf + (e & 0x3F8u));
 }
 
+// ac[run * AC_SIZES + sz] (ac: an LDS table): the address as one
+// v_mad_u32_u24 (the row stride held in a VGPR by the caller: as an SGPR
+// operand it is rematerialised at every site) and one v_lshl_add_u32 - the
+// compiler's own form is a multiply, a shift and an add3.
+typedef const __attribute__((address_space(3))) uint64_t* lds_u64_cp;
+__device__ __forceinline__ uint2 ac_entry(const uint2* ac, uint32_t run, int sz, uint32_t stride)
+{
+    uint32_t row;
+    asm("v_mad_u32_u24 %0, %1, %2, %3"
+        : "=v"(row)
+        : "v"(run), "v"(stride), "v"((uint32_t)(uintptr_t)(lds_u64_cp)ac));
+    const uint64_t v = *(lds_u64_cp)(uintptr_t)(row + ((uint32_t)sz << 3));
+    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+}
+
 template <class Sink>
 __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PRE], const uint32_t* lst, int cnt,
                                              int diff, const float2* qf, const uint2* ac, const uint32_t* dc)
@@ -739,6 +754,8 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
         sink.put(((hc >> 8) << ds) | mag, (int)(hc & 255) + ds);
     }
     const uint2 zrl = ac[15 * AC_SIZES];
+    uint32_t stride = AC_SIZES * sizeof(uint2);  // ac_entry's row stride, once in a VGPR
+    asm("" : "+v"(stride));
     uint32_t last = 0;  // zig-zag index of the last nonzero coefficient
     uint32_t g0[4] = {0u, 0u, 0u, 0u}, g1[4];
     load_group(g1, lst, PRE);
@@ -784,7 +801,7 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
             }
             const uint32_t u = (uint32_t)y;                    // |q| >= 1
             const int sz = __builtin_amdgcn_frexp_expf(y);     // bit length of |q|
-            const uint2 c2 = ac[run * AC_SIZES + sz];
+            const uint2 c2 = ac_entry(ac, run, sz, stride);
             const uint32_t sm = (uint32_t)((int32_t)e >> 31);
             sink.put(c2.x | ((u ^ sm) & ((1u << sz) - 1)), (int)c2.y);
             last = k;
