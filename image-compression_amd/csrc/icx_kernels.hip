@@ -298,7 +298,7 @@ __device__ __forceinline__ void fdct_load(const FdctTile& T, uint32_t (&wv)[2][6
 template <int NB, int STEP>
 struct ListStage {
     uint32_t st[4][STEP * 64];
-    uint32_t dummy[64];
+    uint32_t dummy[64];  // follows st[3]: index 4 * STEP * 64 + lane
     uint16_t meta[NB];
 };
 
@@ -324,6 +324,8 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     uint32_t* st = L.st[wave];
+    uint32_t* const st0 = &L.st[0][0];
+    const int dummy_at = 4 * STEP * 64 + lane;  // L.dummy[lane] as an index into st0
     uint32_t total = 0;
     const int nat = c_zz_to_nat[lane];  // oz holds natural order; lane = zig-zag index
     // wave w takes groups NB/(4 STEP) * w .. (consecutive blocks) and packs their
@@ -348,14 +350,20 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
             const bool cand = fabsf(cf) >= (luma(a) ? thr[0] : thr[1]);
             const uint64_t mask = __ballot(cand);
             const int cnt = __builtin_amdgcn_readfirstlane(__popcll(mask)), r4 = (cnt + 3) & ~3;
-            const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+            // the candidate's stage index: wave base + run + candidates below the lane
+            const int at = (int)__builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, (uint32_t)(wave * (STEP * 64) + run)));
             // the padding to a whole 16-B group is left as it is in the stage:
             // k_huff never codes an entry past the list's length (writing the
             // block's first non-candidates there cost 4 VALU per block: FDCT +9 %)
-            *(cand ? st + run + pos : L.dummy + lane) =
+            // one v_cndmask on the ballot: as a C select the compiler branches
+            // around the candidate address (exec save / restore: SALU)
+            int idx;
+            asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(idx) : "v"(dummy_at), "v"(at), "s"(mask));
+            st0[idx] =
                 __float_as_uint(cf) | ((uint32_t)lane << 3) | (luma(a) ? 0u : 0x200u);
-            meta = writelane(meta, (((int)total + run) >> 2 << 7) | cnt, a);  // scalar arithmetic, one VALU op
+            // total + run is a multiple of 4: (x >> 2) << 7 = x << 5
+            meta = writelane(meta, (((int)total + run) << 5) | cnt, a);  // scalar arithmetic, one VALU op
             run += r4;
         }
         if (lane < STEP && blk0 + lane < nblk) L.meta[blk0 + lane] = (uint16_t)meta;
