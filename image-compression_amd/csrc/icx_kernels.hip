@@ -128,11 +128,11 @@ __device__ __forceinline__ int dot2(uint32_t p, int acc)
 // integer, so the same DESCALE - i.e. two dot2 ops over (t4, t5), (t6, t7)
 // with the rounding constant as the accumulator.  Every t* fits int16 (rows:
 // |t| <= 510 from 8-bit samples; columns: row outputs lie in [-4096, 4080],
-// so |t| <= 16352), checked exhaustively over the extreme inputs on the host.
+// so |t| <= 16352), checked at the extreme inputs (tests/test_ycc_identity.py).
 // 34 instead of ~48 VALU per pass.
 // HI (columns only): every output is left in the high 16 bits of its int32
 // (low bits undefined) for a ds_write_b16_d16_hi store - no shift: doubled
-// weights (all still int16: the largest is 11363) and rounding constant give
+// weights (still int16: the largest is 2 * 11363 = 22726) and rounding constant give
 // 2x + 2^15, whose bits 16.. are DESCALE(x, 15); d0 / d4 are shifted left
 // instead of right.
 template <int PASS, bool HI = false>
