@@ -80,10 +80,45 @@ def pmc_traffic(kernel, units_per_launch):
     if not os.path.exists(path):
         return None
     try:
-        per_unit = json.load(open(path))["bytes_per_unit"][kernel]
-    except (KeyError, ValueError):
+        per_unit = pmc_bytes_per_unit(json.load(open(path)))[kernel]
+    except (KeyError, ValueError, TypeError):
         return None
     return int(per_unit * units_per_launch)
+
+
+PMC_SHORT = {"k_fdct_color": "fdct", "k_fdct_gray": "fdct", "k_huff": "huff", "k_scan": "scan",
+             "k_ffscan": "ffscan", "k_stuff": "stuff", "k_resize": "resize"}
+
+
+def pmc_bytes_per_unit(summary):
+    """bench kernel name -> HBM bytes per unit, from scripts/pmc_summary.py's
+    file form ({"bytes_per_unit": {...}}) or, should a kernel-keyed form
+    ({"icx::k_huff": {"hbm_bytes_per_unit": ...}}) be committed, from that."""
+    if "bytes_per_unit" in summary:
+        return summary["bytes_per_unit"]
+    return {PMC_SHORT[k.split("::")[-1].split("<")[0]]: v["hbm_bytes_per_unit"]
+            for k, v in summary.items() if isinstance(v, dict) and "hbm_bytes_per_unit" in v
+            and k.split("::")[-1].split("<")[0] in PMC_SHORT}
+
+
+def host_cores():
+    """Host cores this process may use: the scheduler affinity set, capped by
+    a cgroup CPU quota when one is set (on the GPU box the affinity mask shows
+    the whole machine while the job's share is a quota).  Returns (cores,
+    how it was determined).  The reference sizes its pool the same way:
+    Runtime.availableProcessors() (CompressionBatch.java:64-68), which in a
+    container honours both the affinity mask and the cgroup quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    how = "sched_getaffinity"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            q = max(1, int(-(-int(quota) // int(period))))
+            if q < n:
+                n, how = q, "cgroup cpu.max quota"
+    except (OSError, ValueError):
+        pass
+    return n, how
 
 
 VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 256 CUs x 4 SIMD-32, 2 cycles each (MI355X_MICROARCH.md)
@@ -110,18 +145,24 @@ def issue_rates(kernel, units_per_launch, launch_s):
             "unit": "G wave-instructions/s"}
 
 
-def cpu_baseline(frames, n_sample, threads):
-    """Oracle (scalar C restatement, test infrastructure) on host cores."""
+def cpu_baseline(frames, n_sample, threads, cores_how="", distinct=320):
+    """Oracle (scalar C restatement, test infrastructure) on host cores: one
+    image per pool task, as the reference's thread pool of
+    availableProcessors() threads runs processImage (CompressionBatch.java:
+    64-88).  At most `distinct` frames are copied to host memory (25 MB each);
+    a larger sample (many cores) cycles over them."""
     from tests.oracle_ffi import Oracle
     o = Oracle()
-    sample = [f.cpu().numpy() for f in frames[:n_sample]]
+    host = [f.cpu().numpy() for f in frames[:min(n_sample, distinct)]]
+    sample = [host[i % len(host)] for i in range(n_sample)]
     t0 = time.perf_counter()
     enc, sizes, qs, scales = o.fit_batch(sample, TARGET, Q0, cached=(Q0, 1.0), threads=threads)
     dt = time.perf_counter() - t0
     mp = n_sample * W * H / 1e6
     return {"value": round(mp / dt, 3), "unit": "MP/s", "cores": threads, "kind": "port",
-            "sample": f"{n_sample} of the 4K frames ({(n_sample + 1) // 2} smooth, {n_sample // 2} noise), "
-                      f"oracle compressJpgWithTargetSize with cache (0.25, 1.0), -t 1MiB, {threads} threads, "
+            "sample": f"{n_sample} of the 4K frames ({len(host)} distinct: {(len(host) + 1) // 2} smooth, "
+                      f"{len(host) // 2} noise), oracle compressJpgWithTargetSize with cache (0.25, 1.0), -t 1MiB, "
+                      f"{threads} threads = every host core this process may use ({cores_how}), "
                       f"{enc} full encodes, {dt:.2f} s wall"}, sizes
 
 
@@ -250,7 +291,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--images", type=int, default=1000, help="4K frames per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=320, help="4K frames for the CPU baseline (~10 s on 16 cores)")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="4K frames for the CPU baseline (0 = 20 per host core, at least 320: ~10 s of wall time)")
     ap.add_argument("--e2e", type=int, default=200, help="frames of the decode+encode leg (0 = skip)")
     ap.add_argument("--host-io-frames", type=int, default=200,
                     help="frames of the PCIe-inclusive leg (pinned host in/out; 0 = skip)")
@@ -370,19 +412,22 @@ def main():
         batch = None
         line["host_io"] = host_io_leg(codec, frames, min(args.host_io_frames, args.images), args.steps,
                                       args.warmup, cached)
+    cores, cores_how = host_cores()
     if rank == 0 and world == 1 and args.e2e and not args.host_io:
         batch = None
         line["e2e"] = e2e_leg(codec, dev, args.e2e, args.steps,
-                              cpu_sample=0 if args.no_cpu_baseline else 64, threads=min(16, os.cpu_count() or 1))
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        cb, _ = cpu_baseline(frames, args.cpu_sample, threads)
+                              cpu_sample=0 if args.no_cpu_baseline else max(64, 4 * cores), threads=cores)
+    if rank == 0 and not args.no_cpu_baseline:
+        # rank 0 only, after the timed region (the other ranks wait at the
+        # final barrier); at N > 1 the line still carries it
+        cb, _ = cpu_baseline(frames, args.cpu_sample or max(320, 20 * cores), cores, cores_how)
         line["cpu_baseline"] = cb
         line["speedup_vs_cpu"] = round(value / cb["value"], 1)
     if rank == 0:
         print(json.dumps(line), flush=True)
     codec.close()
     if dist:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -494,7 +494,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         int it = 0;
         static const char* const sync_names[] = {"dec_sync", "dec_sync_r1", "dec_sync_r2", "dec_sync_r3",
                                                  "dec_sync_r4", "dec_sync_r5", "dec_sync_r6", "dec_sync_r7+"};
-        static const int SYNC_PER_CHECK = getenv("ICX_DEC_CHECK") ? atoi(getenv("ICX_DEC_CHECK")) : 2;
+        static const int SYNC_PER_CHECK = std::max(1, getenv("ICX_DEC_CHECK") ? atoi(getenv("ICX_DEC_CHECK")) : 2);
         for (;;) {
             for (int k = 0; k < SYNC_PER_CHECK && it < max_it; k++, it++) {
                 Timed tm(c, sync_names[std::min(it, 7)], 0);

@@ -536,7 +536,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
     // computes; downloads of s (io_down) while s+1 computes
     struct HostIO {
         std::vector<uint8_t*> px, out;
-        bool up = false, down = false;
+        bool up = false, down = false, wait = false;
     };
     std::vector<HostIO> hio(subs.size());
     struct IoDrain {  // every exit waits for the copies that touch the caller's buffers
@@ -595,7 +595,14 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                 H.down = true;
             }
         }
-        if (e == hipSuccess && H.up) e = hipEventRecord(c->ev_up[si & 1], c->io_up);
+        // ev_up orders c->stream behind the arena's reuse: behind the uploads,
+        // and (recorded after the wait on ev_down above) behind sub-batch
+        // si-2's downloads from the same arena.  Recorded whenever the arena
+        // is written here at all - a sub-batch with device inputs and host
+        // outputs uploads nothing, but its kernels still overwrite the bytes
+        // si-2's downloads may be reading.
+        H.wait = H.up || H.down;
+        if (e == hipSuccess && H.wait) e = hipEventRecord(c->ev_up[si & 1], c->io_up);
         return e == hipSuccess ? ICX_OK : hip_fail(c, e, "input upload");
     };
     if (icx_status ps = prefetch(0)) return ps;
@@ -755,9 +762,10 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
         if (!B.h_state) return fail(c, ICX_E_NOMEM, "pinned staging exhausted");
         icx_status s = upload(c, B.d_nodes, B.nodes.data(), sizeof(QNode) * B.nodes.size());
         if (s) return s;
-        // this sub-batch's pixels have landed before its first kernel; the
-        // next sub-batch's upload starts behind them on io_up
-        if (hio[si].up && (e = hipStreamWaitEvent(c->stream, c->ev_up[si & 1], 0)) != hipSuccess)
+        // this sub-batch's pixels have landed (and the arena's previous
+        // downloads have drained) before its first kernel; the next
+        // sub-batch's upload starts behind them on io_up
+        if (hio[si].wait && (e = hipStreamWaitEvent(c->stream, c->ev_up[si & 1], 0)) != hipSuccess)
             return hip_fail(c, e, "hipStreamWaitEvent");
         if ((s = prefetch(si + 1))) return s;
 

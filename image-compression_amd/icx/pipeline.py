@@ -86,14 +86,19 @@ def _to_array(im):
         return np.asarray(im, dtype=np.uint8)
     if mode in ("I;16", "I;16B", "I", "F", "1"):
         return np.asarray(im.convert("L"), dtype=np.uint8)
-    if mode in ("LA", "PA") or (mode == "P" and "transparency" in im.info):
+    if mode in ("LA", "PA"):
         # grey+alpha is TYPE_CUSTOM there, drawn into TYPE_INT_ARGB: RGBA out
         # (the JDK's linear-grey -> sRGB conversion of that case is not restated)
         mode, im = "RGBA", im.convert("RGBA")
     if mode == "RGBA":
         return np.ascontiguousarray(np.asarray(im, dtype=np.uint8)[:, :, ::-1])  # TYPE_4BYTE_ABGR
     if mode != "RGB":
-        im = im.convert("RGB")  # CMYK / palette without transparency: approximate
+        # CMYK, and palette PNGs with or without tRNS: the JDK reads a palette
+        # PNG as TYPE_BYTE_INDEXED (TYPE_BYTE_BINARY below 8 bits) and
+        # ImageTools keeps that type, so Java2D re-quantises the resized pixels
+        # to the default colour-cube palette of a new TYPE_BYTE_INDEXED image,
+        # whose transparency is lost.  Here: RGB, an approximation
+        im = im.convert("RGB")
     rgb = np.asarray(im, dtype=np.uint8)
     return np.ascontiguousarray(rgb[:, :, ::-1])  # TYPE_3BYTE_BGR
 

@@ -61,9 +61,10 @@ def main(d, bench_json):
                 for k, v in out.items() if "hbm_bytes_per_unit" in v}
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of: bench.py " +
                      " ".join(sys.argv[3:]), "kernels": out, "bytes_per_unit": per_unit}
+    # the file bench.py reads (profiles/pmc_summary.json is a copy of it, not
+    # of stdout): "bytes_per_unit" maps the bench's kernel names to HBM bytes
     json.dump(res, open(os.path.join(d, "pmc_summary.json"), "w"), indent=1)
-    print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "fetch_x2_per_dispatch"} for k, v in out.items()},
-                     indent=1))
+    print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":

@@ -323,6 +323,19 @@ def test_host_buffers_pipelined_over_subbatches(oracle, monkeypatch):
                     assert np.float32(r["learned"].quality) == np.float32(o["quality"])
                     assert r["learned"].scale == o["scale"]
         assert c.profile_query("subbatch")["launches"] >= 6  # >= 3 sub-batches per call
+        # device inputs, host outputs (the pipeline's decoded frames -> files):
+        # nothing is uploaded, so the kernels of sub-batch s must still wait
+        # for s-2's downloads out of the same staging arena
+        dimgs = [torch.from_numpy(im.numpy() if hasattr(im, "numpy") else im).to("cuda:0") for im in imgs]
+        c.profile_reset()
+        for target in (min(targets), max(targets)):
+            res = c.fit(dimgs, target, 0.25)
+            for i, r in enumerate(res):
+                o = oracle.fit(dimgs[i].cpu().numpy(), target, 0.25)
+                assert r["status"] == 0 and r["success"] == o["success"], (i, target)
+                if o["success"]:
+                    assert r["data"] == o["data"], ("device in / host out", i, target)
+        assert c.profile_query("subbatch")["launches"] >= 6
     finally:
         c.close()
 
