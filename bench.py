@@ -29,6 +29,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import icx  # noqa: E402
+from icx.pipeline import host_cores  # noqa: E402,F401  (the CPU baseline's thread count)
 
 W, H = 3840, 2160
 TARGET = 1 << 20
@@ -101,24 +102,6 @@ def pmc_bytes_per_unit(summary):
             and k.split("::")[-1].split("<")[0] in PMC_SHORT}
 
 
-def host_cores():
-    """Host cores this process may use: the scheduler affinity set, capped by
-    a cgroup CPU quota when one is set (on the GPU box the affinity mask shows
-    the whole machine while the job's share is a quota).  Returns (cores,
-    how it was determined).  The reference sizes its pool the same way:
-    Runtime.availableProcessors() (CompressionBatch.java:64-68), which in a
-    container honours both the affinity mask and the cgroup quota."""
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    how = "sched_getaffinity"
-    try:
-        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        if quota != "max":
-            q = max(1, int(-(-int(quota) // int(period))))
-            if q < n:
-                n, how = q, "cgroup cpu.max quota"
-    except (OSError, ValueError):
-        pass
-    return n, how
 
 
 VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 256 CUs x 4 SIMD-32, 2 cycles each (MI355X_MICROARCH.md)

@@ -22,5 +22,20 @@ void launch_stuff(const ImgDesc* d, const ImgState* s, const QNode* n, const Pla
                   hipStream_t st);
 void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int fmt, uint8_t* dst, int dw,
                    int dh, int dstride, hipStream_t st);
+// Batched resize (icx_png_fit_batch): m descriptors of one pixel format in
+// device memory, prefix = exclusive tile counts (prefix[m] = tiles), uniform
+// = tiles per image when every image has as many (2-D grid), else 0.
+struct ResizeArgs {
+    const uint8_t* src;
+    uint8_t* dst;
+    int32_t sw, sh, sstride, fmt;
+    int32_t dw, dh, dstride, tiles_x;
+    int64_t x0l, dxl, y0l, dyl;  // inverse scale (32.32) and the first pixel centre's source position
+};
+ResizeArgs resize_args(const uint8_t* src, int sw, int sh, int sstride, int fmt, uint8_t* dst, int dw, int dh,
+                       int dstride);
+int64_t resize_tiles(int dw, int dh);
+void launch_resize_batch(int fmt, const ResizeArgs* descs, const int64_t* prefix, int m, int64_t tiles,
+                         int64_t uniform, hipStream_t st);
 
 }  // namespace icx

@@ -846,7 +846,6 @@ __global__ __launch_bounds__(CHUNK_BLOCKS, 8) void k_huff(const ImgDesc* __restr
     uint32_t* const s_out = s_tab;
     __shared__ uint32_t s_off[CHUNK_BLOCKS + 1];
     __shared__ uint32_t s_bits[CHUNK_BLOCKS];
-    int32_t* const s_dcq = (int32_t*)s_bits;  // DC exchange; dead before s_bits is written
     __shared__ uint32_t s_wsum[CHUNK_BLOCKS / 64];
 
     // 2-D launch (every image of the plan has as many chunks): slot = y, in
@@ -883,9 +882,14 @@ __global__ __launch_bounds__(CHUNK_BLOCKS, 8) void k_huff(const ImgDesc* __restr
     // even before the image's state says whether it is still searching);
     // then, once the tables are in LDS, the list itself and the predictor's
     // DC entry (the list groups are loaded unconditionally, see load_group).
-    // A DC predictor in the previous chunk (the chunk's first blocks): its
-    // list offset and DC entry are fetched alongside this block's own.
-    const bool ext_prev = pb >= 0 && pb < b0;
+    // The DC predictor (the previous block of the same component: 1, 3 or 6
+    // blocks back) of most blocks is coded by a lane of the same wave, which
+    // hands its quantised DC over by ds_bpermute - no workgroup barrier.  A
+    // predecessor in another wave or in the previous chunk (a wave's first
+    // lanes): its list offset and DC entry are fetched alongside this block's
+    // own, and its DC quantised here.
+    const bool in_wave = pb >= b0 && (int)(pb - b0) >= (t & ~63);
+    const bool ext_prev = valid && pb >= 0 && !in_wave;  // (a lane past the chunk's blocks reads nothing)
     const GAS uint32_t* coff = gp(D.coff);
     const int cnt = valid ? (int)gp(D.ncoef)[b] : 0;
     const uint32_t my_off = coff[valid ? b : b0];
@@ -913,10 +917,9 @@ __global__ __launch_bounds__(CHUNK_BLOCKS, 8) void k_huff(const ImgDesc* __restr
 
     const float2 q0t = s_qf[tb][0];
     const int dq = quant((int)__uint_as_float(ev[0] & ~0x3FFu), q0t.x, q0t.y);
-    s_dcq[t] = dq;
-    __syncthreads();
+    const int from = __builtin_amdgcn_ds_bpermute((in_wave ? (int)(pb - b0) & 63 : lane) << 2, dq);
     int qprev = 0;
-    if (pb >= b0) qprev = s_dcq[pb - b0];
+    if (in_wave) qprev = from;
     else if (ext_prev) qprev = quant((int)__uint_as_float((uint32_t)prev_dc_raw & ~0x3FFu), q0t.x, q0t.y);
 
     // ---- 1. encode_one_block into the slot (rarely: into the block's HBM spill)
@@ -1369,70 +1372,48 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
 // ImageTools.resizeImage -> Graphics2D.drawImage(BILINEAR) -> Java2D
 // TransformHelper: inverse scale in 32.32 fixed point, source sample at the
 // pixel centre minus 0.5, edges clamped, 8-bit fraction weights, rounding at
-// bit 16 (BilinearInterp).  One thread per destination pixel.
-struct ResizeArgs {
-    const uint8_t* src;
-    uint8_t* dst;
-    int32_t sw, sh, sstride, nch;
-    int32_t dw, dh, dstride, pad;
-    int64_t x0l, dxl, y0l, dyl;
-};
+// bit 16 (BilinearInterp).
+//
+// One workgroup = a tile of 64 x 16 destination pixels (4 per thread, one
+// wave per destination row).  The source rectangle the tile's taps touch
+// (monotone in x and y, so the taps of its corner pixels bound it) is staged
+// in LDS first, by 16-B loads of whole rows - coalesced, each source byte
+// fetched once per tile however many taps read it - and the taps are then
+// LDS reads.  A tile whose rectangle does not fit (scales below ~0.2, where
+// the taps skip most of the source anyway) reads its taps from global memory
+// instead.  Several images share one launch (icx_png_fit_batch): a 2-D grid
+// (x = tile, y = image) when they have as many tiles, else a slot search.
+//
+// Pixel classes: BPP 1 (grey), 3 (BGR / RGB: channel order does not
+// matter), 2 (TYPE_USHORT_GRAY: Java2D's UshortGray loops fetch gray >> 8
+// into IntArgbPre, interpolate in 8 bits and store ComposeUshortGrayFrom3-
+// ByteRgb(g, g, g) = (19672 + 38621 + 7500) g >> 8 = 257 g), 4 (four-byte
+// rasters, below).
+constexpr int RS_TW = 64, RS_TH = 16;  // destination tile
+constexpr int RS_LDS = 24576;          // source rectangle staging: 6 workgroups per CU
 
-__global__ __launch_bounds__(256) void k_resize(ResizeArgs a)
+__device__ __forceinline__ int bilerp(int p00, int p01, int p10, int p11, int xf, int yf)
 {
-    const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (dx >= a.dw || dy >= a.dh) return;
-    const int64_t half = (int64_t)1 << 31;
-    const int64_t yl = a.y0l + (int64_t)dy * a.dyl - half;
-    const int64_t xl = a.x0l + (int64_t)dx * a.dxl - half;
-    const int yw = (int)(yl >> 32), xw = (int)(xl >> 32);
-    const int yf = (int)((uint32_t)yl >> 24), xf = (int)((uint32_t)xl >> 24);
-    int ya, yb, xa, xb;
-    if (yw < 0) ya = yb = 0; else if (yw + 1 >= a.sh) ya = yb = yw; else { ya = yw; yb = yw + 1; }
-    if (xw < 0) xa = xb = 0; else if (xw + 1 >= a.sw) xa = xb = xw; else { xa = xw; xb = xw + 1; }
-    const uint8_t* ra = a.src + (size_t)ya * a.sstride;
-    const uint8_t* rb = a.src + (size_t)yb * a.sstride;
-    uint8_t* o = a.dst + (size_t)dy * a.dstride + (size_t)dx * a.nch;
-    for (int c = 0; c < a.nch; c++) {
-        int p00 = ra[a.nch * xa + c], p01 = ra[a.nch * xb + c];
-        int p10 = rb[a.nch * xa + c], p11 = rb[a.nch * xb + c];
-        int top = (p00 << 8) + (p01 - p00) * xf;
-        int bot = (p10 << 8) + (p11 - p10) * xf;
-        int v = (top << 8) + (bot - top) * yf;
-        o[c] = (uint8_t)((v + (1 << 15)) >> 16);
-    }
+    const int top = (p00 << 8) + (p01 - p00) * xf;
+    const int bot = (p10 << 8) + (p11 - p10) * xf;
+    return ((top << 8) + (bot - top) * yf + (1 << 15)) >> 16;
 }
 
 // Four-byte pixels (ImageTools.java:12-15 keeps the source type): Java2D's
 // TransformHelper fetches the four neighbours as IntArgbPre (colours times
 // alpha through AlphaMath's mul8table; an opaque type's alpha is 0xff),
-// interpolates the four channels like k_resize, and the SrcOver mask blit onto
-// the new all-zero image stores alpha 0 as a zero pixel, alpha 0xff as is,
-// else un-premultiplies through div8table.  XRGB (TYPE_INT_RGB) stores 0 in
-// its unused byte.  AB = alpha byte (0: ABGR, 3: BGRA / RGBA).
+// interpolates the four channels, and the SrcOver mask blit onto the new
+// all-zero image stores alpha 0 as a zero pixel, alpha 0xff as is, else
+// un-premultiplies through div8table.  XRGB (TYPE_INT_RGB) stores 0 in its
+// unused byte.  AB = alpha byte (0: ABGR, 3: BGRA / RGBA).
 __device__ __forceinline__ uint32_t mul8(uint32_t a, uint32_t c)  // AlphaMath.c mul8table[a][c]
 {
     return ((c * (a * 0x010101u) + (1u << 23)) >> 24) & 0xffu;
 }
 
 template <int AB, bool OPAQUE>
-__global__ __launch_bounds__(256) void k_resize4(ResizeArgs a)
+__device__ __forceinline__ uint32_t bilerp4(const uint32_t (&p)[4], int xf, int yf)
 {
-    const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (dx >= a.dw || dy >= a.dh) return;
-    const int64_t half = (int64_t)1 << 31;
-    const int64_t yl = a.y0l + (int64_t)dy * a.dyl - half;
-    const int64_t xl = a.x0l + (int64_t)dx * a.dxl - half;
-    const int yw = (int)(yl >> 32), xw = (int)(xl >> 32);
-    const int yf = (int)((uint32_t)yl >> 24), xf = (int)((uint32_t)xl >> 24);
-    int ya, yb, xa, xb;
-    if (yw < 0) ya = yb = 0; else if (yw + 1 >= a.sh) ya = yb = yw; else { ya = yw; yb = yw + 1; }
-    if (xw < 0) xa = xb = 0; else if (xw + 1 >= a.sw) xa = xb = xw; else { xa = xw; xb = xw + 1; }
-    const GAS uint32_t* ra = (const GAS uint32_t*)(a.src + (size_t)ya * a.sstride);
-    const GAS uint32_t* rb = (const GAS uint32_t*)(a.src + (size_t)yb * a.sstride);
-    const uint32_t p[4] = {ra[xa], ra[xb], rb[xa], rb[xb]};
     uint32_t pre[4][4];
 #pragma unroll
     for (int s = 0; s < 4; s++) {
@@ -1442,11 +1423,7 @@ __global__ __launch_bounds__(256) void k_resize4(ResizeArgs a)
     }
     int v[4];
 #pragma unroll
-    for (int b = 0; b < 4; b++) {
-        const int top = ((int)pre[0][b] << 8) + ((int)pre[1][b] - (int)pre[0][b]) * xf;
-        const int bot = ((int)pre[2][b] << 8) + ((int)pre[3][b] - (int)pre[2][b]) * xf;
-        v[b] = (((top << 8) + (bot - top) * yf) + (1 << 15)) >> 16;
-    }
+    for (int b = 0; b < 4; b++) v[b] = bilerp(pre[0][b], pre[1][b], pre[2][b], pre[3][b], xf, yf);
     const uint32_t al = (uint32_t)v[AB];
     uint32_t out = 0;
     if (OPAQUE) {
@@ -1464,7 +1441,137 @@ __global__ __launch_bounds__(256) void k_resize4(ResizeArgs a)
             out |= d << (8 * b);
         }
     }
-    *(GAS uint32_t*)(a.dst + (size_t)dy * a.dstride + (size_t)dx * 4) = out;
+    return out;
+}
+
+// The four taps of destination pixel (dx, dy): rows ya, yb, columns xa, xb,
+// 8-bit fractions xf, yf.
+struct Taps {
+    int ya, yb, xa, xb, xf, yf;
+};
+__device__ __forceinline__ void tap_x(const ResizeArgs& a, int dx, int& xa, int& xb, int& xf)
+{
+    const int64_t xl = a.x0l + (int64_t)dx * a.dxl - ((int64_t)1 << 31);
+    const int xw = (int)(xl >> 32);
+    xf = (int)((uint32_t)xl >> 24);
+    if (xw < 0) xa = xb = 0; else if (xw + 1 >= a.sw) xa = xb = xw; else { xa = xw; xb = xw + 1; }
+}
+__device__ __forceinline__ void tap_y(const ResizeArgs& a, int dy, int& ya, int& yb, int& yf)
+{
+    const int64_t yl = a.y0l + (int64_t)dy * a.dyl - ((int64_t)1 << 31);
+    const int yw = (int)(yl >> 32);
+    yf = (int)((uint32_t)yl >> 24);
+    if (yw < 0) ya = yb = 0; else if (yw + 1 >= a.sh) ya = yb = yw; else { ya = yw; yb = yw + 1; }
+}
+
+// A source sample of type T at byte address p: LDS (L) or global memory.
+#define LAS __attribute__((address_space(3)))
+template <class T, bool L>
+__device__ __forceinline__ uint32_t ldx(const uint8_t* p)
+{
+    if constexpr (L) return *(const LAS T*)p;
+    else return *(const GAS T*)p;
+}
+
+// One destination pixel from the rows ra / rb (addresses of source pixel 0
+// of rows ya / yb: global memory, or LDS rebased so that the same x indexes
+// it), stored at o.
+template <int BPP, int AB, bool OPQ, bool L>
+__device__ __forceinline__ void resize_px(const uint8_t* ra, const uint8_t* rb, int xa, int xb, int xf, int yf,
+                                          uint8_t* o)
+{
+    if constexpr (BPP == 4) {
+        const uint32_t p[4] = {ldx<uint32_t, L>(ra + 4 * xa), ldx<uint32_t, L>(ra + 4 * xb),
+                               ldx<uint32_t, L>(rb + 4 * xa), ldx<uint32_t, L>(rb + 4 * xb)};
+        *(GAS uint32_t*)o = bilerp4<AB, OPQ>(p, xf, yf);
+    } else if constexpr (BPP == 2) {
+        const int v = bilerp(ldx<uint16_t, L>(ra + 2 * xa) >> 8, ldx<uint16_t, L>(ra + 2 * xb) >> 8,
+                             ldx<uint16_t, L>(rb + 2 * xa) >> 8, ldx<uint16_t, L>(rb + 2 * xb) >> 8, xf, yf);
+        *(GAS uint16_t*)o = (uint16_t)(v * 257);
+    } else {
+#pragma unroll
+        for (int c = 0; c < BPP; c++)
+            ((GAS uint8_t*)o)[c] = (uint8_t)bilerp(ldx<uint8_t, L>(ra + BPP * xa + c), ldx<uint8_t, L>(ra + BPP * xb + c),
+                                                   ldx<uint8_t, L>(rb + BPP * xa + c), ldx<uint8_t, L>(rb + BPP * xb + c),
+                                                   xf, yf);
+    }
+}
+
+template <int BPP, int AB, bool OPQ>
+__global__ __launch_bounds__(256) void k_resize(ResizeArgs one, const ResizeArgs* __restrict__ descs,
+                                                const int64_t* __restrict__ prefix, int m)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[RS_LDS];
+    int64_t tile;
+    ResizeArgs a;
+    if (descs) {
+        const int slot = gridDim.y > 1 ? (int)blockIdx.y : find_slot(prefix, m, blockIdx.x);
+        a = descs[slot];
+        tile = gridDim.y > 1 ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - prefix[slot];
+    } else {
+        a = one;
+        tile = blockIdx.x;
+    }
+    const int ty = (int)(tile / a.tiles_x), tx = (int)(tile - (int64_t)ty * a.tiles_x);
+    const int dx0 = tx * RS_TW, dy0 = ty * RS_TH;
+    const int dxe = min(dx0 + RS_TW, a.dw) - 1, dye = min(dy0 + RS_TH, a.dh) - 1;
+    if (dy0 >= a.dh) return;
+    // the tile's source rectangle: columns bx0..bx1, rows by0..by1 (wave-uniform)
+    int bx0, bx1, by0, by1, u0, u1;
+    tap_x(a, dx0, bx0, u0, u1);
+    tap_x(a, dxe, u0, bx1, u1);
+    tap_y(a, dy0, by0, u0, u1);
+    tap_y(a, dye, u0, by1, u1);
+    const int n16 = (((bx1 - bx0 + 1) * BPP + 15) >> 4) + 1;  // 16-B pieces per staged row (any alignment)
+    const int nrows = by1 - by0 + 1;
+    const bool staged = n16 <= 64 && nrows * n16 * 16 <= RS_LDS;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int dx = dx0 + lane;
+    int xa, xb, xf;
+    tap_x(a, min(dx, a.dw - 1), xa, xb, xf);
+    if (staged) {
+        const int lstr = n16 * 16;
+        // rows per wave pass: lanes split into 64 / n16p groups of n16p (power of two >= n16)
+        const int n16p = n16 <= 1 ? 1 : 1 << (32 - __clz(n16 - 1));
+        const int rpp = 64 / n16p, sub = lane / n16p, k = lane & (n16p - 1);
+        for (int r0 = wave * rpp; r0 < nrows; r0 += 4 * rpp) {
+            const int r = r0 + sub;
+            if (r < nrows && k < n16) {
+                const uint8_t* row = a.src + (size_t)(by0 + r) * a.sstride;
+                const uintptr_t s0 = (uintptr_t)(row + (size_t)bx0 * BPP) & ~(uintptr_t)15;
+                const uintptr_t e = ((uintptr_t)(row + (size_t)(bx1 + 1) * BPP) + 15) & ~(uintptr_t)15;
+                // whole 16-B granules holding the row's bytes: never past the page the bytes are on
+                if (s0 + 16 * (uintptr_t)k < e) *(uint4*)&lds[r * lstr + 16 * k] = ld16((const void*)(s0 + 16 * k));
+            }
+        }
+        __syncthreads();
+        if (dx > dxe) return;
+#pragma unroll
+        for (int q = 0; q < RS_TH / 4; q++) {
+            const int dy = dy0 + wave + 4 * q;
+            if (dy > dye) break;
+            int ya, yb, yf;
+            tap_y(a, dy, ya, yb, yf);
+            // LDS row of source row y, rebased to its pixel 0: offset of pixel bx0 in its granule
+            auto lrow = [&](int y) -> const uint8_t* {
+                const uint32_t mis = ((uint32_t)(uintptr_t)a.src + (uint32_t)y * (uint32_t)a.sstride +
+                                      (uint32_t)(bx0 * BPP)) & 15u;
+                return &lds[(y - by0) * lstr + mis] - (ptrdiff_t)bx0 * BPP;
+            };
+            resize_px<BPP, AB, OPQ, true>(lrow(ya), lrow(yb), xa, xb, xf, yf,
+                                    a.dst + (size_t)dy * a.dstride + (size_t)dx * BPP);
+        }
+    } else {
+        if (dx > dxe) return;
+        for (int q = 0; q < RS_TH / 4; q++) {
+            const int dy = dy0 + wave + 4 * q;
+            if (dy > dye) break;
+            int ya, yb, yf;
+            tap_y(a, dy, ya, yb, yf);
+            resize_px<BPP, AB, OPQ, false>(a.src + (size_t)ya * a.sstride, a.src + (size_t)yb * a.sstride, xa, xb,
+                                           xf, yf, a.dst + (size_t)dy * a.dstride + (size_t)dx * BPP);
+        }
+    }
 }
 
 // =================================================================== host side
@@ -1550,27 +1657,54 @@ void launch_stuff(const ImgDesc* d, const ImgState* s, const QNode* n, const Pla
     ICX_LAUNCH(k_stuff, grid, dim3(256), 0, st, d, s, n, plan_ids(p), p.prefix, p.m);
 }
 
-void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int fmt, uint8_t* dst, int dw, int dh,
-                   int dstride, hipStream_t st)
+// AffineTransform.scale(dw/sw, dh/sh).createInverse(): m00 = 1.0 / (dw/sw);
+// the first pixel centre (0.5) maps to 0.5 * m00.
+ResizeArgs resize_args(const uint8_t* src, int sw, int sh, int sstride, int fmt, uint8_t* dst, int dw, int dh,
+                       int dstride)
 {
     ResizeArgs a;
     a.src = src; a.dst = dst;
-    a.sw = sw; a.sh = sh; a.sstride = sstride; a.nch = fmt == ICX_GRAY8 ? 1 : fmt <= ICX_RGB24 ? 3 : 4;
-    a.dw = dw; a.dh = dh; a.dstride = dstride; a.pad = 0;
-    // AffineTransform.scale(dw/sw, dh/sh).createInverse(): m00 = 1.0 / (dw/sw)
+    a.sw = sw; a.sh = sh; a.sstride = sstride; a.fmt = fmt;
+    a.dw = dw; a.dh = dh; a.dstride = dstride;
+    a.tiles_x = (int32_t)grid_of(dw, RS_TW);
     const double ix = 1.0 / ((double)dw / sw), iy = 1.0 / ((double)dh / sh);
     a.dxl = (int64_t)(ix * 4294967296.0);
     a.dyl = (int64_t)(iy * 4294967296.0);
-    a.x0l = (int64_t)(0.5 * ix * 4294967296.0);  // transform of the first pixel centre (0.5)
+    a.x0l = (int64_t)(0.5 * ix * 4294967296.0);
     a.y0l = (int64_t)(0.5 * iy * 4294967296.0);
-    const dim3 grid(grid_of(dw, 64), grid_of(dh, 4));
+    return a;
+}
+
+int64_t resize_tiles(int dw, int dh) { return (int64_t)grid_of(dw, RS_TW) * grid_of(dh, RS_TH); }
+
+// one image (descs == nullptr: `one` by value) or a batch of same-format images
+static void launch_resize_fmt(int fmt, const ResizeArgs& one, const ResizeArgs* descs, const int64_t* prefix, int m,
+                              dim3 grid, hipStream_t st)
+{
     switch (fmt) {
-    case ICX_XRGB32: ICX_LAUNCH((k_resize4<3, true>), grid, dim3(256), 0, st, a); break;
+    case ICX_GRAY8: ICX_LAUNCH((k_resize<1, 0, true>), grid, dim3(256), 0, st, one, descs, prefix, m); break;
+    case ICX_GRAY16: ICX_LAUNCH((k_resize<2, 0, true>), grid, dim3(256), 0, st, one, descs, prefix, m); break;
+    case ICX_XRGB32: ICX_LAUNCH((k_resize<4, 3, true>), grid, dim3(256), 0, st, one, descs, prefix, m); break;
     case ICX_ARGB32:
-    case ICX_RGBA32: ICX_LAUNCH((k_resize4<3, false>), grid, dim3(256), 0, st, a); break;
-    case ICX_ABGR32: ICX_LAUNCH((k_resize4<0, false>), grid, dim3(256), 0, st, a); break;
-    default: ICX_LAUNCH(k_resize, grid, dim3(256), 0, st, a);
+    case ICX_RGBA32: ICX_LAUNCH((k_resize<4, 3, false>), grid, dim3(256), 0, st, one, descs, prefix, m); break;
+    case ICX_ABGR32: ICX_LAUNCH((k_resize<4, 0, false>), grid, dim3(256), 0, st, one, descs, prefix, m); break;
+    default: ICX_LAUNCH((k_resize<3, 0, true>), grid, dim3(256), 0, st, one, descs, prefix, m);
     }
+}
+
+void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int fmt, uint8_t* dst, int dw, int dh,
+                   int dstride, hipStream_t st)
+{
+    const ResizeArgs a = resize_args(src, sw, sh, sstride, fmt, dst, dw, dh, dstride);
+    launch_resize_fmt(fmt, a, nullptr, nullptr, 1, dim3((unsigned)resize_tiles(dw, dh)), st);
+}
+
+void launch_resize_batch(int fmt, const ResizeArgs* descs, const int64_t* prefix, int m, int64_t tiles,
+                         int64_t uniform, hipStream_t st)
+{
+    if (tiles <= 0) return;
+    const dim3 grid = uniform > 0 && m > 1 ? dim3((unsigned)uniform, (unsigned)m) : dim3((unsigned)tiles);
+    launch_resize_fmt(fmt, ResizeArgs{}, descs, prefix, m, grid, st);
 }
 
 }  // namespace icx

@@ -1,19 +1,31 @@
 // icx_png.cpp — the PNG write of the PNG path, native (host threads).
 //
 // Reference: ImageCompressionPng.java:70, ImageIO.write(resized, "png", file)
-// -> the JDK PNGImageWriter: per row an adaptive filter (None, Sub, Up,
-// Average, Paeth) and one zlib stream.  The writer's exact heuristic and
-// deflate settings are not pinnable here (no JDK): parity is
-// on decoded pixels and dimensions, and the filter choice is the one of the
-// previous Python writer (tests/png_ref.py): the least sum of |residual byte
-// read as signed|, ties to the lower filter type.
+// -> the JDK PNGImageWriter (OpenJDK 21 java.desktop, not in /root/reference;
+// restated here from its published source, unverifiable offline: SURVEY.md
+// §8c).  What is restated:
+//   - RowFilter.filterRow: the five filters of each row are costed over the
+//     row's bytes in PNG sample order with the bytesPerPixel bytes left of the
+//     row and the previous row of the first row reading as zero.  None costs
+//     the sum of the unsigned bytes; Sub, Up, Average and Paeth the sum of
+//     |curr - predictor| as ints (the unwrapped difference, not the residual
+//     byte); the first strictly smaller cost wins (ties keep the lower type);
+//   - PNGImageWriter's default deflate level, 4 (DEFAULT_COMPRESSION_LEVEL),
+//     one zlib stream (java.util.zip.Deflater: zlib's default strategy,
+//     window and memory level);
+//   - IDATOutputStream: the stream is cut into IDAT chunks of 32768 bytes
+//     (the last one shorter).
+// The deflate bytes also depend on the JDK's zlib build, so PNG parity is on
+// decoded pixels, dimensions, colour type and bit depth, with the filter
+// choice pinned row for row against tests/png_ref.py.
 //
-// Output colour type follows the raster: GRAY8 -> 0 (grey), BGR24 / RGB24 /
-// XRGB32 -> 2 (RGB), ARGB32 / ABGR32 / RGBA32 -> 6 (RGBA), 8 bits per sample,
-// no interlace.  Rows are converted, filtered and deflated one at a time
-// (three row buffers), straight into the caller's buffer: no image-sized
-// temporary.  The caller's thread does the work; ctypes releases the GIL, so
-// the batch driver's writer pool runs one image per thread.
+// Output colour type follows the raster: GRAY8 -> 0 (grey, 8 bits), GRAY16
+// -> 0 (grey, 16 bits, TYPE_USHORT_GRAY), BGR24 / RGB24 / XRGB32 -> 2 (RGB),
+// ARGB32 / ABGR32 / RGBA32 -> 6 (RGBA), no interlace.  Rows are converted,
+// filtered and deflated one at a time (three row buffers), straight into the
+// caller's buffer: no image-sized temporary.  The caller's thread does the
+// work; ctypes releases the GIL, so the batch driver's writer pool runs one
+// image per thread.
 #include <zlib.h>
 
 #include <algorithm>
@@ -25,22 +37,27 @@
 
 namespace {
 
-int png_channels(int fmt)
+// Bytes per pixel of the PNG row (RowFilter's bytesPerPixel) and of the source.
+int png_bpp(int fmt)
 {
     switch (fmt) {
     case ICX_GRAY8: return 1;
+    case ICX_GRAY16: return 2;
     case ICX_BGR24: case ICX_RGB24: case ICX_XRGB32: return 3;
     default: return 4;
     }
 }
 
-int src_channels(int fmt) { return fmt == ICX_GRAY8 ? 1 : fmt <= ICX_RGB24 ? 3 : 4; }
+int src_bpp(int fmt) { return fmt == ICX_GRAY8 ? 1 : fmt == ICX_GRAY16 ? 2 : fmt <= ICX_RGB24 ? 3 : 4; }
 
 // Source row -> PNG sample order (R, G, B[, A] or grey).
 void convert_row(const uint8_t* s, int w, int fmt, uint8_t* d)
 {
     switch (fmt) {
     case ICX_GRAY8: memcpy(d, s, (size_t)w); break;
+    case ICX_GRAY16:  // native-endian (little) uint16 -> big-endian PNG samples
+        for (int x = 0; x < w; x++) { d[2 * x] = s[2 * x + 1]; d[2 * x + 1] = s[2 * x]; }
+        break;
     case ICX_RGB24: memcpy(d, s, (size_t)w * 3); break;
     case ICX_RGBA32: memcpy(d, s, (size_t)w * 4); break;
     case ICX_BGR24:
@@ -68,19 +85,19 @@ inline int paeth(int a, int b, int c)
     return (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
 }
 
-// Filters `cur` (prev: the previous raw row, zeros for the first) into
-// out[0] = type, out[1..n] = residuals.
+// RowFilter.filterRow: filters `cur` (prev: the previous row in PNG sample
+// order, zeros for the first) into out[0] = type, out[1..n] = residuals.
 void filter_row(const uint8_t* cur, const uint8_t* prev, int n, int bpp, uint8_t* out)
 {
-    // costs of all five filters in one pass
+    // the badness of all five filters in one pass
     long cost[5] = {0, 0, 0, 0, 0};
     for (int i = 0; i < n; i++) {
         const int x = cur[i], a = i >= bpp ? cur[i - bpp] : 0, b = prev[i], c = i >= bpp ? prev[i - bpp] : 0;
-        cost[0] += std::abs((int)(int8_t)(uint8_t)x);
-        cost[1] += std::abs((int)(int8_t)(uint8_t)(x - a));
-        cost[2] += std::abs((int)(int8_t)(uint8_t)(x - b));
-        cost[3] += std::abs((int)(int8_t)(uint8_t)(x - ((a + b) >> 1)));
-        cost[4] += std::abs((int)(int8_t)(uint8_t)(x - paeth(a, b, c)));
+        cost[0] += x;                           // None: the unsigned bytes themselves
+        cost[1] += std::abs(x - a);             // the others: |curr - predictor| as ints
+        cost[2] += std::abs(x - b);
+        cost[3] += std::abs(x - ((a + b) >> 1));
+        cost[4] += std::abs(x - paeth(a, b, c));
     }
     int best = 0;
     for (int f = 1; f < 5; f++)
@@ -119,68 +136,92 @@ size_t close_chunk(uint8_t* p, const char* tag, size_t len)
 
 extern "C" {
 
-// One IDAT chunk holds the whole zlib stream: raw (filtered) data up to 1 GiB.
+// The whole filtered image (raw bytes) up to 1 GiB: zlib's 32-bit counters.
 constexpr size_t kMaxRaw = (size_t)1 << 30;
+constexpr size_t kIdat = 32768;  // IDATOutputStream chunk length
+constexpr int kDefaultLevel = 4; // PNGImageWriter.DEFAULT_COMPRESSION_LEVEL
 
 size_t icx_png_bound(const icx_image* img)
 {
     if (!img || img->width <= 0 || img->height <= 0) return 0;
-    const size_t raw = (size_t)img->height * ((size_t)img->width * png_channels(img->fmt) + 1);
+    const size_t raw = (size_t)img->height * ((size_t)img->width * png_bpp(img->fmt) + 1);
     if (raw > kMaxRaw) return 0;
-    return 8 + 25 + 12 + (size_t)compressBound((uLong)raw) + 12 + 64;
+    const size_t z = (size_t)compressBound((uLong)raw);
+    return 8 + 25 + z + 12 * (z / kIdat + 1) + 12 + 64;
 }
 
 icx_status icx_png_encode(const icx_image* img, int32_t level, uint8_t* out, size_t cap, size_t* out_len)
 {
     if (!img || !img->px || !out || !out_len) return ICX_E_NULL;
-    if (img->width <= 0 || img->height <= 0 || img->fmt < ICX_BGR24 || img->fmt > ICX_RGBA32 ||
-        img->stride < img->width * src_channels(img->fmt) || level < -1 || level > 9)
+    if (img->width <= 0 || img->height <= 0 || img->fmt < ICX_BGR24 || img->fmt > ICX_GRAY16 ||
+        img->stride < img->width * src_bpp(img->fmt) || level < -1 || level > 9)
         return ICX_E_INVALID;
     if (icx::is_device_ptr(img->px)) return ICX_E_INVALID;  // host rows only
     const size_t need = icx_png_bound(img);
     if (need == 0) return ICX_E_UNSUPPORTED;  // over kMaxRaw
     *out_len = need;
     if (cap < need) return ICX_E_BUFFER;
-    const int ch = png_channels(img->fmt);
-    const int n = img->width * ch;
+    const int bpp = png_bpp(img->fmt);
+    const int n = img->width * bpp;
     static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
     memcpy(out, sig, 8);
     size_t pos = 8;
     uint8_t* ih = out + pos + 8;
     put32(ih, (uint32_t)img->width);
     put32(ih + 4, (uint32_t)img->height);
-    ih[8] = 8;                                         // bit depth
-    ih[9] = (uint8_t)(ch == 1 ? 0 : ch == 3 ? 2 : 6);  // colour type
-    ih[10] = ih[11] = ih[12] = 0;                      // deflate, adaptive filtering, no interlace
+    ih[8] = img->fmt == ICX_GRAY16 ? 16 : 8;                  // bit depth
+    ih[9] = (uint8_t)(bpp <= 2 ? 0 : bpp == 3 ? 2 : 6);      // colour type
+    ih[10] = ih[11] = ih[12] = 0;                             // deflate, adaptive filtering, no interlace
     pos += close_chunk(out + pos, "IHDR", 13);
 
     z_stream z{};
-    if (deflateInit(&z, level) != Z_OK) return ICX_E_NOMEM;
+    if (deflateInit(&z, level < 0 ? kDefaultLevel : level) != Z_OK) return ICX_E_NOMEM;
     std::vector<uint8_t> rows(3 * (size_t)n + 1);
     uint8_t *cur = rows.data(), *prev = cur + n, *filt = prev + n;
     memset(prev, 0, (size_t)n);
+    // deflate straight into IDAT chunks of kIdat data bytes: a full chunk is
+    // closed (length, tag, CRC) and the next one opened behind it
     uint8_t* idat = out + pos;
+    // this chunk's data capacity: kIdat, or less when the caller's buffer ends
+    // first (then a full chunk means the buffer is exhausted)
+    auto room = [&](size_t at) -> size_t { return cap > at + 32 ? std::min(kIdat, cap - at - 32) : 0; };
+    size_t ccap = room(pos);
     z.next_out = idat + 8;
-    z.avail_out = (uInt)std::min<size_t>(cap - pos - 8 - 12 - 12, 0xFFFFFFFFu);
+    z.avail_out = (uInt)ccap;
     int zr = Z_OK;
     bool finished = false;
     for (int y = 0; y < img->height && zr == Z_OK; y++) {
         convert_row(img->px + (size_t)y * img->stride, img->width, img->fmt, cur);
-        filter_row(cur, prev, n, ch, filt);
+        filter_row(cur, prev, n, bpp, filt);
         z.next_in = filt;
         z.avail_in = (uInt)n + 1;
-        zr = deflate(&z, y + 1 == img->height ? Z_FINISH : Z_NO_FLUSH);
-        if (zr == Z_STREAM_END) {
-            finished = true;
+        const int flush = y + 1 == img->height ? Z_FINISH : Z_NO_FLUSH;
+        for (;;) {
+            zr = deflate(&z, flush);
+            if (zr == Z_STREAM_END) {
+                finished = true;
+                zr = Z_OK;
+                break;
+            }
+            if (zr != Z_OK && zr != Z_BUF_ERROR) break;
             zr = Z_OK;
+            if (z.avail_out > 0) break;  // input consumed (NO_FLUSH) - next row
+            // chunk full: close it, open the next one
+            if (ccap < kIdat) { zr = Z_BUF_ERROR; break; }
+            pos += close_chunk(idat, "IDAT", kIdat);
+            idat = out + pos;
+            ccap = room(pos);
+            if (ccap == 0) { zr = Z_BUF_ERROR; break; }
+            z.next_out = idat + 8;
+            z.avail_out = (uInt)ccap;
         }
         std::swap(cur, prev);
     }
-    const size_t zlen = z.total_out;
-    const bool ok = finished && z.avail_in == 0;
+    const size_t last = ccap - z.avail_out;
+    const bool ok = finished && z.avail_in == 0 && zr == Z_OK;
     deflateEnd(&z);
     if (!ok) return ICX_E_BUFFER;
-    pos += close_chunk(idat, "IDAT", zlen);
+    if (last > 0) pos += close_chunk(idat, "IDAT", last);
     pos += close_chunk(out + pos, "IEND", 0);
     *out_len = pos;
     return ICX_OK;

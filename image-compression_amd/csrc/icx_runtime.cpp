@@ -142,7 +142,8 @@ int build_tree(float lo, float hi, int iter, std::vector<QNode>& nodes, int& dep
     return idx;
 }
 
-int channels(int fmt) { return fmt == ICX_GRAY8 ? 1 : fmt <= ICX_RGB24 ? 3 : 4; }
+// bytes per pixel of a raster (GRAY16: one 2-byte sample)
+int channels(int fmt) { return fmt == ICX_GRAY8 ? 1 : fmt == ICX_GRAY16 ? 2 : fmt <= ICX_RGB24 ? 3 : 4; }
 
 void geometry(ImgDesc& d, int w, int h, int fmt)
 {
@@ -448,9 +449,10 @@ icx_status validate(const icx_image* img)
 {
     if (!img || !img->px) return ICX_E_NULL;
     if (img->width <= 0 || img->height <= 0 || img->width > 65535 || img->height > 65535) return ICX_E_INVALID;
-    if (img->fmt < ICX_BGR24 || img->fmt > ICX_RGBA32) return ICX_E_INVALID;
+    if (img->fmt < ICX_BGR24 || img->fmt > ICX_GRAY16) return ICX_E_INVALID;
     if (img->stride < img->width * channels(img->fmt)) return ICX_E_INVALID;
     if (channels(img->fmt) == 4 && (((uintptr_t)img->px | (uintptr_t)img->stride) & 3)) return ICX_E_INVALID;
+    if (channels(img->fmt) == 2 && (((uintptr_t)img->px | (uintptr_t)img->stride) & 1)) return ICX_E_INVALID;
     return ICX_OK;
 }
 
@@ -1186,6 +1188,25 @@ icx_status icx_debug_fdct(icx_ctx* ctx, const icx_image* img, int16_t* coefs, si
     return s ? s : j.status;
 }
 
+// Source pixels the bilinear taps of a w -> dw resize read along one axis
+// (the algorithmic read bytes of k_resize: each touched pixel once).
+static int64_t touched(int sw, int dw, int64_t x0l, int64_t dxl)
+{
+    int64_t n = 0;
+    int last = -1;
+    for (int dx = 0; dx < dw; dx++) {
+        const int64_t xl = x0l + (int64_t)dx * dxl - ((int64_t)1 << 31);
+        const int xw = (int)(xl >> 32);
+        const int xa = xw < 0 ? 0 : xw, xb = xw < 0 ? 0 : std::min(xw + 1, sw - 1);
+        for (int x : {xa, xb})
+            if (x > last) {
+                n++;
+                last = x;
+            }
+    }
+    return n;
+}
+
 icx_status icx_resize_bilinear(icx_ctx* ctx, const icx_image* src, uint8_t* dst, int32_t dst_w, int32_t dst_h,
                                int32_t dst_stride)
 {
@@ -1215,7 +1236,13 @@ icx_status icx_resize_bilinear(icx_ctx* ctx, const icx_image* src, uint8_t* dst,
     }
     uint8_t* d = dout ? dst : (uint8_t*)ctx->dev.take((size_t)dst_stride * dst_h);
     {
-        Timed tm(ctx, "resize", (int64_t)dst_w * dst_h);
+        if (ctx->prof) {
+            const ResizeArgs a = resize_args(s, src->width, src->height, sstride, src->fmt, d, dst_w, dst_h, dst_stride);
+            ctx->stats["resize.bytes"].units += (touched(src->width, dst_w, a.x0l, a.dxl) *
+                                                     touched(src->height, dst_h, a.y0l, a.dyl) +
+                                                 (int64_t)dst_w * dst_h) * nch;
+        }
+        Timed tm(ctx, "resize", (int64_t)dst_w * dst_h, true);
         launch_resize(s, src->width, src->height, sstride, src->fmt, d, dst_w, dst_h, dst_stride, ctx->stream);
     }
     if (!dout) {
@@ -1249,19 +1276,134 @@ icx_status icx_png_fit(icx_ctx* ctx, const icx_image* src, int32_t min_width, in
                        size_t cap, int32_t* out_w, int32_t* out_h, int32_t* resized)
 {
     if (!ctx || !src || !src->px || !dst || !resized) return ICX_E_NULL;
-    icx_status v = validate(src);
-    if (v) return v;
-    *resized = 0;
-    if (src->width <= min_width && src->height <= min_height) {  // ImageCompressionPng.java:49-53
-        if (out_w) *out_w = src->width;
-        if (out_h) *out_h = src->height;
-        return ICX_OK;
-    }
-    const double wr = (double)min_width / src->width, hr = (double)min_height / src->height;
-    const double scale = std::min(wr, hr);  // ImageCompressionPng.java:57-61
-    icx_status s = icx_resize_image(ctx, src, scale, dst, cap, out_w, out_h);
-    if (s == ICX_OK) *resized = 1;
+    icx_png_fit_job j{};
+    j.src = *src;
+    j.min_width = min_width;
+    j.min_height = min_height;
+    j.dst = dst;
+    j.cap = cap;
+    icx_status s = icx_png_fit_batch(ctx, &j, 1);
+    if (s == ICX_OK) s = j.status;
+    *resized = j.resized;
+    if (out_w) *out_w = j.out_w;
+    if (out_h) *out_h = j.out_h;
     return s;
+}
+
+icx_status icx_png_fit_batch(icx_ctx* ctx, icx_png_fit_job* jobs, int32_t n)
+{
+    if (!ctx || (!jobs && n > 0)) return ICX_E_NULL;
+    if (n < 0) return ICX_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    hipSetDevice(ctx->device);
+    // ImageCompressionPng.java:45-66: the box test and scale per image
+    std::vector<int> todo;
+    for (int i = 0; i < n; i++) {
+        icx_png_fit_job& j = jobs[i];
+        j.resized = 0;
+        j.out_w = j.out_h = 0;
+        j.status = validate(&j.src);
+        if (j.status) continue;
+        if (j.src.width <= j.min_width && j.src.height <= j.min_height) {  // :49-53, the reference returns false
+            j.out_w = j.src.width;
+            j.out_h = j.src.height;
+            continue;
+        }
+        if (!j.dst) {  // needed only for an image that is resized
+            j.status = ICX_E_NULL;
+            continue;
+        }
+        const double scale = std::min((double)j.min_width / j.src.width, (double)j.min_height / j.src.height);
+        if (!(scale > 0.0)) {
+            j.status = ICX_E_INVALID;
+            continue;
+        }
+        icx_scaled_dims(j.src.width, j.src.height, scale, &j.out_w, &j.out_h);  // ImageTools.java:8-9
+        if (j.cap < (size_t)j.out_w * j.out_h * channels(j.src.fmt)) {
+            j.status = ICX_E_BUFFER;
+            continue;
+        }
+        todo.push_back(i);
+    }
+    // by format (one kernel instantiation per launch), then in workspace-sized groups
+    std::stable_sort(todo.begin(), todo.end(), [&](int a, int b) { return jobs[a].src.fmt < jobs[b].src.fmt; });
+    size_t pos = 0;
+    while (pos < todo.size()) {
+        const int fmt = jobs[todo[pos]].src.fmt;
+        std::vector<int> grp;
+        size_t need = 1 << 20;
+        while (pos < todo.size() && jobs[todo[pos]].src.fmt == fmt) {
+            const icx_png_fit_job& j = jobs[todo[pos]];
+            const size_t nch = channels(fmt);
+            size_t per = 4096;
+            if (!is_device_ptr(j.src.px)) per += (size_t)j.src.width * j.src.height * nch + 256;
+            if (!is_device_ptr(j.dst)) per += (size_t)j.out_w * j.out_h * nch + 256;
+            if (!grp.empty() && need + per > ctx->budget) break;
+            need += per;
+            grp.push_back(todo[pos++]);
+        }
+        hipError_t e = ctx->dev.reserve(need + grp.size() * (sizeof(ResizeArgs) + 8) + 4096);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            for (int i : grp) jobs[i].status = ICX_E_NOMEM;
+            continue;
+        }
+        ctx->dev.used = 0;
+        const int m = (int)grp.size();
+        std::vector<ResizeArgs> args(m);
+        std::vector<int64_t> prefix(m + 1, 0);
+        std::vector<uint8_t*> dl(m, nullptr);  // device staging of host destinations
+        int64_t dpx = 0, algo = 0, uniform = -1;
+        for (int k = 0; k < m && e == hipSuccess; k++) {
+            const icx_png_fit_job& j = jobs[grp[k]];
+            const int nch = channels(fmt);
+            const uint8_t* sp = j.src.px;
+            int sstride = j.src.stride;
+            if (!is_device_ptr(sp)) {
+                const size_t row = (size_t)j.src.width * nch;
+                uint8_t* st = (uint8_t*)ctx->dev.take(row * j.src.height);
+                e = hipMemcpy2DAsync(st, row, sp, j.src.stride, row, j.src.height, hipMemcpyHostToDevice, ctx->stream);
+                sp = st;
+                sstride = (int)row;
+            }
+            uint8_t* dp = j.dst;
+            if (!is_device_ptr(dp)) dp = dl[k] = (uint8_t*)ctx->dev.take((size_t)j.out_w * j.out_h * nch);
+            args[k] = resize_args(sp, j.src.width, j.src.height, sstride, fmt, dp, j.out_w, j.out_h, j.out_w * nch);
+            const int64_t tiles = resize_tiles(j.out_w, j.out_h);
+            prefix[k + 1] = prefix[k] + tiles;
+            uniform = uniform < 0 || uniform == tiles ? tiles : 0;
+            dpx += (int64_t)j.out_w * j.out_h;
+            if (ctx->prof)
+                algo += (touched(j.src.width, j.out_w, args[k].x0l, args[k].dxl) *
+                             touched(j.src.height, j.out_h, args[k].y0l, args[k].dyl) +
+                         (int64_t)j.out_w * j.out_h) * nch;
+        }
+        ResizeArgs* d_args = (ResizeArgs*)ctx->dev.take(sizeof(ResizeArgs) * m);
+        int64_t* d_prefix = (int64_t*)ctx->dev.take(sizeof(int64_t) * (m + 1));
+        if (e == hipSuccess) e = hipMemcpyAsync(d_args, args.data(), sizeof(ResizeArgs) * m, hipMemcpyHostToDevice, ctx->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(d_prefix, prefix.data(), sizeof(int64_t) * (m + 1), hipMemcpyHostToDevice, ctx->stream);
+        if (e == hipSuccess) {
+            if (ctx->prof) ctx->stats["resize.bytes"].units += algo;
+            Timed tm(ctx, "resize", dpx, true);
+            launch_resize_batch(fmt, d_args, d_prefix, m, prefix[m], uniform > 0 ? uniform : 0, ctx->stream);
+        }
+        for (int k = 0; k < m && e == hipSuccess; k++) {
+            if (!dl[k]) continue;
+            const icx_png_fit_job& j = jobs[grp[k]];
+            e = hipMemcpyAsync(j.dst, dl[k], (size_t)j.out_w * j.out_h * channels(fmt), hipMemcpyDeviceToHost,
+                               ctx->stream);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e == hipSuccess) e = hipGetLastError();
+        if (e != hipSuccess) {
+            for (int i : grp) jobs[i].status = ICX_E_DEVICE;
+            return hip_fail(ctx, e, "png fit batch");
+        }
+        for (int i : grp) jobs[i].resized = 1;
+    }
+    resolve_profile(ctx);
+    return ICX_OK;
 }
 
 icx_status icx_profile_enable(icx_ctx* ctx, int32_t on)

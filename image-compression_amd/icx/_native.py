@@ -12,9 +12,11 @@ LIB_PATH = os.environ.get("ICX_LIB") or os.path.join(os.path.dirname(_HERE), "li
 
 # icx_status
 OK, E_INVALID, E_NOMEM, E_DEVICE, E_BUFFER, E_UNSUPPORTED, E_CORRUPT, E_NULL = range(8)
-# icx_fmt (XRGB32/ARGB32: TYPE_INT_RGB/ARGB int rasters, ABGR32: TYPE_4BYTE_ABGR, RGBA32: PNG order)
-BGR24, RGB24, GRAY8, XRGB32, ARGB32, ABGR32, RGBA32 = range(7)
-CHANNELS = {BGR24: 3, RGB24: 3, GRAY8: 1, XRGB32: 4, ARGB32: 4, ABGR32: 4, RGBA32: 4}
+# icx_fmt (XRGB32/ARGB32: TYPE_INT_RGB/ARGB int rasters, ABGR32: TYPE_4BYTE_ABGR, RGBA32: PNG order,
+# GRAY16: TYPE_USHORT_GRAY, uint16 samples)
+BGR24, RGB24, GRAY8, XRGB32, ARGB32, ABGR32, RGBA32, GRAY16 = range(8)
+CHANNELS = {BGR24: 3, RGB24: 3, GRAY8: 1, XRGB32: 4, ARGB32: 4, ABGR32: 4, RGBA32: 4, GRAY16: 1}
+BYTES_PER_PX = {**CHANNELS, GRAY16: 2}
 
 EXPORTS = [
     "icx_abi_version", "icx_create", "icx_destroy", "icx_status_string", "icx_last_error",
@@ -25,7 +27,7 @@ EXPORTS = [
     "icx_profile_enable", "icx_profile_reset", "icx_profile_query",
     "icx_jpeg_info", "icx_decode_jpg", "icx_decode_jpg_batch", "icx_debug_decode_coefs",
     "icx_device_alloc", "icx_device_free", "icx_memcpy", "icx_host_alloc", "icx_host_free",
-    "icx_png_bound", "icx_png_encode",
+    "icx_png_bound", "icx_png_encode", "icx_png_fit_batch",
 ]
 
 
@@ -60,6 +62,13 @@ class FitJob(ctypes.Structure):
                 ("success", ctypes.c_int32), ("cache_hit", ctypes.c_int32),
                 ("out_len", ctypes.c_size_t), ("learned", LearnedParams),
                 ("encodes", ctypes.c_int32), ("status", ctypes.c_int32)]
+
+
+class PngFitJob(ctypes.Structure):
+    _fields_ = [("src", Image), ("min_width", ctypes.c_int32), ("min_height", ctypes.c_int32),
+                ("dst", ctypes.c_void_p), ("cap", ctypes.c_size_t),
+                ("out_w", ctypes.c_int32), ("out_h", ctypes.c_int32), ("resized", ctypes.c_int32),
+                ("status", ctypes.c_int32)]
 
 
 class DecodeJob(ctypes.Structure):
@@ -124,12 +133,13 @@ def load():
         "icx_host_free": (c.c_int, [c.c_void_p, c.c_void_p]),
         "icx_png_bound": (c.c_size_t, [P(Image)]),
         "icx_png_encode": (c.c_int, [P(Image), c.c_int32, c.c_void_p, c.c_size_t, P(c.c_size_t)]),
+        "icx_png_fit_batch": (c.c_int, [c.c_void_p, P(PngFitJob), c.c_int32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
-    if lib.icx_abi_version() != 2:
+    if lib.icx_abi_version() != 3:
         raise NativeLibraryError("libicx ABI version mismatch")
     _lib = lib
     return lib

@@ -95,6 +95,8 @@ def _fmt_of(img):
     """The BufferedImage type of an array: (H, W) grey = TYPE_BYTE_GRAY,
     (H, W, 3) = TYPE_3BYTE_BGR, (H, W, 4) = TYPE_4BYTE_ABGR (bytes A, B, G, R:
     how ImageIO reads an RGBA PNG).  Other layouts: pass fmt explicitly."""
+    if img.ndim == 2 and str(getattr(img, "dtype", "")) in ("uint16", "torch.uint16", "torch.int16"):
+        return N.GRAY16  # TYPE_USHORT_GRAY
     if img.ndim == 2 or (img.ndim == 3 and img.shape[2] == 1):
         return N.GRAY8
     if img.ndim == 3 and img.shape[2] == 3:
@@ -107,6 +109,10 @@ def _fmt_of(img):
 def _out_shape(h, w, fmt):
     nch = N.CHANNELS[fmt]
     return (h, w) if nch == 1 else (h, w, nch)
+
+
+def _out_dtype(fmt):
+    return np.uint16 if fmt == N.GRAY16 else np.uint8
 
 
 class DeviceImage:
@@ -214,22 +220,25 @@ def _image_struct(img, fmt=None):
     if fmt is None:
         fmt = _fmt_of(img)
     h, w = int(img.shape[0]), int(img.shape[1])
+    bpp = N.BYTES_PER_PX[fmt]
     if getattr(img, "icx_device", False):
-        return N.Image(img.data_ptr(), w, h, w * N.CHANNELS[fmt], fmt), img
+        return N.Image(img.data_ptr(), w, h, w * bpp, fmt), img
     if isinstance(img, np.ndarray):
-        if img.dtype != np.uint8:
-            raise ValueError("image must be uint8")
+        want = np.uint16 if fmt == N.GRAY16 else np.uint8
+        if img.dtype != want:
+            raise ValueError(f"image must be {np.dtype(want).name}")
         nch = N.CHANNELS[fmt]
-        if not (img.flags["C_CONTIGUOUS"] or (img.strides[-1] == 1 and (img.ndim == 2 or img.strides[1] == nch)
-                                              and (nch != 4 or img.strides[0] % 4 == 0))):
+        if not (img.flags["C_CONTIGUOUS"] or (img.strides[-1] == img.itemsize
+                                              and (img.ndim == 2 or img.strides[1] == nch)
+                                              and (bpp != 4 or img.strides[0] % 4 == 0))):
             img = np.ascontiguousarray(img)
         ptr, stride = img.ctypes.data, img.strides[0]
     else:  # torch tensor (CUDA or CPU)
-        if str(img.dtype) != "torch.uint8":
-            raise ValueError("image must be uint8")
+        if str(img.dtype) not in ("torch.uint8",) + (("torch.uint16", "torch.int16") if fmt == N.GRAY16 else ()):
+            raise ValueError("image must be uint8 (uint16 / int16 bits for GRAY16)")
         if not img.is_contiguous():
             raise ValueError("tensor image must be contiguous")
-        ptr, stride = img.data_ptr(), img.stride(0)
+        ptr, stride = img.data_ptr(), img.stride(0) * img.element_size()
     return N.Image(ptr, w, h, stride, fmt), img
 
 
@@ -273,7 +282,7 @@ class Codec:
         w = ctypes.c_int32()
         h = ctypes.c_int32()
         self._lib.icx_scaled_dims(img.width, img.height, float(scale), ctypes.byref(w), ctypes.byref(h))
-        out = np.empty(_out_shape(h.value, w.value, img.fmt), np.uint8)
+        out = np.empty(_out_shape(h.value, w.value, img.fmt), _out_dtype(img.fmt))
         st = self._lib.icx_resize_image(self._ctx, ctypes.byref(img), float(scale), out.ctypes.data, out.nbytes,
                                         ctypes.byref(w), ctypes.byref(h))
         self._check(st, "icx_resize_image")
@@ -281,9 +290,9 @@ class Codec:
 
     def resize_to(self, original_image, width: int, height: int, fmt=None) -> np.ndarray:
         img, keep = _image_struct(original_image, fmt)
-        out = np.empty(_out_shape(height, width, img.fmt), np.uint8)
+        out = np.empty(_out_shape(height, width, img.fmt), _out_dtype(img.fmt))
         st = self._lib.icx_resize_bilinear(self._ctx, ctypes.byref(img), out.ctypes.data, width, height,
-                                           width * N.CHANNELS[img.fmt])
+                                           width * N.BYTES_PER_PX[img.fmt])
         self._check(st, "icx_resize_bilinear")
         return out
 
@@ -418,6 +427,36 @@ class Codec:
             return None
         scale = min(params.min_width / w, params.min_height / h)
         return self.resize_image(original_image, scale)
+
+    def png_fit_batch(self, images, params: CompressionParams, fmts=None):
+        """The device part of compressPngWithTargetSize for a group of images
+        in one launch (icx_png_fit_batch): per image None when it already
+        fits the (minWidth x minHeight) box (ImageCompressionPng.java:49-53),
+        else the bilinear resize by min(minWidth/w, minHeight/h) (:57-66),
+        keeping the raster type (ImageTools.java:12-15)."""
+        n = len(images)
+        jobs = (N.PngFitJob * n)()
+        keep, outs = [], [None] * n
+        for i, im in enumerate(images):
+            img, k = _image_struct(im, fmts[i] if fmts else None)
+            keep.append(k)
+            j = jobs[i]
+            j.src = img
+            j.min_width, j.min_height = int(params.min_width), int(params.min_height)
+            if img.width <= params.min_width and img.height <= params.min_height:
+                continue
+            dw, dh = scaled_dims(img.width, img.height,
+                                 min(params.min_width / img.width, params.min_height / img.height))
+            outs[i] = np.empty(_out_shape(dh, dw, img.fmt), _out_dtype(img.fmt))
+            j.dst, j.cap = outs[i].ctypes.data, outs[i].nbytes
+        with self._lock:
+            st = self._lib.icx_png_fit_batch(self._ctx, jobs, n)
+        self._check(st, "icx_png_fit_batch")
+        res = []
+        for i in range(n):
+            self._check(jobs[i].status, "icx_png_fit_batch job")
+            res.append(outs[i] if jobs[i].resized else None)
+        return res
 
     # -------------------------------------------------------------- A11 decode
     def decode_jpg_batch(self, datas, subsampling: int = 0, device_out: bool = False):

@@ -78,13 +78,19 @@ def format_file_size(size: int) -> str:
 
 def _to_array(im):
     """Decoded raster as the BufferedImage type the JDK reader returns:
-    TYPE_BYTE_GRAY (H, W), TYPE_3BYTE_BGR (H, W, 3) or, with an alpha channel,
-    TYPE_4BYTE_ABGR (H, W, 4) - ImageTools.resizeImage keeps that type and
-    the PNG is written back with its alpha (ImageTools.java:12-15)."""
+    TYPE_BYTE_GRAY (H, W), TYPE_USHORT_GRAY (H, W) uint16 for a 16-bit grey
+    PNG, TYPE_3BYTE_BGR (H, W, 3) or, with an alpha channel, TYPE_4BYTE_ABGR
+    (H, W, 4) - ImageTools.resizeImage keeps that type and the PNG is written
+    back with it (ImageTools.java:12-15)."""
     mode = im.mode
     if mode == "L":
         return np.asarray(im, dtype=np.uint8)
-    if mode in ("I;16", "I;16B", "I", "F", "1"):
+    if mode in ("I;16", "I;16B", "I;16L") or (mode == "I" and im.format == "PNG"):
+        # 16-bit grey PNG (Pillow: I;16, or I in older versions): TYPE_USHORT_GRAY
+        return np.ascontiguousarray(np.asarray(im).astype(np.uint16))
+    if mode in ("I", "F", "1"):
+        # 1-bit PNGs are TYPE_BYTE_BINARY in the JDK (re-thresholded by Java2D
+        # after the resize); here 8-bit grey, an approximation (DESIGN.md §11)
         return np.asarray(im.convert("L"), dtype=np.uint8)
     if mode in ("LA", "PA"):
         # grey+alpha is TYPE_CUSTOM there, drawn into TYPE_INT_ARGB: RGBA out
@@ -355,6 +361,30 @@ def compress_png_item(codec, it: _Item, params: CompressionParams, writer=None):
         _fail(it, e)
 
 
+def compress_png_group(codec, items: List[_Item], params: CompressionParams, writer=None):
+    """compressPngWithTargetSize for a group of PNGs: the resizes in one device
+    launch (icx_png_fit_batch), filter + deflate + file write per image on
+    `writer`.  A codec without the batched entry point takes them one by one."""
+    if writer is None or not hasattr(codec, "png_fit_batch"):
+        for it in items:
+            compress_png_item(codec, it, params, writer)
+        return
+    try:
+        res = codec.png_fit_batch([it.decoded.image for it in items], params)
+    except Exception:  # a bad image fails alone: redo the group one by one
+        for it in items:
+            compress_png_item(codec, it, params, writer)
+        return
+    for it, resized in zip(items, res):
+        if resized is None:  # ImageCompressionPng.java:49-53: already fits the box
+            w, h = it.decoded.image.shape[1], it.decoded.image.shape[0]
+            log.info("PNG 圖片尺寸 %dx%d 未超過目標 %dx%d，不處理。", w, h, params.min_width, params.min_height)
+            _finish(it, False)
+            continue
+        it.decoded = None
+        writer.submit(_png_write, it, resized)
+
+
 def compress_image_iteratively(codec, it: _Item, params, cache):
     """The format switch (ImageCompression.java:167-183) for one item."""
     fmt = it.decoded.format_name
@@ -429,6 +459,27 @@ class BatchReport:
         log.info(" 總空間節省百分比: %.2f %%", pct)
 
 
+def host_cores():
+    """Host cores this process may use: the scheduler affinity set, capped by
+    a cgroup CPU quota when one is set (on the GPU box the affinity mask shows
+    the whole machine while the job's share is a quota).  Returns (cores, how
+    it was determined).  The reference sizes its pool the same way:
+    Runtime.availableProcessors() (CompressionBatch.java:64-68), which in a
+    container honours both the affinity mask and the cgroup quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    how = "sched_getaffinity"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, -(-int(quota) // int(period)))
+            if q < n:
+                n, how = q, "cgroup cpu.max quota"
+    except (OSError, ValueError):
+        pass
+    return n, how
+
+
 def read_file_list(path) -> List[str]:
     with open(path, encoding="utf-8") as f:
         return [ln.strip() for ln in f if ln.strip()]
@@ -482,7 +533,7 @@ class CompressionBatch:
         self.h2_cache_path = h2_cache_path
         self.codecs = codecs or []
         self.group_size = max(1, group_size)
-        self.decode_threads = decode_threads or min(16, os.cpu_count() or 1)
+        self.decode_threads = decode_threads or host_cores()[0]
         self.rank, self.world = rank, world
         # JPEG decode on the GPU when every codec can (the default for icx.Codec)
         if device_decode is None:
@@ -548,8 +599,7 @@ class CompressionBatch:
                 if kind == "jpeg":
                     compress_jpeg_group(codec, its, self.params, cache, writer)
                 elif kind == "png":
-                    for it in its:
-                        compress_png_item(codec, it, self.params, writer)
+                    compress_png_group(codec, its, self.params, writer)
                 else:
                     for it in its:
                         compress_image_iteratively(codec, it, self.params, cache)
@@ -558,6 +608,7 @@ class CompressionBatch:
         for w in workers:
             w.start()
         pending_jpeg: List[_Item] = []
+        pending_png: List[_Item] = []
         with cf.ThreadPoolExecutor(self.decode_threads) as pool:
             futs = [pool.submit(_prepare, i, p, self.save_dir, self.params, self.device_decode) for i, p in mine]
             try:
@@ -577,7 +628,10 @@ class CompressionBatch:
                             work.put(("jpeg", pending_jpeg))
                             pending_jpeg = []
                     elif fmt == "png":
-                        work.put(("png", [it]))
+                        pending_png.append(it)
+                        if len(pending_png) >= self.group_size:
+                            work.put(("png", pending_png))
+                            pending_png = []
                     else:
                         work.put(("other", [it]))
             except cf.TimeoutError:
@@ -586,6 +640,8 @@ class CompressionBatch:
                     f.cancel()
         if pending_jpeg:
             work.put(("jpeg", pending_jpeg))
+        if pending_png:
+            work.put(("png", pending_png))
         for _ in workers:
             work.put(None)
         for w in workers:

@@ -3,8 +3,10 @@ host thread; ctypes releases the GIL, so the batch driver's writer pool
 encodes one image per thread).
 
 Reference: ImageCompressionPng.java:70, ImageIO.write(img, "png", file).
-The JDK writer's filter heuristic and deflate bytes are not pinnable here (no
-JDK): parity is on decoded pixels, dimensions and colour type,
+The JDK writer's row-filter choice (RowFilter.filterRow), default deflate
+level (4) and 32 KiB IDAT chunks are restated (icx_png.cpp); its deflate
+bytes depend on the JDK's zlib and are not pinnable here (no JDK, SURVEY.md
+§8c): parity is on decoded pixels, dimensions, colour type and bit depth,
 and the per-row filter choice is checked against tests/png_ref.py.
 """
 import ctypes
@@ -14,9 +16,10 @@ import numpy as np
 from . import _native as N
 
 
-def encode_png(img, fmt=None, level: int = 6) -> bytes:
-    """img: host (H, W) grey, (H, W, 3) BGR or (H, W, 4) ABGR uint8 array (or
-    another icx_fmt given explicitly) -> PNG file bytes (grey, RGB or RGBA)."""
+def encode_png(img, fmt=None, level: int = -1) -> bytes:
+    """img: host (H, W) grey, (H, W, 3) BGR or (H, W, 4) ABGR uint8 array,
+    (H, W) uint16 grey (TYPE_USHORT_GRAY, a 16-bit PNG), or another icx_fmt
+    given explicitly -> PNG file bytes.  level -1 = PNGImageWriter's default."""
     from .core import _image_struct
     lib = N.load()
     im, keep = _image_struct(np.ascontiguousarray(img), fmt)

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ICX_ABI_VERSION 2  /* 2: four-byte pixel formats, icx_png_encode */
+#define ICX_ABI_VERSION 3  /* 2: four-byte pixel formats, icx_png_encode; 3: ICX_GRAY16, icx_png_fit_batch */
 
 typedef struct icx_ctx icx_ctx;
 
@@ -59,7 +59,12 @@ typedef enum icx_status {
  *   ICX_XRGB32  TYPE_INT_RGB    int 0x00RRGGBB: B, G, R, 0 (alpha ignored, written 0)
  *   ICX_ARGB32  TYPE_INT_ARGB   int 0xAARRGGBB: B, G, R, A
  *   ICX_ABGR32  TYPE_4BYTE_ABGR bytes A, B, G, R (ImageIO's reading of an RGBA PNG)
- *   ICX_RGBA32  bytes R, G, B, A (PNG colour type 6 row order) */
+ *   ICX_RGBA32  bytes R, G, B, A (PNG colour type 6 row order)
+ * ICX_GRAY16 is TYPE_USHORT_GRAY (a 16-bit grey PNG as the JDK reads it):
+ * native-endian uint16 samples, rows and px 2-byte aligned; resize / PNG
+ * entry points only.  Java2D's bilinear loops carry it through 8-bit
+ * IntArgbPre (UshortGray.h: the high byte in, gray * 257 out), and so does
+ * icx_resize_image; icx_png_encode writes it as a 16-bit grey PNG. */
 typedef enum icx_fmt {
     ICX_BGR24 = 0,
     ICX_RGB24 = 1,
@@ -67,7 +72,8 @@ typedef enum icx_fmt {
     ICX_XRGB32 = 3,
     ICX_ARGB32 = 4,
     ICX_ABGR32 = 5,
-    ICX_RGBA32 = 6
+    ICX_RGBA32 = 6,
+    ICX_GRAY16 = 7
 } icx_fmt;
 
 /* A decoded image (BufferedImage).  stride in bytes. */
@@ -187,12 +193,35 @@ icx_status icx_png_fit(icx_ctx* ctx, const icx_image* src, int32_t min_width, in
                        uint8_t* dst, size_t cap, int32_t* out_w, int32_t* out_h,
                        int32_t* resized);
 
+/* Batched icx_png_fit: the resizes of all jobs share one launch (a group of
+ * PNGs of a CompressionBatch, ImageCompressionPng.java:57-70 per image).
+ * Per-job results/status are filled in; a job whose image already fits the
+ * box gets resized = 0 and nothing written.  Sources and destinations may be
+ * host or device memory.  Returns ICX_OK unless a context-level failure
+ * occurred. */
+typedef struct icx_png_fit_job {
+    /* inputs */
+    icx_image src;
+    int32_t min_width, min_height; /* CompressionParams.minWidth / minHeight */
+    uint8_t* dst;                  /* host or device; packed rows of out_w * channels (may be NULL
+                                      for an image that already fits the box) */
+    size_t cap;
+    /* outputs */
+    int32_t out_w, out_h;
+    int32_t resized;               /* 0: the reference returns false (ImageCompressionPng.java:49-53) */
+    icx_status status;
+} icx_png_fit_job;
+icx_status icx_png_fit_batch(icx_ctx* ctx, icx_png_fit_job* jobs, int32_t n);
+
 /* The PNG write of ImageCompressionPng (ImageCompressionPng.java:70,
  * ImageIO.write(img, "png", file)) for host pixels: 8-bit grey (GRAY8), RGB
- * (BGR24/RGB24/XRGB32) or RGBA (ARGB32/ABGR32/RGBA32); per row the filter
- * (None, Sub, Up, Average, Paeth) with the least sum of |residual byte as
- * signed| (ties: the lower type), one zlib stream at `level` (0-9, -1 = 6)
- * in one IDAT.  Needs cap >= icx_png_bound(img); *out_len = file bytes. */
+ * (BGR24/RGB24/XRGB32), RGBA (ARGB32/ABGR32/RGBA32) or 16-bit grey (GRAY16).
+ * Restates OpenJDK's PNGImageWriter: per row RowFilter.filterRow's choice
+ * (None costs the sum of the unsigned sample bytes; Sub, Up, Average and
+ * Paeth the sum of |unwrapped int difference|; ties keep the lower type), one
+ * zlib stream at `level` (0-9; -1 = the writer's default, 4) cut into IDAT
+ * chunks of 32768 bytes.  Needs cap >= icx_png_bound(img); *out_len = file
+ * bytes. */
 size_t icx_png_bound(const icx_image* img);
 icx_status icx_png_encode(const icx_image* img, int32_t level, uint8_t* out, size_t cap, size_t* out_len);
 

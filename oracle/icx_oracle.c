@@ -748,10 +748,37 @@ static int resize4(const uint8_t* src, int sw, int sh, int sstride, int fmt, uin
     return 0;
 }
 
+/* TYPE_USHORT_GRAY (a 16-bit grey PNG as the JDK reads it; ImageTools keeps
+ * the type).  Java2D's UshortGray loops (UshortGray.h) carry it through the
+ * 8-bit IntArgbPre the bilinear TransformHelper works in: the fetch keeps
+ * gray >> 8, the four taps are interpolated as for 8-bit grey, and the
+ * store composes a 16-bit grey from r = g = b = v as (19672 r + 38621 g +
+ * 7500 b) >> 8 = 257 v.  Restated from the published OpenJDK source, no JDK
+ * here to pin it (parity unpinned, like the rest of A12). */
+static int resize16(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dw, int dh, int dstride)
+{
+    uint8_t* hi = (uint8_t*)malloc((size_t)sw * sh);
+    uint8_t* lo = (uint8_t*)malloc((size_t)dw * dh);
+    if (!hi || !lo) { free(hi); free(lo); return 1; }
+    for (int y = 0; y < sh; y++) {
+        const uint16_t* r = (const uint16_t*)(src + (size_t)y * sstride);
+        for (int x = 0; x < sw; x++) hi[(size_t)y * sw + x] = (uint8_t)(r[x] >> 8);
+    }
+    oracle_resize(hi, sw, sh, sw, OR_GRAY8, lo, dw, dh, dw);
+    for (int y = 0; y < dh; y++) {
+        uint16_t* o = (uint16_t*)(dst + (size_t)y * dstride);
+        for (int x = 0; x < dw; x++) o[x] = (uint16_t)(lo[(size_t)y * dw + x] * 257);
+    }
+    free(hi);
+    free(lo);
+    return 0;
+}
+
 int oracle_resize(const uint8_t* src, int sw, int sh, int sstride, int fmt, uint8_t* dst, int dw,
                   int dh, int dstride)
 {
     if (sw <= 0 || sh <= 0 || dw <= 0 || dh <= 0 || !src || !dst) return 1;
+    if (fmt == OR_GRAY16) return resize16(src, sw, sh, sstride, dst, dw, dh, dstride);
     if (fmt >= OR_XRGB32) return resize4(src, sw, sh, sstride, fmt, dst, dw, dh, dstride);
     int nch = (fmt == OR_GRAY8) ? 1 : 3;
     double ix = 1.0 / ((double)dw / sw), iy = 1.0 / ((double)dh / sh);

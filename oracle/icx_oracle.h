@@ -32,7 +32,8 @@ extern "C" {
 #endif
 
 /* pixel formats, same numbering as include/icx.h */
-enum { OR_BGR24 = 0, OR_RGB24 = 1, OR_GRAY8 = 2, OR_XRGB32 = 3, OR_ARGB32 = 4, OR_ABGR32 = 5, OR_RGBA32 = 6 };
+enum { OR_BGR24 = 0, OR_RGB24 = 1, OR_GRAY8 = 2, OR_XRGB32 = 3, OR_ARGB32 = 4, OR_ABGR32 = 5, OR_RGBA32 = 6,
+       OR_GRAY16 = 7 /* TYPE_USHORT_GRAY, native-endian uint16 */ };
 
 /* A6: JDK quality -> natural-order tables (JPEG.convertToLinearQuality +
  * JPEGQTable.getScaledInstance(lin, true)). */

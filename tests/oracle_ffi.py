@@ -101,14 +101,16 @@ class Oracle:
         return a.value, b.value
 
     def resize(self, img, dw, dh, fmt=None):
-        """fmt: icx_fmt numbering; default grey / BGR24 / ABGR32 by channels."""
+        """fmt: icx_fmt numbering; default grey / BGR24 / ABGR32 by channels,
+        GRAY16 (7) for a uint16 (H, W) array."""
         img = np.ascontiguousarray(img)
         h, w = img.shape[:2]
         nch = 1 if img.ndim == 2 else img.shape[2]
         if fmt is None:
-            fmt = 2 if nch == 1 else 0 if nch == 3 else 5
-        out = np.empty((dh, dw, nch) if nch > 1 else (dh, dw), np.uint8)
-        self.L.oracle_resize(img.ctypes.data, w, h, img.strides[0], fmt, out.ctypes.data, dw, dh, dw * nch)
+            fmt = 7 if img.dtype == np.uint16 else 2 if nch == 1 else 0 if nch == 3 else 5
+        out = np.empty((dh, dw, nch) if nch > 1 else (dh, dw), img.dtype)
+        self.L.oracle_resize(img.ctypes.data, w, h, img.strides[0], fmt, out.ctypes.data, dw, dh,
+                             dw * nch * img.itemsize)
         return out
 
     def fit(self, img, target, q0, cached=None):

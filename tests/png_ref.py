@@ -2,11 +2,16 @@
 per-row filter choice that libicx's icx_png_encode must reproduce.
 
 The reference writes PNG through the JDK's PNGImageWriter
-(ImageCompressionPng.java:70): per row it picks the filter (None, Sub, Up,
-Average, Paeth) with the smallest sum of |filtered byte as signed|, then
-deflates.  This writer uses the same row-filter heuristic (vectorised over the
-whole image) and zlib; the deflate bytes themselves are not pinned (no JDK
-here) — parity for PNG is on decoded pixels and dimensions.
+(ImageCompressionPng.java:70).  Restated from OpenJDK's published
+com.sun.imageio.plugins.png sources (not in /root/reference, no JDK here:
+SURVEY.md §8c): RowFilter.filterRow costs None as the sum of the row's
+unsigned bytes and Sub / Up / Average / Paeth as the sum of |curr -
+predictor| over ints (the unwrapped difference), keeping the first strictly
+smallest (ties: the lower type); PNGImageWriter deflates at its default level
+4 and IDATOutputStream cuts the stream into 32768-byte IDAT chunks.  The
+deflate bytes are not pinned (they depend on the JDK's zlib) — parity for PNG
+is on decoded pixels, dimensions, colour type and bit depth, plus the filter
+choice row for row.
 """
 import struct
 import zlib
@@ -20,8 +25,9 @@ def _chunk(tag, data):
 
 
 def filter_rows(raw: np.ndarray, bpp: int) -> np.ndarray:
-    """raw (h, rowbytes) u8 -> (h, 1 + rowbytes) u8 with the per-row filter of
-    minimum sum of absolute signed residuals (ties: the lower filter type)."""
+    """raw (h, rowbytes) u8 -> (h, 1 + rowbytes) u8 with RowFilter.filterRow's
+    per-row choice (None: sum of unsigned bytes; the others: sum of |int
+    difference|; ties: the lower filter type)."""
     h, n = raw.shape
     x = raw.astype(np.int16)
     a = np.zeros_like(x)
@@ -36,8 +42,9 @@ def filter_rows(raw: np.ndarray, bpp: int) -> np.ndarray:
     best_cost = None
     out = np.empty((h, n + 1), np.uint8)
     for ftype, pred in enumerate((None, a, b, (a + b) >> 1, paeth)):
-        res = (x if pred is None else x - pred).astype(np.uint8)  # mod 256
-        cost = np.abs(res.view(np.int8).astype(np.int32)).sum(axis=1)
+        diff = x if pred is None else x - pred            # int16: the unwrapped difference
+        res = diff.astype(np.uint8)                       # the residual byte (mod 256)
+        cost = np.abs(diff.astype(np.int32)).sum(axis=1)  # None: x >= 0, the unsigned bytes
         if best_cost is None:
             best_cost = cost
             out[:, 1:] = res
@@ -51,18 +58,22 @@ def filter_rows(raw: np.ndarray, bpp: int) -> np.ndarray:
     return out
 
 
-def encode_png(img: np.ndarray, level: int = 6) -> bytes:
-    """img: (H, W, 3) BGR, (H, W, 4) ABGR or (H, W) grey uint8."""
+def encode_png(img: np.ndarray, level: int = 4) -> bytes:
+    """img: (H, W, 3) BGR, (H, W, 4) ABGR, (H, W) grey uint8 or (H, W) grey
+    uint16 (TYPE_USHORT_GRAY: a 16-bit PNG)."""
+    depth = 16 if img.dtype == np.uint16 else 8
     if img.ndim == 2:
-        rgb, ctype, bpp = img, 0, 1
+        ctype, bpp = 0, depth // 8
+        rgb = img.astype(">u2").view(np.uint8) if depth == 16 else img
     else:
         bpp = img.shape[2]
         rgb, ctype = np.ascontiguousarray(img[:, :, ::-1]), 2 if bpp == 3 else 6
-    h, w = rgb.shape[:2]
-    raw = filter_rows(rgb.reshape(h, -1), bpp)
-    ihdr = struct.pack(">IIBBBBB", w, h, 8, ctype, 0, 0, 0)
-    return (b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", ihdr) +
-            _chunk(b"IDAT", zlib.compress(raw.tobytes(), level)) + _chunk(b"IEND", b""))
+    h, w = img.shape[:2]
+    raw = filter_rows(np.ascontiguousarray(rgb).reshape(h, -1), bpp)
+    ihdr = struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, 0)
+    z = zlib.compress(raw.tobytes(), level)
+    idat = b"".join(_chunk(b"IDAT", z[i:i + 32768]) for i in range(0, len(z), 32768))
+    return b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", ihdr) + idat + _chunk(b"IEND", b"")
 
 
 def write_png(path, img: np.ndarray) -> None:

@@ -44,6 +44,9 @@ class OracleCodec:
         dw, dh = self.o.scaled_dims(w, h, s)
         return self.o.resize(img, dw, dh)  # (H, W, 4) = ABGR, as icx.core._fmt_of
 
+    def png_fit_batch(self, images, params):
+        return [self.png_resize(im, params) for im in images]
+
     def compress_png_with_target_size(self, img, output_file, params):
         r = self.png_resize(img, params)
         if r is None:

@@ -30,7 +30,7 @@ def test_library_exports_all_header_symbols():
 
 def test_abi_version_and_status_strings():
     lib = N.load()
-    assert lib.icx_abi_version() == 2
+    assert lib.icx_abi_version() == 3
     assert lib.icx_status_string(N.E_BUFFER) == b"output buffer too small"
     assert lib.icx_jpeg_header_size(N.BGR24) == 623 and lib.icx_jpeg_header_size(N.GRAY8) == 328
 

@@ -182,6 +182,91 @@ def test_png_fit_keeps_alpha(codec, oracle, tmp_path):
     assert (np.asarray(im)[:20, :, 3] == 0).all()
 
 
+def test_resize_tiles_staged_and_direct_match_restatement(codec, oracle):
+    """k_resize stages each 64 x 16 tile's source rectangle in LDS when it
+    fits (scales down to ~0.2) and reads the taps from global memory below
+    that: both paths, tile edges (widths and heights that are not multiples
+    of the tile), unaligned rows (odd widths, a row stride that is not a
+    multiple of 16) and upscaling equal the restatement for every pixel
+    class."""
+    rng = np.random.default_rng(11)
+    cases = [(2160, 3840, 1920, 1080), (1081, 1921, 999, 563), (77, 131, 13, 7), (77, 131, 211, 150),
+             (500, 700, 60, 40), (3, 5, 64, 17), (1, 1, 3, 2)]
+    for h, w, dw, dh in cases:
+        for nch in (1, 3):
+            img = rng.integers(0, 256, (h, w, nch) if nch > 1 else (h, w), dtype=np.uint8)
+            got = codec.resize_to(img, dw, dh)
+            assert np.array_equal(got, oracle.resize(img, dw, dh)), (h, w, dw, dh, nch)
+        # a padded row stride (not a multiple of 16): a view of a wider array
+        wide = rng.integers(0, 256, (h, w + 3, 3), dtype=np.uint8)
+        view = wide[:, :w]
+        assert np.array_equal(codec.resize_to(view, dw, dh), oracle.resize(np.ascontiguousarray(view), dw, dh))
+
+
+def test_resize_16bit_grey_matches_restatement(codec, oracle):
+    """TYPE_USHORT_GRAY (a 16-bit grey PNG; ImageTools.java:12-15 keeps the
+    type): Java2D's UshortGray loops interpolate the high byte in 8 bits and
+    store 257 * v - k_resize<2> equals the oracle's restatement bit for bit,
+    and the result is a uint16 raster of 257 multiples."""
+    rng = np.random.default_rng(16)
+    for h, w, s in [(2160, 3840, 0.5), (301, 517, 0.85), (40, 30, 0.3)]:
+        img = rng.integers(0, 65536, (h, w), dtype=np.uint16)
+        got = codec.resize_image(img, s)
+        dw, dh = oracle.scaled_dims(w, h, s)
+        assert got.dtype == np.uint16 and got.shape == (dh, dw)
+        assert np.array_equal(got, oracle.resize(img, dw, dh)), (h, w, s)
+        assert (got % 257 == 0).all()
+
+
+def test_png_fit_batch_matches_restatement(codec, oracle):
+    """icx_png_fit_batch: one launch per pixel format for a mixed group -
+    sizes (same-size groups take the 2-D grid, mixed ones the slot search),
+    formats, images that already fit the box (None, nothing written) - each
+    result equals the one-image fit and the oracle."""
+    rng = np.random.default_rng(21)
+    p = icx.CompressionParams(0.25, 0, 1920, 1920, 0)
+    imgs = [rng.integers(0, 256, (2160, 3840, 3), dtype=np.uint8) for _ in range(3)]
+    imgs += [rng.integers(0, 256, (1500, 2500), dtype=np.uint8), rng.integers(0, 256, (2001, 1999, 4), dtype=np.uint8),
+             rng.integers(0, 65536, (2400, 3000), dtype=np.uint16), rng.integers(0, 256, (800, 600, 3), dtype=np.uint8),
+             rng.integers(0, 256, (1080, 4096, 3), dtype=np.uint8)]
+    codec.profile(True)
+    codec.profile_reset()
+    res = codec.png_fit_batch(imgs, p)
+    st = codec.profile_query("resize")
+    codec.profile(False)
+    assert st["launches"] == 4  # BGR, grey, ABGR, grey16: one launch each
+    for img, r in zip(imgs, res):
+        h, w = img.shape[:2]
+        if w <= 1920 and h <= 1920:
+            assert r is None
+            continue
+        dw, dh = oracle.scaled_dims(w, h, min(1920 / w, 1920 / h))
+        assert r.shape[:2] == (dh, dw) and r.dtype == img.dtype
+        assert np.array_equal(r, oracle.resize(img, dw, dh)), img.shape
+
+
+def test_png_16bit_grey_through_the_pipeline(codec, oracle, tmp_path):
+    """A 16-bit grey PNG keeps its type (ImageTools.java:12-15): read as
+    TYPE_USHORT_GRAY, resized on the device and written as a 16-bit grey PNG
+    whose samples equal the restatement (not clipped to 8 bits)."""
+    from PIL import Image
+
+    from icx.pipeline import process_image
+    rng = np.random.default_rng(3)
+    src = (rng.integers(0, 256, (300, 400), dtype=np.uint16) * 257 + rng.integers(0, 257, (300, 400))).astype(np.uint16)
+    Image.fromarray(src).save(tmp_path / "g16.png")  # uint16 (H, W): mode I;16, a 16-bit grey PNG
+    out = tmp_path / "out"
+    out.mkdir()
+    rep = process_image(tmp_path / "g16.png", out, icx.CompressionParams(0.25, 10, 100, 100, 10 ** 6), {}, codec)
+    assert rep.result == icx.CompressionResult.COMPRESSED_SUCCESS
+    im = Image.open(out / "g16.png")
+    assert im.mode.startswith("I") and im.size == (100, 75)
+    got = np.asarray(im).astype(np.uint16)
+    assert np.array_equal(got, oracle.resize(src, 100, 75))
+    raw = open(out / "g16.png", "rb").read()
+    assert raw[24] == 16 and raw[25] == 0  # IHDR bit depth 16, colour type 0
+
+
 def test_jpeg_rejects_alpha_rasters(codec):
     """The JDK JPEG writer refuses alpha rasters: the JPEG entry points return
     ICX_E_UNSUPPORTED for four-byte formats."""

@@ -268,6 +268,77 @@ def test_png_writer_adaptive_filters_round_trip():
     assert len(types) >= 2  # the smooth gradient picks predictive filters, not only "None"
 
 
+def _png_chunks(data):
+    import struct
+    pos, out = 8, []
+    while pos < len(data):
+        n, = struct.unpack(">I", data[pos:pos + 4])
+        out.append((data[pos + 4:pos + 8], n))
+        pos += 12 + n
+    return out
+
+
+def test_png_row_filter_is_the_jdk_heuristic():
+    """RowFilter.filterRow (OpenJDK PNGImageWriter, restated in icx_png.cpp):
+    None costs the sum of the unsigned bytes, the predictors the sum of
+    |int difference| - not the residual bytes read as signed, which would
+    score a row of 0xFF as 1 per byte and keep None.  Ties keep the lower
+    type."""
+    from icx.pngio import encode_png
+    from tests.png_ref import filter_rows
+    # row 0: all 255 -> None costs 255 n, Sub 255 (the first byte only): Sub;
+    # row 1: the same row again -> Up costs 0: Up;
+    # row 2: a ramp 0, 3, 6, ... -> Sub costs 3 per byte, Up |ramp - 255|: Sub;
+    # row 3: all zero -> None costs 0, as does nothing else before it: None (tie rule)
+    w = 40
+    img = np.zeros((4, w), np.uint8)
+    img[0] = 255
+    img[1] = 255
+    img[2] = (np.arange(w) * 3).astype(np.uint8)
+    rows = filter_rows(img, 1)
+    assert rows[:, 0].tolist() == [1, 2, 1, 0]
+    assert np.array_equal(_png_idat_rows(encode_png(img), 4), rows)
+    # the old signed-residual heuristic would have kept None for row 0
+    assert np.abs(img[0].view(np.int8).astype(int)).sum() < 255
+
+
+def test_png_idat_chunks_and_default_level():
+    """IDATOutputStream cuts the zlib stream into 32768-byte IDAT chunks; the
+    stream is zlib's at PNGImageWriter's default level 4 (FLEVEL 1 in the
+    header: levels 2-5)."""
+    from icx.pngio import encode_png
+    rng = np.random.default_rng(2)
+    img = rng.integers(0, 256, (300, 200, 3), dtype=np.uint8)  # incompressible: ~180 KB of IDAT data
+    data = encode_png(img)
+    ch = _png_chunks(data)
+    assert [t for t, _ in ch][0] == b"IHDR" and ch[-1] == (b"IEND", 0)
+    idat = [n for t, n in ch if t == b"IDAT"]
+    assert len(idat) >= 5 and all(n == 32768 for n in idat[:-1]) and 0 < idat[-1] <= 32768
+    zhdr = data[8 + 25 + 8: 8 + 25 + 10]
+    assert zhdr[0] == 0x78 and (zhdr[1] >> 6) == 1  # deflate, 32K window; FLEVEL 1 (zlib levels 2..5)
+
+
+def test_png_16bit_grey_is_written_as_16bit():
+    """TYPE_USHORT_GRAY is kept (ImageTools.java:12-15): a uint16 raster is
+    written as a 16-bit grey PNG (big-endian samples, bytesPerPixel 2 for the
+    row filter) that decodes to the same samples."""
+    import io
+
+    from PIL import Image
+
+    from icx.pngio import encode_png
+    from tests.png_ref import filter_rows
+    rng = np.random.default_rng(8)
+    img = rng.integers(0, 65536, (23, 41), dtype=np.uint16)
+    img[5:] = np.arange(41, dtype=np.uint16) * 1601  # smooth rows: predictive filters
+    data = encode_png(img)
+    assert data[24] == 16 and data[25] == 0
+    back = np.asarray(Image.open(io.BytesIO(data))).astype(np.uint16)
+    assert np.array_equal(back, img)
+    be = img.astype(">u2").view(np.uint8).reshape(23, -1)
+    assert np.array_equal(_png_idat_rows(data, 23), filter_rows(be, 2))
+
+
 def test_png_alpha_kept_through_the_pipeline(tmp_path):
     """ImageTools.java:12-15 keeps the alpha channel: an RGBA PNG is resized
     as TYPE_4BYTE_ABGR (premultiplied bilinear, icx_resize restatement) and
