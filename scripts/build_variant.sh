@@ -1,10 +1,11 @@
 #!/bin/bash
 # Build a libicx variant with tuning macros (ICX_PRE, ICX_SLOT_WORDS, ICX_FDCT_TILES): build_variant.sh NAME "-DFLAG=..." -> image-compression_amd/lib/libicx_NAME.so
+# KSRC=path: the kernels source to build instead of csrc/icx_kernels.hip (e.g. a git revision's, for an A/B)
 set -e
 cd "$(dirname "$0")/../image-compression_amd"
 mkdir -p build/var lib
 F="-O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-result -Wno-unused-value $2"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 $F -c csrc/icx_kernels.hip -o build/var/k_$1.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 $F -I csrc -c ${KSRC:-csrc/icx_kernels.hip} -o build/var/k_$1.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $F -x hip -c csrc/icx_runtime.cpp -o build/var/r_$1.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $F -c csrc/icx_decode.hip -o build/var/d_$1.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $F -x hip -c csrc/icx_decode.cpp -o build/var/dh_$1.o

@@ -224,6 +224,55 @@ def test_two_codecs_share_the_work_queue(tmp_path):
         assert (out / n).read_bytes() == (ref_out / n).read_bytes()
 
 
+def test_four_devices_share_one_learned_cache(tmp_path, monkeypatch):
+    """Single-process multi-device mode (--devices): four codecs, one L1
+    cache - the reference's one ConcurrentHashMap (CompressionBatch.java:71,
+    ImageCompressionJpg.java:79-85, 111).  Four files with the same
+    SimilarityKey arrive one after another: the first is searched and its
+    LearnedParams put; every later one, whichever device takes its group, is a
+    cache hit (one encode at the learned quality), and the hits are served by
+    more than one device."""
+    import threading
+    import time
+    served = []
+    lock = threading.Lock()
+
+    class RecCodec(OracleCodec):
+        def fit(self, images, target, quality, cached=None, outputs=None):
+            res = super().fit(images, target, quality, cached=cached, outputs=outputs)
+            with lock:
+                served.extend((id(self), c is not None, r["cache_hit"]) for c, r in zip(cached or [None], res))
+            return res
+
+    img = smooth(180, 260, 7)
+    files = []
+    for i in range(4):  # same pixels and file size: the same (w/100, h/100, size/102400) key
+        f = tmp_path / f"same{i}.jpg"
+        write_jpeg(f, img)
+        files.append(str(f))
+    lst = tmp_path / "list.txt"
+    lst.write_text("\n".join(files))
+    orig = pipeline._prepare
+
+    def staggered(index, *a, **k):  # file k is decoded 0.4 k s after the first
+        time.sleep(0.4 * index)
+        return orig(index, *a, **k)
+
+    monkeypatch.setattr(pipeline, "_prepare", staggered)
+    codecs = [RecCodec() for _ in range(4)]
+    cache = {}
+    b = pipeline.CompressionBatch(str(lst), str(tmp_path / "out"), P, 1, str(tmp_path / "c"), codecs=codecs,
+                                  group_size=1, decode_threads=4)
+    rep = b.execute(cache=cache, save_cache=False)
+    assert rep.total == 4 and rep.success == 4
+    assert len(served) == 4
+    assert [(c, h) for _, c, h in served] == [(False, False)] + [(True, True)] * 3
+    assert len({dev for dev, _, _ in served}) >= 2  # hits on devices other than the learner's
+    assert rep.cache_size == 1
+    outs = {(tmp_path / "out" / os.path.basename(f)).read_bytes() for f in files}
+    assert len(outs) == 1  # the cached-parameter encode reproduces the searched file
+
+
 def _png_idat_rows(data, h):
     """Inflated IDAT of a single-IDAT PNG, as (h, 1 + rowbytes) filtered rows."""
     import struct

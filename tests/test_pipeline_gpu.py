@@ -70,3 +70,42 @@ def test_cli_main(codec, tmp_path):
     assert rc == 0
     outs = os.listdir(tmp_path / "out")
     assert len(outs) >= 10 and all(os.path.getsize(tmp_path / "out" / o) <= 60000 for o in outs if o.endswith(".jpg"))
+
+
+def test_config_c1_single_1080p_jpeg(codec, tmp_path):
+    """BASELINE configs[0]: one 1920x1080 q95 JPG file ->
+    -t 524288 through CompressionBatch with -w 1000 -i 1000 -s 0 (the default
+    -w/-i 1920 would reject a 1080-high image, ImageCompression.java:129-135).
+    The file equals the oracle-driven pipeline's byte for byte, and the binary
+    search ran (4-5 trial encodes, ImageCompressionJpg.java:158-200)."""
+    src = tmp_path / "c1.jpg"
+    Image.fromarray(np.ascontiguousarray(noise(1080, 1920, 1)[:, :, ::-1])).save(src, "JPEG", quality=95,
+                                                                                   subsampling=2)
+    assert os.path.getsize(src) > 524288  # a file above -t: the search has work to do
+    lst = tmp_path / "list.txt"
+    lst.write_text(str(src))
+    params = CompressionParams(0.25, 0, 1000, 1000, 524288)
+    calls = []
+
+    class Counting:
+        def __init__(self, c):
+            self.c = c
+
+        def __getattr__(self, k):
+            return getattr(self.c, k)
+
+        def fit(self, *a, **k):
+            r = self.c.fit(*a, **k)
+            calls.extend(x["encodes"] for x in r)
+            return r
+
+    gpu = pipeline.CompressionBatch(lst, tmp_path / "gpu", params, 1, tmp_path / "gc", codecs=[Counting(codec)]
+                                    ).execute()
+    cpu = pipeline.CompressionBatch(lst, tmp_path / "cpu", params, 1, tmp_path / "cc", codecs=[OracleCodec()]
+                                    ).execute()
+    assert gpu.counts[CompressionResult.COMPRESSED_SUCCESS] == cpu.counts[CompressionResult.COMPRESSED_SUCCESS] == 1
+    a = (tmp_path / "gpu" / "c1.jpg").read_bytes()
+    assert a == (tmp_path / "cpu" / "c1.jpg").read_bytes()
+    assert len(a) <= 524288 and calls and 4 <= calls[0] <= 5
+    with Image.open(tmp_path / "gpu" / "c1.jpg") as im:
+        assert im.size == (1920, 1080)
