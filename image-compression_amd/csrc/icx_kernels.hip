@@ -410,8 +410,11 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
     int16_t (*oz)[WSTR] = ws;     // natural-order output (phase D)
     const QNode& CN = nodes[D.cand_node];
     const float thr[2] = {(t & 63) ? CN.qf[0][t & 63].x : -1.0f, (t & 63) ? CN.qf[1][t & 63].x : -1.0f};
+    const int crows = (H + 1) >> 1;             // chroma rows with image data
+    const bool tail = crows - my * 8 < 8;       // ... ending inside this tile (workgroup-uniform)
 
     // ---- B: YCbCr, two Y row-DCTs, h2v2_downsample of this thread's 2x8 chroma
+    // (+ C: the chroma row DCTs, except in tail tiles)
     {
         const int i = t >> 5, sg = t & 31;
         int csum[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};  // 2x2 sums of Cb, Cr
@@ -437,20 +440,39 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
             const int blk = (sg >> 1) * 6 + (r >> 3) * 2 + (sg & 1);
             st_row8(&ws[blk][(r & 7) * 8], yv);
         }
+        uint32_t w[2];
 #pragma unroll
         for (int c = 0; c < 2; c++) {  // h2v2_downsample: bias 1, 2, 1, 2 by output column
-            uint32_t w = 0;
+            w[c] = 0;
 #pragma unroll
-            for (int j = 0; j < 4; j++) w |= (uint32_t)((csum[c][j] + 1 + (j & 1)) >> 2) << (8 * j);
-            *(uint32_t*)&cds[c][i][sg * 4] = w;
+            for (int j = 0; j < 4; j++) w[c] |= (uint32_t)((csum[c][j] + 1 + (j & 1)) >> 2) << (8 * j);
+        }
+        if (!tail) {
+            // C, fused: chroma row i of chroma block sg >> 1 is 4 + 4 samples of
+            // this lane and its neighbour (lanes 2k, 2k + 1).  The pair swaps
+            // one word by DPP (quad_perm 1,0,3,2): the even lane then holds the
+            // block row's 8 Cb samples, the odd lane its 8 Cr samples - one
+            // chroma row DCT per thread, no LDS round trip, one barrier less.
+            const int comp = sg & 1;
+            const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)(comp ? w[0] : w[1]), 0xB1, 0xF, 0xF, false);
+            const uint32_t lo = comp ? recv : w[0], hi = comp ? w[1] : recv;
+            int v[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[j] = (int)(((j < 4 ? lo : hi) >> (8 * (j & 3))) & 255) - 128;
+            fdct8<0>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+            st_row8(&ws[(sg >> 1) * 6 + 4 + comp][i * 8], v);
+        } else {
+#pragma unroll
+            for (int c = 0; c < 2; c++) *(uint32_t*)&cds[c][i][sg * 4] = w[c];
         }
     }
     __syncthreads();
 
-    // ---- C: chroma row DCT, 256 row tasks
-    {
+    // ---- C (bottom tiles whose chroma rows end inside the tile): the rows
+    // past the image replicate the last chroma row (jcprepct.c
+    // expand_bottom_edge), by index from the staged samples; 256 row tasks
+    if (tail) {
         const int comp = t >> 7, cr = (t >> 4) & 7, cb = t & 15;
-        const int crows = (H + 1) >> 1;  // chroma rows with image data
         const int re = min(cr, crows - 1 - my * 8);
         const uint2 u = *(const uint2*)&cds[comp][re][cb * 8];
         int v[8];
@@ -458,8 +480,8 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
         for (int j = 0; j < 8; j++) v[j] = (int)(((j < 4 ? u.x : u.y) >> (8 * (j & 3))) & 255) - 128;
         fdct8<0>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
         st_row8(&ws[cb * 6 + 4 + comp][cr * 8], v);
+        __syncthreads();
     }
-    __syncthreads();
 
     // ---- D: column DCT, 3 tasks per thread, in place: the thread of (block,
     // column) is the only reader and writer of that column, so the natural-

@@ -3,10 +3,15 @@
 over a file list on local disk -> output files, one MI355X.  JPEG files are
 read and header-parsed on host threads, decoded on the GPU straight into HBM,
 compressed there (compressJpgWithTargetSize, -t 1 MiB), and written back.
-Inputs: synthetic 4K q95 JPEGs (half smooth, half noise), written to a
-scratch directory first (not timed).  Runs the batch twice with the same
-cache DB: run 1 learns (full search), run 2 is the warm-cache run (C5's
-timing rule).  Prints one JSON line."""
+Inputs: synthetic 4K q95 JPEGs (half smooth, half noise), and with --png N
+as many 3840x2160 PNGs (BASELINE configs[4]'s mix: the PNG half is fitted
+into the 1920 x 1920 box on the device, icx_png_fit_batch, and re-written on
+host threads), written to a scratch directory first (not timed).  Runs the
+batch twice with the same cache DB: run 1 learns (full search), run 2 is the
+warm-cache run (C5's timing rule).  Per run: wall time, and the device time
+of each kernel family (HIP events) - the rest is host work (file reads,
+header parses, PNG decode and deflate, file writes) not hidden behind it.
+Prints one JSON line."""
 import argparse
 import io
 import json
@@ -29,6 +34,8 @@ def main():
     ap.add_argument("--distinct", type=int, default=8)
     ap.add_argument("--group", type=int, default=64)
     ap.add_argument("--dir", default=None)
+    ap.add_argument("--png", type=int, default=0, help="4K PNG files added to the list (configs[4] mix)")
+    ap.add_argument("--devices", default="0", help="GPUs driven by this process (one worker each)")
     a = ap.parse_args()
     from PIL import Image
 
@@ -51,25 +58,54 @@ def main():
         with open(p, "wb") as f:
             f.write(blobs[i % a.distinct])
         paths.append(p)
+    png_blobs = []
+    if a.png:
+        from icx.pngio import encode_png
+        for i in range(min(a.distinct, a.png)):
+            img = (smooth if i % 2 == 0 else noise)(2160, 3840, 170 + i)
+            png_blobs.append(encode_png(img, level=1))
+        for i in range(a.png):
+            p = os.path.join(src, f"p{i:05d}.png")
+            with open(p, "wb") as f:
+                f.write(png_blobs[i % len(png_blobs)])
+            paths.insert(2 * i + 1 if 2 * i + 1 <= len(paths) else len(paths), p)  # interleaved
     lst = os.path.join(work, "list.txt")
     with open(lst, "w") as f:
         f.write("\n".join(paths))
     params = CompressionParams(0.25, 1 << 20, 1920, 1920, 1 << 20)  # Execute.java defaults
-    codec = icx.Codec(0)
+    codecs = [icx.Codec(int(d)) for d in a.devices.split(",")]
+    kernels = ("dec_unstuff", "dec_init", "dec_sync", "dec_sync_r1", "dec_sync_r2", "dec_sync_r3", "dec_write",
+               "dec_dc", "dec_idct", "dec_color", "fdct", "huff", "scan", "ffscan", "stuff", "resize")
     runs = []
     for r in range(2):
         out = os.path.join(work, f"out{r}")
+        for c in codecs:
+            c.profile(True)
+            c.profile_reset()
         t0 = time.perf_counter()
-        rep = pipeline.CompressionBatch(lst, out, params, 1, os.path.join(work, "cache"), codecs=[codec],
+        rep = pipeline.CompressionBatch(lst, out, params, 1, os.path.join(work, "cache"), codecs=codecs,
                                         group_size=a.group).execute()
         dt = time.perf_counter() - t0
+        dev = {}
+        for c in codecs:
+            c.profile(False)
+            for k in kernels:
+                ms = c.profile_query(k)["ms"]
+                if ms:
+                    dev[k] = round(dev.get(k, 0.0) + ms, 2)
         runs.append({"run": "learn" if r == 0 else "warm cache", "seconds": round(dt, 3),
                      "images_per_s": round(rep.total / dt, 1), "mp_per_s": round(rep.megapixels / dt, 1),
                      "success": rep.success, "failed": rep.failed, "skipped": rep.skipped,
-                     "in_bytes": rep.original_size, "out_bytes": rep.compressed_size})
-    codec.close()
-    print(json.dumps({"metric": "CompressionBatch end-to-end (files -> files), 4K q95 JPEG, -t 1MiB, 1 GPU",
-                      "files": a.files, "group_size": a.group, "mean_src_bytes": int(np.mean([len(b) for b in blobs])),
+                     "in_bytes": rep.original_size, "out_bytes": rep.compressed_size,
+                     "device_ms": dev, "device_ms_total": round(sum(dev.values()), 1),
+                     "host_threads": pipeline.host_cores()[0]})
+    for c in codecs:
+        c.close()
+    print(json.dumps({"metric": "CompressionBatch end-to-end (files -> files), 4K q95 JPEG" +
+                                (" + 4K PNG (configs[4] mix)" if a.png else "") + ", -t 1MiB, devices " + a.devices,
+                      "files": a.files, "png_files": a.png, "group_size": a.group,
+                      "mean_src_bytes": int(np.mean([len(b) for b in blobs])),
+                      "mean_png_src_bytes": int(np.mean([len(b) for b in png_blobs])) if png_blobs else 0,
                       "runs": runs}))
     if not a.dir:
         shutil.rmtree(work, ignore_errors=True)
