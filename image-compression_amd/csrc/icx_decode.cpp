@@ -12,9 +12,13 @@
 // launches (to learn whether the entry states have settled) and once at the end.
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "../../include/icx.h"
@@ -191,13 +195,168 @@ WPlan plan_of(Uploader& U, const std::vector<int64_t>& counts, const int32_t* d_
     return out;
 }
 
+// Host threads for the progressive entropy decode: the affinity set, at most
+// 16 (ICX_HOST_THREADS overrides).
+int host_threads()
+{
+    if (const char* e = getenv("ICX_HOST_THREADS")) return std::max(1, atoi(e));
+    cpu_set_t set;
+    int n = 1;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+    return std::max(1, std::min(n, 16));
+}
+
+// Progressive files (SOF2).  Each file's scans are entropy-decoded on a host
+// thread (icx_progressive.cpp: one sequential walk per scan) straight into
+// pinned staging, in the coefficient layout k_dec_write leaves for baseline
+// files; one copy per file takes the coefficients and DC values to HBM, and
+// the device's IDCT and colour passes (the same launches as the baseline
+// tail) produce the pixels.  Device-resident files are downloaded first.
+icx_status run_progressive(icx_ctx* c, std::vector<DecItem>& items, int16_t* coef_out, size_t coef_cap)
+{
+    size_t pos = 0;
+    while (pos < items.size()) {
+        std::vector<DecItem*> sub;
+        std::vector<DecDesc> desc;
+        size_t need = 2 << 20, hneed = 2 << 20;
+        while (pos < items.size()) {
+            DecItem& it = items[pos];
+            DecDesc d{};
+            dec_geometry(it.J, it.s, d);
+            const size_t nb = (size_t)d.nblocks;
+            size_t per = align_up(nb * 128, 256) + align_up(nb * 4, 256) + 4096;
+            for (int k = 0; k < 3; k++) per += align_up((size_t)d.pw[k] * d.ph[k], 256);
+            const bool host_out = !coef_out && !is_device_ptr(it.job->out);
+            if (host_out) per += align_up(it.job->out_len, 256);
+            const size_t hper = align_up(nb * 128, 64) + align_up(nb * 4, 64) + (it.dev_in ? align_up(it.job->len, 64) : 0);
+            if (!sub.empty() && (need + per > c->budget || hneed + hper > c->budget)) break;
+            need += per;
+            hneed += hper;
+            it.host_out = host_out;
+            sub.push_back(&it);
+            desc.push_back(d);
+            pos++;
+        }
+        const int m = (int)sub.size();
+        const size_t up = Uploader::need<DecTab>(m) + Uploader::need<DecDesc>(m) + Uploader::need<DecState>(m) +
+                          Uploader::need<int32_t>(m) + 2 * Uploader::need<int64_t>(m + 1) + 4096;
+        hipError_t e = c->dev.reserve(need + up);
+        if (e == hipSuccess) e = c->host.reserve(hneed + up);
+        if (e != hipSuccess) return hip_fail(c, e, "progressive decode workspace");
+        c->dev.used = c->host.used = 0;
+        Uploader U(c, up);
+        std::vector<int16_t*> hco(m);
+        std::vector<int32_t*> hdc(m);
+        std::vector<const uint8_t*> file(m);
+        for (int k = 0; k < m; k++) {
+            const size_t nb = (size_t)desc[k].nblocks;
+            hco[k] = (int16_t*)c->host.take(nb * 128);
+            hdc[k] = (int32_t*)c->host.take(nb * 4);
+            file[k] = sub[k]->job->data;
+            if (sub[k]->dev_in) {
+                uint8_t* h = (uint8_t*)c->host.take(sub[k]->job->len);
+                if (!h) return fail(c, ICX_E_NOMEM, "pinned staging exhausted");
+                e = hipMemcpyAsync(h, file[k], sub[k]->job->len, hipMemcpyDeviceToHost, c->stream);
+                if (e != hipSuccess) return hip_fail(c, e, "progressive file download");
+                file[k] = h;
+            }
+            if (!hco[k] || !hdc[k]) return fail(c, ICX_E_NOMEM, "pinned staging exhausted");
+        }
+        // the previous sub-batch's (and the dev-in files') copies from this staging have finished
+        e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "progressive staging");
+        DecTab* h_tab;
+        DecTab* d_tab = U.alloc<DecTab>(m, &h_tab);
+        if (U.overflow) return fail(c, ICX_E_NOMEM, "upload staging exhausted");
+        std::vector<icx_status> st(m, ICX_OK);
+        {
+            HostSpan hs{c, "host.dec_progressive"};
+            std::atomic<int> next{0};
+            auto work = [&]() {
+                for (int k; (k = next++) < m;) {
+                    memset(hco[k], 0, (size_t)desc[k].nblocks * 128);
+                    h_tab[k] = DecTab{};
+                    st[k] = prog_decode(file[k], sub[k]->job->len, sub[k]->J, hco[k], hdc[k], h_tab[k].qt);
+                }
+            };
+            const int nt = std::min(m, host_threads());
+            std::vector<std::thread> pool;
+            for (int t = 1; t < nt; t++) pool.emplace_back(work);
+            work();
+            for (auto& t : pool) t.join();
+        }
+        std::vector<DecState> states(m);
+        std::vector<int32_t> ids;
+        std::vector<int64_t> cnt_blk, cnt_px, cnt_rows;
+        int64_t tpx = 0;
+        for (int k = 0; k < m; k++) {
+            icx_decode_job& j = *sub[k]->job;
+            DecDesc& d = desc[k];
+            if (st[k] != ICX_OK) {
+                j.status = st[k];
+                states[k].status = 6;
+                continue;
+            }
+            if (coef_out) {
+                const size_t nb = (size_t)d.nblocks;
+                if (nb * 64 > coef_cap) j.status = ICX_E_BUFFER;
+                else memcpy(coef_out, hco[k], nb * 128);
+                continue;
+            }
+            d.coefs = (int16_t*)c->dev.take((size_t)d.nblocks * 128);
+            d.dc = (int32_t*)c->dev.take((size_t)d.nblocks * 4);
+            e = hipMemcpyAsync(d.coefs, hco[k], (size_t)d.nblocks * 128, hipMemcpyHostToDevice, c->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(d.dc, hdc[k], (size_t)d.nblocks * 4, hipMemcpyHostToDevice, c->stream);
+            if (e != hipSuccess) return hip_fail(c, e, "coefficient upload");
+            for (int q = d.fuse420 ? 1 : 0; q < d.ncomp; q++)
+                d.plane[q] = (uint8_t*)c->dev.take((size_t)d.pw[q] * d.ph[q]);
+            d.out = sub[k]->host_out ? (uint8_t*)c->dev.take(j.out_len) : j.out;
+            d.ostride = d.ow * sub[k]->nch;
+            d.tab = d_tab + k;
+            const int64_t nmcu = (int64_t)d.mcux * d.mcuy;
+            ids.push_back(k);
+            cnt_blk.push_back(d.fuse420 ? (2 * nmcu + 31) / 32 : (d.nblocks + 31) / 32);
+            cnt_px.push_back(d.fuse420 ? 0 : ((int64_t)d.oh * ((d.ow + 3) / 4) + 255) / 256);
+            cnt_rows.push_back(d.fuse420 ? (int64_t)d.mcuy * ((d.mcux + 7) / 8) : 0);
+            tpx += (int64_t)d.w * d.h;
+        }
+        if (coef_out || ids.empty()) continue;
+        const DecDesc* d_desc = U.put(desc.data(), m);
+        const DecState* d_state = U.put(states.data(), m);
+        const int32_t* d_ids = U.put(ids.data(), ids.size());
+        const WPlan Wb = plan_of(U, cnt_blk, d_ids), Wr = plan_of(U, cnt_rows, d_ids), Wp = plan_of(U, cnt_px, d_ids);
+        if (icx_status s = U.flush()) return s;
+        {
+            Timed tm(c, "dec_idct", tpx);
+            launch_dec_idct(d_desc, d_state, Wb.p, Wb.total, c->stream);
+        }
+        {
+            Timed tm(c, "dec_color", tpx);
+            launch_dec_luma_color_420(d_desc, d_state, Wr.p, Wr.total, c->stream);
+            launch_dec_color(d_desc, d_state, Wp.p, Wp.total, c->stream);
+        }
+        for (int k : ids)
+            if (sub[k]->host_out) {
+                e = hipMemcpyAsync(sub[k]->job->out, desc[k].out, sub[k]->job->out_len, hipMemcpyDeviceToHost,
+                                   c->stream);
+                if (e != hipSuccess) return hip_fail(c, e, "output download");
+            }
+        e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(c, e, "progressive decode");
+        resolve_profile(c);
+    }
+    return ICX_OK;
+}
+
 // mode 0: decode to pixels; mode 1: coefficients only (debug: natural order, DC in [0])
 icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out, size_t coef_cap)
 {
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     hipError_t he = hipSetDevice(c->device);
     if (he != hipSuccess) return hip_fail(c, he, "hipSetDevice");
-    std::vector<DecItem> items;
+    std::vector<DecItem> items, prog;
     items.reserve(n);
     std::vector<char> dev_in(n, 0);
     for (int i = 0; i < n; i++) dev_in[i] = jobs[i].data && is_device_ptr(jobs[i].data);
@@ -243,8 +402,10 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             j.status = ICX_E_BUFFER;
             continue;
         }
-        items.push_back(it);
+        (it.J.progressive ? prog : items).push_back(it);
     }
+    if (!prog.empty())
+        if (icx_status s = run_progressive(c, prog, coef_out, coef_cap)) return s;
     size_t pos = 0;
     while (pos < items.size()) {
         // ---- size a sub-batch against the workspace budget

@@ -68,7 +68,10 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
             break;
         }
         case 0xC0:
-        case 0xC1: {  // baseline / extended sequential, Huffman
+        case 0xC1:
+        case 0xC2: {  // baseline / extended sequential / progressive, Huffman
+            if (sof) return ICX_E_CORRUPT;
+            J.progressive = m == 0xC2;
             if (n < 6) return ICX_E_CORRUPT;
             J.h = (s[1] << 8) | s[2];
             J.w = (s[3] << 8) | s[4];
@@ -102,14 +105,16 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
             if (!sof) return ICX_E_CORRUPT;
             if (unsupported) return ICX_E_UNSUPPORTED;
             const int ns = n >= 1 ? s[0] : 0;
-            if (ns != J.ncomp || n < 1 + 2 * (size_t)ns + 3) return ICX_E_UNSUPPORTED;  // multi-scan
-            for (int k = 0; k < ns; k++) {
-                if (s[1 + 2 * k] != J.id[k]) return ICX_E_UNSUPPORTED;
-                J.td[k] = s[2 + 2 * k] >> 4;
-                J.ta[k] = s[2 + 2 * k] & 15;
-                if (J.td[k] > 3 || J.ta[k] > 3) return ICX_E_CORRUPT;
+            if (!J.progressive) {
+                if (ns != J.ncomp || n < 1 + 2 * (size_t)ns + 3) return ICX_E_UNSUPPORTED;  // multi-scan
+                for (int k = 0; k < ns; k++) {
+                    if (s[1 + 2 * k] != J.id[k]) return ICX_E_UNSUPPORTED;
+                    J.td[k] = s[2 + 2 * k] >> 4;
+                    J.ta[k] = s[2 + 2 * k] & 15;
+                    if (J.td[k] > 3 || J.ta[k] > 3) return ICX_E_CORRUPT;
+                }
+                if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0) return ICX_E_UNSUPPORTED;
             }
-            if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0) return ICX_E_UNSUPPORTED;
             J.scan_off = i;
             // colour space (jdapimin.c default_decompress_parms): JFIF or ids 1,2,3 -> YCbCr
             if (J.ncomp == 3) {
@@ -118,13 +123,15 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
                 if (J.hs[1] != 1 || J.vs[1] != 1 || J.hs[2] != 1 || J.vs[2] != 1) return ICX_E_UNSUPPORTED;
                 if (J.hs[0] > 2 || J.vs[0] > 2 || (J.hs[0] == 1 && J.vs[0] == 2)) return ICX_E_UNSUPPORTED;
             }
-            for (int c = 0; c < J.ncomp; c++)
-                if (!J.qt_ok[J.tq[c]] || !J.h_ok[0][J.td[c]] || !J.h_ok[1][J.ta[c]]) return ICX_E_CORRUPT;
+            // progressive: tables may be (re)defined between scans; prog_decode checks each scan's
+            if (!J.progressive)
+                for (int c = 0; c < J.ncomp; c++)
+                    if (!J.qt_ok[J.tq[c]] || !J.h_ok[0][J.td[c]] || !J.h_ok[1][J.ta[c]]) return ICX_E_CORRUPT;
             return ICX_OK;
         }
         default:
-            if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
-                // progressive / lossless / arithmetic: dimensions only
+            if (m >= 0xC3 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+                // lossless / hierarchical / arithmetic: dimensions only
                 if (n >= 6) {
                     J.h = (s[1] << 8) | s[2];
                     J.w = (s[3] << 8) | s[4];

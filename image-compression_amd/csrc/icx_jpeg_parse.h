@@ -3,8 +3,10 @@
 // The JDK reader (reached from ImageCompression.java:119-155) parses the
 // header with libjpeg's jdmarker.c; this is the baseline subset the device
 // decoder implements: SOF0/SOF1 8-bit, one interleaved scan (or a single grey
-// component), Huffman coding, optional DRI.  Everything else (progressive,
-// arithmetic, lossless, 12-bit, CMYK/YCCK, Adobe RGB, multi-scan sequential,
+// component), Huffman coding, optional DRI; and SOF2 progressive files (8-bit
+// Huffman, same components and sampling) whose scans icx_progressive.cpp
+// decodes on the host.  Everything else (arithmetic, lossless, 12-bit,
+// CMYK/YCCK, Adobe RGB, multi-scan sequential,
 // 4:4:0 and exotic sampling) is reported as ICX_E_UNSUPPORTED with the image
 // dimensions filled in, so the caller can still apply the dimension gate
 // (ImageCompression.java:131) and route the file to a host decoder.
@@ -26,7 +28,8 @@ struct JpegHeader {
     uint8_t hvals[2][4][256] = {};
     int hn[2][4] = {};
     bool h_ok[2][4] = {};
-    size_t scan_off = 0;  // first byte of the entropy-coded segment
+    size_t scan_off = 0;  // first byte of the entropy-coded segment (progressive: of the first scan)
+    bool progressive = false;  // SOF2: td/ta/scan_off unused, prog_decode walks every scan
 };
 
 // Parse markers up to the SOS.  `avail` bytes of the file are present at p
@@ -43,5 +46,15 @@ bool build_dec_tab(const JpegHeader& J, DecTab& T);
 
 // DecTab::sel packed 4 bits per entry, as dec_walk takes it.
 uint32_t dec_selector(const DecTab& T);
+
+// Entropy decode of a progressive file (icx_progressive.cpp) whose header
+// parse_jpeg accepted: all scans into coefs (nblocks x 64, zeroed by the
+// caller, natural order, MCU order as dec_geometry lays blocks out; DC value
+// in [0]) and dc (nblocks DC values); qt receives each component's latched
+// dequantisation table (natural order).  ICX_E_UNSUPPORTED: the JDK would
+// block-smooth this file (AC 1..5 not fully refined); ICX_E_CORRUPT: any
+// stream anomaly libjpeg would only warn about.
+icx_status prog_decode(const uint8_t* p, size_t len, const JpegHeader& J, int16_t* coefs, int32_t* dc,
+                       uint16_t (*qt)[64]);
 
 }  // namespace icx

@@ -26,6 +26,7 @@ EXPORTS = [
     "icx_resize_bilinear", "icx_png_fit", "icx_num_blocks", "icx_debug_fdct",
     "icx_profile_enable", "icx_profile_reset", "icx_profile_query",
     "icx_jpeg_info", "icx_decode_jpg", "icx_decode_jpg_batch", "icx_debug_decode_coefs",
+    "icx_debug_progressive_coefs",
     "icx_device_alloc", "icx_device_free", "icx_memcpy", "icx_host_alloc", "icx_host_free",
     "icx_png_bound", "icx_png_encode", "icx_png_fit_batch",
 ]
@@ -126,6 +127,7 @@ def load():
         "icx_decode_jpg": (c.c_int, [c.c_void_p, P(DecodeJob)]),
         "icx_decode_jpg_batch": (c.c_int, [c.c_void_p, P(DecodeJob), c.c_int32]),
         "icx_debug_decode_coefs": (c.c_int, [c.c_void_p, c.c_void_p, c.c_size_t, P(c.c_int16), c.c_size_t]),
+        "icx_debug_progressive_coefs": (c.c_int, [c.c_void_p, c.c_size_t, P(c.c_int16), c.c_size_t]),
         "icx_device_alloc": (c.c_int, [c.c_void_p, c.c_size_t, P(c.c_void_p)]),
         "icx_device_free": (c.c_int, [c.c_void_p, c.c_void_p]),
         "icx_memcpy": (c.c_int, [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]),

@@ -580,7 +580,7 @@ def _scan_blocks(a):
             i += 1
             continue
         m = int(a[i + 1])
-        if m in (0xC0, 0xC1):
+        if m in (0xC0, 0xC1, 0xC2):
             h = int(a[i + 5]) << 8 | int(a[i + 6])
             w = int(a[i + 7]) << 8 | int(a[i + 8])
             nc = int(a[i + 9])
@@ -592,7 +592,20 @@ def _scan_blocks(a):
             i += 1
             continue
         i += 2 + (int(a[i + 2]) << 8 | int(a[i + 3]))
-    raise ValueError("no SOF0/SOF1 marker")
+    raise ValueError("no SOF0/SOF1/SOF2 marker")
+
+
+def progressive_coefs(data) -> np.ndarray:
+    """Coefficients of a progressive JPEG from the host entropy decode the
+    device decoder's progressive path uses (icx_debug_progressive_coefs)."""
+    lib = N.load()
+    a = np.frombuffer(bytes(data), np.uint8)
+    out = np.zeros((_scan_blocks(a), 64), np.int16)
+    st = lib.icx_debug_progressive_coefs(a.ctypes.data, a.nbytes, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)),
+                                         out.size)
+    if st != N.OK:
+        raise N.IcxError(st, "icx_debug_progressive_coefs")
+    return out
 
 
 def quality_tables(quality: float):

@@ -14,14 +14,17 @@ Differences that are design, not semantics:
     (the reference's lookups also race with other tasks' puts: results of
     both depend on completion order).
 JPEG files the device decoder supports (baseline/extended Huffman, one
-interleaved scan or grey, any restart interval — icx_jpeg_info) are only read
-and header-parsed on the host threads; each device group decodes them on the
-GPU (icx_decode_jpg_batch: the JDK reader's IJG 6b arithmetic plus source
-subsampling) straight into HBM tensors that the encoder then reads, so no
-decoded pixel crosses PCIe.  Other files (progressive/CMYK JPEG, PNG, GIF,
-BMP, ...) and JPEGs the device decoder rejects as corrupt are decoded on the
-host with libjpeg-turbo / Pillow (6b-lineage ISLOW IDCT + h2v2 fancy
-upsampling for JPEG).
+interleaved scan or grey, any restart interval; progressive Huffman files with
+the same layouts — icx_jpeg_info) are only read and header-parsed on the host
+threads; each device group decodes them on the GPU (icx_decode_jpg_batch: the
+JDK reader's IJG 6b arithmetic plus source subsampling; a progressive file's
+scans are entropy-decoded by libicx on host threads, its IDCT and colour run
+on the device) straight into HBM tensors that the encoder then reads, so no
+decoded pixel crosses PCIe.  Other files (CMYK/YCCK or arithmetic JPEG, PNG,
+GIF, BMP, ...) and JPEGs the device decoder rejects (corrupt, or a truncated
+progressive script the JDK would block-smooth) are decoded on the host with
+libjpeg-turbo / Pillow (6b-lineage ISLOW IDCT + h2v2 fancy upsampling for
+JPEG).
 """
 import concurrent.futures as cf
 import logging

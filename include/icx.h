@@ -276,6 +276,11 @@ icx_status icx_memcpy(icx_ctx* ctx, void* dst, const void* src, size_t bytes);
 /* Quantised coefficients after DC prediction (natural order, 64 per block,
  * scan/MCU block order incl. dummy blocks) as the device decoder produced them. */
 icx_status icx_debug_decode_coefs(icx_ctx* ctx, const uint8_t* data, size_t len, int16_t* coefs, size_t ncoefs);
+/* Host-only: the progressive (SOF2) entropy decode the device decoder's
+ * progressive path runs on host threads (every scan, jdphuff.c semantics),
+ * same layout as icx_debug_decode_coefs (DC value in [0]).  ICX_E_INVALID for
+ * a sequential file; no context and no GPU needed. */
+icx_status icx_debug_progressive_coefs(const uint8_t* data, size_t len, int16_t* coefs, size_t ncoefs);
 
 /* Raw jpeg_fdct_islow coefficients (x8 scale, before quantisation) in scan
  * block order (MCU: Y0 Y1 Y2 Y3 Cb Cr), zig-zag within each block: the

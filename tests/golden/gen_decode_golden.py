@@ -15,8 +15,12 @@ out on purpose: libjpeg-turbo upsamples it with a triangle filter where 6b
 replicates rows, so it cannot pin the JDK there.
 
 Inputs are synthetic (seeded), encoded by Pillow at several qualities,
-chroma layouts and restart intervals, plus a progressive file that the
-decoder must refuse (the device path is baseline-only; the JDK reads it).
+chroma layouts and restart intervals, plus progressive (SOF2) files: the
+oracle restates the baseline decoder only and refuses them ("unsupported"),
+the device decoder reads them ("progressive": host entropy decode of every
+scan, device IDCT and colour).  libjpeg-turbo applies no block smoothing to
+these (every scan script Pillow writes refines AC 1..5 fully), so it pins the
+JDK's final output pass for them as for baseline files.
 """
 import io
 import json
@@ -103,12 +107,30 @@ def main():
         expect[name] = out
         meta["cases"][name] = {"w": int(out.shape[1]), "h": int(out.shape[0]),
                                "ncomp": 1 if out.ndim == 2 else 3, "params": kw, "bytes": len(data)}
-    # progressive: refused by the baseline decoder (status 5)
+    # progressive: refused by the baseline oracle (status 5), decoded by the device path
     seed += 1
     prog = encode(smooth(32, 48, seed), quality=80, progressive=True)
     jpegs["progressive_32x48"] = np.frombuffer(prog, np.uint8)
-    meta["cases"]["progressive_32x48"] = {"w": 48, "h": 32, "ncomp": 3, "unsupported": True,
+    expect["progressive_32x48"] = decode_bgr(prog)
+    meta["cases"]["progressive_32x48"] = {"w": 48, "h": 32, "ncomp": 3, "unsupported": True, "progressive": True,
                                           "params": {"progressive": True}, "bytes": len(prog)}
+    pcases = [("prog_c130x250_s2_q95", smooth(130, 250, 501), dict(quality=95, subsampling=2)),
+              ("prog_c66x130_s1_q50", noise(66, 130, 502), dict(quality=50, subsampling=1)),
+              ("prog_c47x61_s0_q90", smooth(47, 61, 503), dict(quality=90, subsampling=0)),
+              ("prog_g66x130_q85", smooth(66, 130, 504)[:, :, 1], dict(quality=85)),
+              ("prog_rst3_130x250", smooth(130, 250, 505), dict(quality=85, subsampling=2, restart_marker_blocks=3)),
+              ("prog_rstrows_g47x61", smooth(47, 61, 506)[:, :, 2], dict(quality=75, restart_marker_rows=1)),
+              ("prog_c7x9_s2_q95", noise(7, 9, 507), dict(quality=95, subsampling=2)),
+              ("prog_c1x1_s2_q75", smooth(1, 1, 508), dict(quality=75, subsampling=2)),
+              ("prog_q100_noise_40x72", noise(40, 72, 509), dict(quality=100, subsampling=2))]
+    for name, img, kw in pcases:
+        data = encode(img, progressive=True, **kw)
+        out = decode_bgr(data)
+        jpegs[name] = np.frombuffer(data, np.uint8)
+        expect[name] = out
+        meta["cases"][name] = {"w": int(out.shape[1]), "h": int(out.shape[0]), "ncomp": 1 if out.ndim == 2 else 3,
+                               "unsupported": True, "progressive": True, "params": dict(kw, progressive=True),
+                               "bytes": len(data)}
     np.savez_compressed(os.path.join(HERE, "decode_golden.npz"),
                         **{f"jpg:{k}": v for k, v in jpegs.items()},
                         **{f"px:{k}": v for k, v in expect.items()})

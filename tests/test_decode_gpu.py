@@ -29,12 +29,13 @@ def test_decode_coefficients_match_oracle(codec, oracle, dgolden):
 
 
 def test_decode_pixels_match_golden_batch(codec, dgolden):
-    """All golden files in one batch (grey, 4:2:0, 4:2:2, 4:4:4, DRI, q1..q100)."""
+    """All golden files in one batch (grey, 4:2:0, 4:2:2, 4:4:4, DRI, q1..q100,
+    and progressive files, which take the host-entropy / device-pixel path)."""
     meta, jpgs, pxs = dgolden
     names = list(jpgs)
     res = codec.decode_jpg_batch([jpgs[k] for k in names], subsampling=1)
     for name, (st, img) in zip(names, res):
-        if meta["cases"][name].get("unsupported"):
+        if meta["cases"][name].get("unsupported") and not meta["cases"][name].get("progressive"):
             assert st == N.E_UNSUPPORTED, name
             continue
         assert st == N.OK, (name, st)
@@ -208,3 +209,60 @@ def test_decode_device_inputs_unaligned_and_long_headers(codec, dgolden):
     res = codec.decode_jpg_batch([d.cpu().numpy().tobytes() for d in datas], subsampling=1)
     for i, (st, img) in enumerate(res):
         assert st == N.OK and np.array_equal(img, want[i]), i
+
+
+def _sos_offsets(data):
+    return [i for i in range(len(data) - 1) if data[i] == 0xFF and data[i + 1] == 0xDA]
+
+
+def test_progressive_golden_subsampled_device_io(codec, dgolden):
+    """Progressive golden files (libjpeg-turbo pixels) at s = 1, 2, 3, with
+    host, libicx and CUDA-tensor inputs and device outputs: the device IDCT /
+    colour passes over the host entropy decode."""
+    import torch
+
+    import icx
+    meta, jpgs, pxs = dgolden
+    names = [k for k in jpgs if meta["cases"][k].get("progressive")]
+    for s in (1, 2, 3):
+        for name in names:
+            want = pxs[name][::s, ::s]
+            img = codec.decode_jpg(jpgs[name], subsampling=s, device_out=True)
+            assert isinstance(img, icx.DeviceImage) and np.array_equal(img.numpy(), want), (name, s)
+            dev_in = icx.DeviceImage.from_host(codec, jpgs[name])
+            assert np.array_equal(codec.decode_jpg(dev_in, subsampling=s), want), (name, s)
+            t_in = torch.from_numpy(np.frombuffer(jpgs[name], np.uint8).copy()).cuda()
+            assert np.array_equal(codec.decode_jpg(t_in, subsampling=s), want), (name, s)
+
+
+@pytest.mark.parametrize("shape,sub", [((2160, 3840), 2), ((1080, 1920), 1), ((1081, 1917), 0), ((999, 1001), 2)])
+def test_progressive_equals_baseline_twin_decode(codec, oracle, shape, sub):
+    """A progressive file decodes to exactly the oracle's decode of its
+    baseline twin (same pixels, same tables: same coefficients), at BASELINE
+    sizes, in a batch mixed with baseline files."""
+    from PIL import Image
+    img = smooth(*shape, 21)
+    pil = Image.fromarray(np.ascontiguousarray(img[:, :, ::-1]))
+    a, b = io.BytesIO(), io.BytesIO()
+    pil.save(a, "JPEG", quality=95, subsampling=sub)
+    pil.save(b, "JPEG", quality=95, subsampling=sub, progressive=True)
+    base, prog = a.getvalue(), b.getvalue()
+    rc, ref = oracle.jpeg_decode(base)
+    assert rc == 0
+    res = codec.decode_jpg_batch([prog, base, prog], subsampling=1)
+    for st, got in res:
+        assert st == N.OK and np.array_equal(got, ref)
+    assert np.array_equal(codec.debug_decode_coefs(prog), oracle.jpeg_coefs(base))
+
+
+def test_progressive_refusals_in_a_batch(codec, dgolden):
+    """A truncated scan script (the JDK would block-smooth it) is unsupported,
+    a scan cut short is corrupt; neither spoils its batch neighbours."""
+    meta, jpgs, pxs = dgolden
+    good = jpgs["prog_c130x250_s2_q95"]
+    sos = _sos_offsets(good)
+    bad = [good[:sos[5]] + b"\xff\xd9", good[:sos[3] + 50]]
+    res = codec.decode_jpg_batch(bad + [good, jpgs["c130x250_s2_q95"]], subsampling=1)
+    assert res[0][0] == N.E_UNSUPPORTED and res[1][0] == N.E_CORRUPT
+    assert res[2][0] == N.OK and np.array_equal(res[2][1], pxs["prog_c130x250_s2_q95"])
+    assert res[3][0] == N.OK and np.array_equal(res[3][1], pxs["c130x250_s2_q95"])

@@ -27,6 +27,11 @@ def _make_inputs(d):
     g = d / "grey.jpg"
     Image.fromarray(smooth(400, 500, 99)[:, :, 1]).save(g, "JPEG", quality=95)
     files.append(str(g))
+    # progressive: device pixel path here, host Pillow decode on the oracle side
+    pj = d / "prog.jpg"
+    Image.fromarray(np.ascontiguousarray(smooth(480, 640, 98)[:, :, ::-1])).save(pj, "JPEG", quality=95,
+                                                                                progressive=True)
+    files.append(str(pj))
     p = d / "pic.png"
     Image.fromarray(smooth(500, 700, 5)[:, :, ::-1]).save(p)
     files.append(str(p))
