@@ -559,11 +559,12 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         DecState* d_state = U.put(states.data(), m);
         const int32_t* d_ids = U.put(ids.data(), m);
 
-        std::vector<int64_t> cnt_tiles(m), cnt_subs(m), cnt_blk(m), cnt_px(m), cnt_rows(m);
+        std::vector<int64_t> cnt_tiles(m), cnt_subs(m), cnt_pieces(m), cnt_blk(m), cnt_px(m), cnt_rows(m);
         int64_t stuffed = 0;
         for (int k = 0; k < m; k++) {
             cnt_tiles[k] = sub[k]->ntiles;
             cnt_subs[k] = (desc[k].nsub_max + 1 + 255) / 256;
+            cnt_pieces[k] = ((int64_t)(desc[k].nsub_max + 1) * dec_pieces(S) + 255) / 256;  // k_dec_write
             // colour: luma IDCT fused with upsampling + conversion for s == 1 4:2:0 fancy (chroma
             // blocks alone go through k_dec_idct), the per-pixel gather kernel otherwise
             const DecDesc& q = desc[k];
@@ -603,7 +604,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             std::vector<int64_t> a, b, r, q;
             int64_t stf = 0, tpx = 0;
             for (int k : ks) {
-                a.push_back(cnt_subs[k]);
+                a.push_back(cnt_pieces[k]);
                 b.push_back(cnt_blk[k]);
                 r.push_back(cnt_rows[k]);
                 q.push_back(cnt_px[k]);

@@ -600,6 +600,44 @@ ICX_HD uint64_t dec_sync_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, 
     return w.state();
 }
 
+// Write-pass pieces.  After the sync has settled, the checkpoints of
+// subsequence j are states of its true walk (the last walk of j started from
+// the final E[j]; a re-walk that met its previous walk spliced the rest with
+// the block-count difference), so the write pass splits every subsequence
+// at them: piece p of j starts at E[j] (p = 0) or at checkpoint p - 1, with
+// the blocks completed before it (boff[j] + the checkpoint's count), and
+// stops at the first symbol boundary at or beyond the next mark (the end of
+// the subsequence for the last piece).  Ownership is as for subsequences: a
+// block belongs to the piece where its DC symbol starts.  A piece whose
+// checkpoint was never reached (the walk ended first) has nothing to do.
+struct DecPiece {
+    uint64_t e;     // entry state
+    int64_t blk;    // blocks completed before it
+    uint32_t stop;  // exit mark
+    bool have;
+};
+ICX_HD int dec_pieces(uint32_t sub_bits) { return dec_ck_slots(sub_bits) + 1; }
+
+template <class P64, class P32>
+ICX_HD DecPiece dec_piece(P64 est, P64 ck, P32 boff, uint32_t j, int p, uint32_t sub_bits)
+{
+    const int np = dec_pieces(sub_bits);
+    const uint32_t base = j * sub_bits;
+    DecPiece r;
+    r.stop = p + 1 < np ? base + (uint32_t)(p + 1) * dec_ck_bits(sub_bits) : base + sub_bits;
+    r.have = true;
+    if (p == 0) {
+        r.e = est[j];
+        r.blk = (int64_t)boff[j];
+        return r;
+    }
+    const uint64_t c = ck[(int64_t)j * DEC_CK_MAX + p - 1];
+    r.have = c != DEC_CK_NONE;
+    r.e = c & DEC_CK_STATE;
+    r.blk = (int64_t)boff[j] + (int64_t)(c >> 48);
+    return r;
+}
+
 // Unstuffing rule for stuffed byte i (jdhuff.c fill_bit_buffer / jdmarker.c):
 // returns output bytes it contributes (0, 1, or DEC_PAD for an RSTn code byte);
 // *rst = 1 for an RSTn code byte.

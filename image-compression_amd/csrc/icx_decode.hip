@@ -605,8 +605,13 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
     const DecDesc& d = D[img];
     const DecState& st = S[img];
     if (st.status) return;
-    const int64_t j = wg * 256 + threadIdx.x;
-    if (wg * 256 >= (int64_t)st.nsub) return;
+    // thread = one piece of a subsequence (dec_piece): the pieces of one
+    // subsequence sit in neighbouring lanes, so a wave reads a contiguous
+    // stretch of the stream
+    const int np = dec_pieces(sub_bits);
+    const int64_t t = wg * 256 + threadIdx.x;
+    if (wg * 256 >= (int64_t)st.nsub * np) return;
+    const int64_t j = t / np;
     const int lane = threadIdx.x & 63;
     uint32_t* wave_slots = slots + (threadIdx.x - lane) * SLOT_DW;
     uint32_t* mys = slots + threadIdx.x * SLOT_DW;
@@ -619,17 +624,19 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
         }
         __syncthreads();
     }
-    const uint32_t stop = (uint32_t)(j + 1) * sub_bits;
+    DecPiece pc{0, 0, 0, false};
+    if (j < st.nsub)
+        pc = dec_piece((const ICX_GLOBAL uint64_t*)d.est, (const ICX_GLOBAL uint64_t*)d.ck,
+                       (const ICX_GLOBAL uint32_t*)d.boff, (uint32_t)j, (int)(t - j * np), sub_bits);
+    const uint32_t stop = pc.stop;
     const SplitHuff H{(const uint16_t (*)[1 << DEC_LUT_BITS])L1, (const ICX_GLOBAL DecHuff*)d.tab->h};
     DecWalker<true, SplitHuff> w = dec_walker<true>(d, H, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent,
-                                                    d.seg, st.nseg, st.ent_len * 8,
-                                                    j < st.nsub ? (int64_t)d.boff[j] : 0);
+                                                    d.seg, st.nseg, st.ent_len * 8, pc.blk);
     bool run = false;
-    if (j < st.nsub) {
-        const uint64_t e = d.est[j];
-        run = !(dec_pos(e) >= stop && (e & 63) == 0);
+    if (pc.have) {
+        run = !(dec_pos(pc.e) >= stop && (pc.e & 63) == 0);
         if (run) {
-            w.start(e);
+            w.start(pc.e);
             run = w.running(stop);
         }
     }

@@ -167,20 +167,23 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
             memset(buf, 0, sizeof(buf));
         }
     };
+    // (as k_dec_write: one walk per piece of a subsequence, split at its checkpoints)
     bool bad = false;
-    std::vector<uint32_t> order(nsub);
-    for (uint32_t j = 0; j < nsub; j++) order[j] = j;
+    const int np = dec_pieces(S);
+    std::vector<uint32_t> order((size_t)nsub * np);
+    for (uint32_t t = 0; t < order.size(); t++) order[t] = t;
     if (seed) std::shuffle(order.begin(), order.end(), rng);
-    for (uint32_t j : order) {
+    for (uint32_t t : order) {
         Sink sk;
         sk.out = coefs.data();
         sk.dcs = dc.data();
-        const uint64_t e = est[j];
-        if (dec_pos(e) >= (j + 1) * S && (e & 63) == 0) continue;
+        const uint32_t j = t / np;
+        const DecPiece pc = dec_piece(est.data(), ck.data(), boff.data(), j, (int)(t % np), S);
+        if (!pc.have || (dec_pos(pc.e) >= pc.stop && (pc.e & 63) == 0)) continue;
         DecWalker<true, const DecHuff*> w = dec_walker<true>(d, (const DecHuff*)T.h, T.slow, sel, words.data(),
-                                                             seg.data(), (uint32_t)seg.size(), ent_len * 8, boff[j]);
-        w.start(e);
-        while (w.running((j + 1) * S)) w.step(sk);
+                                                             seg.data(), (uint32_t)seg.size(), ent_len * 8, pc.blk);
+        w.start(pc.e);
+        while (w.running(pc.stop)) w.step(sk);
         bad |= w.bad;  // as k_dec_write: an invalid code on the true path = corrupt data
     }
     if (bad) return ICX_E_CORRUPT;
