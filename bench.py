@@ -278,8 +278,8 @@ def main():
                     help="4K frames for the CPU baseline (0 = 20 per host core, at least 320: ~10 s of wall time)")
     ap.add_argument("--e2e", type=int, default=200,
                     help="frames (distinct sources) of the decode+encode leg (0 = skip)")
-    ap.add_argument("--host-io-frames", type=int, default=200,
-                    help="frames of the PCIe-inclusive leg (pinned host in/out; 0 = skip)")
+    ap.add_argument("--host-io-frames", type=int, default=1000,
+                    help="frames of the PCIe-inclusive leg (pinned host in/out; 0 = skip; default: configs[1]'s 1000)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
     ap.add_argument("--target", type=int, default=TARGET, help="-t bytes (default 1 MiB)")
