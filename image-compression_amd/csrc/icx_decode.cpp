@@ -131,7 +131,9 @@ void dec_geometry(const JpegHeader& J, int s, DecDesc& d)
         d.ph[c] = (d.ch[c] + 7) / 8 * 8;
     }
     d.fancy = J.ncomp == 3 && d.hs == 2 && d.cw[1] > 2;  // do_fancy_upsampling && downsampled_width > 2
-    d.fuse420 = s == 1 && J.ncomp == 3 && d.hs == 2 && d.vs == 2 && d.fancy;
+    d.rgb = J.ncomp == 3 && J.rgb;
+    d.wmcu = dec_walk_mcu(J.ncomp, d.nbmcu, J.td, J.ta);
+    d.fuse420 = s == 1 && J.ncomp == 3 && d.hs == 2 && d.vs == 2 && d.fancy && !d.rgb;
     d.s = s;
     d.ow = (J.w + s - 1) / s;
     d.oh = (J.h + s - 1) / s;

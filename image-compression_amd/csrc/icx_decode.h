@@ -104,7 +104,23 @@ struct DecDesc {
     int32_t fancy;         // chroma upsampled with the triangle filter (cw > 2)
     int32_t fuse420;       // s == 1, 4:2:0, fancy: luma IDCT fused into the colour pass (no luma plane)
     int32_t s, ow, oh, ostride;
+    int32_t rgb;           // components are R, G, B (jdcolor.c null_convert), not YCbCr
+    int32_t wmcu;          // blocks per MCU as the entropy walk sees them (dec_walk_mcu)
 };
+
+// Blocks per MCU for the entropy walks: a walk's block-in-MCU index only
+// selects Huffman tables, so when every component of the scan uses the same
+// DC and the same AC table (RGB files, for one) all indices are equivalent
+// and the walks keep it at 0.  Otherwise two walks that differ only in it
+// would never compare equal - the relaxation would carry that phantom
+// difference through every subsequence (one launch each).  Block counts,
+// ownership and the DC predictors use absolute block indices and are
+// unaffected.
+ICX_HD int dec_walk_mcu(int ncomp, int nbmcu, const int* td, const int* ta)
+{
+    if (ncomp != 3) return nbmcu;
+    return td[0] == td[1] && td[0] == td[2] && ta[0] == ta[1] && ta[0] == ta[2] ? 1 : nbmcu;
+}
 
 // One k_stage copy: len bytes from src (any alignment, device memory) to dst
 // (16-byte aligned), then zeros up to dst_len (a multiple of 16).  src may
@@ -287,14 +303,15 @@ ICX_HD int dec_nat(int z)
     return N[z > 63 ? 63 : z];
 }
 
-// First interval start strictly after byte `byte` (DEC_END if none).
-ICX_HD uint32_t dec_next_seg(const ICX_GLOBAL uint32_t* seg, uint32_t nseg, uint32_t byte)
+// First interval start strictly after byte `byte` (DEC_END if none); *k = its index.
+ICX_HD uint32_t dec_next_seg(const ICX_GLOBAL uint32_t* seg, uint32_t nseg, uint32_t byte, uint32_t* k)
 {
     uint32_t lo = 0, hi = nseg;  // find first k with seg[k] > byte
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
         if (seg[mid] > byte) hi = mid; else lo = mid + 1;
     }
+    *k = lo;
     return lo < nseg ? seg[lo] : DEC_END;
 }
 
@@ -345,6 +362,7 @@ struct DecWalker {
     const ICX_GLOBAL uint32_t* seg;
     uint32_t nseg, ent_bits;
     int nby, nbmcu;    // descriptor fields the walk uses, held in registers
+    int ri, nbm;       // restart interval (MCUs) and blocks per MCU: the interval-end check
     int64_t nblocks;
     uint32_t pos, n;
     int b, z, comp;
@@ -410,7 +428,8 @@ struct DecWalker {
     // in an interval's padding move to the next interval or the end.
     ICX_HD void invalid()
     {
-        const uint32_t nx = dec_next_seg(seg, nseg, pos >> 3);
+        uint32_t k;
+        const uint32_t nx = dec_next_seg(seg, nseg, pos >> 3, &k);
         const uint32_t bound = nx == DEC_END ? ent_bits : (nx - DEC_PAD) * 8;  // end of interval data
         b = 0;
         z = 0;
@@ -427,6 +446,10 @@ struct DecWalker {
             pos = DEC_END;
             return;
         }
+        // the true walk leaves interval k-1 after exactly its ri MCUs; an RSTn
+        // anywhere else (a stray or missing marker) is corrupt data, on which
+        // libjpeg's resynchronisation and zero fill would give other pixels
+        if (OWNED && ri > 0 && blk_base + (int64_t)n != (int64_t)k * ri * nbm) bad = true;
         pos = nx * 8;
         R.init(words, pos);
     }
@@ -446,7 +469,9 @@ ICX_HD DecWalker<OWNED, HuffPtr> dec_walker(const DecDesc& d, HuffPtr H, const D
     w.nseg = nseg;
     w.ent_bits = ent_bits;
     w.nby = d.nby;
-    w.nbmcu = d.nbmcu;
+    w.nbmcu = d.wmcu;
+    w.ri = d.ri;
+    w.nbm = d.nbmcu;
     w.nblocks = d.nblocks;
     w.blk_base = blk_base;
     return w;

@@ -949,6 +949,12 @@ __global__ void __launch_bounds__(256) k_dec_color(const DecDesc* D, const DecSt
         const int yy = yrow[X];
         const int cb = chroma_at(d, d.plane[1], d.pw[1], d.cw[1], d.ch[1], X, Y) - 128;
         const int cr = chroma_at(d, d.plane[2], d.pw[2], d.cw[1], d.ch[1], X, Y) - 128;
+        if (d.rgb) {  // null_convert (jdcolor.c): R, G, B as stored
+            px[3 * k + 0] = (uint8_t)(cr + 128);
+            px[3 * k + 1] = (uint8_t)(cb + 128);
+            px[3 * k + 2] = (uint8_t)yy;
+            continue;
+        }
         // ycc_rgb_convert (jdcolor.c), SCALEBITS 16
         px[3 * k + 0] = clamp255(yy + ((116130 * cb + 32768) >> 16));
         px[3 * k + 1] = clamp255(yy + ((-22554 * cb + 32768 - 46802 * cr) >> 16));

@@ -12,6 +12,23 @@ const uint8_t kNat[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11
                           58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 }
 
+// Colour space of a 3-component file as the JDK reader settles it: libjpeg's
+// guess (jdapimin.c default_decompress_parms: JFIF -> YCbCr; an Adobe marker's
+// transform 0 -> RGB, else YCbCr; no marker: ids 1,2,3 -> YCbCr, 'R','G','B'
+// -> RGB, else YCbCr), then OpenJDK imageioJPEG.c's override of a YCbCr
+// guess: an Adobe transform other than 1 -> unknown (-1: left to the host
+// reader); no JFIF and no EXIF marker, ids other than 1,2,3 and every
+// component sampled alike -> RGB.  0 YCbCr, 1 RGB.
+int colour_space(const JpegHeader& J, bool jfif, bool exif, bool adobe, int transform)
+{
+    if (jfif) return 0;
+    if (adobe) return transform == 0 ? 1 : transform == 1 ? 0 : -1;
+    if (J.id[0] == 1 && J.id[1] == 2 && J.id[2] == 3) return 0;
+    if (J.id[0] == 'R' && J.id[1] == 'G' && J.id[2] == 'B') return 1;
+    if (exif) return 0;
+    return J.hs[1] == J.hs[0] && J.hs[2] == J.hs[0] && J.vs[1] == J.vs[0] && J.vs[2] == J.vs[0];
+}
+
 icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& J)
 {
     J = JpegHeader{};
@@ -19,7 +36,8 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
     if (avail < 4) return ICX_E_BUFFER;
     if (p[0] != 0xFF || p[1] != 0xD8) return ICX_E_CORRUPT;
     size_t i = 2;
-    bool sof = false, unsupported = false, adobe_rgb = false, jfif = false;
+    bool sof = false, unsupported = false, adobe = false, jfif = false, exif = false;
+    int transform = 0;
     for (;;) {
         // next marker: skip non-0xFF garbage, then fill bytes (jdmarker.c next_marker)
         while (i < avail && p[i] != 0xFF) i++;
@@ -98,8 +116,14 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
         case 0xE0:  // APP0: JFIF
             if (n >= 5 && !memcmp(s, "JFIF\0", 5)) jfif = true;
             break;
+        case 0xE1:  // APP1: EXIF
+            if (n >= 6 && !memcmp(s, "Exif\0\0", 6)) exif = true;
+            break;
         case 0xEE:  // APP14: Adobe colour transform (jdmarker.c examine_app14)
-            if (n >= 12 && !memcmp(s, "Adobe", 5) && s[11] == 0) adobe_rgb = true;
+            if (n >= 12 && !memcmp(s, "Adobe", 5)) {
+                adobe = true;
+                transform = s[11];
+            }
             break;
         case 0xDA: {  // SOS
             if (!sof) return ICX_E_CORRUPT;
@@ -116,10 +140,10 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
                 if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0) return ICX_E_UNSUPPORTED;
             }
             J.scan_off = i;
-            // colour space (jdapimin.c default_decompress_parms): JFIF or ids 1,2,3 -> YCbCr
             if (J.ncomp == 3) {
-                const bool rgb_ids = J.id[0] == 'R' && J.id[1] == 'G' && J.id[2] == 'B';
-                if (!jfif && (adobe_rgb || rgb_ids)) return ICX_E_UNSUPPORTED;
+                const int cs = colour_space(J, jfif, exif, adobe, transform);
+                if (cs < 0) return ICX_E_UNSUPPORTED;
+                J.rgb = cs == 1;
                 if (J.hs[1] != 1 || J.vs[1] != 1 || J.hs[2] != 1 || J.vs[2] != 1) return ICX_E_UNSUPPORTED;
                 if (J.hs[0] > 2 || J.vs[0] > 2 || (J.hs[0] == 1 && J.vs[0] == 2)) return ICX_E_UNSUPPORTED;
             }

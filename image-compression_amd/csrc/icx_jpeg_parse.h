@@ -5,8 +5,10 @@
 // decoder implements: SOF0/SOF1 8-bit, one interleaved scan (or a single grey
 // component), Huffman coding, optional DRI; and SOF2 progressive files (8-bit
 // Huffman, same components and sampling) whose scans icx_progressive.cpp
-// decodes on the host.  Everything else (arithmetic, lossless, 12-bit,
-// CMYK/YCCK, Adobe RGB, multi-scan sequential,
+// decodes on the host; 3-component files in the colour space the JDK reader
+// settles on (colour_space: YCbCr, or RGB without conversion).  Everything
+// else (arithmetic, lossless, 12-bit, CMYK/YCCK, an unknown colour space,
+// multi-scan sequential,
 // 4:4:0 and exotic sampling) is reported as ICX_E_UNSUPPORTED with the image
 // dimensions filled in, so the caller can still apply the dimension gate
 // (ImageCompression.java:131) and route the file to a host decoder.
@@ -30,12 +32,16 @@ struct JpegHeader {
     bool h_ok[2][4] = {};
     size_t scan_off = 0;  // first byte of the entropy-coded segment (progressive: of the first scan)
     bool progressive = false;  // SOF2: td/ta/scan_off unused, prog_decode walks every scan
+    bool rgb = false;          // 3 components stored as R, G, B (colour_space): no YCbCr conversion
 };
 
 // Parse markers up to the SOS.  `avail` bytes of the file are present at p
 // (the file is `total` bytes long).  Returns ICX_OK, ICX_E_UNSUPPORTED (w, h,
 // ncomp valid), ICX_E_CORRUPT, or ICX_E_BUFFER when more bytes are needed.
 icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& J);
+
+// 0 YCbCr, 1 RGB, -1 unknown: the JDK reader's colour space of a 3-component file.
+int colour_space(const JpegHeader& J, bool jfif, bool exif, bool adobe, int transform);
 
 // jpeg_make_d_derived_tbl equivalent; false if the table is invalid.
 bool build_dec_huff(const uint8_t* bits, const uint8_t* vals, int n, DecHuff& t, DecSlow& slow);

@@ -40,6 +40,7 @@ typedef struct {
 
 typedef struct {
     int w, h, ncomp, ri;
+    int rgb; /* 3 components stored as R, G, B (colour_space below): no ycc_rgb_convert */
     int id[3], hs[3], vs[3], tq[3], td[3], ta[3];
     int hmax, vmax, mcux, mcuy;
     uint16_t qt[4][64]; /* natural order */
@@ -81,13 +82,30 @@ static int build_dhuff(const uint8_t* counts, const uint8_t* vals, int nvals, dh
     return 0;
 }
 
+/* Colour space of a 3-component file as the JDK reader settles it: libjpeg's
+ * guess (jdapimin.c default_decompress_parms: JFIF -> YCbCr; an Adobe marker's
+ * transform 0 -> RGB, else YCbCr; no marker: ids 1,2,3 -> YCbCr, 'R','G','B'
+ * -> RGB, else YCbCr), then OpenJDK imageioJPEG.c's override of a YCbCr guess:
+ * an Adobe transform other than 1 -> unknown (here: unsupported, -1); no JFIF
+ * and no EXIF marker, ids other than 1,2,3 and every component sampled alike
+ * -> RGB.  0 YCbCr, 1 RGB. */
+static int colour_space(const jinfo_t* J, int jfif, int exif, int adobe, int transform)
+{
+    if (jfif) return 0;
+    if (adobe) return transform == 0 ? 1 : transform == 1 ? 0 : -1;
+    if (J->id[0] == 1 && J->id[1] == 2 && J->id[2] == 3) return 0;
+    if (J->id[0] == 'R' && J->id[1] == 'G' && J->id[2] == 'B') return 1;
+    if (exif) return 0;
+    return J->hs[1] == J->hs[0] && J->hs[2] == J->hs[0] && J->vs[1] == J->vs[0] && J->vs[2] == J->vs[0];
+}
+
 /* jdmarker.c, baseline subset.  0 ok, 5 unsupported, 6 corrupt. */
 static int parse(const uint8_t* p, size_t len, jinfo_t* J)
 {
     memset(J, 0, sizeof(*J));
     if (len < 4 || p[0] != 0xFF || p[1] != 0xD8) return 6;
     size_t i = 2;
-    int have_sof = 0;
+    int have_sof = 0, jfif = 0, exif = 0, adobe = 0, transform = 0;
     for (;;) {
         while (i < len && p[i] != 0xFF) i++; /* jdmarker next_marker: skip garbage */
         while (i < len && p[i] == 0xFF) i++; /* fill bytes */
@@ -153,6 +171,15 @@ static int parse(const uint8_t* p, size_t len, jinfo_t* J)
         } else if (m == 0xDD) { /* DRI */
             if (n < 2) return 6;
             J->ri = (s[0] << 8) | s[1];
+        } else if (m == 0xE0) { /* APP0: JFIF (jdmarker.c examine_app0) */
+            if (n >= 5 && !memcmp(s, "JFIF\0", 5)) jfif = 1;
+        } else if (m == 0xE1) { /* APP1 */
+            if (n >= 6 && !memcmp(s, "Exif\0\0", 6)) exif = 1;
+        } else if (m == 0xEE) { /* APP14: Adobe (jdmarker.c examine_app14) */
+            if (n >= 12 && !memcmp(s, "Adobe", 5)) {
+                adobe = 1;
+                transform = s[11];
+            }
         } else if (m == 0xDA) { /* SOS */
             if (!have_sof) return 6;
             int ns = s[0];
@@ -176,6 +203,9 @@ static int parse(const uint8_t* p, size_t len, jinfo_t* J)
      * whose 6b upsampler is not the one libjpeg-turbo uses); grey = any */
     J->hmax = J->vmax = 1;
     if (J->ncomp == 3) {
+        int cs = colour_space(J, jfif, exif, adobe, transform);
+        if (cs < 0) return 5;
+        J->rgb = cs;
         if (J->hs[1] != 1 || J->vs[1] != 1 || J->hs[2] != 1 || J->vs[2] != 1) return 5;
         if (J->hs[0] > 2 || J->vs[0] > 2) return 5;
         if (J->hs[0] == 1 && J->vs[0] == 2) return 5;
@@ -531,10 +561,16 @@ int oracle_jpeg_decode(const uint8_t* jpg, size_t len, int s, uint8_t* out, size
         for (int x = 0; x < dw; x++) {
             int X = x * s;
             int yy = yrow[X], cb = up[0][X] - 128, cr = up[1][X] - 128;
-            /* ycc_rgb_convert: FIX(x) = (int)(x * 65536 + 0.5), ONE_HALF = 1 << 15 */
-            int rr = yy + ((91881 * cr + 32768) >> 16);
-            int gg = yy + ((-22554 * cb + 32768 - 46802 * cr) >> 16);
-            int bb = yy + ((116130 * cb + 32768) >> 16);
+            int rr, gg, bb;
+            if (J.rgb) { /* jdcolor.c null_convert: the components are R, G, B */
+                rr = yy;
+                gg = cb + 128;
+                bb = cr + 128;
+            } else { /* ycc_rgb_convert: FIX(x) = (int)(x * 65536 + 0.5), ONE_HALF = 1 << 15 */
+                rr = yy + ((91881 * cr + 32768) >> 16);
+                gg = yy + ((-22554 * cb + 32768 - 46802 * cr) >> 16);
+                bb = yy + ((116130 * cb + 32768) >> 16);
+            }
             orow[3 * x + 0] = clamp255(bb);
             orow[3 * x + 1] = clamp255(gg);
             orow[3 * x + 2] = clamp255(rr);

@@ -55,6 +55,7 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
     }
     d.ri = J.ri;
     d.nblocks = (int64_t)d.mcux * d.mcuy * d.nbmcu;
+    d.wmcu = dec_walk_mcu(J.ncomp, d.nbmcu, J.td, J.ta);
     if ((size_t)d.nblocks > nblocks_cap) return ICX_E_BUFFER;
 
     // ---- unstuff

@@ -55,6 +55,45 @@ def encode(rgb, **kw):
     return buf.getvalue()
 
 
+def segments(data):
+    """(marker, bytes) of the segments before the first SOS, then ('scan', rest)."""
+    out, i = [], 2
+    while True:
+        m = data[i + 1]
+        n = int.from_bytes(data[i + 2:i + 4], "big")
+        out.append((m, data[i:i + 2 + n]))
+        i += 2 + n
+        if m == 0xDA:
+            out.append(("scan", data[i:]))
+            return out
+
+
+def rewrite(data, app, ids):
+    """data with its APP0/APP14 segments replaced by `app` (None: dropped) and
+    the component ids of SOF and SOS set to `ids` (None: kept)."""
+    parts = [b"\xff\xd8"] + ([app] if app else [])
+    for m, seg in segments(data):
+        if m in (0xE0, 0xEE):
+            continue
+        if ids is not None and m in (0xC0, 0xC2):
+            seg = bytearray(seg)
+            for c in range(seg[9]):
+                seg[10 + 3 * c] = ids[c]
+            seg = bytes(seg)
+        if ids is not None and m == 0xDA:
+            seg = bytearray(seg)
+            for c in range(seg[4]):
+                seg[5 + 2 * c] = ids[c]
+            seg = bytes(seg)
+        parts.append(seg)
+    return b"".join(parts)
+
+
+def adobe_app14(transform):
+    body = b"Adobe" + bytes([0, 100, 0, 0, 0, 0, transform])
+    return b"\xff\xee" + (len(body) + 2).to_bytes(2, "big") + body
+
+
 def decode_bgr(data):
     im = Image.open(io.BytesIO(data))
     im.load()
@@ -131,6 +170,43 @@ def main():
         meta["cases"][name] = {"w": int(out.shape[1]), "h": int(out.shape[0]), "ncomp": 1 if out.ndim == 2 else 3,
                                "unsupported": True, "progressive": True, "params": dict(kw, progressive=True),
                                "bytes": len(data)}
+    # colour space as the JDK reader settles it (oracle/icx_oracle_decode.c
+    # colour_space): Adobe transform 0 -> RGB (Pillow keep_rgb writes it, and
+    # libjpeg-turbo reads it the same way), and files derived from it or from a
+    # YCbCr file by rewriting markers and component ids only (same tables and
+    # entropy data, so the expected pixels are those of the file they come from):
+    #   ids 'R','G','B', no marker          -> RGB   (libjpeg's guess)
+    #   ids 0,1,2, no marker, equal sampling -> RGB   (OpenJDK imageioJPEG.c override;
+    #                                                  libjpeg-turbo would say YCbCr)
+    #   ids 0,1,2 with an EXIF APP1          -> YCbCr (the override needs no EXIF)
+    #   Adobe transform 1, ids 'R','G','B'   -> YCbCr (the Adobe marker wins)
+    #   Adobe transform 2                    -> unknown: refused ("unsupported")
+    seed += 1
+    rgb_img = smooth(66, 130, seed)
+    adobe = encode(rgb_img, quality=90, subsampling=0, keep_rgb=True)
+    ycc = encode(rgb_img, quality=90, subsampling=0)
+    rgb_px, ycc_px = decode_bgr(adobe), decode_bgr(ycc)
+    derived = [("rgb_adobe0_66x130", adobe, rgb_px, False),
+               ("rgb_ids_nomarker_66x130", rewrite(adobe, app=None, ids=b"RGB"), rgb_px, False),
+               ("rgb_ids012_nomarker_66x130", rewrite(adobe, app=None, ids=bytes([0, 1, 2])), rgb_px, False),
+               ("ycc_ids012_exif_66x130", rewrite(ycc, app=b"\xff\xe1\x00\x08Exif\x00\x00", ids=bytes([0, 1, 2])),
+                ycc_px, False),
+               ("ycc_adobe1_rgbids_66x130", rewrite(ycc, app=adobe_app14(1), ids=b"RGB"), ycc_px, False),
+               ("unknown_adobe2_66x130", rewrite(ycc, app=adobe_app14(2), ids=None), None, True)]
+    for name, data, px, refused in derived:
+        jpegs[name] = np.frombuffer(data, np.uint8)
+        meta["cases"][name] = {"w": 130, "h": 66, "ncomp": 3, "bytes": len(data), "colour": True,
+                               "params": {"derived": True}}
+        if refused:
+            meta["cases"][name]["unsupported"] = True
+        else:
+            expect[name] = px
+    prog_rgb = encode(smooth(47, 61, seed + 1), quality=85, subsampling=0, keep_rgb=True, progressive=True)
+    jpegs["prog_rgb_adobe0_47x61"] = np.frombuffer(prog_rgb, np.uint8)
+    expect["prog_rgb_adobe0_47x61"] = decode_bgr(prog_rgb)
+    meta["cases"]["prog_rgb_adobe0_47x61"] = {"w": 61, "h": 47, "ncomp": 3, "unsupported": True, "progressive": True,
+                                              "colour": True, "params": {"progressive": True, "keep_rgb": True},
+                                              "bytes": len(prog_rgb)}
     np.savez_compressed(os.path.join(HERE, "decode_golden.npz"),
                         **{f"jpg:{k}": v for k, v in jpegs.items()},
                         **{f"px:{k}": v for k, v in expect.items()})

@@ -266,3 +266,27 @@ def test_progressive_refusals_in_a_batch(codec, dgolden):
     assert res[0][0] == N.E_UNSUPPORTED and res[1][0] == N.E_CORRUPT
     assert res[2][0] == N.OK and np.array_equal(res[2][1], pxs["prog_c130x250_s2_q95"])
     assert res[3][0] == N.OK and np.array_equal(res[3][1], pxs["c130x250_s2_q95"])
+
+
+def test_decode_stray_restart_markers(codec, oracle, dgolden):
+    """RSTn markers where the DRI interval does not end (inserted, or one
+    removed): the device decoder refuses the file or decodes it exactly as the
+    oracle does - every interval must end after ri MCUs (DecWalker::invalid)."""
+    meta, jpgs, pxs = dgolden
+    good = jpgs["rst7_130x250"]
+    sos = good.index(b"\xff\xda")
+    body = sos + 2 + int.from_bytes(good[sos + 2:sos + 4], "big")
+    rsts = [i for i in range(body, len(good) - 1) if good[i] == 0xFF and 0xD0 <= good[i + 1] <= 0xD7]
+    datas = []
+    for k in range(12):
+        p = body + (len(good) - body) * (k + 1) // 14
+        datas.append(good[:p] + bytes([0xFF, 0xD0 + k % 8]) + good[p:])
+    for r in rsts[::5]:
+        datas.append(good[:r] + good[r + 2:])  # one marker removed
+    res = codec.decode_jpg_batch(datas + [good], subsampling=1)
+    for i, (d, (st, img)) in enumerate(zip(datas, res)):
+        assert st in (N.OK, N.E_CORRUPT), (i, st)
+        if st == N.OK:
+            rc, ref = oracle.jpeg_decode(d)
+            assert rc == 0 and np.array_equal(img, ref), i
+    assert res[-1][0] == N.OK and np.array_equal(res[-1][1], pxs["rst7_130x250"])

@@ -24,7 +24,7 @@ def test_decode_matches_golden(oracle, dgolden):
         assert rc == 0, (name, rc)
         assert img.shape == pxs[name].shape and np.array_equal(img, pxs[name]), name
         n += 1
-    assert n == 103
+    assert n == 108
 
 
 @pytest.mark.parametrize("s", [2, 3, 4])
