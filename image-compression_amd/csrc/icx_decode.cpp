@@ -231,7 +231,9 @@ icx_status run_progressive(icx_ctx* c, std::vector<DecItem>& items, int16_t* coe
             const bool host_out = !coef_out && !is_device_ptr(it.job->out);
             if (host_out) per += align_up(it.job->out_len, 256);
             const size_t hper = align_up(nb * 128, 64) + align_up(nb * 4, 64) + (it.dev_in ? align_up(it.job->len, 64) : 0);
-            if (!sub.empty() && (need + per > c->budget || hneed + hper > c->budget)) break;
+            // pinned staging of coefficients: at most 2 GiB per sub-batch
+            if (!sub.empty() && (need + per > c->budget || hneed + hper > std::min<size_t>(c->budget, 2ull << 30)))
+                break;
             need += per;
             hneed += hper;
             it.host_out = host_out;
