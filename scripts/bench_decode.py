@@ -17,14 +17,14 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 
-def sources(h, w, distinct):
+def sources(h, w, distinct, progressive=False):
     from PIL import Image
     from tests.oracle_ffi import noise, smooth
     out = []
     for i in range(distinct):
         img = (smooth if i % 2 == 0 else noise)(h, w, 100 + i)[:, :, ::-1]
         b = io.BytesIO()
-        Image.fromarray(np.ascontiguousarray(img)).save(b, "JPEG", quality=95, subsampling=2)
+        Image.fromarray(np.ascontiguousarray(img)).save(b, "JPEG", quality=95, subsampling=2, progressive=progressive)
         out.append(b.getvalue())
     return out
 
@@ -38,10 +38,12 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--kind", default="mixed", choices=["mixed", "smooth", "noise"])
+    ap.add_argument("--progressive", action="store_true",
+                    help="progressive sources (host scan decode on libicx threads + device IDCT / colour)")
     a = ap.parse_args()
     import torch
     import icx
-    srcs = sources(a.height, a.width, a.distinct)
+    srcs = sources(a.height, a.width, a.distinct, a.progressive)
     if a.kind != "mixed":
         srcs = [s for i, s in enumerate(srcs) if (i % 2 == 0) == (a.kind == "smooth")]
     codec = icx.Codec(0)
@@ -78,7 +80,8 @@ def main():
                       "sync_relaunch_ms": {k: round(v["ms"] / a.steps, 3) for k, v in relaunch.items() if v["launches"]},
                       "sync_walks_per_step": walks / a.steps,
                       "host_ms_per_step": {k: round(codec.profile_query(k)["ms"] / a.steps, 3)
-                                           for k in ("host.dec_headers", "host.dec_setup")}}))
+                                           for k in ("host.dec_headers", "host.dec_setup", "host.dec_progressive")},
+                      "progressive": a.progressive}))
     codec.close()
 
 
