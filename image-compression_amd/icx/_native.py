@@ -29,6 +29,8 @@ EXPORTS = [
     "icx_debug_progressive_coefs",
     "icx_device_alloc", "icx_device_free", "icx_memcpy", "icx_host_alloc", "icx_host_free",
     "icx_png_bound", "icx_png_encode", "icx_png_fit_batch",
+    "icx_pool_create", "icx_pool_destroy", "icx_pool_size", "icx_pool_context", "icx_pool_compress_jpg_batch",
+    "icx_pool_decode_jpg_batch", "icx_pool_png_fit_batch",
 ]
 
 
@@ -136,6 +138,13 @@ def load():
         "icx_png_bound": (c.c_size_t, [P(Image)]),
         "icx_png_encode": (c.c_int, [P(Image), c.c_int32, c.c_void_p, c.c_size_t, P(c.c_size_t)]),
         "icx_png_fit_batch": (c.c_int, [c.c_void_p, P(PngFitJob), c.c_int32]),
+        "icx_pool_create": (c.c_int, [P(c.c_int32), c.c_int32, P(c.c_void_p)]),
+        "icx_pool_destroy": (None, [c.c_void_p]),
+        "icx_pool_size": (c.c_int32, [c.c_void_p]),
+        "icx_pool_context": (c.c_void_p, [c.c_void_p, c.c_int32]),
+        "icx_pool_compress_jpg_batch": (c.c_int, [c.c_void_p, P(FitJob), c.c_int32]),
+        "icx_pool_decode_jpg_batch": (c.c_int, [c.c_void_p, P(DecodeJob), c.c_int32]),
+        "icx_pool_png_fit_batch": (c.c_int, [c.c_void_p, P(PngFitJob), c.c_int32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

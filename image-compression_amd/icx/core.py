@@ -269,6 +269,9 @@ class Codec:
     def last_error(self) -> str:
         return self._lib.icx_last_error(self._ctx).decode()
 
+    def _batch_call(self, what, jobs, n):
+        return getattr(self._lib, f"icx_{what}_batch")(self._ctx, jobs, n)
+
     def _check(self, st, what):
         if st != N.OK:
             raise N.IcxError(st, f"{what}: {self._lib.icx_status_string(st).decode()} "
@@ -356,7 +359,7 @@ class Codec:
                 j.cap = buf.nbytes
             bufs.append(buf)
         with self._lock:
-            st = self._lib.icx_compress_jpg_batch(self._ctx, jobs, n)
+            st = self._batch_call("compress_jpg", jobs, n)
         self._check(st, "icx_compress_jpg_batch")
         res = []
         for i in range(n):
@@ -450,7 +453,7 @@ class Codec:
             outs[i] = np.empty(_out_shape(dh, dw, img.fmt), _out_dtype(img.fmt))
             j.dst, j.cap = outs[i].ctypes.data, outs[i].nbytes
         with self._lock:
-            st = self._lib.icx_png_fit_batch(self._ctx, jobs, n)
+            st = self._batch_call("png_fit", jobs, n)
         self._check(st, "icx_png_fit_batch")
         res = []
         for i in range(n):
@@ -498,7 +501,7 @@ class Codec:
             else:
                 jobs[i].out, jobs[i].cap = None, 0
         with self._lock:
-            st = self._lib.icx_decode_jpg_batch(self._ctx, jobs, n)
+            st = self._batch_call("decode_jpg", jobs, n)
         self._check(st, "icx_decode_jpg_batch")
         return [(jobs[i].status, outs[i] if jobs[i].status == N.OK else None) for i in range(n)]
 
@@ -546,6 +549,44 @@ class Codec:
         self._check(self._lib.icx_profile_query(self._ctx, kernel.encode(), ctypes.byref(n), ctypes.byref(ms),
                                                 ctypes.byref(u)), "icx_profile_query")
         return {"launches": n.value, "ms": ms.value, "units": u.value}
+
+
+class Pool(Codec):
+    """Several GPUs behind one libicx handle (icx_pool_*, include/icx.h): the
+    batched calls - fit, png_fit_batch, decode_jpg_batch - split the images
+    into per-device shares balanced by pixels, run them concurrently and
+    return the results in the caller's order, as one Codec would.  Host
+    buffers only (device_out / CUDA tensors belong with one device's Codec);
+    single-image helpers run on the first device's context.  The shape of a
+    JVM host that drives every GPU of the node from one process
+    (CompressionBatch.java:64-88)."""
+
+    def __init__(self, devices):
+        self._lib = N.load()
+        self._pool = ctypes.c_void_p()
+        arr = (ctypes.c_int32 * len(devices))(*devices)
+        st = self._lib.icx_pool_create(arr, len(devices), ctypes.byref(self._pool))
+        if st != N.OK:
+            raise N.IcxError(st, f"icx_pool_create({list(devices)}) failed: "
+                                 f"{self._lib.icx_status_string(st).decode()}")
+        self.devices = list(devices)
+        self.device = self.devices[0]
+        self._ctx = ctypes.c_void_p(self._lib.icx_pool_context(self._pool, 0))
+        self._lock = threading.Lock()
+
+    def close(self):
+        if self._pool:
+            self._lib.icx_pool_destroy(self._pool)
+            self._pool = ctypes.c_void_p()
+            self._ctx = ctypes.c_void_p()
+
+    def _batch_call(self, what, jobs, n):
+        return getattr(self._lib, f"icx_pool_{what}_batch")(self._pool, jobs, n)
+
+    def decode_jpg_batch(self, datas, subsampling: int = 0, device_out: bool = False):
+        if device_out:
+            raise ValueError("a Pool decodes into host memory; use one device's Codec for device_out")
+        return super().decode_jpg_batch(datas, subsampling, False)
 
 
 def jpeg_info(data):

@@ -104,6 +104,22 @@ typedef struct icx_similarity_key {
 icx_status icx_create(int device, icx_ctx** out);
 void icx_destroy(icx_ctx* ctx);
 const char* icx_status_string(icx_status s);
+
+/* Several GPUs behind one handle, for a host process that drives every GPU of
+ * the node (a JVM's CompressionBatch thread pool, CompressionBatch.java:64-88):
+ * one context per listed device (ordinals may repeat: several contexts on one
+ * GPU).  The pool's batched calls split the jobs into per-device shares
+ * balanced by pixels (decode: compressed bytes), run them concurrently on one
+ * host thread per device and fill in every job's results as the single-context
+ * call would.  Pool calls take host buffers only (a job with a device pointer
+ * gets ICX_E_INVALID); icx_pool_context(pool, i) is device i's own context for
+ * device-resident work.  The return value is the first context-level failure,
+ * else ICX_OK. */
+typedef struct icx_pool icx_pool;
+icx_status icx_pool_create(const int32_t* devices, int32_t ndev, icx_pool** out);
+void icx_pool_destroy(icx_pool* pool);
+int32_t icx_pool_size(const icx_pool* pool);
+icx_ctx* icx_pool_context(icx_pool* pool, int32_t i);
 /* Last error text recorded on this context (never NULL). */
 const char* icx_last_error(const icx_ctx* ctx);
 int icx_abi_version(void);
@@ -172,6 +188,7 @@ icx_status icx_compress_jpg_with_target_size(icx_ctx* ctx, icx_fit_job* job);
  * kernel launches.  Per-job results/status are filled in; the return value is
  * ICX_OK unless a context-level failure occurred. */
 icx_status icx_compress_jpg_batch(icx_ctx* ctx, icx_fit_job* jobs, int32_t n);
+icx_status icx_pool_compress_jpg_batch(icx_pool* pool, icx_fit_job* jobs, int32_t n);
 
 /* A12  ImageTools.resizeImage (ImageTools.java:7-26): Java2D bilinear resize
  * to (max(1,(int)(w*scale)), max(1,(int)(h*scale))).  dst gets the same fmt,
@@ -212,6 +229,7 @@ typedef struct icx_png_fit_job {
     icx_status status;
 } icx_png_fit_job;
 icx_status icx_png_fit_batch(icx_ctx* ctx, icx_png_fit_job* jobs, int32_t n);
+icx_status icx_pool_png_fit_batch(icx_pool* pool, icx_png_fit_job* jobs, int32_t n);
 
 /* The PNG write of ImageCompressionPng (ImageCompressionPng.java:70,
  * ImageIO.write(img, "png", file)) for host pixels: 8-bit grey (GRAY8), RGB
@@ -258,6 +276,7 @@ icx_status icx_decode_jpg(icx_ctx* ctx, icx_decode_job* job);
  * is filled in; the return value is ICX_OK unless a context-level failure
  * occurred. */
 icx_status icx_decode_jpg_batch(icx_ctx* ctx, icx_decode_job* jobs, int32_t n);
+icx_status icx_pool_decode_jpg_batch(icx_pool* pool, icx_decode_job* jobs, int32_t n);
 
 /* ------------------------------------------------------------ device memory */
 /* Buffers in the context GPU's HBM, so a decoded frame can stay on the device

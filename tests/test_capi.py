@@ -69,6 +69,21 @@ def test_null_arguments_rejected_without_gpu():
     assert lib.icx_compress_jpg_batch(None, None, 0) == N.E_NULL
 
 
+def test_pool_arguments_rejected_without_gpu():
+    """icx_pool_* validates its arguments before touching a device."""
+    lib = N.load()
+    p = ctypes.c_void_p()
+    assert lib.icx_pool_create(None, 1, ctypes.byref(p)) == N.E_NULL
+    devs = (ctypes.c_int32 * 1)(0)
+    assert lib.icx_pool_create(devs, 0, ctypes.byref(p)) == N.E_INVALID
+    assert lib.icx_pool_create(devs, 1, None) == N.E_NULL
+    assert lib.icx_pool_size(None) == 0 and not lib.icx_pool_context(None, 0)
+    assert lib.icx_pool_compress_jpg_batch(None, None, 0) == N.E_NULL
+    assert lib.icx_pool_decode_jpg_batch(None, None, 0) == N.E_NULL
+    assert lib.icx_pool_png_fit_batch(None, None, 0) == N.E_NULL
+    lib.icx_pool_destroy(None)
+
+
 def test_missing_library_fails_loudly(monkeypatch):
     monkeypatch.setattr(N, "_lib", None)
     monkeypatch.setattr(N, "LIB_PATH", "/nonexistent/libicx.so")

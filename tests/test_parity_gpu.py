@@ -456,3 +456,54 @@ def test_bench_headline_frames_match_oracle(codec, oracle):
         assert r["learned"].scale == ref["scale"] and r["encodes"] == trials, (i, r["encodes"], ref["encodes"])
         assert r["cache_hit"] == ref["cache_hit"], i
     assert [r["cache_hit"] for r in res] == [True, False, True, False]
+
+
+def test_pool_splits_batches_across_contexts(codec, oracle):
+    """icx_pool over two contexts of the box's GPU (the shape of a JVM host
+    driving every GPU of a node): fit, PNG fit and decode batches come back
+    in the caller's order, equal to one context's results and the oracle's;
+    a job with a device pointer is refused alone."""
+    import torch
+
+    pool = icx.Pool([0, 0])
+    try:
+        imgs = [smooth(136 + 8 * i, 200 + 16 * i, 60 + i) if i % 2 else noise(96, 120 + 8 * i, 60 + i)
+                for i in range(9)]
+        target = 20000
+        got = pool.fit(imgs, target, 0.25)
+        ref = codec.fit(imgs, target, 0.25)
+        for i, (g, r) in enumerate(zip(got, ref)):
+            o = oracle.fit(imgs[i], target, 0.25)
+            assert g["success"] == r["success"] == o["success"], i
+            assert g.get("data") == r.get("data") == o["data"], i
+        big = [smooth(1080, 1920, 70 + i)[:, :, ::-1].copy() for i in range(3)]
+        params = icx.CompressionParams(0.25, 1 << 20, 960, 960, 1 << 20)
+        pf = pool.png_fit_batch(big + [imgs[0]], params)
+        cf = codec.png_fit_batch(big + [imgs[0]], params)
+        assert pf[3] is None and cf[3] is None
+        for a, b in zip(pf[:3], cf[:3]):
+            assert np.array_equal(a, b)
+        jpgs = [oracle.encode(im, 0.9) for im in imgs]
+        dec = pool.decode_jpg_batch(jpgs, subsampling=1)
+        for d, (st, img) in zip(jpgs, dec):
+            rc, want = oracle.jpeg_decode(d)
+            assert st == N.OK and rc == 0 and np.array_equal(img, want)
+        # a device-resident job is not for the pool: ICX_E_INVALID for it alone
+        lib = N.load()
+        dev = torch.from_numpy(np.frombuffer(jpgs[0], np.uint8).copy()).cuda()
+        jobs = (N.DecodeJob * 2)()
+        outs = [np.empty((136, 200, 3), np.uint8) for _ in range(2)]
+        a = np.frombuffer(jpgs[1], np.uint8)
+        jobs[0].data, jobs[0].len = dev.data_ptr(), dev.numel()
+        jobs[1].data, jobs[1].len = a.ctypes.data, a.nbytes
+        for k in range(2):
+            jobs[k].subsampling = 1
+            jobs[k].out, jobs[k].cap = outs[k].ctypes.data, outs[k].nbytes
+        outs[1] = np.empty((imgs[1].shape[0], imgs[1].shape[1], 3), np.uint8)
+        jobs[1].out, jobs[1].cap = outs[1].ctypes.data, outs[1].nbytes
+        assert lib.icx_pool_decode_jpg_batch(pool._pool, jobs, 2) == N.OK
+        assert jobs[0].status == N.E_INVALID and jobs[1].status == N.OK
+        assert np.array_equal(outs[1], oracle.jpeg_decode(jpgs[1])[1])
+        assert lib.icx_pool_size(pool._pool) == 2
+    finally:
+        pool.close()
