@@ -78,6 +78,7 @@ struct Bits {
     uint64_t buf = 0;  // left-aligned
     int cnt = 0, zbits = 0;
     int marker = 0;    // unread marker code, 0 while in the data
+    bool eof = false;  // the file ended inside the scan (marker = 0xD9 stands for it)
     bool over = false;  // a zero bit past the marker was consumed
 
     void fill()
@@ -87,14 +88,17 @@ struct Bits {
             if (!marker) {
                 if (pos >= end) {
                     marker = 0xD9;  // end of file: as libjpeg's inserted EOI
+                    eof = true;
                     continue;
                 }
                 b = p[pos++];
                 if (b == 0xFF) {
-                    uint32_t c;
-                    do {
-                        c = pos < end ? p[pos++] : 0xD9;
-                    } while (c == 0xFF);
+                    uint32_t c = 0xFF;
+                    while (c == 0xFF && pos < end) c = p[pos++];
+                    if (c == 0xFF) {  // the file ends in FF fill bytes
+                        c = 0xD9;
+                        eof = true;
+                    }
                     if (c != 0) {
                         marker = (int)c;
                         continue;
@@ -207,10 +211,15 @@ icx_status prog_decode(const uint8_t* p, size_t len, const JpegHeader& J, int16_
     size_t i = 2;
     if (len < 4 || p[0] != 0xFF || p[1] != 0xD8) return ICX_E_CORRUPT;
     for (;;) {
-        while (i < len && p[i] != 0xFF) i++;
-        while (i < len && p[i] == 0xFF) i++;
-        if (i >= len) return ICX_E_CORRUPT;  // no EOI
-        const int m = p[i++];
+        // jdmarker.c next_marker: skip anything up to FF, the FF fill bytes, and
+        // FF 00 pairs (stuffed data the scan's reader did not need)
+        int m = 0;
+        while (m == 0) {
+            while (i < len && p[i] != 0xFF) i++;
+            while (i < len && p[i] == 0xFF) i++;
+            if (i >= len) return ICX_E_CORRUPT;  // no EOI
+            m = p[i++];
+        }
         if (m == 0xD9) break;
         if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
         if (i + 2 > len) return ICX_E_CORRUPT;
@@ -332,7 +341,7 @@ icx_status prog_decode(const uint8_t* p, size_t len, const JpegHeader& J, int16_
                                 if (t > 11) return ICX_E_CORRUPT;
                                 d = extend((int)B.get(t), t);
                             }
-                            last_dc[bc[q]] += d;
+                            last_dc[bc[q]] = (int)((unsigned)last_dc[bc[q]] + (unsigned)d);  // wraps, no UB
                             co[0] = (int16_t)(last_dc[bc[q]] * (1 << Al));
                         } else if (B.get(1)) {  // decode_mcu_DC_refine
                             co[0] = (int16_t)(co[0] | p1);
@@ -407,12 +416,11 @@ icx_status prog_decode(const uint8_t* p, size_t len, const JpegHeader& J, int16_
             }
             // continue the marker walk at the marker that ended the scan (bytes the
             // reader fetched past the last needed bit are padding)
-            if (B.marker) {
-                i = B.pos;
-                while (i > 0 && p[i - 1] != 0xFF) i--;  // back to the marker's FF
+            if (B.eof) return ICX_E_CORRUPT;  // the file ends inside a scan
+            i = B.pos;
+            if (B.marker) {  // back to the marker's FF
+                while (i > 0 && p[i - 1] != 0xFF) i--;
                 if (i > 0) i--;
-            } else {
-                i = B.pos;
             }
         } else if ((m >= 0xC0 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) || m == 0xDC) {
             return ICX_E_CORRUPT;  // a second frame / DNL: not a single progressive frame
