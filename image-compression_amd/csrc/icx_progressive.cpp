@@ -37,10 +37,11 @@ const uint8_t kNat[64 + 16] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 1
                                29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
                                47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
 
-// Canonical Huffman table (jdhuff.c jpeg_make_d_derived_tbl): an 8-bit
+// Canonical Huffman table (jdhuff.c jpeg_make_d_derived_tbl): a LOOK-bit
 // lookahead table, then maxcode / valoff per code length.
+constexpr int LOOK = 11;
 struct Huff {
-    uint16_t look[256];  // (length << 8) | symbol, 0 = longer than 8 bits
+    uint16_t look[1 << LOOK];  // (length << 8) | symbol, 0 = longer than LOOK bits
     int32_t maxcode[18];
     int32_t valoff[17];
     uint8_t vals[256];
@@ -56,8 +57,9 @@ bool build_huff(const uint8_t* bits, const uint8_t* vals, int n, Huff& t)
         if (code + cnt >= (1 << l) || k + cnt > n) return false;
         t.valoff[l] = k - code;
         for (int i = 0; i < cnt; i++, code++, k++)
-            if (l <= 8)
-                for (int f = 0; f < (1 << (8 - l)); f++) t.look[(code << (8 - l)) | f] = (uint16_t)((l << 8) | vals[k]);
+            if (l <= LOOK)
+                for (int f = 0; f < (1 << (LOOK - l)); f++)
+                    t.look[(code << (LOOK - l)) | f] = (uint16_t)((l << 8) | vals[k]);
         t.maxcode[l] = cnt ? code - 1 : -1;
         code <<= 1;
     }
@@ -83,6 +85,16 @@ struct Bits {
 
     void fill()
     {
+        // fast path: 4 plain bytes (no 0xFF among them) at once
+        while (cnt <= 32 && !marker && pos + 4 <= end) {
+            uint32_t v;
+            memcpy(&v, p + pos, 4);
+            const uint32_t x = ~v;  // a 0xFF byte of v is a zero byte of x
+            if ((x - 0x01010101u) & ~x & 0x80808080u) break;
+            buf |= (uint64_t)__builtin_bswap32(v) << (32 - cnt);
+            cnt += 32;
+            pos += 4;
+        }
         while (cnt <= 56) {
             uint32_t b = 0;
             if (!marker) {
@@ -132,12 +144,12 @@ struct Bits {
     int decode(const Huff& t)
     {
         const uint32_t w = peek(16);
-        const uint16_t e = t.look[w >> 8];
+        const uint16_t e = t.look[w >> (16 - LOOK)];
         if (e) {
             skip(e >> 8);
             return e & 255;
         }
-        for (int l = 9; l <= 16; l++) {
+        for (int l = LOOK + 1; l <= 16; l++) {
             const int32_t code = (int32_t)(w >> (16 - l));
             if (code <= t.maxcode[l]) {
                 skip(l);
