@@ -149,15 +149,32 @@ def cpu_baseline(frames, n_sample, threads, cores_how="", distinct=320):
                       f"{enc} full encodes, {dt:.2f} s wall"}, sizes
 
 
-def e2e_leg(codec, dev, frames, n_frames, steps, cpu_sample=0, threads=16):
+def e2e_leg(codec, dev, frames, n_frames, steps, cpu_sample=0, threads=16, small=200):
     """Secondary measurement: the whole per-image hot loop of processImage on
     the device — q95 4:2:0 4K JPEG files resident in HBM -> decode (A11,
     decodeImageWithSubsampling) -> compressJpgWithTargetSize at -t 1 MiB with
     the cached q = 0.25 (A2-A10) -> output bytes in HBM.  Sources: n_frames
-    DISTINCT files (1.5 GB for 200: far past the 256 MiB Infinity Cache, so no
-    source is re-read from it), made from the headline's frames by this
-    library's own encoder at quality 0.95 - JPEGQTable scaling by 0.1, the
-    same tables, 4:2:0 sampling and Annex-K Huffman codes as libjpeg's q95."""
+    DISTINCT files (7.8 GB for configs[1]'s 1000 frames, 1.5 GB for 200: far
+    past the 256 MiB Infinity Cache, so no source is re-read from it), made
+    from the headline's frames by this library's own encoder at quality 0.95 -
+    JPEGQTable scaling by 0.1, the same tables, 4:2:0 sampling and Annex-K
+    Huffman codes as libjpeg's q95.  The same loop over the first `small`
+    sources is reported beside it (`at_small_batch`): the decoder's
+    relaxation tail (the last few re-walk launches, single waves) is a fixed
+    latency per call, so a smaller call runs at a lower rate."""
+    line = _e2e_run(codec, dev, frames, n_frames, steps)
+    if small and small < n_frames:
+        line["at_small_batch"] = {k: v for k, v in _e2e_run(codec, dev, frames, small, steps).items()
+                                  if k in ("value", "frames", "ms_per_step", "decode_ms_per_step",
+                                           "encode_ms_per_step", "decode_mp_s")}
+    if cpu_sample:
+        srcs = _e2e_sources(codec, dev, frames, min(16, n_frames))[0]
+        line["cpu_baseline"] = e2e_cpu_baseline([s.cpu().numpy().tobytes() for s in srcs], cpu_sample, threads)
+    return line
+
+
+def _e2e_sources(codec, dev, frames, n_frames):
+    """q95 JPEG sources of the first n_frames frames, in HBM (see e2e_leg)."""
     srcs_buf = torch.empty((n_frames, 12 << 20), dtype=torch.uint8, device=dev)
     enc = codec.prepare(frames[:n_frames], 12 << 20, 0.95, cached=[icx.LearnedParams(0.95, 1.0)] * n_frames,
                         outputs=[srcs_buf[i] for i in range(n_frames)])
@@ -165,6 +182,11 @@ def e2e_leg(codec, dev, frames, n_frames, steps, cpu_sample=0, threads=16):
     lens = [r["out_len"] for r in enc.results()]
     assert all(r["success"] and r["cache_hit"] for r in enc.results()), "source encode"
     srcs = [srcs_buf[i, :lens[i]] for i in range(n_frames)]
+    return srcs, lens
+
+
+def _e2e_run(codec, dev, frames, n_frames, steps):
+    srcs, lens = _e2e_sources(codec, dev, frames, n_frames)
     px = [torch.empty((H, W, 3), dtype=torch.uint8, device=dev) for _ in range(n_frames)]
     outs = torch.empty((n_frames, TARGET + 1), dtype=torch.uint8, device=dev)
     dec = codec.prepare_decode(srcs, px, subsampling=0)
@@ -193,9 +215,6 @@ def e2e_leg(codec, dev, frames, n_frames, steps, cpu_sample=0, threads=16):
             "encode_ms_per_step": round(tf / steps * 1e3, 3),
             "decode_mp_s": round(mp * steps / td, 1),
             "mean_src_jpeg_bytes": int(np.mean(lens))}
-    if cpu_sample:
-        line["cpu_baseline"] = e2e_cpu_baseline([srcs[i].cpu().numpy().tobytes() for i in range(min(16, n_frames))],
-                                                cpu_sample, threads)
     return line
 
 
@@ -276,8 +295,9 @@ def main():
     ap.add_argument("--images", type=int, default=1000, help="4K frames per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="4K frames for the CPU baseline (0 = 20 per host core, at least 320: ~10 s of wall time)")
-    ap.add_argument("--e2e", type=int, default=200,
-                    help="frames (distinct sources) of the decode+encode leg (0 = skip)")
+    ap.add_argument("--e2e", type=int, default=1000,
+                    help="frames (distinct sources) of the decode+encode leg (0 = skip; default: configs[1]'s "
+                         "1000, with the first 200 timed beside them)")
     ap.add_argument("--host-io-frames", type=int, default=1000,
                     help="frames of the PCIe-inclusive leg (pinned host in/out; 0 = skip; default: configs[1]'s 1000)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -242,10 +242,33 @@ __device__ __forceinline__ FdctTile fdct_tile(const ImgDesc* __restrict__ descs,
     return FdctTile{D, img, tile - my * tiles_x, my};
 }
 
+// Wave-local tiles (ICX_FDCT_WAVE): wave w of the workgroup owns MCUs 4w..4w+3
+// of the tile (pixels 64w..64w+63, blocks 24w..24w+23, its own list region and
+// stage) in every phase, so the phases hand over with wave barriers only and
+// the four waves never wait for one another.  Lane = (row pair i, 8-px group):
+// i = lane >> 3, sg = 8w + (lane & 7).  Otherwise a phase spans the tile:
+// i = t >> 5, sg = t & 31, with workgroup barriers between phases.
+// Measured (scripts/ab.sh, 300 4K frames, 3 rounds): FDCT -1.0 % against the
+// tile-wide phases (profiles/r3/ab_r3y_fdct_wave.txt).
+#ifndef ICX_FDCT_WAVE
+#define ICX_FDCT_WAVE 1
+#endif
+constexpr bool FDCT_WAVE = ICX_FDCT_WAVE != 0;
+__device__ __forceinline__ int fdct_row_pair(int t) { return FDCT_WAVE ? (t & 63) >> 3 : t >> 5; }
+__device__ __forceinline__ int fdct_px_group(int t) { return FDCT_WAVE ? ((t >> 6) << 3) | (t & 7) : t & 31; }
+// the hand-over between two phases of a tile
+__device__ __forceinline__ void fdct_phase_sync()
+{
+    if (FDCT_WAVE)
+        __builtin_amdgcn_wave_barrier();
+    else
+        __syncthreads();
+}
+
 __device__ __forceinline__ void fdct_load(const FdctTile& T, uint32_t (&wv)[2][6])
 {
     const ImgDesc& D = *T.D;
-    const int t = threadIdx.x, i = t >> 5, sg = t & 31;
+    const int t = threadIdx.x, i = fdct_row_pair(t), sg = fdct_px_group(t);
     const int W = D.w, H = D.h, x0 = T.tx * FDC_PX, y0 = T.my * 16;
     const uint8_t* px = D.px;
     const bool fast = (x0 + FDC_PX <= W) && (((uintptr_t)px & 7) == 0) && ((D.stride & 7) == 0);
@@ -383,13 +406,14 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
 }
 
 // After the barrier that ends emit_lists: lengths and 16-B-unit offsets.
-template <int NB, int STEP>
+template <int NB, int STEP, bool WAVE = false>
 __device__ __forceinline__ void store_list_meta(const ImgDesc& D, int64_t base, uint32_t bbase, int nblk,
                                                 const ListStage<NB, STEP>& L)
 {
-    const int t = threadIdx.x;
     constexpr int GPW = NB / (4 * STEP);
-    if (t < nblk) {
+    // WAVE: after a wave barrier, each wave stores the meta of its own blocks
+    const int t = WAVE ? (threadIdx.x >> 6) * (GPW * STEP) + (threadIdx.x & 63) : threadIdx.x;
+    if ((!WAVE || (threadIdx.x & 63) < GPW * STEP) && t < nblk) {
         const uint32_t m = L.meta[t];
         D.ncoef[bbase + t] = (uint8_t)(m & 127);
         D.coff[bbase + t] = (uint32_t)((base + (t / (GPW * STEP)) * (GPW * STEP * COEF_SLOTS)) >> 2) + (m >> 7);
@@ -413,10 +437,14 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
     const int crows = (H + 1) >> 1;             // chroma rows with image data
     const bool tail = crows - my * 8 < 8;       // ... ending inside this tile (workgroup-uniform)
 
+    // wave-local tiles stage a tail tile's downsampled chroma in the wave's own
+    // list stage (free until phase E): [comp][chroma row][its 32 columns]
+    uint8_t (*const cdw)[8][32] = (uint8_t (*)[8][32])&L.st[t >> 6][0];
+
     // ---- B: YCbCr, two Y row-DCTs, h2v2_downsample of this thread's 2x8 chroma
     // (+ C: the chroma row DCTs, except in tail tiles)
     {
-        const int i = t >> 5, sg = t & 31;
+        const int i = fdct_row_pair(t), sg = fdct_px_group(t);
         int csum[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};  // 2x2 sums of Cb, Cr
         int ky = YCC_KY, kc = YCC_KC;
         asm("" : "+v"(ky), "+v"(kc));
@@ -461,36 +489,42 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
             for (int j = 0; j < 8; j++) v[j] = (int)(((j < 4 ? lo : hi) >> (8 * (j & 3))) & 255) - 128;
             fdct8<0>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
             st_row8(&ws[(sg >> 1) * 6 + 4 + comp][i * 8], v);
+        } else if (FDCT_WAVE) {
+#pragma unroll
+            for (int c = 0; c < 2; c++) *(uint32_t*)&cdw[c][i][(sg & 7) * 4] = w[c];
         } else {
 #pragma unroll
             for (int c = 0; c < 2; c++) *(uint32_t*)&cds[c][i][sg * 4] = w[c];
         }
     }
-    __syncthreads();
+    fdct_phase_sync();
 
     // ---- C (bottom tiles whose chroma rows end inside the tile): the rows
     // past the image replicate the last chroma row (jcprepct.c
     // expand_bottom_edge), by index from the staged samples; 256 row tasks
+    // (wave-local: the wave's 4 chroma blocks x 2 components x 8 rows)
     if (tail) {
-        const int comp = t >> 7, cr = (t >> 4) & 7, cb = t & 15;
+        const int comp = FDCT_WAVE ? (t >> 5) & 1 : t >> 7, cr = (t >> (FDCT_WAVE ? 2 : 4)) & 7;
+        const int cb = FDCT_WAVE ? ((t >> 6) << 2) | (t & 3) : t & 15;
         const int re = min(cr, crows - 1 - my * 8);
-        const uint2 u = *(const uint2*)&cds[comp][re][cb * 8];
+        const uint2 u = FDCT_WAVE ? *(const uint2*)&cdw[comp][re][(t & 3) * 8] : *(const uint2*)&cds[comp][re][cb * 8];
         int v[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) v[j] = (int)(((j < 4 ? u.x : u.y) >> (8 * (j & 3))) & 255) - 128;
         fdct8<0>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
         st_row8(&ws[cb * 6 + 4 + comp][cr * 8], v);
-        __syncthreads();
+        fdct_phase_sync();
     }
 
     // ---- D: column DCT, 3 tasks per thread, in place: the thread of (block,
     // column) is the only reader and writer of that column, so the natural-
     // order output needs no barrier between the reads and the writes
+    // (wave-local: wave w's 24 blocks)
     {
         const int col = t & 7;
 #pragma unroll
         for (int rep = 0; rep < 3; rep++) {
-            const int blk = (t >> 3) + 32 * rep;
+            const int blk = FDCT_WAVE ? (t >> 6) * 24 + ((t & 63) >> 3) + 8 * rep : (t >> 3) + 32 * rep;
             int32_t d[8];
 #pragma unroll
             for (int v = 0; v < 8; v++) d[v] = ws[blk][v * 8 + col];
@@ -499,7 +533,7 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
             for (int v = 0; v < 8; v++) oz[blk][v * 8 + col] = (int16_t)(d[v] >> 16);  // ds_write_b16_d16_hi
         }
     }
-    __syncthreads();
+    fdct_phase_sync();
 
     // ---- E: dummy blocks + candidate lists.  jccoefct.c compress_data: a Y
     // block right of ceil(W/8) or below ceil(H/8) gets AC = 0 and the DC of
@@ -533,9 +567,13 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
         emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, L, thr, ent, [](int, int, int c) { return c; }, luma);
     else
         emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, L, thr, ent, fix, luma);
-    __syncthreads();
-    store_list_meta(D, base, bbase, nblk, L);
-    __syncthreads();  // LDS free for the next tile
+    fdct_phase_sync();
+    store_list_meta<FDC_BLK, 6, FDCT_WAVE>(D, base, bbase, nblk, L);
+    // LDS free for the next tile (wave-local: the wave's next phase B writes
+    // only its own blocks and stage, after its own reads above)
+#if !ICX_FDCT_NOTAIL
+    if (!FDCT_WAVE) __syncthreads();
+#endif
 }
 
 // FDCT_TILES consecutive tiles per workgroup, software-pipelined: the next
