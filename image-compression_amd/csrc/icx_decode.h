@@ -66,10 +66,31 @@ struct DecSlow {
     uint8_t vals[256];
 };
 
+// The same table for the walks that only track the decoder state (k_dec_init,
+// k_dec_sync): each entry says what the symbol does to the state instead of
+// what it is - bits 0..4 the bits it consumes (code length + extra bits, at
+// most 16 + 15), bits 5..11 what it adds to the zig-zag index (DC 1; AC
+// run + 1, ZRL 16, EOB and the other size-0 symbols 64, which ends the block),
+// 0 = no valid code here (also a DC size over 11, jdhuff.c's "bad DC").  Long
+// codes: DEC_SUB | k / DEC_SLOW exactly as in DecHuff.  One step is then a
+// look-up, a skip and an add, no symbol decoding.
+struct DecLean {
+    uint16_t lut[1 << DEC_LUT_BITS];
+    uint16_t lut2[DEC_NSUB][1 << (16 - DEC_LUT_BITS)];
+};
+ICX_HD uint16_t dec_lean_entry(int len, int sym, bool ac)
+{
+    if (!ac) return sym > 11 ? (uint16_t)0 : (uint16_t)((len + sym) | (1 << 5));
+    const int sz = sym & 15, run = sym >> 4;
+    const int zadd = sz ? run + 1 : (run == 15 ? 16 : 64);
+    return (uint16_t)((len + sz) | (zadd << 5));
+}
+
 // Per-image tables.  Components share tables (Cb/Cr normally do): h[] holds
 // the distinct ones, sel[2*c] / sel[2*c+1] index the DC / AC table of component c.
 struct DecTab {
     DecHuff h[4];
+    DecLean lean[4];  // h[] as state-transition entries (DecLean), for the state-only walks
     DecSlow slow[4];
     uint16_t qt[3][64];    // dequantisation tables, natural order, per component
     uint8_t sel[6];
@@ -513,6 +534,165 @@ ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, uint3
 }
 
 // ---------------------------------------------------------------------------
+// The state-only walk (k_dec_init warm-ups, k_dec_sync): DecWalker<false>'s
+// transitions over DecLean entries.  Per symbol: refill, one look-up, skip
+// the consumed bits, add to the zig-zag index, next block at >= 64 - the
+// symbol itself (run, size, extra bits, value) is never decoded.  Every
+// transition equals DecWalker<false>::step's (tests/dec_emu.cpp
+// dec_emu_lean_check walks both from the same states), so the states the
+// relaxation settles on are the ones the write pass's DecWalker<true> walks.
+template <class LeanPtr>
+ICX_HD uint32_t dec_lean_symbol(LeanPtr t, const ICX_GLOBAL DecSlow* slow, uint32_t pk, bool ac)
+{
+    uint32_t e = t->lut[pk >> (16 - DEC_LUT_BITS)];
+    if (!(e & (DEC_SUB | DEC_SLOW))) return e;  // codes of at most 10 bits: one branch on the common path
+    if (e & DEC_SUB) return t->lut2[e & (DEC_NSUB - 1)][pk & ((1u << (16 - DEC_LUT_BITS)) - 1)];
+    {
+        e = 0;
+        for (int l = DEC_LUT_BITS + 1; l <= 16; l++) {
+            const int code = (int)(pk >> (16 - l));
+            if (code <= slow->maxcode[l]) {
+                e = dec_lean_entry(l, slow->vals[(slow->valoff[l] + code) & 255], ac);
+                break;
+            }
+        }
+    }
+    return e;
+}
+
+template <class P>
+struct dec_is_lean {
+    static constexpr bool value = false;
+};
+template <>
+struct dec_is_lean<DecLean*> {
+    static constexpr bool value = true;
+};
+template <>
+struct dec_is_lean<const DecLean*> {
+    static constexpr bool value = true;
+};
+
+template <class LeanPtr>
+struct DecLeanWalker {
+    static_assert(dec_is_lean<LeanPtr>::value, "state-only walks read DecLean tables");
+    LeanPtr H;
+    const ICX_GLOBAL DecSlow* slow;
+    uint32_t selp;
+    const ICX_GLOBAL uint32_t* seg;
+    uint32_t nseg, ent_bits;
+    int nby, nbmcu;
+    uint32_t pos, n;
+    int b, z, ti;  // ti: table of the next symbol (component of block b, DC at z == 0)
+    DecReader R;
+    const uint32_t* words;
+
+    ICX_HD int table(int bb, int zz) const { return dec_sel(selp, bb < nby ? 0 : bb - nby + 1, zz != 0 ? 1 : 0); }
+    ICX_HD void start(uint64_t st)
+    {
+        pos = dec_pos(st);
+        b = (int)((st >> 8) & 7);
+        z = (int)(st & 63);
+        n = 0;
+        ti = table(b, z);
+        R.init(words, pos);
+    }
+    ICX_HD bool running(uint32_t stop) const { return pos < stop; }
+    ICX_HD uint64_t state() const { return dec_pack(pos, b, z); }
+    ICX_HD void step()
+    {
+        R.refill();
+        const uint32_t e = dec_lean_symbol(&H[ti], &slow[ti], R.peek16(), z != 0);
+        const int c = (int)(e & 31);
+        // straight-line transition (an invalid entry, 0, leaves the state as
+        // it is), then the rare invalid-code path overrides it
+        R.skip(c);
+        pos += (uint32_t)c;
+        z += (int)((e >> 5) & 127);
+        const bool end = z >= 64;
+        n += end ? 1u : 0u;
+        const int bn = b + 1 == nbmcu ? 0 : b + 1;
+        b = end ? bn : b;
+        z = end ? 0 : z;
+        ti = table(b, z);
+        if (c == 0) invalid();  // no valid code here
+    }
+    // DecWalker<false>::invalid: resume a bit later mid-interval, else the
+    // next interval (or the end)
+    ICX_HD void invalid()
+    {
+        uint32_t k;
+        const uint32_t nx = dec_next_seg(seg, nseg, pos >> 3, &k);
+        const uint32_t bound = nx == DEC_END ? ent_bits : (nx - DEC_PAD) * 8;
+        b = 0;
+        z = 0;
+        ti = table(0, 0);
+        if (pos + 8 < bound) {
+            pos++;
+            R.init(words, pos);
+            return;
+        }
+        if (nx == DEC_END) {
+            pos = DEC_END;
+            return;
+        }
+        pos = nx * 8;
+        R.init(words, pos);
+    }
+};
+
+template <class LeanPtr>
+ICX_HD DecLeanWalker<LeanPtr> dec_lean_walker(const DecDesc& d, LeanPtr H, const DecSlow* slow, uint32_t selp,
+                                              const uint32_t* words, const uint32_t* seg, uint32_t nseg,
+                                              uint32_t ent_bits)
+{
+    DecLeanWalker<LeanPtr> w;
+    w.H = H;
+    w.slow = (const ICX_GLOBAL DecSlow*)slow;
+    w.selp = selp;
+    w.words = words;
+    w.seg = (const ICX_GLOBAL uint32_t*)seg;
+    w.nseg = nseg;
+    w.ent_bits = ent_bits;
+    w.nby = d.nby;
+    w.nbmcu = d.wmcu;
+    return w;
+}
+
+// dec_walk<false> over the lean tables (k_dec_init's warm-up walk).
+template <class LeanPtr>
+ICX_HD uint64_t dec_lean_walk(const DecDesc& d, LeanPtr H, const DecSlow* slow, uint32_t selp, const uint32_t* words,
+                              const uint32_t* seg, uint32_t nseg, uint32_t ent_bits, uint64_t st, uint32_t stop,
+                              uint32_t& nblk, bool active = true)
+{
+    nblk = 0;
+    DecLeanWalker<LeanPtr> w = dec_lean_walker(d, H, slow, selp, words, seg, nseg, ent_bits);
+    const bool started = active && dec_pos(st) < stop;
+    bool run = false;
+    if (started) {
+        w.start(st);
+        run = w.running(stop);
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    while (__any(run)) {
+        if (run) {
+            w.step();
+            run = w.running(stop);
+        }
+        if (__any(run && w.R.low()) && run && w.R.wants()) w.R.top_up();
+    }
+#else
+    while (run) {
+        w.step();
+        run = w.running(stop);
+    }
+#endif
+    if (!started) return st;
+    nblk = w.n;
+    return w.state();
+}
+
+// ---------------------------------------------------------------------------
 // Sync-walk checkpoints.  A walk records its state at the first symbol boundary
 // at or beyond each interior mark base + (k + 1) * dec_ck_bits of its
 // subsequence, with the blocks completed before it in bits 48..63.  The state
@@ -574,8 +754,8 @@ struct CkCompare {
     }
 };
 
-// One sync walk of subsequence [base, base + sub_bits) from entry state st,
-// with checkpoints (policy ck).  Returns the exit state, or st with early ==
+// One sync walk of subsequence [base, base + sub_bits) from entry state st
+// (H: the image's DecLean tables), with checkpoints (policy ck).  Returns the exit state, or st with early ==
 // true when the walk met the previous walk (exit unchanged); nblk = blocks
 // completed inside the subsequence either way.
 template <class HuffPtr, class Ck>
@@ -588,7 +768,7 @@ ICX_HD uint64_t dec_sync_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, 
     const int nck = dec_ck_slots(sub_bits);
     nblk = 0;
     early = false;
-    DecWalker<false, HuffPtr> w = dec_walker<false>(d, H, slow, selp, words, seg, nseg, ent_bits, 0);
+    DecLeanWalker<HuffPtr> w = dec_lean_walker(d, H, slow, selp, words, seg, nseg, ent_bits);
     const bool started = active && dec_pos(st) < stop;
     bool run = false;
     if (started) {
@@ -597,14 +777,13 @@ ICX_HD uint64_t dec_sync_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, 
     }
     int k = 0;
     uint32_t ckpos = base + ckb;
-    NoSink ns;
 #if defined(__HIP_DEVICE_COMPILE__)
     while (__any(run)) {
 #else
     while (run) {
 #endif
         if (run) {
-            w.step(ns);
+            w.step();
             while (k < nck && w.pos >= ckpos) {  // a jump (END, next interval) may pass several marks
                 if (ck.visit(k, w.state() | ((uint64_t)w.n << 48), nblk)) {
                     early = true;

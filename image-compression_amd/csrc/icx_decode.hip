@@ -438,13 +438,13 @@ __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const
 // resynchronises within a few hundred bits on typical content, so most
 // estimates are already the fixed point and the first sync launch confirms
 // them; the rest are repaired by the relaxation like any other guess.
-__device__ __forceinline__ void load_tables(const DecTab* T, DecHuff* L);
+__device__ __forceinline__ void load_tables(const DecTab* T, DecLean* L);
 __device__ __forceinline__ uint32_t selector(const DecTab* T);
 
 __global__ void __launch_bounds__(256) k_dec_init(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
                                                   uint32_t warm)
 {
-    __shared__ __attribute__((aligned(16))) DecHuff L[4];
+    __shared__ __attribute__((aligned(16))) DecLean L[4];
     int slot;
     int64_t wg;
     if (!plan_slot(p, slot, wg)) return;
@@ -460,19 +460,19 @@ __global__ void __launch_bounds__(256) k_dec_init(const DecDesc* D, const DecSta
     if (live && j > 0 && j < st.nsub && warm > 0) {
         const uint32_t from = start > warm ? start - warm : 0;
         uint32_t n;
-        NoSink ns;
-        e = dec_walk<false>(d, L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
-                            st.ent_len * 8, dec_pack(from, 0, 0), start, n, 0, ns);
+        e = dec_lean_walk(d, (const DecLean*)L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg,
+                          st.nseg, st.ent_len * 8, dec_pack(from, 0, 0), start, n);
     }
     d.est[j] = e;
 }
 
-// Stage the image's distinct Huffman tables in LDS (all threads participate).
-__device__ __forceinline__ void load_tables(const DecTab* T, DecHuff* L)
+// Stage the image's distinct Huffman tables, as state transitions (DecLean),
+// in LDS (all threads participate).
+__device__ __forceinline__ void load_tables(const DecTab* T, DecLean* L)
 {
-    const uint4* src = (const uint4*)T->h;
+    const uint4* src = (const uint4*)T->lean;
     uint4* dst = (uint4*)L;
-    const int n = (int)(sizeof(DecHuff) * T->ntab / 16);
+    const int n = (int)(sizeof(DecLean) * T->ntab / 16);
     for (int k = threadIdx.x; k < n; k += blockDim.x) dst[k] = src[k];
     __syncthreads();
 }
@@ -495,7 +495,7 @@ template <bool FIRST>
 __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
                                                   int iter, int nimg, uint32_t* changed)
 {
-    __shared__ __attribute__((aligned(16))) DecHuff L[4];
+    __shared__ __attribute__((aligned(16))) DecLean L[4];
     __shared__ uint64_t ckl[FIRST ? 1 : 256][DEC_CK_MAX];
     int slot;
     int64_t wg;
@@ -519,13 +519,13 @@ __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecSta
     uint64_t x;
     if (FIRST) {
         CkRecord<ICX_GLOBAL uint64_t*> ck{ckg, nck};
-        x = dec_sync_walk(d, L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
+        x = dec_sync_walk(d, (const DecLean*)L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
                           st.ent_len * 8, e, j * sub_bits, sub_bits, nb, early, ck);
     } else {
         uint64_t* mine = ckl[FIRST ? 0 : threadIdx.x];
         for (int q = 0; q < nck; q++) mine[q] = ckg[q];
         CkCompare<ICX_GLOBAL uint64_t*, uint64_t*> ck{ckg, mine, nck, d.ncnt[j]};
-        x = dec_sync_walk(d, L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
+        x = dec_sync_walk(d, (const DecLean*)L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
                           st.ent_len * 8, e, j * sub_bits, sub_bits, nb, early, ck);
     }
     d.ncnt[j] = nb;

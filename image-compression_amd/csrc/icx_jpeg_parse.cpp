@@ -204,6 +204,18 @@ bool build_dec_huff(const uint8_t* bits, const uint8_t* vals, int n, DecHuff& t,
     return true;
 }
 
+// DecLean of a built table (DC or AC class): every code's state transition.
+void build_dec_lean(const DecHuff& h, bool ac, DecLean& lean)
+{
+    auto conv = [ac](uint16_t e) -> uint16_t {
+        if (e & (DEC_SUB | DEC_SLOW)) return e;  // long-code prefix: same second level / slow path
+        return e ? dec_lean_entry(e >> 8, e & 255, ac) : (uint16_t)0;
+    };
+    for (int i = 0; i < (1 << DEC_LUT_BITS); i++) lean.lut[i] = conv(h.lut[i]);
+    for (int k = 0; k < DEC_NSUB; k++)
+        for (int i = 0; i < (1 << (16 - DEC_LUT_BITS)); i++) lean.lut2[k][i] = conv(h.lut2[k][i]);
+}
+
 bool build_dec_tab(const JpegHeader& J, DecTab& T)
 {
     memset(&T, 0, sizeof(T));
@@ -219,6 +231,7 @@ bool build_dec_tab(const JpegHeader& J, DecTab& T)
                 if (ntab == 4) return false;
                 sl = ntab++;
                 if (!build_dec_huff(J.hbits[ac][id], J.hvals[ac][id], J.hn[ac][id], T.h[sl], T.slow[sl])) return false;
+                build_dec_lean(T.h[sl], ac != 0, T.lean[sl]);
             }
             T.sel[2 * c + ac] = (uint8_t)sl;
         }

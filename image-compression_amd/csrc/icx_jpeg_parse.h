@@ -45,6 +45,7 @@ int colour_space(const JpegHeader& J, bool jfif, bool exif, bool adobe, int tran
 
 // jpeg_make_d_derived_tbl equivalent; false if the table is invalid.
 bool build_dec_huff(const uint8_t* bits, const uint8_t* vals, int n, DecHuff& t, DecSlow& slow);
+void build_dec_lean(const DecHuff& h, bool ac, DecLean& lean);
 
 // Per-image decode tables (distinct Huffman tables + per-component selectors,
 // dequantisation per component).

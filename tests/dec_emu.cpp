@@ -96,9 +96,9 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
         est[j] = dec_pack(j * S, 0, 0);
         if (j > 0 && j < nsub && warm_up) {
             uint32_t n;
-            NoSink ns;
-            est[j] = dec_walk<false>(d, T.h, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8,
-                                     dec_pack(j * S > warm ? j * S - warm : 0, 0, 0), j * S, n, 0, ns);
+            est[j] = dec_lean_walk(d, (const DecLean*)T.lean, T.slow, sel, words.data(), seg.data(),
+                                   (uint32_t)seg.size(), ent_len * 8, dec_pack(j * S > warm ? j * S - warm : 0, 0, 0),
+                                   j * S, n);
         }
     }
     std::mt19937 rng((uint32_t)seed);
@@ -124,13 +124,13 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
             uint64_t* mine = ck.data() + (size_t)j * DEC_CK_MAX;
             if (it == 0) {
                 CkRecord<uint64_t*> rec{mine, nck};
-                x = dec_sync_walk(d, T.h, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8,
+                x = dec_sync_walk(d, (const DecLean*)T.lean, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8,
                                   est[j], j * S, S, n, early, rec);
             } else {
                 uint64_t old[DEC_CK_MAX];
                 memcpy(old, mine, sizeof(old));
                 CkCompare<uint64_t*, uint64_t*> cmp{mine, old, nck, ncnt[j]};
-                x = dec_sync_walk(d, T.h, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8,
+                x = dec_sync_walk(d, (const DecLean*)T.lean, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8,
                                   est[j], j * S, S, n, early, cmp);
                 if (early) dec_emu_early++;
             }
@@ -201,3 +201,70 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
     memcpy(out, coefs.data(), coefs.size() * sizeof(int16_t));
     return 0;
 }
+
+// DecLeanWalker (k_dec_init / k_dec_sync) against DecWalker<false> (the write
+// pass's state machine): from `nstarts` random states - any bit position,
+// block-in-MCU and zig-zag index, i.e. mostly wrong-start paths, which meet
+// invalid codes, overshooting runs and interval jumps - both walk `steps`
+// symbols and must agree on the state and block count after every one.
+// Returns the number of disagreeing steps (0), or a negative status.
+extern "C" long dec_emu_lean_check(const uint8_t* jpg, size_t len, int nstarts, int steps, int seed)
+{
+    JpegHeader J;
+    icx_status st = parse_jpeg(jpg, len, len, J);
+    if (st) return -(long)st;
+    static DecTab T;
+    if (!build_dec_tab(J, T)) return -(long)ICX_E_CORRUPT;
+    const uint32_t sel = dec_selector(T);
+    DecDesc d{};
+    d.ncomp = J.ncomp;
+    d.nby = J.ncomp == 3 ? J.hs[0] * J.vs[0] : 1;
+    d.nbmcu = J.ncomp == 3 ? d.nby + 2 : 1;
+    d.wmcu = dec_walk_mcu(J.ncomp, d.nbmcu, J.td, J.ta);
+    d.ri = J.ri;
+    const uint8_t* sc = jpg + J.scan_off;
+    const int64_t sl = (int64_t)(len - J.scan_off);
+    std::vector<uint8_t> ent;
+    std::vector<uint32_t> seg{0};
+    for (int64_t i = 0; i < sl; i++) {
+        if (i + 1 < sl && sc[i] == 0xFF && sc[i + 1] != 0x00 && sc[i + 1] != 0xFF && !(sc[i + 1] >= 0xD0 && sc[i + 1] <= 0xD7))
+            break;
+        int rst;
+        const int k = dec_unstuff_rule(i ? sc[i - 1] : 0, sc[i], i + 1 < sl ? sc[i + 1] : 0, &rst);
+        if (rst) {
+            for (int p = 0; p < DEC_PAD; p++) ent.push_back(0xFF);
+            seg.push_back((uint32_t)ent.size());
+        } else if (k) {
+            ent.push_back(sc[i]);
+        }
+    }
+    const uint32_t ent_len = (uint32_t)ent.size();
+    if (!ent_len) return 0;
+    for (int p = 0; p < DEC_TAIL + 64 + 4 * DEC_WIN; p++) ent.push_back(0xFF);
+    while (ent.size() % 4) ent.push_back(0xFF);
+    std::vector<uint32_t> words(ent.size() / 4 + 2, 0xFFFFFFFFu);
+    memcpy(words.data(), ent.data(), ent.size());
+    std::mt19937 rng((uint32_t)seed);
+    long bad = 0;
+    for (int s = 0; s < nstarts; s++) {
+        const uint64_t e0 = dec_pack(rng() % (ent_len * 8), (int)(rng() % (uint32_t)d.wmcu), (int)(rng() % 64));
+        DecWalker<false, const DecHuff*> a = dec_walker<false>(d, (const DecHuff*)T.h, T.slow, sel, words.data(),
+                                                               seg.data(), (uint32_t)seg.size(), ent_len * 8, 0);
+        DecLeanWalker<const DecLean*> b = dec_lean_walker(d, (const DecLean*)T.lean, T.slow, sel, words.data(),
+                                                          seg.data(), (uint32_t)seg.size(), ent_len * 8);
+        a.start(e0);
+        b.start(e0);
+        NoSink ns;
+        for (int k = 0; k < steps && a.running(DEC_END) && b.running(DEC_END); k++) {
+            a.step(ns);
+            b.step();
+            if (a.state() != b.state() || a.n != b.n) {
+                bad++;
+                break;
+            }
+        }
+        if (a.running(DEC_END) != b.running(DEC_END)) bad++;
+    }
+    return bad;
+}
+

@@ -147,3 +147,25 @@ def test_emulated_checkpoint_early_exit(emu, oracle, sub):
             assert rc == 0 and np.array_equal(got, ref), (h, w, q, seed)
             early += ctypes.c_long.in_dll(emu, "dec_emu_early").value
     assert early > 0
+
+
+def test_lean_walk_equals_full_walk(emu, oracle):
+    """k_dec_init / k_dec_sync walk DecLean tables (state transitions only:
+    bits consumed, zig-zag advance) while the write pass walks the full
+    tables.  From random states (almost all wrong starts: invalid codes,
+    runs past index 63, jumps over restart pads) both state machines must
+    agree after every symbol, on the golden files (restart intervals, grey,
+    4:2:2 / 4:4:4, RGB) and on q95-1.0 noise, where most symbols carry
+    long extra-bit fields."""
+    emu.dec_emu_lean_check.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    emu.dec_emu_lean_check.restype = ctypes.c_long
+    meta, jpgs, _ = load_decode_golden()
+    files = [d for n, d in jpgs.items() if not meta["cases"][n].get("unsupported")]
+    files += [oracle.encode(noise(96, 128, 5), q) for q in (0.95, 1.0)] + [oracle.encode(smooth(64, 80, 2), 0.5)]
+    checked = 0
+    for k, data in enumerate(files):
+        buf = np.frombuffer(data, np.uint8)
+        bad = emu.dec_emu_lean_check(buf.ctypes.data, buf.size, 64, 400, k + 1)
+        assert bad == 0, (k, bad)
+        checked += 1
+    assert checked > 100
