@@ -66,24 +66,27 @@ struct DecSlow {
     uint8_t vals[256];
 };
 
-// The same table for the walks that only track the decoder state (k_dec_init,
-// k_dec_sync): each entry says what the symbol does to the state instead of
-// what it is - bits 0..4 the bits it consumes (code length + extra bits, at
-// most 16 + 15), bits 5..11 what it adds to the zig-zag index (DC 1; AC
-// run + 1, ZRL 16, EOB and the other size-0 symbols 64, which ends the block),
-// 0 = no valid code here (also a DC size over 11, jdhuff.c's "bad DC").  Long
-// codes: DEC_SUB | k / DEC_SLOW exactly as in DecHuff.  One step is then a
-// look-up, a skip and an add, no symbol decoding.
+// The same table for the walks themselves (k_dec_init, k_dec_sync, k_dec_write):
+// each entry says what the symbol does instead of what it is - bits 0..4 the
+// bits it consumes (code length + extra bits, at most 16 + 15), bits 5..11
+// what it adds to the zig-zag index (DC 1; AC run + 1, ZRL 16, EOB and the
+// other size-0 symbols 64, which ends the block), bits 12..15 the extra bits
+// (the magnitude category: the value is the last of the consumed bits).  0 =
+// no valid code here (also a DC size over 11, jdhuff.c's "bad DC").  A 10-bit
+// prefix of longer codes consumes 0 bits: DEC_LEAN_LONG | k << 5 (second
+// level lut2[k]) or DEC_LEAN_LONG | DEC_LEAN_SLOW (canonical maxcode loop).
+// One step is then a look-up, a skip and an add; no symbol decoding.
+constexpr uint32_t DEC_LEAN_LONG = 0x400u, DEC_LEAN_SLOW = 0x200u;
 struct DecLean {
     uint16_t lut[1 << DEC_LUT_BITS];
     uint16_t lut2[DEC_NSUB][1 << (16 - DEC_LUT_BITS)];
 };
 ICX_HD uint16_t dec_lean_entry(int len, int sym, bool ac)
 {
-    if (!ac) return sym > 11 ? (uint16_t)0 : (uint16_t)((len + sym) | (1 << 5));
+    if (!ac) return sym > 11 ? (uint16_t)0 : (uint16_t)((len + sym) | (1 << 5) | (sym << 12));
     const int sz = sym & 15, run = sym >> 4;
     const int zadd = sz ? run + 1 : (run == 15 ? 16 : 64);
-    return (uint16_t)((len + sz) | (zadd << 5));
+    return (uint16_t)((len + sz) | (zadd << 5) | (sz << 12));
 }
 
 // Per-image tables.  Components share tables (Cb/Cr normally do): h[] holds
@@ -544,20 +547,31 @@ ICX_HD uint64_t dec_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, uint3
 template <class LeanPtr>
 ICX_HD uint32_t dec_lean_symbol(LeanPtr t, const ICX_GLOBAL DecSlow* slow, uint32_t pk, bool ac)
 {
-    uint32_t e = t->lut[pk >> (16 - DEC_LUT_BITS)];
-    if (!(e & (DEC_SUB | DEC_SLOW))) return e;  // codes of at most 10 bits: one branch on the common path
-    if (e & DEC_SUB) return t->lut2[e & (DEC_NSUB - 1)][pk & ((1u << (16 - DEC_LUT_BITS)) - 1)];
-    {
-        e = 0;
-        for (int l = DEC_LUT_BITS + 1; l <= 16; l++) {
-            const int code = (int)(pk >> (16 - l));
-            if (code <= slow->maxcode[l]) {
-                e = dec_lean_entry(l, slow->vals[(slow->valoff[l] + code) & 255], ac);
-                break;
-            }
-        }
+    const uint32_t e = t->lut[pk >> (16 - DEC_LUT_BITS)];
+    if ((e & 31) || !e) return e;  // codes of at most 10 bits (or none): one branch on the common path
+    if (!(e & DEC_LEAN_SLOW)) return t->lut2[(e >> 5) & (DEC_NSUB - 1)][pk & ((1u << (16 - DEC_LUT_BITS)) - 1)];
+    for (int l = DEC_LUT_BITS + 1; l <= 16; l++) {
+        const int code = (int)(pk >> (16 - l));
+        if (code <= slow->maxcode[l]) return dec_lean_entry(l, slow->vals[(slow->valoff[l] + code) & 255], ac);
     }
-    return e;
+    return 0;
+}
+
+// First levels in one place (LDS) and the whole tables in global memory
+// (k_dec_write keeps only the 10-bit first levels in LDS).
+struct SplitLean {
+    const uint16_t (*lut)[1 << DEC_LUT_BITS];
+    const ICX_GLOBAL DecLean* full;
+};
+template <class LeanPtr>
+ICX_HD uint32_t dec_lean_lookup(LeanPtr H, int ti, const ICX_GLOBAL DecSlow* slow, uint32_t pk, bool ac)
+{
+    return dec_lean_symbol(&H[ti], &slow[ti], pk, ac);
+}
+ICX_HD uint32_t dec_lean_lookup(const SplitLean& H, int ti, const ICX_GLOBAL DecSlow* slow, uint32_t pk, bool ac)
+{
+    const uint32_t e = H.lut[ti][pk >> (16 - DEC_LUT_BITS)];
+    return (e & 31) || !e ? e : dec_lean_symbol(&H.full[ti], &slow[ti], pk, ac);
 }
 
 template <class P>
@@ -570,6 +584,10 @@ struct dec_is_lean<DecLean*> {
 };
 template <>
 struct dec_is_lean<const DecLean*> {
+    static constexpr bool value = true;
+};
+template <>
+struct dec_is_lean<SplitLean> {
     static constexpr bool value = true;
 };
 
@@ -602,7 +620,7 @@ struct DecLeanWalker {
     ICX_HD void step()
     {
         R.refill();
-        const uint32_t e = dec_lean_symbol(&H[ti], &slow[ti], R.peek16(), z != 0);
+        const uint32_t e = dec_lean_lookup(H, ti, slow, R.peek16(), z != 0);
         const int c = (int)(e & 31);
         // straight-line transition (an invalid entry, 0, leaves the state as
         // it is), then the rare invalid-code path overrides it
@@ -690,6 +708,120 @@ ICX_HD uint64_t dec_lean_walk(const DecDesc& d, LeanPtr H, const DecSlow* slow, 
     if (!started) return st;
     nblk = w.n;
     return w.state();
+}
+
+// The write pass's walk (k_dec_write): DecWalker<true>'s transitions and
+// sink calls over DecLean entries - the coefficient's value is the last
+// `extra bits` of the bits the entry consumes, its zig-zag index z + zadd - 1.
+// tests/dec_emu.cpp dec_emu_lean_check records both walkers' sink calls from
+// random states and entry points and compares them.
+template <class LeanPtr>
+struct DecLeanWriter {
+    static_assert(dec_is_lean<LeanPtr>::value, "the write walk reads DecLean tables");
+    LeanPtr H;
+    const ICX_GLOBAL DecSlow* slow;
+    uint32_t selp;
+    const ICX_GLOBAL uint32_t* seg;
+    uint32_t nseg, ent_bits;
+    int nby, nbmcu;
+    int ri, nbm;
+    int64_t nblocks;
+    uint32_t pos, n;
+    int b, z, ti;
+    bool own;
+    bool bad;
+    int64_t blk_base;
+    DecReader R;
+    const uint32_t* words;
+
+    ICX_HD int table(int bb, int zz) const { return dec_sel(selp, bb < nby ? 0 : bb - nby + 1, zz != 0 ? 1 : 0); }
+    ICX_HD void start(uint64_t st)
+    {
+        pos = dec_pos(st);
+        b = (int)((st >> 8) & 7);
+        z = (int)(st & 63);
+        n = 0;
+        own = z == 0;
+        bad = false;
+        ti = table(b, z);
+        R.init(words, pos);
+    }
+    ICX_HD bool running(uint32_t stop) const { return pos < stop || z != 0; }
+    ICX_HD uint64_t state() const { return dec_pack(pos, b, z); }
+    template <class Sink>
+    ICX_HD void step(Sink& sink)
+    {
+        R.refill();
+        const uint32_t e = dec_lean_lookup(H, ti, slow, R.peek16(), z != 0);
+        const int c = (int)(e & 31);
+        if (c == 0) {  // no valid code here
+            invalid();
+            return;
+        }
+        const int sz = (int)(e >> 12), zadd = (int)((e >> 5) & 127);
+        const uint32_t v = (uint32_t)(R.buf >> (64 - c)) & ((1u << sz) - 1u);
+        R.skip(c);
+        pos += (uint32_t)c;
+        const int x = sz ? dec_extend((int)v, sz) : 0;
+        const int zc = z + zadd - 1;  // zig-zag index of a coefficient (DC: 0)
+        sink.put(!own ? 0 : sz ? (zc > 63 ? 63 : zc) : z, x);
+        z += zadd;
+        const bool end = z >= 64;
+        const int64_t bi = blk_base + n;
+        sink.flush_if(end && own && bi < nblocks, bi);
+        own = own || end;
+        n += end ? 1u : 0u;
+        const int bn = b + 1 == nbmcu ? 0 : b + 1;
+        b = end ? bn : b;
+        z = end ? 0 : z;
+        ti = table(b, z);
+    }
+    // DecWalker<true>::invalid
+    ICX_HD void invalid()
+    {
+        uint32_t k;
+        const uint32_t nx = dec_next_seg(seg, nseg, pos >> 3, &k);
+        const uint32_t bound = nx == DEC_END ? ent_bits : (nx - DEC_PAD) * 8;
+        b = 0;
+        z = 0;
+        ti = table(0, 0);
+        own = true;
+        if (pos + 8 < bound) {
+            bad = true;
+            pos++;
+            R.init(words, pos);
+            return;
+        }
+        if (nx == DEC_END) {
+            pos = DEC_END;
+            return;
+        }
+        if (ri > 0 && blk_base + (int64_t)n != (int64_t)k * ri * nbm) bad = true;
+        pos = nx * 8;
+        R.init(words, pos);
+    }
+};
+
+template <class LeanPtr>
+ICX_HD DecLeanWriter<LeanPtr> dec_lean_writer(const DecDesc& d, LeanPtr H, const DecSlow* slow, uint32_t selp,
+                                              const uint32_t* words, const uint32_t* seg, uint32_t nseg,
+                                              uint32_t ent_bits, int64_t blk_base)
+{
+    DecLeanWriter<LeanPtr> w;
+    w.H = H;
+    w.slow = (const ICX_GLOBAL DecSlow*)slow;
+    w.selp = selp;
+    w.words = words;
+    w.seg = (const ICX_GLOBAL uint32_t*)seg;
+    w.nseg = nseg;
+    w.ent_bits = ent_bits;
+    w.nby = d.nby;
+    w.nbmcu = d.wmcu;
+    w.ri = d.ri;
+    w.nbm = d.nbmcu;
+    w.nblocks = d.nblocks;
+    w.blk_base = blk_base;
+    return w;
 }
 
 // ---------------------------------------------------------------------------

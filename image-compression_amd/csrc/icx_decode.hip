@@ -620,7 +620,7 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
         const int n = (int)(d.tab->ntab * sizeof(L1[0]) / 16);
         for (int k = threadIdx.x; k < n; k += blockDim.x) {
             const int t = k / (int)(sizeof(L1[0]) / 16), o = k % (int)(sizeof(L1[0]) / 16);
-            ((uint4*)L1[t])[o] = ((const uint4*)d.tab->h[t].lut)[o];
+            ((uint4*)L1[t])[o] = ((const uint4*)d.tab->lean[t].lut)[o];
         }
         __syncthreads();
     }
@@ -629,9 +629,9 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
         pc = dec_piece((const ICX_GLOBAL uint64_t*)d.est, (const ICX_GLOBAL uint64_t*)d.ck,
                        (const ICX_GLOBAL uint32_t*)d.boff, (uint32_t)j, (int)(t - j * np), sub_bits);
     const uint32_t stop = pc.stop;
-    const SplitHuff H{(const uint16_t (*)[1 << DEC_LUT_BITS])L1, (const ICX_GLOBAL DecHuff*)d.tab->h};
-    DecWalker<true, SplitHuff> w = dec_walker<true>(d, H, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent,
-                                                    d.seg, st.nseg, st.ent_len * 8, pc.blk);
+    const SplitLean H{(const uint16_t (*)[1 << DEC_LUT_BITS])L1, (const ICX_GLOBAL DecLean*)d.tab->lean};
+    DecLeanWriter<SplitLean> w = dec_lean_writer(d, H, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg,
+                                                 st.nseg, st.ent_len * 8, pc.blk);
     bool run = false;
     if (pc.have) {
         run = !(dec_pos(pc.e) >= stop && (pc.e & 63) == 0);

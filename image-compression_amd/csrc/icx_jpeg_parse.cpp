@@ -208,7 +208,8 @@ bool build_dec_huff(const uint8_t* bits, const uint8_t* vals, int n, DecHuff& t,
 void build_dec_lean(const DecHuff& h, bool ac, DecLean& lean)
 {
     auto conv = [ac](uint16_t e) -> uint16_t {
-        if (e & (DEC_SUB | DEC_SLOW)) return e;  // long-code prefix: same second level / slow path
+        if (e & DEC_SUB) return (uint16_t)(DEC_LEAN_LONG | ((e & (DEC_NSUB - 1)) << 5));  // long-code prefix:
+        if (e & DEC_SLOW) return (uint16_t)(DEC_LEAN_LONG | DEC_LEAN_SLOW);                // same second level
         return e ? dec_lean_entry(e >> 8, e & 255, ac) : (uint16_t)0;
     };
     for (int i = 0; i < (1 << DEC_LUT_BITS); i++) lean.lut[i] = conv(h.lut[i]);

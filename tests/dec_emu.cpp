@@ -181,8 +181,8 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
         const uint32_t j = t / np;
         const DecPiece pc = dec_piece(est.data(), ck.data(), boff.data(), j, (int)(t % np), S);
         if (!pc.have || (dec_pos(pc.e) >= pc.stop && (pc.e & 63) == 0)) continue;
-        DecWalker<true, const DecHuff*> w = dec_walker<true>(d, (const DecHuff*)T.h, T.slow, sel, words.data(),
-                                                             seg.data(), (uint32_t)seg.size(), ent_len * 8, pc.blk);
+        DecLeanWriter<const DecLean*> w = dec_lean_writer(d, (const DecLean*)T.lean, T.slow, sel, words.data(),
+                                                          seg.data(), (uint32_t)seg.size(), ent_len * 8, pc.blk);
         w.start(pc.e);
         while (w.running(pc.stop)) w.step(sk);
         bad |= w.bad;  // as k_dec_write: an invalid code on the true path = corrupt data
@@ -264,6 +264,36 @@ extern "C" long dec_emu_lean_check(const uint8_t* jpg, size_t len, int nstarts, 
             }
         }
         if (a.running(DEC_END) != b.running(DEC_END)) bad++;
+    }
+    // the write walks: every sink call (index, value; flushed block) in order
+    struct Rec {
+        std::vector<int64_t> ev;
+        void put(int z, int v) { ev.push_back(((int64_t)z << 32) ^ (uint32_t)v); }
+        void flush_if(bool c, int64_t bi)
+        {
+            if (c) ev.push_back(-1 - bi);
+        }
+    };
+    d.nblocks = 1 << 20;
+    for (int s = 0; s < nstarts; s++) {
+        const uint64_t e0 = dec_pack(rng() % (ent_len * 8), (int)(rng() % (uint32_t)d.wmcu), (int)(rng() % 64));
+        const int64_t base = (int64_t)(rng() % 4096);
+        DecWalker<true, const DecHuff*> a = dec_walker<true>(d, (const DecHuff*)T.h, T.slow, sel, words.data(),
+                                                             seg.data(), (uint32_t)seg.size(), ent_len * 8, base);
+        DecLeanWriter<const DecLean*> b = dec_lean_writer(d, (const DecLean*)T.lean, T.slow, sel, words.data(),
+                                                          seg.data(), (uint32_t)seg.size(), ent_len * 8, base);
+        a.start(e0);
+        b.start(e0);
+        Rec ra, rb;
+        for (int k = 0; k < steps && a.running(DEC_END) && b.running(DEC_END); k++) {
+            a.step(ra);
+            b.step(rb);
+            if (a.state() != b.state() || a.n != b.n || a.bad != b.bad || a.own != b.own) {
+                bad++;
+                break;
+            }
+        }
+        if (ra.ev != rb.ev) bad++;
     }
     return bad;
 }
