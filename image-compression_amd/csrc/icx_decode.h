@@ -617,23 +617,39 @@ struct DecLeanWalker {
     }
     ICX_HD bool running(uint32_t stop) const { return pos < stop; }
     ICX_HD uint64_t state() const { return dec_pack(pos, b, z); }
-    ICX_HD void step()
+    // a lane with no walk (it only keeps the wave's loop company, step(false)):
+    // a state that reads no memory
+    ICX_HD void park()
+    {
+        pos = DEC_END;
+        b = z = ti = 0;
+        n = 0;
+        R.buf = 0;
+        R.avail = 64;
+        R.wi = 0;
+        R.nq = DEC_WIN;
+        for (int j = 0; j < DEC_WIN; j++) R.q[j] = 0;
+    }
+    // act == false: a lane whose walk has ended keeps the wave's loop company
+    // without changing its state (no exec-masked region around the step: the
+    // loop state then needs no merge copies at the loop head)
+    ICX_HD void step(bool act = true)
     {
         R.refill();
         const uint32_t e = dec_lean_lookup(H, ti, slow, R.peek16(), z != 0);
-        const int c = (int)(e & 31);
+        const int c = act ? (int)(e & 31) : 0;
         // straight-line transition (an invalid entry, 0, leaves the state as
         // it is), then the rare invalid-code path overrides it
         R.skip(c);
         pos += (uint32_t)c;
-        z += (int)((e >> 5) & 127);
+        z += act ? (int)((e >> 5) & 127) : 0;
         const bool end = z >= 64;
         n += end ? 1u : 0u;
         const int bn = b + 1 == nbmcu ? 0 : b + 1;
         b = end ? bn : b;
         z = end ? 0 : z;
         ti = table(b, z);
-        if (c == 0) invalid();  // no valid code here
+        if (act && c == 0) invalid();  // no valid code here
     }
     // DecWalker<false>::invalid: resume a bit later mid-interval, else the
     // next interval (or the end)
@@ -690,13 +706,13 @@ ICX_HD uint64_t dec_lean_walk(const DecDesc& d, LeanPtr H, const DecSlow* slow, 
     if (started) {
         w.start(st);
         run = w.running(stop);
+    } else {
+        w.park();
     }
 #if defined(__HIP_DEVICE_COMPILE__)
     while (__any(run)) {
-        if (run) {
-            w.step();
-            run = w.running(stop);
-        }
+        w.step(run);  // predicated: lanes that are done keep their state
+        run = run && w.running(stop);
         if (__any(run && w.R.low()) && run && w.R.wants()) w.R.top_up();
     }
 #else
@@ -906,6 +922,8 @@ ICX_HD uint64_t dec_sync_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, 
     if (started) {
         w.start(st);
         run = w.running(stop);
+    } else {
+        w.park();
     }
     int k = 0;
     uint32_t ckpos = base + ckb;
@@ -914,18 +932,16 @@ ICX_HD uint64_t dec_sync_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, 
 #else
     while (run) {
 #endif
-        if (run) {
-            w.step();
-            while (k < nck && w.pos >= ckpos) {  // a jump (END, next interval) may pass several marks
-                if (ck.visit(k, w.state() | ((uint64_t)w.n << 48), nblk)) {
-                    early = true;
-                    break;
-                }
-                k++;
-                ckpos += ckb;
+        w.step(run);  // predicated: lanes that are done keep their state
+        while (run && k < nck && w.pos >= ckpos) {  // a jump (END, next interval) may pass several marks
+            if (ck.visit(k, w.state() | ((uint64_t)w.n << 48), nblk)) {
+                early = true;
+                break;
             }
-            run = !early && w.running(stop);
+            k++;
+            ckpos += ckb;
         }
+        run = run && !early && w.running(stop);
 #if defined(__HIP_DEVICE_COMPILE__)
         if (__any(run && w.R.low()) && run && w.R.wants()) w.R.top_up();
 #endif
