@@ -173,6 +173,69 @@ __device__ __forceinline__ void fdct8(int32_t& d0, int32_t& d1, int32_t& d2, int
     d1 = dot2<K * 9633, K * 11363>(b, dot2<K * 2260, K * 6437>(a, r)) >> OS;
 }
 
+// The column pass of jpeg_fdct_islow over two adjacent columns at once: p[v] =
+// (row v of column c, row v of column c + 1) as an int16 pair, as one
+// ds_read_b32 of the natural-order workspace returns it.  The butterflies and
+// the DC/Nyquist sums run as packed 16-bit adds (v_pk_add/sub_u16: every
+// partial fits int16 - row outputs lie in [-4096, 4080], so |t10 +- t11| <=
+// 32768 - 128 and the +2 of DESCALE stays inside), the rotations as the same
+// dot2 chains as fdct8<1, true> per column (operand pairs picked from the
+// packed partials by v_perm), and each output row leaves as one int16 pair
+// for one ds_write_b32: 8 LDS reads and 8 stores per column pair instead of
+// 16 and 16, and half the butterfly VALU.  Equal to fdct8<1> per column.
+__device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b)
+{
+    uint32_t d;
+    asm("v_pk_add_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b)
+{
+    uint32_t d;
+    asm("v_pk_sub_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+__device__ __forceinline__ uint32_t pk_sra2(uint32_t a)  // both halves >> 2, arithmetic
+{
+    uint32_t d;
+    asm("v_pk_ashrrev_i16 %0, %1, %2" : "=v"(d) : "s"(0x00020002u), "v"(a));
+    return d;
+}
+__device__ __forceinline__ void fdct_col_pair(uint32_t (&p)[8])
+{
+    const uint32_t t0 = pk_add16(p[0], p[7]), t7 = pk_sub16(p[0], p[7]);
+    const uint32_t t1 = pk_add16(p[1], p[6]), t6 = pk_sub16(p[1], p[6]);
+    const uint32_t t2 = pk_add16(p[2], p[5]), t5 = pk_sub16(p[2], p[5]);
+    const uint32_t t3 = pk_add16(p[3], p[4]), t4 = pk_sub16(p[3], p[4]);
+    const uint32_t t10 = pk_add16(t0, t3), t13 = pk_sub16(t0, t3);
+    const uint32_t t11 = pk_add16(t1, t2), t12 = pk_sub16(t1, t2);
+    uint32_t k2 = 0x00020002u;  // DESCALE(x, PASS1_BITS) rounding, both halves
+    asm("" : "+v"(k2));
+    const uint32_t t10r = pk_add16(t10, k2);
+    p[0] = pk_sra2(pk_add16(t10r, t11));
+    p[4] = pk_sra2(pk_sub16(t10r, t11));
+    int r = 1 << 15;  // fdct8<1, true>'s rounding constant
+    asm("" : "+v"(r));
+    int o[2][6];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        // (lo of x, lo of y) or (hi of x, hi of y)
+        const uint32_t sel = h ? 0x07060302u : 0x05040100u;
+        const uint32_t e = __builtin_amdgcn_perm(t13, t12, sel);
+        const uint32_t a = __builtin_amdgcn_perm(t5, t4, sel), b = __builtin_amdgcn_perm(t7, t6, sel);
+        o[h][0] = dot2<2 * 9633, 2 * 11363>(b, dot2<2 * 2260, 2 * 6437>(a, r));      // d1
+        o[h][1] = dot2<2 * 4433, 2 * 10703>(e, r);                                   // d2
+        o[h][2] = dot2<2 * -2259, 2 * 9633>(b, dot2<2 * -6436, 2 * -11362>(a, r));   // d3
+        o[h][3] = dot2<2 * -11362, 2 * 6437>(b, dot2<2 * 9633, 2 * 2261>(a, r));     // d5
+        o[h][4] = dot2<2 * -10704, 2 * 4433>(e, r);                                  // d6
+        o[h][5] = dot2<2 * -6436, 2 * 2260>(b, dot2<2 * -11363, 2 * 9633>(a, r));    // d7
+    }
+    // each output's value is its int32's high half: (column c, column c + 1)
+    constexpr int at[6] = {1, 2, 3, 5, 6, 7};
+#pragma unroll
+    for (int j = 0; j < 6; j++) p[at[j]] = __builtin_amdgcn_perm((uint32_t)o[1][j], (uint32_t)o[0][j], 0x07060302u);
+}
+
 // rgb_ycc_convert (jccolor.c): 16-bit fixed point, FIX(x) = (int)(x*65536+0.5):
 //   y  = (19595 r + 38470 g + 7471 b + 32768) >> 16
 //   cb = (-11059 r - 21709 g + 32768 b + (128 << 16) + 32767) >> 16
@@ -192,6 +255,15 @@ __device__ __forceinline__ void rgb_ycc(int r, int g, int b, int ky, int kc, int
     y128 = g + (dot2<-19595, -7471>(n, ky) >> 16);
     cb = dot2<11059, -32768>(n, kc) >> 16;
     cr = dot2<-32768, 5329>(n, kc) >> 16;
+}
+// The same, with Cb and Cr left as an int16 pair (cb, cr): both sums lie in
+// [0, 2^24) before the shift, so each sample is its int32's high half - one
+// v_perm for the two shifts and the packing.
+__device__ __forceinline__ uint32_t rgb_ycc_pk(int r, int g, int b, int ky, int kc, int& y128)
+{
+    const uint32_t n = pack16(g - r, g - b);
+    y128 = g + (dot2<-19595, -7471>(n, ky) >> 16);
+    return __builtin_amdgcn_perm((uint32_t)dot2<-32768, 5329>(n, kc), (uint32_t)dot2<11059, -32768>(n, kc), 0x07060302u);
 }
 
 // =================================================================== FDCT
@@ -254,6 +326,16 @@ __device__ __forceinline__ FdctTile fdct_tile(const ImgDesc* __restrict__ descs,
 #define ICX_FDCT_WAVE 1
 #endif
 constexpr bool FDCT_WAVE = ICX_FDCT_WAVE != 0;
+// Column DCT of two thirds of a wave's blocks on packed column pairs
+// (fdct_col_pair), the rest one column per lane.
+#ifndef ICX_FDCT_PKCOL
+#define ICX_FDCT_PKCOL 1
+#endif
+// Phase B: each pixel's Cb, Cr as one int16 pair (rgb_ycc_pk), the 2x2 sums
+// and the h2v2 bias as packed adds, the downsampled bytes by v_perm.
+#ifndef ICX_FDCT_PKSUM
+#define ICX_FDCT_PKSUM 1
+#endif
 __device__ __forceinline__ int fdct_row_pair(int t) { return FDCT_WAVE ? (t & 63) >> 3 : t >> 5; }
 __device__ __forceinline__ int fdct_px_group(int t) { return FDCT_WAVE ? ((t >> 6) << 3) | (t & 7) : t & 31; }
 // the hand-over between two phases of a tile
@@ -446,6 +528,7 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
     {
         const int i = fdct_row_pair(t), sg = fdct_px_group(t);
         int csum[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};  // 2x2 sums of Cb, Cr
+        uint32_t psum[4];                               // ICX_FDCT_PKSUM: the same as (Cb, Cr) pairs
         int ky = YCC_KY, kc = YCC_KC;
         asm("" : "+v"(ky), "+v"(kc));
 #pragma unroll
@@ -458,10 +541,18 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
                 const int c1 = (wv[h][o1 >> 2] >> ((o1 & 3) * 8)) & 255;
                 const int c2 = (wv[h][o2 >> 2] >> ((o2 & 3) * 8)) & 255;
                 const int R = BGR ? c2 : c0, G = c1, B = BGR ? c0 : c2;
-                int cb, cr;
-                rgb_ycc(R, G, B, ky, kc, yv[k], cb, cr);
-                csum[0][k >> 1] += cb;
-                csum[1][k >> 1] += cr;
+                if (ICX_FDCT_PKSUM) {
+                    const uint32_t cc = rgb_ycc_pk(R, G, B, ky, kc, yv[k]);
+                    // the h2v2 bias (1, 2, 1, 2 by output column) rides on the
+                    // group's first pair: sums stay < 2^10 per half
+                    psum[k >> 1] = pk_add16(h == 0 && !(k & 1) ? (((k >> 1) & 1) ? 0x00020002u : 0x00010001u)
+                                                               : psum[k >> 1], cc);
+                } else {
+                    int cb, cr;
+                    rgb_ycc(R, G, B, ky, kc, yv[k], cb, cr);
+                    csum[0][k >> 1] += cb;
+                    csum[1][k >> 1] += cr;
+                }
             }
             fdct8<0>(yv[0], yv[1], yv[2], yv[3], yv[4], yv[5], yv[6], yv[7]);
             const int r = 2 * i + h;
@@ -469,11 +560,22 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
             st_row8(&ws[blk][(r & 7) * 8], yv);
         }
         uint32_t w[2];
+        if (ICX_FDCT_PKSUM) {
+            uint32_t q[4];
 #pragma unroll
-        for (int c = 0; c < 2; c++) {  // h2v2_downsample: bias 1, 2, 1, 2 by output column
-            w[c] = 0;
+            for (int j = 0; j < 4; j++) asm("v_pk_lshrrev_b16 %0, %1, %2" : "=v"(q[j]) : "s"(0x00020002u), "v"(psum[j]));
+            // (cb_j, cr_j) halves -> (cb0 cb1 cr0 cr1), (cb2 cb3 cr2 cr3) -> Cb word, Cr word
+            const uint32_t x01 = __builtin_amdgcn_perm(q[1], q[0], 0x06020400u);
+            const uint32_t x23 = __builtin_amdgcn_perm(q[3], q[2], 0x06020400u);
+            w[0] = __builtin_amdgcn_perm(x23, x01, 0x05040100u);
+            w[1] = __builtin_amdgcn_perm(x23, x01, 0x07060302u);
+        } else {
 #pragma unroll
-            for (int j = 0; j < 4; j++) w[c] |= (uint32_t)((csum[c][j] + 1 + (j & 1)) >> 2) << (8 * j);
+            for (int c = 0; c < 2; c++) {  // h2v2_downsample: bias 1, 2, 1, 2 by output column
+                w[c] = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) w[c] |= (uint32_t)((csum[c][j] + 1 + (j & 1)) >> 2) << (8 * j);
+            }
         }
         if (!tail) {
             // C, fused: chroma row i of chroma block sg >> 1 is 4 + 4 samples of
@@ -520,6 +622,31 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
     // column) is the only reader and writer of that column, so the natural-
     // order output needs no barrier between the reads and the writes
     // (wave-local: wave w's 24 blocks)
+#if ICX_FDCT_PKCOL
+    if (FDCT_WAVE) {
+        // wave-local: blocks 0..15 of the wave as column pairs (lane = block *
+        // 4 + pair: a ds_read_b32 row of 32 lanes covers 8 blocks x 4 pairs on
+        // distinct banks), blocks 16..23 one column per lane
+        {
+            const int blk = (t >> 6) * 24 + ((t & 63) >> 2), c = (t & 3) * 2;
+            uint32_t p[8];
+#pragma unroll
+            for (int v = 0; v < 8; v++) p[v] = *(const uint32_t*)&ws[blk][v * 8 + c];
+            fdct_col_pair(p);
+#pragma unroll
+            for (int v = 0; v < 8; v++) *(uint32_t*)&oz[blk][v * 8 + c] = p[v];
+        }
+        {
+            const int blk = (t >> 6) * 24 + 16 + ((t & 63) >> 3), col = t & 7;
+            int32_t d[8];
+#pragma unroll
+            for (int v = 0; v < 8; v++) d[v] = ws[blk][v * 8 + col];
+            fdct8<1, true>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+#pragma unroll
+            for (int v = 0; v < 8; v++) oz[blk][v * 8 + col] = (int16_t)(d[v] >> 16);  // ds_write_b16_d16_hi
+        }
+    } else
+#endif
     {
         const int col = t & 7;
 #pragma unroll
