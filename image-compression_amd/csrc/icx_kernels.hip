@@ -400,6 +400,9 @@ __device__ __forceinline__ void fdct_load(const FdctTile& T, uint32_t (&wv)[2][6
 // the lanes with nothing to store write to (never read, shared by the waves,
 // so the stores need no exec mask), and per block (offset in its group << 7)
 // | list length.
+#ifndef ICX_FDCT_EMIT_LA
+#define ICX_FDCT_EMIT_LA 1
+#endif
 template <int NB, int STEP>
 struct ListStage {
     uint32_t st[4][STEP * 64];
@@ -456,17 +459,29 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
             const uint64_t mask = __ballot(cand);
             const int cnt = __builtin_amdgcn_readfirstlane(__popcll(mask)), r4 = (cnt + 3) & ~3;
             // the candidate's stage index: wave base + run + candidates below the lane
-            const int at = (int)__builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, (uint32_t)(wave * (STEP * 64) + run)));
             // the padding to a whole 16-B group is left as it is in the stage:
             // k_huff never codes an entry past the list's length (writing the
             // block's first non-candidates there cost 4 VALU per block: FDCT +9 %)
             // one v_cndmask on the ballot: as a C select the compiler branches
             // around the candidate address (exec save / restore: SALU)
-            int idx;
-            asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(idx) : "v"(dummy_at), "v"(at), "s"(mask));
-            st0[idx] =
-                __float_as_uint(cf) | ((uint32_t)lane << 3) | (luma(a) ? 0u : 0x200u);
+            const uint32_t ent_v = __float_as_uint(cf) | ((uint32_t)lane << 3) | (luma(a) ? 0u : 0x200u);
+            if (ICX_FDCT_EMIT_LA) {
+                // byte address: candidates below the lane counted from 0 (no
+                // move of the wave-uniform base into a VGPR), then one
+                // v_lshl_add_u32 with the scalar byte base
+                const uint32_t below =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+                const uint32_t at_b = below * 4u + (uint32_t)(wave * (STEP * 64) + run) * 4u;
+                uint32_t addr;
+                asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(addr) : "v"(dummy_at * 4), "v"(at_b), "s"(mask));
+                *(uint32_t*)((char*)st0 + addr) = ent_v;
+            } else {
+                const int at = (int)__builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, (uint32_t)(wave * (STEP * 64) + run)));
+                int idx;
+                asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(idx) : "v"(dummy_at), "v"(at), "s"(mask));
+                st0[idx] = ent_v;
+            }
             // total + run is a multiple of 4: (x >> 2) << 7 = x << 5
             meta = writelane(meta, (((int)total + run) << 5) | cnt, a);  // scalar arithmetic, one VALU op
             run += r4;
