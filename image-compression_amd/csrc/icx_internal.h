@@ -69,6 +69,10 @@ struct ImgDesc {
     int32_t w, h, stride, fmt;
     int32_t ncomp, mcux, mcuy, ywb, yhb;
     int32_t nchunks, hdr_len, cand_node;  // cand_node: QNode whose thr[] filters the FDCT's lists
+    // FDCT tiles per tile row (16 MCUs / 16 grey blocks each) and its
+    // reciprocal for a multiply-high division (tiles_xm = ceil(2^32 / tiles_x),
+    // exact for tile * tiles_x < 2^32; 0 when tiles_x == 1)
+    uint32_t tiles_x, tiles_xm;
     int64_t nblocks;
     int64_t target;
     int32_t* coefs;        // candidate lists, COEF_SLOTS entries reserved per block (see above)

@@ -269,7 +269,8 @@ __device__ __forceinline__ uint32_t rgb_ycc_pk(int r, int g, int b, int ky, int 
 // =================================================================== FDCT
 
 // Colour: one workgroup = 16 rows x 256 px = 16 MCUs of one MCU row (96 blocks);
-// every phase has 1-3 equal tasks per thread.  LDS 15 KiB -> 8 workgroups/CU.
+// every phase has 1-3 equal tasks per thread.  LDS 20.4 KiB; three tiles per
+// workgroup at 74 VGPRs -> 6 workgroups/CU.
 //   B. one row pair x 8 px per thread straight from HBM (24 B runs; a wave
 //      reads four contiguous 768 B row pieces; edges clamped): YCbCr, two Y
 //      row-DCTs in registers -> workspace; h2v2_downsample of its own 2x8
@@ -296,6 +297,16 @@ __device__ __forceinline__ void st_row8(int16_t* p, const int (&v)[8])  // 8 int
 // Phase B loads: this thread's rows 2i, 2i+1 of the tile, pixels 8sg..8sg+7
 // (24 bytes each), edges clamped.  Separate from the arithmetic so the kernel
 // can issue the next tile's loads before it computes the current one.
+#ifndef ICX_FDCT_NOHOIST
+#define ICX_FDCT_NOHOIST 1
+#endif
+// tile / tiles_x by one scalar multiply-high (a 32-bit division is ~30
+// scalar instructions in front of every tile)
+__device__ __forceinline__ int fdct_tile_row(const ImgDesc& D, int tile)
+{
+    return D.tiles_xm ? (int)__umulhi((uint32_t)tile, D.tiles_xm) : tile;
+}
+
 struct FdctTile {
     const ImgDesc* D;
     int img, tx, my;
@@ -309,9 +320,8 @@ __device__ __forceinline__ FdctTile fdct_tile(const ImgDesc* __restrict__ descs,
     const int img = ids ? ids[slot] : slot;
     const ImgDesc* D = &descs[img];
     const int tile = gridDim.y > 1 ? (int)item : (int)(item - prefix[slot]);
-    const int tiles_x = (D->mcux + FDC_MCU - 1) / FDC_MCU;
-    const int my = tile / tiles_x;
-    return FdctTile{D, img, tile - my * tiles_x, my};
+    const int my = fdct_tile_row(*D, tile);
+    return FdctTile{D, img, tile - my * (int)D->tiles_x, my};
 }
 
 // Wave-local tiles (ICX_FDCT_WAVE): wave w of the workgroup owns MCUs 4w..4w+3
@@ -365,11 +375,17 @@ __device__ __forceinline__ void fdct_load(const FdctTile& T, uint32_t (&wv)[2][6
             wv[h][3] = b.y; wv[h][4] = c.x; wv[h][5] = c.y;
         } else {
             const GAS uint8_t* g = gp(row);
+            // opaque here, so the compiler does not hoist this path's eight
+            // clamped pixel offsets in front of the (wave-uniform) branch
+            int xb = x0 + sg * 8;
+#if ICX_FDCT_NOHOIST
+            asm volatile("" : "+v"(xb));
+#endif
 #pragma unroll
             for (int k = 0; k < 6; k++) wv[h][k] = 0;
 #pragma unroll
             for (int k = 0; k < 8; k++) {
-                const int sx = min(x0 + sg * 8 + k, W - 1);
+                const int sx = min(xb + k, W - 1);
 #pragma unroll
                 for (int c = 0; c < 3; c++) {
                     const int o = 3 * k + c;
@@ -701,7 +717,7 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
         }
         return c;
     };
-    const int64_t tile_id = (int64_t)my * ((D.mcux + FDC_MCU - 1) / FDC_MCU) + tx;
+    const int64_t tile_id = (int64_t)my * D.tiles_x + tx;
     const int64_t base = tile_id * (FDC_BLK * COEF_SLOTS);
     unsigned long long* ent = (unsigned long long*)states[T.img].list_entries;
     auto luma = [](int a) { return a < 4; };  // one MCU per step: Y0 Y1 Y2 Y3 Cb Cr
@@ -722,10 +738,13 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
 // tile's pixel loads are issued before the current tile is computed, so each
 // CU keeps more bytes in flight than one tile's phase B alone would.
 // Measured (300 4K frames): T = 1 6.65-6.81 ms, T = 2 6.29-6.33 ms, T = 4
-// 6.39-6.46 ms.  T = 2 takes 79 VGPRs (6 waves/SIMD); capping it to 64 or 72
-// with amdgpu_waves_per_eu spills to scratch.
+// 6.39-6.46 ms (round 1).  Round 3, after the packed column pass and the
+// multiply-high tile row: T = 3 (74 VGPRs, 6 waves/SIMD) -2.1 % against T = 2
+// (54 VGPRs, 8 waves/SIMD), T = 4 +1.1 % (profiles/r3/ab_r3ze_fdct_tiles.txt,
+// 5 interleaved rounds): three tiles' worth of pixel loads in flight per
+// workgroup hide more than the two extra waves per SIMD did.
 #ifndef ICX_FDCT_TILES
-#define ICX_FDCT_TILES 2
+#define ICX_FDCT_TILES 3
 #endif
 constexpr int FDCT_TILES = ICX_FDCT_TILES;
 
@@ -736,8 +755,9 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
                                                     const int64_t* __restrict__ prefix, int m)
 {
     // 13.5 KiB row-pass output / coefficients + 6.4 KiB shared by the
-    // downsampled chroma (phases B, C) and the list stages (phase E): 20416 B,
-    // eight workgroups per CU
+    // downsampled chroma (phases B, C) and the list stages (phase E): 20416 B
+    // (room for eight workgroups per CU; the VGPRs of three pipelined tiles
+    // allow six)
     __shared__ __attribute__((aligned(16))) int16_t ws[FDC_BLK][WSTR];
     __shared__ __attribute__((aligned(16))) union {
         uint8_t cds[2][8][FDC_PX / 2];
@@ -780,8 +800,7 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
     const int img = ids ? ids[slot] : slot;
     const ImgDesc& D = descs[img];
     const int tile = gridDim.y > 1 ? (int)blockIdx.x : (int)(blockIdx.x - prefix[slot]);
-    const int tiles_x = (D.mcux + 15) >> 4;
-    const int by = tile / tiles_x, tx = tile - by * tiles_x;
+    const int by = fdct_tile_row(D, tile), tx = tile - by * (int)D.tiles_x;
     const int W = D.w, H = D.h, x0 = tx * 128;
     const int t = threadIdx.x;
     if (t < 128) {

@@ -165,6 +165,8 @@ void geometry(ImgDesc& d, int w, int h, int fmt)
         d.hdr_len = HDR_COLOR;
     }
     d.nchunks = (int)((d.nblocks + CHUNK_BLOCKS - 1) / CHUNK_BLOCKS);
+    d.tiles_x = (uint32_t)((d.mcux + 15) / 16);
+    d.tiles_xm = d.tiles_x > 1 ? (uint32_t)(((1ull << 32) + d.tiles_x - 1) / d.tiles_x) : 0u;
 }
 
 int64_t fdct_tiles(const ImgDesc& d)
