@@ -363,7 +363,7 @@ def main():
 
     mp_step = world * args.images * W * H / 1e6
     value = mp_step * args.steps / dt
-    kstats = {k: codec.profile_query(k) for k in ("fdct", "huff", "scan", "ffscan",
+    kstats = {k: codec.profile_query(k) for k in ("fdct", "count", "huff", "scan", "ffscan",
                                                   "stuff", "resize")}
     kstats = {k: v for k, v in kstats.items() if v["launches"]}
     sb = codec.profile_query("subbatch")

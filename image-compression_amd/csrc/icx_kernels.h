@@ -11,6 +11,8 @@ hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat
                             const uint8_t hdr[2][HDR_COLOR]);
 
 // kind: 0 = BGR24, 1 = RGB24, 2 = GRAY8
+// ImgState::list_entries of a plan's images after their FDCT (byte accounting)
+void launch_list_count(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st);
 void launch_fdct(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, int64_t tiles, int kind,
                  hipStream_t st);
 void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, bool rev,

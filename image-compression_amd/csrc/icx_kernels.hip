@@ -288,10 +288,22 @@ constexpr int FDC_BLK = FDC_MCU * 6;  // 96 blocks
 constexpr int WSTR = 72;              // workspace int16 per block (row-pass writes, column reads and
                                       // the natural-order output of phase D are LDS-bank-conflict-free)
 
-__device__ __forceinline__ void st_row8(int16_t* p, const int (&v)[8])  // 8 int16, 8-B aligned
+// One row of a block (8 int16, 16-B aligned: WSTR * 2 = 144 B per block) as
+// one ds_write_b128: its 8-lane groups put the eight blocks of a phase-B row
+// on distinct banks, where two ds_write_b64 (16-lane groups) were 2-way
+// conflicted (phase B's rows r and r + 2 of one group are 8 dwords apart,
+// as are blocks 6 apart).
+#ifndef ICX_FDCT_ST128
+#define ICX_FDCT_ST128 1
+#endif
+__device__ __forceinline__ void st_row8(int16_t* p, const int (&v)[8])
 {
-    *(uint2*)p = make_uint2(pack16(v[0], v[1]), pack16(v[2], v[3]));  // one v_perm per pair
-    *(uint2*)(p + 4) = make_uint2(pack16(v[4], v[5]), pack16(v[6], v[7]));
+    if (ICX_FDCT_ST128) {
+        *(uint4*)p = make_uint4(pack16(v[0], v[1]), pack16(v[2], v[3]), pack16(v[4], v[5]), pack16(v[6], v[7]));
+    } else {
+        *(uint2*)p = make_uint2(pack16(v[0], v[1]), pack16(v[2], v[3]));  // one v_perm per pair
+        *(uint2*)(p + 4) = make_uint2(pack16(v[4], v[5]), pack16(v[6], v[7]));
+    }
 }
 
 // Phase B loads: this thread's rows 2i, 2i+1 of the tile, pixels 8sg..8sg+7
@@ -441,9 +453,8 @@ __device__ __forceinline__ int writelane(int v, int x, int a)
 #undef ICX_WRITELANE
 
 template <int NB, int STEP, bool FULL, class Fix, class Luma>
-__device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int nblk, int16_t (*oz)[WSTR],
-                                           ListStage<NB, STEP>& L, const float (&thr)[2],
-                                           unsigned long long* ent, Fix fix, Luma luma)
+__device__ __forceinline__ uint32_t emit_lists(const ImgDesc& D, int64_t base, int nblk, int16_t (*oz)[WSTR],
+                                               ListStage<NB, STEP>& L, const float (&thr)[2], Fix fix, Luma luma)
 {
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -514,8 +525,7 @@ __device__ __forceinline__ void emit_lists(const ImgDesc& D, int64_t base, int n
         total += run;
         __builtin_amdgcn_wave_barrier();
     }
-    if (lane == 0 && total)
-        atomicAdd(ent + ((blockIdx.x * 4 + wave) & (ENT_SLOTS - 1)), (unsigned long long)total);
+    return total;  // wave-uniform: the caller credits it to the image's counter
 }
 
 // After the barrier that ends emit_lists: lengths and 16-B-unit offsets.
@@ -535,7 +545,7 @@ __device__ __forceinline__ void store_list_meta(const ImgDesc& D, int64_t base, 
 
 // Phases B (arithmetic) .. E of one tile; LDS is free again on return.
 template <bool BGR>
-__device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (&wv)[2][6],
+__device__ __forceinline__ uint32_t fdct_compute(const FdctTile& T, const uint32_t (&wv)[2][6],
                                              const QNode* __restrict__ nodes, ImgState* states,
                                              uint8_t (*cds)[8][FDC_PX / 2], int16_t (*ws)[WSTR],
                                              ListStage<FDC_BLK, 6>& L)
@@ -668,7 +678,10 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
             for (int v = 0; v < 8; v++) *(uint32_t*)&oz[blk][v * 8 + c] = p[v];
         }
         {
-            const int blk = (t >> 6) * 24 + 16 + ((t & 63) >> 3), col = t & 7;
+            // even columns on lanes 0..31, odd ones on 32..63: the two lanes
+            // of one dword (columns 2c, 2c + 1) sit in different halves of
+            // the wave, so neither the reads nor the 16-bit stores conflict
+            const int blk = (t >> 6) * 24 + 16 + ((t >> 2) & 7), col = ((t & 3) << 1) | ((t >> 5) & 1);
             int32_t d[8];
 #pragma unroll
             for (int v = 0; v < 8; v++) d[v] = ws[blk][v * 8 + col];
@@ -719,12 +732,12 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
     };
     const int64_t tile_id = (int64_t)my * D.tiles_x + tx;
     const int64_t base = tile_id * (FDC_BLK * COEF_SLOTS);
-    unsigned long long* ent = (unsigned long long*)states[T.img].list_entries;
     auto luma = [](int a) { return a < 4; };  // one MCU per step: Y0 Y1 Y2 Y3 Cb Cr
+    uint32_t entries;
     if (plain)  // interior tile: no dummy blocks
-        emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, L, thr, ent, [](int, int, int c) { return c; }, luma);
+        entries = emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, L, thr, [](int, int, int c) { return c; }, luma);
     else
-        emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, L, thr, ent, fix, luma);
+        entries = emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, L, thr, fix, luma);
     fdct_phase_sync();
     store_list_meta<FDC_BLK, 6, FDCT_WAVE>(D, base, bbase, nblk, L);
     // LDS free for the next tile (wave-local: the wave's next phase B writes
@@ -732,7 +745,15 @@ __device__ __forceinline__ void fdct_compute(const FdctTile& T, const uint32_t (
 #if !ICX_FDCT_NOTAIL
     if (!FDCT_WAVE) __syncthreads();
 #endif
+    return entries;
 }
+
+// The FDCT keeps no count of the list entries it writes: the byte
+// accounting (profiling only) gets them from k_list_count.  A global atomic
+// per wave and tile (16 counters per image) cost 5.7 % of the FDCT time, one
+// per workgroup still 4.3 % (profiles/r3/ab_r3zg_fdct_lds.txt,
+// ab_r3zh_fdct_ent.txt): a wave whose last instruction is a device-scope
+// atomic holds its slot for the atomic's round trip.
 
 // FDCT_TILES consecutive tiles per workgroup, software-pipelined: the next
 // tile's pixel loads are issued before the current tile is computed, so each
@@ -830,10 +851,43 @@ __global__ __launch_bounds__(256) void k_fdct_gray(const ImgDesc* __restrict__ d
     const uint32_t bbase = (uint32_t)by * D.mcux + tx * 16;
     const float thr[2] = {(t & 63) ? nodes[D.cand_node].qf[0][t & 63].x : -1.0f, 0.0f};
     const int64_t base = (int64_t)tile * (16 * COEF_SLOTS);
-    emit_lists<16, 4, false>(D, base, nblk, oz, ls, thr, (unsigned long long*)states[img].list_entries,
-                             [](int, int, int c) { return c; }, [](int) { return true; });
+    emit_lists<16, 4, false>(D, base, nblk, oz, ls, thr, [](int, int, int c) { return c; }, [](int) { return true; });
     __syncthreads();
     store_list_meta(D, base, bbase, nblk, ls);
+}
+
+// Candidate-list entries an FDCT wrote for each image of a plan (ImgState::
+// list_entries, the byte accounting's list size): sum over the image's blocks
+// of the list length padded to whole 16-B groups, as emit_lists lays them
+// out.  One workgroup per image; lengths 16 at a time ((n + 3) & ~3 per byte
+// without carries: every length is <= 64), summed by v_dot4_u32_u8.
+__global__ __launch_bounds__(1024) void k_list_count(const ImgDesc* __restrict__ descs, ImgState* states,
+                                                     const int32_t* __restrict__ ids, int m)
+{
+    __shared__ uint32_t s_w[16];
+    const int img = ids ? ids[blockIdx.x] : (int)blockIdx.x;
+    const ImgDesc& D = descs[img];
+    const int64_t n = D.nblocks;
+    const uint8_t* nc = D.ncoef;
+    const int64_t n16 = ((uintptr_t)nc & 15) ? 0 : n >> 4;
+    uint32_t sum = 0;
+    for (int64_t i = threadIdx.x; i < n16; i += blockDim.x) {
+        const uint4 v = ld16(nc + 16 * i);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            sum = __builtin_amdgcn_udot4((w[k] + 0x03030303u) & 0xFCFCFCFCu, 0x01010101u, sum, false);
+    }
+    for (int64_t i = n16 * 16 + threadIdx.x; i < n; i += blockDim.x) sum += ((uint32_t)gp(nc)[i] + 3u) & ~3u;
+    sum = (uint32_t)wave_incl_scan((int)sum);
+    const int lane = threadIdx.x & 63;
+    if (lane == 63) s_w[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t tot = 0;
+        for (int i = 0; i < (int)(blockDim.x >> 6); i++) tot += s_w[i];
+        atomicAdd((unsigned long long*)states[img].list_entries, (unsigned long long)tot);
+    }
 }
 
 // =================================================================== Huffman
@@ -1850,6 +1904,11 @@ void launch_fdct(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, i
         ICX_LAUNCH(k_fdct_color<true>, grid, dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
     else
         ICX_LAUNCH(k_fdct_color<false>, grid, dim3(256), 0, st, d, n, s, plan_ids(p), p.prefix, p.m);
+}
+
+void launch_list_count(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st)
+{
+    ICX_LAUNCH(k_list_count, dim3(p.m), dim3(1024), 0, st, d, s, plan_ids(p), p.m);
 }
 
 void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, bool rev,

@@ -370,8 +370,14 @@ icx_status run_fdct(Batch& B, const std::vector<int>& ids)
         int64_t px = 0;
         for (int i : sel) px += (int64_t)B.desc[i].w * B.desc[i].h;
         if ((s = B.up->flush())) return s;
-        Timed tm(B.c, "fdct", px, true);
-        launch_fdct(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, kind, B.c->stream);
+        {
+            Timed tm(B.c, "fdct", px, true);
+            launch_fdct(B.d_desc, B.d_state, B.d_nodes, P.p, P.total, kind, B.c->stream);
+        }
+        if (B.c->prof) {  // list sizes for the byte accounting (the FDCT keeps no count)
+            Timed tm(B.c, "count", (int64_t)sel.size(), true);
+            launch_list_count(B.d_desc, B.d_state, P.p, B.c->stream);
+        }
     }
     return ICX_OK;
 }
