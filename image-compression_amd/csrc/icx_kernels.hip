@@ -1105,7 +1105,10 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
 //   4. gather: every 32-bit word of the chunk stream is assembled by the
 //      thread whose block holds the word's first bit (reading the following
 //      blocks' slots as needed) and stored once to scratch[cur].
-__global__ __launch_bounds__(CHUNK_BLOCKS, 8) void k_huff(const ImgDesc* __restrict__ descs,
+#ifndef ICX_HUFF_WGS
+#define ICX_HUFF_WGS 8  // workgroups per CU k_huff is compiled for (8: <= 64 VGPRs)
+#endif
+__global__ __launch_bounds__(CHUNK_BLOCKS, ICX_HUFF_WGS) void k_huff(const ImgDesc* __restrict__ descs,
                                                        const ImgState* __restrict__ states,
                                                        const QNode* __restrict__ nodes,
                                                        const int32_t* __restrict__ ids,
