@@ -492,7 +492,7 @@ __device__ __forceinline__ uint32_t selector(const DecTab* T)
 // Launch 0 records each walk's checkpoints; a re-walk compares against them
 // (staged in LDS) and stops where it meets its previous walk (dec_sync_walk).
 #ifndef ICX_DEC_AGG
-#define ICX_DEC_AGG 1  // k_dec_sync: wave-aggregated worklist / change-count atomics
+#define ICX_DEC_AGG 0  // k_dec_sync: wave-aggregated worklist / change-count atomics (+-0: few lanes change)
 #endif
 template <bool FIRST>
 __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
