@@ -1,0 +1,7 @@
+set -o pipefail
+# final tree: GPU parity tests, smoke, default bench line
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_r3zo.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_r3zo.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu_r3zo.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+timeout -k 10 400 python bench.py > gpurun_out/bench_r3zo_default.json 2> gpurun_out/bench_r3zo.err || { tail -20 gpurun_out/bench_r3zo.err; exit 1; }
+cat gpurun_out/bench_r3zo_default.json
