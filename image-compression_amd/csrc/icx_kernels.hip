@@ -1105,6 +1105,9 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
 //   4. gather: every 32-bit word of the chunk stream is assembled by the
 //      thread whose block holds the word's first bit (reading the following
 //      blocks' slots as needed) and stored once to scratch[cur].
+#ifndef ICX_HUFF_ZERO16
+#define ICX_HUFF_ZERO16 1  // zero the assembly LDS with 16-B stores (-0.9 % huff, ab_r3zp_huff_zero16.txt)
+#endif
 #ifndef ICX_HUFF_WGS
 #define ICX_HUFF_WGS 8  // workgroups per CU k_huff is compiled for (8: <= 64 VGPRs)
 #endif
@@ -1236,7 +1239,13 @@ __global__ __launch_bounds__(CHUNK_BLOCKS, ICX_HUFF_WGS) void k_huff(const ImgDe
     if (total > (uint32_t)OUT_WORDS * 32) {
         if (t < 8 * FF_COPIES) s_bin[t] = 0u;
     } else {  // the assembled stream and its bins start zeroed (tables are dead)
+#if ICX_HUFF_ZERO16
+        static_assert((OUT_WORDS + 8 + 8 * FF_COPIES) % 4 == 0, "whole 16-B groups");
+        for (uint32_t i = t; i < (OUT_WORDS + 8 + 8 * FF_COPIES) / 4; i += CHUNK_BLOCKS)
+            ((uint4*)s_tab)[i] = make_uint4(0u, 0u, 0u, 0u);
+#else
         for (uint32_t i = t; i < OUT_WORDS + 8 + 8 * FF_COPIES; i += CHUNK_BLOCKS) s_tab[i] = 0u;
+#endif
     }
     __syncthreads();
 
