@@ -16,16 +16,24 @@ const uint8_t kNat[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11
 // guess (jdapimin.c default_decompress_parms: JFIF -> YCbCr; an Adobe marker's
 // transform 0 -> RGB, else YCbCr; no marker: ids 1,2,3 -> YCbCr, 'R','G','B'
 // -> RGB, else YCbCr), then OpenJDK imageioJPEG.c's override of a YCbCr
-// guess: an Adobe transform other than 1 -> unknown (-1: left to the host
-// reader); no JFIF and no EXIF marker, ids other than 1,2,3 and every
-// component sampled alike -> RGB.  0 YCbCr, 1 RGB.
+// guess: an Adobe marker with a transform other than 1 -> unknown (-1: left to
+// the host reader), also next to a JFIF marker; no JFIF and no EXIF marker
+// (IS_EXIF: the first saved COM/APPn marker is an APP1), ids other than 1,2,3
+// and every component sampled alike -> RGB.  0 YCbCr, 1 RGB.
 int colour_space(const JpegHeader& J, bool jfif, bool exif, bool adobe, int transform)
 {
-    if (jfif) return 0;
-    if (adobe) return transform == 0 ? 1 : transform == 1 ? 0 : -1;
+    /* libjpeg's guess */
+    int ycc;
+    if (jfif) ycc = 1;
+    else if (adobe) ycc = transform != 0;
+    else ycc = !(J.id[0] == 'R' && J.id[1] == 'G' && J.id[2] == 'B');
+    if (!ycc) return 1;
+    /* imageioJPEG.c's override of a YCbCr guess: an Adobe marker whose
+     * transform is not 1 -> unknown, even next to a JFIF marker; else, with
+     * neither JFIF nor EXIF, ids 1,2,3 keep YCbCr and equal sampling -> RGB */
+    if (adobe) return transform == 1 ? 0 : -1;
+    if (jfif || exif) return 0;
     if (J.id[0] == 1 && J.id[1] == 2 && J.id[2] == 3) return 0;
-    if (J.id[0] == 'R' && J.id[1] == 'G' && J.id[2] == 'B') return 1;
-    if (exif) return 0;
     return J.hs[1] == J.hs[0] && J.hs[2] == J.hs[0] && J.vs[1] == J.vs[0] && J.vs[2] == J.vs[0];
 }
 
@@ -36,7 +44,7 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
     if (avail < 4) return ICX_E_BUFFER;
     if (p[0] != 0xFF || p[1] != 0xD8) return ICX_E_CORRUPT;
     size_t i = 2;
-    bool sof = false, unsupported = false, adobe = false, jfif = false, exif = false;
+    bool sof = false, unsupported = false, adobe = false, jfif = false, exif = false, saved_any = false;
     int transform = 0;
     for (;;) {
         // next marker: skip non-0xFF garbage, then fill bytes (jdmarker.c next_marker)
@@ -53,6 +61,12 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
         const uint8_t* s = p + i + 2;
         const size_t n = seg - 2;
         i += seg;
+        // imageioJPEG.c IS_EXIF: the first marker the reader saves (COM, APP0..15)
+        // is an APP1, whatever it holds
+        if (!saved_any && (m == 0xFE || (m >= 0xE0 && m <= 0xEF))) {
+            saved_any = true;
+            exif = m == 0xE1;
+        }
         switch (m) {
         case 0xDB: {  // DQT
             size_t o = 0;
@@ -115,9 +129,6 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
             break;
         case 0xE0:  // APP0: JFIF
             if (n >= 5 && !memcmp(s, "JFIF\0", 5)) jfif = true;
-            break;
-        case 0xE1:  // APP1: EXIF
-            if (n >= 6 && !memcmp(s, "Exif\0\0", 6)) exif = true;
             break;
         case 0xEE:  // APP14: Adobe colour transform (jdmarker.c examine_app14)
             if (n >= 12 && !memcmp(s, "Adobe", 5)) {

@@ -440,7 +440,11 @@ icx_status prog_decode(const uint8_t* p, size_t len, const JpegHeader& J, int16_
         // APPn, COM: skipped
     }
     if (!sof || !any_scan) return ICX_E_CORRUPT;
-    // jdcoefct.c smoothing_ok(): every component's DC known and AC 1..5 final -> no smoothing
+    // Deliberately more conservative than jdcoefct.c smoothing_ok(): the device
+    // path takes a file only when every component's DC is known and AC 1..5
+    // are final (then no block smoothing happens); everything else goes to the
+    // host reader, including cases smoothing_ok() would also leave unsmoothed
+    // (a component without any DC scan, a zero Q00..Q20 quantiser entry)
     for (int c = 0; c < nc; c++) {
         if (C[c].coef_bits[0] < 0) return ICX_E_UNSUPPORTED;
         for (int k = 1; k <= 5; k++)

@@ -245,6 +245,8 @@ def _image_struct(img, fmt=None):
 class Codec:
     """One libicx context (one GPU).  Thread-safe."""
 
+    supports_device_out = True  # decode_jpg_batch(device_out=True) leaves frames in this GPU's HBM
+
     def __init__(self, device: int = 0):
         self._lib = N.load()
         self._ctx = ctypes.c_void_p()
@@ -560,6 +562,8 @@ class Pool(Codec):
     single-image helpers run on the first device's context.  The shape of a
     JVM host that drives every GPU of the node from one process
     (CompressionBatch.java:64-88)."""
+
+    supports_device_out = False  # decode_jpg_batch returns host frames (the pipeline asks for those)
 
     def __init__(self, devices):
         self._lib = N.load()

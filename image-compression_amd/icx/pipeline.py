@@ -266,7 +266,10 @@ def decode_group(codec, items: List[_Item]):
     todo = [it for it in items if it.decoded.image is None]
     if not todo:
         return
-    res = codec.decode_jpg_batch([it.decoded.data for it in todo], subsampling=0, device_out=True)
+    # a codec that decodes into host memory only (icx.Pool: its images may
+    # land on any of its devices) hands back numpy frames, which its fit uploads
+    res = codec.decode_jpg_batch([it.decoded.data for it in todo], subsampling=0,
+                                 device_out=getattr(codec, "supports_device_out", True))
     for it, (st, img) in zip(todo, res):
         it.decoded.data = None
         if st == N.OK:

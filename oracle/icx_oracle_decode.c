@@ -86,16 +86,24 @@ static int build_dhuff(const uint8_t* counts, const uint8_t* vals, int nvals, dh
  * guess (jdapimin.c default_decompress_parms: JFIF -> YCbCr; an Adobe marker's
  * transform 0 -> RGB, else YCbCr; no marker: ids 1,2,3 -> YCbCr, 'R','G','B'
  * -> RGB, else YCbCr), then OpenJDK imageioJPEG.c's override of a YCbCr guess:
- * an Adobe transform other than 1 -> unknown (here: unsupported, -1); no JFIF
- * and no EXIF marker, ids other than 1,2,3 and every component sampled alike
- * -> RGB.  0 YCbCr, 1 RGB. */
+ * an Adobe marker with a transform other than 1 -> unknown (here: unsupported,
+ * -1), also next to a JFIF marker; no JFIF and no EXIF marker (IS_EXIF: the
+ * first saved COM/APPn marker is an APP1), ids other than 1,2,3 and every
+ * component sampled alike -> RGB.  0 YCbCr, 1 RGB. */
 static int colour_space(const jinfo_t* J, int jfif, int exif, int adobe, int transform)
 {
-    if (jfif) return 0;
-    if (adobe) return transform == 0 ? 1 : transform == 1 ? 0 : -1;
+    /* libjpeg's guess */
+    int ycc;
+    if (jfif) ycc = 1;
+    else if (adobe) ycc = transform != 0;
+    else ycc = !(J->id[0] == 'R' && J->id[1] == 'G' && J->id[2] == 'B');
+    if (!ycc) return 1;
+    /* imageioJPEG.c's override of a YCbCr guess: an Adobe marker whose
+     * transform is not 1 -> unknown, even next to a JFIF marker; else, with
+     * neither JFIF nor EXIF, ids 1,2,3 keep YCbCr and equal sampling -> RGB */
+    if (adobe) return transform == 1 ? 0 : -1;
+    if (jfif || exif) return 0;
     if (J->id[0] == 1 && J->id[1] == 2 && J->id[2] == 3) return 0;
-    if (J->id[0] == 'R' && J->id[1] == 'G' && J->id[2] == 'B') return 1;
-    if (exif) return 0;
     return J->hs[1] == J->hs[0] && J->hs[2] == J->hs[0] && J->vs[1] == J->vs[0] && J->vs[2] == J->vs[0];
 }
 
@@ -105,7 +113,7 @@ static int parse(const uint8_t* p, size_t len, jinfo_t* J)
     memset(J, 0, sizeof(*J));
     if (len < 4 || p[0] != 0xFF || p[1] != 0xD8) return 6;
     size_t i = 2;
-    int have_sof = 0, jfif = 0, exif = 0, adobe = 0, transform = 0;
+    int have_sof = 0, jfif = 0, exif = 0, adobe = 0, transform = 0, saved_any = 0;
     for (;;) {
         while (i < len && p[i] != 0xFF) i++; /* jdmarker next_marker: skip garbage */
         while (i < len && p[i] == 0xFF) i++; /* fill bytes */
@@ -119,6 +127,12 @@ static int parse(const uint8_t* p, size_t len, jinfo_t* J)
         const uint8_t* s = p + i + 2;
         size_t n = seg - 2;
         i += seg;
+        /* imageioJPEG.c IS_EXIF: the first marker the reader saves (COM,
+         * APP0..15) is an APP1, whatever it holds */
+        if (!saved_any && (m == 0xFE || (m >= 0xE0 && m <= 0xEF))) {
+            saved_any = 1;
+            exif = m == 0xE1;
+        }
         if (m == 0xDB) { /* DQT */
             size_t o = 0;
             while (o < n) {
@@ -173,8 +187,6 @@ static int parse(const uint8_t* p, size_t len, jinfo_t* J)
             J->ri = (s[0] << 8) | s[1];
         } else if (m == 0xE0) { /* APP0: JFIF (jdmarker.c examine_app0) */
             if (n >= 5 && !memcmp(s, "JFIF\0", 5)) jfif = 1;
-        } else if (m == 0xE1) { /* APP1 */
-            if (n >= 6 && !memcmp(s, "Exif\0\0", 6)) exif = 1;
         } else if (m == 0xEE) { /* APP14: Adobe (jdmarker.c examine_app14) */
             if (n >= 12 && !memcmp(s, "Adobe", 5)) {
                 adobe = 1;

@@ -94,6 +94,11 @@ def adobe_app14(transform):
     return b"\xff\xee" + (len(body) + 2).to_bytes(2, "big") + body
 
 
+JFIF_APP0 = b"\xff\xe0\x00\x10JFIF\x00\x01\x01\x00\x00\x01\x00\x01\x00\x00"
+XMP_APP1 = b"\xff\xe1\x00\x23http://ns.adobe.com/xap/1.0/\x00<x/>"
+COM = b"\xff\xfe\x00\x06note"
+
+
 def decode_bgr(data):
     im = Image.open(io.BytesIO(data))
     im.load()
@@ -192,7 +197,15 @@ def main():
                ("ycc_ids012_exif_66x130", rewrite(ycc, app=b"\xff\xe1\x00\x08Exif\x00\x00", ids=bytes([0, 1, 2])),
                 ycc_px, False),
                ("ycc_adobe1_rgbids_66x130", rewrite(ycc, app=adobe_app14(1), ids=b"RGB"), ycc_px, False),
-               ("unknown_adobe2_66x130", rewrite(ycc, app=adobe_app14(2), ids=None), None, True)]
+               ("unknown_adobe2_66x130", rewrite(ycc, app=adobe_app14(2), ids=None), None, True),
+               # (round 4) the override also reaches a JFIF file with an Adobe
+               # marker: transform 0 -> unknown, 1 -> YCbCr; IS_EXIF only asks
+               # whether the first saved COM/APPn marker is an APP1
+               ("unknown_jfif_adobe0_66x130", rewrite(ycc, app=JFIF_APP0 + adobe_app14(0), ids=None), None, True),
+               ("ycc_jfif_adobe1_66x130", rewrite(ycc, app=JFIF_APP0 + adobe_app14(1), ids=None), ycc_px, False),
+               ("ycc_ids012_xmp_first_66x130", rewrite(ycc, app=XMP_APP1, ids=bytes([0, 1, 2])), ycc_px, False),
+               ("rgb_ids012_com_exif_66x130", rewrite(adobe, app=COM + b"\xff\xe1\x00\x08Exif\x00\x00",
+                                                      ids=bytes([0, 1, 2])), rgb_px, False)]
     for name, data, px, refused in derived:
         jpegs[name] = np.frombuffer(data, np.uint8)
         meta["cases"][name] = {"w": 130, "h": 66, "ncomp": 3, "bytes": len(data), "colour": True,

@@ -24,7 +24,7 @@ def test_decode_matches_golden(oracle, dgolden):
         assert rc == 0, (name, rc)
         assert img.shape == pxs[name].shape and np.array_equal(img, pxs[name]), name
         n += 1
-    assert n == 108
+    assert n == 111
 
 
 @pytest.mark.parametrize("s", [2, 3, 4])
@@ -65,3 +65,24 @@ def test_coefficients_of_own_encodes(oracle):
         qt = np.array([lum if (b % 6) < 4 else chrom for b in range(raw.shape[0])])[:, zz] * 8
         quant = np.sign(raw) * ((np.abs(raw) + qt // 2) // qt)
         assert np.array_equal(co[:, zz], quant), (h, w, q)
+
+
+def test_libicx_header_colour_rules_match_oracle(oracle, dgolden):
+    """libicx's header parse (icx_jpeg_info, host code, no GPU) settles the
+    colour-space cases as the oracle does: the JDK's Adobe override also next
+    to a JFIF marker, IS_EXIF = the first saved COM/APPn marker is an APP1
+    (imageioJPEG.c); pixels of the supported ones are checked on the GPU."""
+    from icx.core import jpeg_info
+    meta, jpgs, _ = dgolden
+    n = 0
+    for name, data in jpgs.items():
+        c = meta["cases"][name]
+        if not c.get("colour"):
+            continue
+        st = jpeg_info(data)[0]
+        if c.get("progressive"):
+            assert st == 0, name  # progressive files are the device path's too
+        else:
+            assert st == (5 if c.get("unsupported") else 0), (name, st)
+        n += 1
+    assert n == 11

@@ -476,6 +476,37 @@ def test_corrupt_jpeg_fails_alone_in_its_group(tmp_path):
     assert not (tmp_path / "out" / "bad.jpg").exists()
 
 
+def test_host_output_codec_in_the_batch(tmp_path):
+    """A codec that decodes into host memory only (icx.Pool declares
+    supports_device_out = False) is asked for host frames by the pipeline,
+    never for device_out (every JPEG of a Pool's group failed)."""
+    files = []
+    for i in range(4):
+        f = tmp_path / f"h{i}.jpg"
+        write_jpeg(f, noise(60 + i, 100, 40 + i))
+        files.append(str(f))
+
+    class HostOnlyCodec(OracleCodec):
+        supports_device_out = False
+
+        def decode_jpg_batch(self, datas, subsampling=0, device_out=False):
+            if device_out:
+                raise ValueError("host output only")
+            return super().decode_jpg_batch(datas, subsampling, device_out)
+
+    lst = tmp_path / "list.txt"
+    lst.write_text("\n".join(files) + "\n")
+    P = CompressionParams(0.25, 1000, 50, 50, 20000)
+    rep = pipeline.CompressionBatch(lst, tmp_path / "out", P, 1, tmp_path / "cache", codecs=[HostOnlyCodec()],
+                                    group_size=4).execute(cache=LockedDict())
+    ref = pipeline.CompressionBatch(lst, tmp_path / "ref", P, 1, tmp_path / "cache2", codecs=[OracleCodec()],
+                                    group_size=4).execute(cache=LockedDict())
+    assert rep.success == ref.success == 4, rep.counts
+    for f in files:
+        n = os.path.basename(f)
+        assert (tmp_path / "out" / n).read_bytes() == (tmp_path / "ref" / n).read_bytes()
+
+
 def test_cache_errors_do_not_abort(tmp_path, caplog):
     """H2CacheManager.loadAllToMap / saveAllFromMap catch SQLException, log it
     and carry on (cache/H2CacheManager.java:89-92, 148-152); the JDBC path has

@@ -67,6 +67,27 @@ def test_batch_end_to_end_matches_oracle(codec, tmp_path):
             assert (tmp_path / "gpu2" / name).read_bytes() == (tmp_path / "gpu" / name).read_bytes()
 
 
+def test_batch_through_a_pool_matches_one_codec(codec, tmp_path):
+    """CompressionBatch driven by icx.Pool([0, 0]) (one process over a device
+    list, the JVM shape of CompressionBatch.java:64-88): JPEGs decode on the
+    pool's devices into host frames and fit there; the files equal one
+    codec's (every JPEG of a Pool's group used to fail)."""
+    lst, files = _make_inputs(tmp_path)
+    params = CompressionParams(0.25, 1000, 150, 150, 60000)
+    pool = icx.Pool([0, 0])
+    try:
+        got = pipeline.CompressionBatch(lst, tmp_path / "pool", params, 1, tmp_path / "pcache", codecs=[pool],
+                                        group_size=4).execute()
+    finally:
+        pool.close()
+    one = pipeline.CompressionBatch(lst, tmp_path / "one", params, 1, tmp_path / "ocache", codecs=[codec],
+                                    group_size=4).execute()
+    assert got.counts == one.counts and got.success >= 10, got.counts
+    for name in sorted(os.listdir(tmp_path / "one")):
+        if name.endswith(".jpg"):
+            assert (tmp_path / "pool" / name).read_bytes() == (tmp_path / "one" / name).read_bytes(), name
+
+
 def test_cli_main(codec, tmp_path):
     lst, files = _make_inputs(tmp_path)
     from icx.cli import main
