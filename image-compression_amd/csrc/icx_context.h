@@ -175,6 +175,7 @@ struct icx_ctx {
     std::vector<hipEvent_t> evpool;
     std::map<std::string, icx::KStat> stats;
     size_t budget = 0;  // device workspace budget per sub-batch
+    int table_layout = 0;  // ICX_TABLES_SEPARATE / ICX_TABLES_GROUPED (icx_set_table_layout)
     DevPool pool;
     DevPool hpool;  // pinned host buffers (hpool.host = true)
     // Host-buffer batches: inputs are uploaded (io_up) into one of two staging

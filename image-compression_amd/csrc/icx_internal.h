@@ -44,6 +44,14 @@ constexpr int FD_TILE_PX = 128;          // FDCT tile width in pixels (8 colour 
 constexpr int MAX_TRIALS = 8;            // findBestQualityByBinarySearch loop bound (:167)
 constexpr int HDR_COLOR = 623;           // SOI+APP0+2 DQT+SOF0+4 DHT+SOS
 constexpr int HDR_GRAY = 328;            // SOI+APP0+DQT+SOF0+2 DHT+SOS
+// ICX_TABLES_GROUPED: one DQT segment for every quantisation table, one DHT
+// for every Huffman table (3 + 12 B less for colour, 4 B less for grey)
+constexpr int HDR_COLOR_GROUPED = 607;
+constexpr int HDR_GRAY_GROUPED = 324;
+// offsets inside the header template that k_stuff patches: the chroma DQT
+// payload and the SOF0 marker (the luma DQT payload starts at 25 in both)
+constexpr int hdr_dqt1(bool grouped) { return grouped ? 90 : 94; }
+constexpr int hdr_sof(bool colour, bool grouped) { return colour ? (grouped ? 154 : 158) : 89; }
 
 // One trial quality: a node of the binary-search tree of
 // findBestQualityByBinarySearch (ImageCompressionJpg.java:158-200), or a fixed

@@ -8,7 +8,7 @@ namespace icx {
 
 hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat[64],
                             const uint32_t dc[2][16], const uint32_t ac[2][256],
-                            const uint8_t hdr[2][HDR_COLOR]);
+                            const uint8_t hdr[4][HDR_COLOR]);
 
 // kind: 0 = BGR24, 1 = RGB24, 2 = GRAY8
 // ImgState::list_entries of a plan's images after their FDCT (byte accounting)

@@ -32,7 +32,7 @@ __constant__ uint32_t c_ac[2][256];   // (code << 8) | length, by run/size symbo
 // k_huff's AC table, pre-shifted per (run, size) slot: (code << size, len + size)
 // at [run * 11 + size]; built once by upload_constants.
 __constant__ uint2 c_acx[2][16 * 11];
-__constant__ uint8_t c_hdr[2][HDR_COLOR];  // [0] grey template, [1] colour template
+__constant__ uint8_t c_hdr[4][HDR_COLOR];  // [grouped * 2 + colour]: grey / colour templates, per table layout
 
 // ------------------------------------------------------------------ helpers
 // Pointers read from descriptors are generic; casting them to the global
@@ -1573,12 +1573,13 @@ __global__ __launch_bounds__(256) void k_stuff(const ImgDesc* __restrict__ descs
 
     if (c == 0) {  // marker segments: template + DQT payload + SOF dimensions
         const QNode& N = nodes[S.best_node];
-        const uint8_t* tpl = c_hdr[D.ncomp == 3 ? 1 : 0];
+        const bool colour = D.ncomp == 3, grouped = hdr == HDR_COLOR_GROUPED || hdr == HDR_GRAY_GROUPED;
+        const uint8_t* tpl = c_hdr[2 * grouped + colour];
+        const int q1 = hdr_dqt1(grouped), sof = hdr_sof(colour, grouped);
         for (int i = lane; i < hdr; i += 64) {
             uint8_t v = tpl[i];
             if (i >= 25 && i < 89) v = (uint8_t)N.qt[0][c_zz_to_nat[i - 25]];
-            else if (D.ncomp == 3 && i >= 94 && i < 158) v = (uint8_t)N.qt[1][c_zz_to_nat[i - 94]];
-            const int sof = D.ncomp == 3 ? 158 : 89;
+            else if (colour && i >= q1 && i < q1 + 64) v = (uint8_t)N.qt[1][c_zz_to_nat[i - q1]];
             if (i == sof + 5) v = (uint8_t)(D.h >> 8);
             if (i == sof + 6) v = (uint8_t)D.h;
             if (i == sof + 7) v = (uint8_t)(D.w >> 8);
@@ -1864,7 +1865,7 @@ __global__ __launch_bounds__(256) void k_resize(ResizeArgs one, const ResizeArgs
 // =================================================================== host side
 hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat[64],
                             const uint32_t dc[2][16], const uint32_t ac[2][256],
-                            const uint8_t hdr[2][HDR_COLOR])
+                            const uint8_t hdr[4][HDR_COLOR])
 {
     hipError_t e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_nat_to_zz), nat_to_zz, 64))) return e;
@@ -1879,7 +1880,7 @@ hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat
                 acx[c][run * 11 + sz] = make_uint2((h >> 8) << sz, (h & 255) + sz);
             }
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_acx), acx, sizeof(acx)))) return e;
-    return hipMemcpyToSymbol(HIP_SYMBOL(c_hdr), hdr, 2 * HDR_COLOR);
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_hdr), hdr, 4 * HDR_COLOR);
 }
 
 thread_local LaunchTiming g_launch_timing;

@@ -145,7 +145,7 @@ int build_tree(float lo, float hi, int iter, std::vector<QNode>& nodes, int& dep
 // bytes per pixel of a raster (GRAY16: one 2-byte sample)
 int channels(int fmt) { return fmt == ICX_GRAY8 ? 1 : fmt == ICX_GRAY16 ? 2 : fmt <= ICX_RGB24 ? 3 : 4; }
 
-void geometry(ImgDesc& d, int w, int h, int fmt)
+void geometry(ImgDesc& d, int w, int h, int fmt, int layout = ICX_TABLES_SEPARATE)
 {
     d.w = w;
     d.h = h;
@@ -157,12 +157,12 @@ void geometry(ImgDesc& d, int w, int h, int fmt)
         d.mcux = d.ywb;
         d.mcuy = d.yhb;
         d.nblocks = (int64_t)d.mcux * d.mcuy;
-        d.hdr_len = HDR_GRAY;
+        d.hdr_len = layout == ICX_TABLES_GROUPED ? HDR_GRAY_GROUPED : HDR_GRAY;
     } else {
         d.mcux = (w + 15) / 16;
         d.mcuy = (h + 15) / 16;
         d.nblocks = (int64_t)d.mcux * d.mcuy * 6;
-        d.hdr_len = HDR_COLOR;
+        d.hdr_len = layout == ICX_TABLES_GROUPED ? HDR_COLOR_GROUPED : HDR_COLOR;
     }
     d.nchunks = (int)((d.nblocks + CHUNK_BLOCKS - 1) / CHUNK_BLOCKS);
     d.tiles_x = (uint32_t)((d.mcux + 15) / 16);
@@ -326,11 +326,11 @@ void stage_pixels(Batch& B, int i, double scale)
             launch_resize(I.dpx, I.orig.w, I.orig.h, I.orig.stride, I.orig.fmt, I.dresize, dw, dh, dw * I.nch,
                           c->stream);
         }
-        geometry(d, dw, dh, I.orig.fmt);
+        geometry(d, dw, dh, I.orig.fmt, c->table_layout);
         d.px = I.dresize;
         d.stride = dw * I.nch;
     } else {
-        geometry(d, I.orig.w, I.orig.h, I.orig.fmt);
+        geometry(d, I.orig.w, I.orig.h, I.orig.fmt, c->table_layout);
         d.px = I.dpx;
         d.stride = I.orig.stride;
     }
@@ -673,7 +673,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             I.root = I.cached_node = -1;
             I.depth = 0;
             ImgDesc& d = B.desc[k];
-            geometry(d, j.img.width, j.img.height, j.img.fmt);
+            geometry(d, j.img.width, j.img.height, j.img.fmt, c->table_layout);
             d.stride = j.img.stride;
             d.target = j.target_max_size;
             d.coefs = (int32_t*)c->dev.take(coef_bytes(d));
@@ -1005,25 +1005,39 @@ icx_status icx_create(int device, icx_ctx** out)
         derive(kDcChrBits, kDcVals, dc[1]);
         derive(kAcLumBits, kAcLumVals, ac[0]);
         derive(kAcChrBits, kAcChrVals, ac[1]);
-        uint8_t hdr[2][HDR_COLOR] = {};
-        for (int g = 0; g < 2; g++) {
-            const int nc = g ? 3 : 1;
+        uint8_t hdr[4][HDR_COLOR] = {};
+        for (int g = 0; g < 4; g++) {
+            const int nc = (g & 1) ? 3 : 1;
+            const bool grouped = g >= 2;  // ICX_TABLES_GROUPED: one DQT and one DHT segment
             std::vector<uint8_t> h;
             auto put = [&](std::initializer_list<int> v) { for (int x : v) h.push_back((uint8_t)x); };
             put({0xFF, 0xD8});
             // APP0 as the JDK's JFIFMarkerSegment writes it: JFIF 1.02, aspect-ratio units, 1x1
             put({0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0x00, 0x01, 0x02, 0x00, 0x00, 0x01, 0x00, 0x01, 0x00, 0x00});
-            for (int t = 0; t < (nc == 3 ? 2 : 1); t++) {
-                put({0xFF, 0xDB, 0x00, 0x43, t});
+            const int nt = nc == 3 ? 2 : 1;
+            for (int t = 0; t < nt; t++) {
+                if (t == 0 || !grouped) put({0xFF, 0xDB, 0x00, 2 + (grouped ? nt : 1) * 65});
+                put({t});
                 for (int i = 0; i < 64; i++) h.push_back(0);  // DQT payload patched on device
             }
             put({0xFF, 0xC0, 0x00, 8 + 3 * nc, 8, 0, 0, 0, 0, nc});
             if (nc == 1) put({1, 0x11, 0});
             else put({1, 0x22, 0, 2, 0x11, 1, 3, 0x11, 1});
-            auto dht = [&](int idx, const uint8_t* bits, const uint8_t* vals) {
+            auto count = [](const uint8_t* bits) {
                 int cnt = 0;
                 for (int i = 0; i < 16; i++) cnt += bits[i];
-                put({0xFF, 0xC4, (19 + cnt) >> 8, (19 + cnt) & 255, idx});
+                return cnt;
+            };
+            // grouped: one segment whose length covers every table of the header
+            int all = 2 * 17 + count(kDcLumBits) + count(kAcLumBits);
+            if (nc == 3) all += 2 * 17 + count(kDcChrBits) + count(kAcChrBits);
+            bool first = true;
+            auto dht = [&](int idx, const uint8_t* bits, const uint8_t* vals) {
+                const int cnt = count(bits);
+                if (!grouped) put({0xFF, 0xC4, (19 + cnt) >> 8, (19 + cnt) & 255});
+                else if (first) put({0xFF, 0xC4, (2 + all) >> 8, (2 + all) & 255});
+                first = false;
+                put({idx});
                 for (int i = 0; i < 16; i++) h.push_back(bits[i]);
                 for (int i = 0; i < cnt; i++) h.push_back(vals[i]);
             };
@@ -1035,6 +1049,8 @@ icx_status icx_create(int device, icx_ctx** out)
             }
             if (nc == 1) put({0xFF, 0xDA, 0x00, 0x08, 1, 1, 0x00, 0, 63, 0});
             else put({0xFF, 0xDA, 0x00, 0x0C, 3, 1, 0x00, 2, 0x11, 3, 0x11, 0, 63, 0});
+            if ((int)h.size() != (nc == 3 ? (grouped ? HDR_COLOR_GROUPED : HDR_COLOR)
+                                          : (grouped ? HDR_GRAY_GROUPED : HDR_GRAY))) abort();
             memcpy(hdr[g], h.data(), h.size());
         }
         up = upload_constants(nat2zz, zz2nat, dc, ac, hdr);
@@ -1123,6 +1139,21 @@ void icx_scaled_dims(int32_t width, int32_t height, double scale, int32_t* out_w
 }
 
 int32_t icx_jpeg_header_size(int32_t fmt) { return fmt == ICX_GRAY8 ? HDR_GRAY : HDR_COLOR; }
+
+int32_t icx_jpeg_header_size_layout(int32_t fmt, int32_t layout)
+{
+    const bool grouped = layout == ICX_TABLES_GROUPED;
+    return fmt == ICX_GRAY8 ? (grouped ? HDR_GRAY_GROUPED : HDR_GRAY) : (grouped ? HDR_COLOR_GROUPED : HDR_COLOR);
+}
+
+icx_status icx_set_table_layout(icx_ctx* ctx, int32_t layout)
+{
+    if (!ctx) return ICX_E_NULL;
+    if (layout != ICX_TABLES_SEPARATE && layout != ICX_TABLES_GROUPED) return fail(ctx, ICX_E_INVALID, "table layout");
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    ctx->table_layout = layout;
+    return ICX_OK;
+}
 
 int64_t icx_num_blocks(int32_t width, int32_t height, int32_t fmt)
 {

@@ -17,11 +17,13 @@ OK, E_INVALID, E_NOMEM, E_DEVICE, E_BUFFER, E_UNSUPPORTED, E_CORRUPT, E_NULL = r
 BGR24, RGB24, GRAY8, XRGB32, ARGB32, ABGR32, RGBA32, GRAY16 = range(8)
 CHANNELS = {BGR24: 3, RGB24: 3, GRAY8: 1, XRGB32: 4, ARGB32: 4, ABGR32: 4, RGBA32: 4, GRAY16: 1}
 BYTES_PER_PX = {**CHANNELS, GRAY16: 2}
+# icx_set_table_layout: one DQT/DHT segment per table (623 B header) / all in one (607 B)
+TABLES_SEPARATE, TABLES_GROUPED = 0, 1
 
 EXPORTS = [
     "icx_abi_version", "icx_create", "icx_destroy", "icx_status_string", "icx_last_error",
     "icx_quality_tables", "icx_create_key", "icx_subsampling_factor", "icx_scaled_dims",
-    "icx_jpeg_header_size", "icx_compress_jpg_to_stream", "icx_find_best_quality",
+    "icx_jpeg_header_size", "icx_jpeg_header_size_layout", "icx_set_table_layout", "icx_compress_jpg_to_stream", "icx_find_best_quality",
     "icx_compress_jpg_with_target_size", "icx_compress_jpg_batch", "icx_resize_image",
     "icx_resize_bilinear", "icx_png_fit", "icx_num_blocks", "icx_debug_fdct",
     "icx_profile_enable", "icx_profile_reset", "icx_profile_query",
@@ -109,6 +111,8 @@ def load():
         "icx_subsampling_factor": (c.c_int32, [c.c_int32, c.c_int32]),
         "icx_scaled_dims": (None, [c.c_int32, c.c_int32, c.c_double, P(c.c_int32), P(c.c_int32)]),
         "icx_jpeg_header_size": (c.c_int32, [c.c_int32]),
+        "icx_jpeg_header_size_layout": (c.c_int32, [c.c_int32, c.c_int32]),
+        "icx_set_table_layout": (c.c_int, [c.c_void_p, c.c_int32]),
         "icx_compress_jpg_to_stream": (c.c_int, [c.c_void_p, P(Image), c.c_float, c.c_void_p, c.c_size_t,
                                                  P(c.c_size_t)]),
         "icx_find_best_quality": (c.c_int, [c.c_void_p, P(Image), c.c_int64, c.c_float, P(c.c_float),
@@ -150,7 +154,7 @@ def load():
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
-    if lib.icx_abi_version() != 3:
+    if lib.icx_abi_version() != 4:
         raise NativeLibraryError("libicx ABI version mismatch")
     _lib = lib
     return lib

@@ -541,6 +541,11 @@ class Codec:
     def profile(self, on=True):
         self._check(self._lib.icx_profile_enable(self._ctx, 1 if on else 0), "icx_profile_enable")
 
+    def set_table_layout(self, layout: int):
+        """JPEG table marker layout of later encodes (icx_set_table_layout):
+        N.TABLES_SEPARATE (default, 623-B header) or N.TABLES_GROUPED (607 B)."""
+        self._check(self._lib.icx_set_table_layout(self._ctx, int(layout)), "icx_set_table_layout")
+
     def profile_reset(self):
         self._check(self._lib.icx_profile_reset(self._ctx), "icx_profile_reset")
 
@@ -586,6 +591,11 @@ class Pool(Codec):
 
     def _batch_call(self, what, jobs, n):
         return getattr(self._lib, f"icx_pool_{what}_batch")(self._pool, jobs, n)
+
+    def set_table_layout(self, layout: int):
+        for i in range(self._lib.icx_pool_size(self._pool)):
+            st = self._lib.icx_set_table_layout(self._lib.icx_pool_context(self._pool, i), int(layout))
+            self._check(st, "icx_set_table_layout")
 
     def decode_jpg_batch(self, datas, subsampling: int = 0, device_out: bool = False):
         if device_out:

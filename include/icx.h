@@ -33,7 +33,8 @@
 extern "C" {
 #endif
 
-#define ICX_ABI_VERSION 3  /* 2: four-byte pixel formats, icx_png_encode; 3: ICX_GRAY16, icx_png_fit_batch */
+#define ICX_ABI_VERSION 4  /* 2: four-byte pixel formats, icx_png_encode; 3: ICX_GRAY16, icx_png_fit_batch;
+                              4: icx_set_table_layout */
 
 typedef struct icx_ctx icx_ctx;
 
@@ -144,6 +145,19 @@ void icx_scaled_dims(int32_t width, int32_t height, double scale, int32_t* out_w
  * (headers + EOI).  Header layout: SOI, JFIF APP0, DQT per table, SOF0, DHT per
  * table, SOS (623 B for 3 components, 328 B for grey). */
 int32_t icx_jpeg_header_size(int32_t fmt);
+
+/* Marker layout of the writer's tables (A5; SURVEY.md §7 hard part 2: the
+ * JDK's grouping cannot be checked without a JVM, so both are available).
+ * ICX_TABLES_SEPARATE (default): one DQT segment per quantisation table and
+ * one DHT segment per Huffman table, as libjpeg 6b's jcmarker.c writes the
+ * tables the JDK hands it (623 / 328 B).  ICX_TABLES_GROUPED: every
+ * quantisation table in one DQT segment and every Huffman table in one DHT
+ * segment (607 / 324 B).  The entropy-coded data is the same; the size every
+ * search decision compares against -t (ImageCompressionJpg.java:176) is not. */
+enum { ICX_TABLES_SEPARATE = 0, ICX_TABLES_GROUPED = 1 };
+int32_t icx_jpeg_header_size_layout(int32_t fmt, int32_t layout);
+/* Layout of every later encode on this context (ICX_E_INVALID for others). */
+icx_status icx_set_table_layout(icx_ctx* ctx, int32_t layout);
 
 /* ------------------------------------------------------------- hot path */
 /* A4  ImageCompressionJpg.compressJpgToStream (ImageCompressionJpg.java:136-147):

@@ -513,36 +513,56 @@ static void put16(bw_t* w, int v)
     put_byte(w, (uint8_t)v);
 }
 
-static void emit_dht(bw_t* w, int index, const uint8_t* bits, const uint8_t* vals)
+static void emit_dqt_table(bw_t* w, int index, const uint16_t* tbl)
+{
+    put_byte(w, (uint8_t)index);
+    for (int k = 0; k < 64; k++) put_byte(w, (uint8_t)tbl[ZZ[k]]);
+}
+
+static void emit_dht_table(bw_t* w, int index, const uint8_t* bits, const uint8_t* vals)
 {
     int n = 0;
     for (int i = 0; i < 16; i++) n += bits[i];
-    put_byte(w, 0xFF); put_byte(w, 0xC4);
-    put16(w, 2 + 1 + 16 + n);
     put_byte(w, (uint8_t)index);
     for (int i = 0; i < 16; i++) put_byte(w, bits[i]);
     for (int i = 0; i < n; i++) put_byte(w, vals[i]);
 }
 
-static void emit_dqt(bw_t* w, int index, const uint16_t* tbl)
+static int dht_len(const uint8_t* bits)
 {
-    put_byte(w, 0xFF); put_byte(w, 0xDB);
-    put16(w, 2 + 1 + 64);
-    put_byte(w, (uint8_t)index);
-    for (int k = 0; k < 64; k++) put_byte(w, (uint8_t)tbl[ZZ[k]]);
+    int n = 0;
+    for (int i = 0; i < 16; i++) n += bits[i];
+    return 17 + n;
 }
 
+/* Marker layout of the tables (SURVEY.md §7 hard part 2): 0 = one DQT and
+ * one DHT segment per table, as libjpeg 6b's jcmarker.c writes them when the
+ * JDK hands it the tables (623 B colour / 328 B grey header); 1 = every
+ * quantisation table in one DQT segment and every Huffman table in one DHT
+ * segment, the grouping of a JDK DQT/DHT metadata marker segment holding
+ * several tables (607 B / 324 B).  Same entropy-coded data either way.
+ * Process-wide; set before encoding (test infrastructure). */
+static int g_table_layout = 0;
+
+void oracle_set_table_layout(int grouped) { g_table_layout = grouped ? 1 : 0; }
+
 /* Marker layout: SOI; APP0 JFIF written by the JDK's Java metadata writer
- * (JFIFMarkerSegment: version 1.02, aspect-ratio units, density 1x1); DQT per
- * table, SOF0, DHT per table, SOS written by libjpeg (jcmarker.c). */
+ * (JFIFMarkerSegment: version 1.02, aspect-ratio units, density 1x1); DQT,
+ * SOF0, DHT, SOS written by libjpeg (jcmarker.c), tables per g_table_layout. */
 static void write_header(bw_t* w, const geom_t* g, const uint16_t* lum, const uint16_t* chrom)
 {
     static const uint8_t app0[18] = {0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0x00,
                                      0x01, 0x02, 0x00, 0x00, 0x01, 0x00, 0x01, 0x00, 0x00};
+    const int nt = g->ncomp == 3 ? 2 : 1; /* tables of each kind */
     put_byte(w, 0xFF); put_byte(w, 0xD8);
     for (int i = 0; i < 18; i++) put_byte(w, app0[i]);
-    emit_dqt(w, 0, lum);
-    if (g->ncomp == 3) emit_dqt(w, 1, chrom);
+    for (int t = 0; t < nt; t++) {
+        if (t == 0 || !g_table_layout) {
+            put_byte(w, 0xFF); put_byte(w, 0xDB);
+            put16(w, 2 + (g_table_layout ? nt : 1) * 65);
+        }
+        emit_dqt_table(w, t, t ? chrom : lum);
+    }
     put_byte(w, 0xFF); put_byte(w, 0xC0);
     put16(w, 8 + 3 * g->ncomp);
     put_byte(w, 8);
@@ -556,11 +576,17 @@ static void write_header(bw_t* w, const geom_t* g, const uint16_t* lum, const ui
         put_byte(w, 2); put_byte(w, 0x11); put_byte(w, 1);
         put_byte(w, 3); put_byte(w, 0x11); put_byte(w, 1);
     }
-    emit_dht(w, 0x00, DC_L_BITS, DC_VALS);
-    emit_dht(w, 0x10, AC_L_BITS, AC_L_VALS);
-    if (g->ncomp == 3) {
-        emit_dht(w, 0x01, DC_C_BITS, DC_VALS);
-        emit_dht(w, 0x11, AC_C_BITS, AC_C_VALS);
+    const uint8_t* bits[4] = {DC_L_BITS, AC_L_BITS, DC_C_BITS, AC_C_BITS};
+    const uint8_t* vals[4] = {DC_VALS, AC_L_VALS, DC_VALS, AC_C_VALS};
+    const int idx[4] = {0x00, 0x10, 0x01, 0x11};
+    int total = 0;
+    for (int t = 0; t < 2 * nt; t++) total += dht_len(bits[t]);
+    for (int t = 0; t < 2 * nt; t++) {
+        if (t == 0 || !g_table_layout) {
+            put_byte(w, 0xFF); put_byte(w, 0xC4);
+            put16(w, 2 + (g_table_layout ? total : dht_len(bits[t])));
+        }
+        emit_dht_table(w, idx[t], bits[t], vals[t]);
     }
     put_byte(w, 0xFF); put_byte(w, 0xDA);
     put16(w, 6 + 2 * g->ncomp);

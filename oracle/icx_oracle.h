@@ -53,6 +53,12 @@ long oracle_fdct(const uint8_t* px, int w, int h, int stride, int fmt, int16_t* 
 int oracle_encode(const uint8_t* px, int w, int h, int stride, int fmt, float q,
                   uint8_t* out, size_t cap, size_t* len);
 
+/* Table marker layout (A5/A10, SURVEY.md §7 hard part 2): 0 = one DQT / DHT
+ * segment per table (libjpeg 6b jcmarker.c: 623 B colour / 328 B grey
+ * header, the default), 1 = all tables of a kind in one segment (607 / 324 B).
+ * Process-wide. */
+void oracle_set_table_layout(int grouped);
+
 /* A3: binary search.  Trial qualities/sizes are reported (up to 8). */
 float oracle_find_best_quality(const uint8_t* px, int w, int h, int stride, int fmt,
                                int64_t target, float q0,

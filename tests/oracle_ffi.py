@@ -58,7 +58,13 @@ class Oracle:
         L.oracle_jpeg_coefs.argtypes = [c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t]
         L.oracle_jpeg_decode.argtypes = [c.c_void_p, c.c_size_t, c.c_int, c.c_void_p, c.c_size_t, P(c.c_int),
                                          P(c.c_int), P(c.c_int)]
+        L.oracle_set_table_layout.argtypes = [c.c_int]
         self.L = L
+
+    def set_table_layout(self, grouped):
+        """Process-wide table marker layout (0: one DQT/DHT per table, the
+        default; 1: grouped).  Tests that change it restore 0."""
+        self.L.oracle_set_table_layout(1 if grouped else 0)
 
     def encode(self, img, q):
         img = np.ascontiguousarray(img)

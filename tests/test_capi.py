@@ -30,9 +30,12 @@ def test_library_exports_all_header_symbols():
 
 def test_abi_version_and_status_strings():
     lib = N.load()
-    assert lib.icx_abi_version() == 3
+    assert lib.icx_abi_version() == 4
     assert lib.icx_status_string(N.E_BUFFER) == b"output buffer too small"
     assert lib.icx_jpeg_header_size(N.BGR24) == 623 and lib.icx_jpeg_header_size(N.GRAY8) == 328
+    assert lib.icx_jpeg_header_size_layout(N.BGR24, N.TABLES_GROUPED) == 607
+    assert lib.icx_jpeg_header_size_layout(N.GRAY8, N.TABLES_GROUPED) == 324
+    assert lib.icx_jpeg_header_size_layout(N.BGR24, N.TABLES_SEPARATE) == 623
 
 
 def test_quality_tables_match_oracle(oracle):

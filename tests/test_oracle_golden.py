@@ -106,3 +106,55 @@ def test_fit_scale_loop(oracle, golden):
     assert r["success"] and r["scale"] < 1.0 and len(r["data"]) <= target
     r2 = oracle.fit(img, target, 0.25, cached=(r["quality"], r["scale"]))
     assert r2["cache_hit"] and r2["data"] == r["data"] and r2["encodes"] == 1
+
+
+def _segments(d):
+    out, i = [], 2
+    while True:
+        m, ln = d[i + 1], d[i + 2] * 256 + d[i + 3]
+        out.append((m, d[i:i + 2 + ln]))
+        i += 2 + ln
+        if m == 0xDA:
+            return out, i
+
+
+def test_grouped_table_layout_differs_only_in_the_markers(oracle, golden):
+    """SURVEY.md §7 hard part 2: the JDK's grouping of DQT/DHT cannot be
+    checked without a JVM, so the layout is switchable.  Over every golden
+    encode the grouped file (one DQT, one DHT segment) is exactly 16 B (colour)
+    / 4 B (grey) shorter, carries the same tables, SOF0, SOS and entropy-coded
+    bytes, and decodes to the same pixels (oracle decode, libjpeg-turbo via
+    Pillow, and libicx's header parse accepts it)."""
+    import io
+
+    from PIL import Image
+
+    from icx.core import jpeg_info
+    meta, inputs, _ = golden
+    n = 0
+    try:
+        for name, img in inputs.items():
+            for q in meta["images"][name]["encodes"]:
+                oracle.set_table_layout(False)
+                a = oracle.encode(img, float(q))
+                oracle.set_table_layout(True)
+                b = oracle.encode(img, float(q))
+                colour = img.ndim == 3
+                assert len(a) - len(b) == (16 if colour else 4), (name, q)
+                sa, ea = _segments(a)
+                sb, eb = _segments(b)
+                assert a[ea:] == b[eb:], (name, q)  # entropy-coded data + EOI
+                assert [m for m, _ in sb] == [0xE0, 0xDB, 0xC0, 0xC4, 0xDA]
+                body = lambda segs, m: b"".join(s[4:] for k, s in segs if k == m)  # noqa: E731
+                for m in (0xE0, 0xDB, 0xC0, 0xC4, 0xDA):
+                    assert body(sa, m) == body(sb, m), (name, q, hex(m))
+                if n % 7 == 0:  # decodes: a sample of the 121 keeps the CPU suite fast
+                    ra, pa = oracle.jpeg_decode(a)
+                    rb, pb = oracle.jpeg_decode(b)
+                    assert ra == rb == 0 and np.array_equal(pa, pb)
+                    assert np.array_equal(np.asarray(Image.open(io.BytesIO(a))), np.asarray(Image.open(io.BytesIO(b))))
+                    assert jpeg_info(b)[0] == 0
+                n += 1
+    finally:
+        oracle.set_table_layout(False)
+    assert n == 121

@@ -121,6 +121,38 @@ def test_batch_mixed_sizes_matches_oracle(codec, oracle):
                 assert r["data"] == o["data"] and r["learned"].scale == o["scale"]
 
 
+def test_grouped_table_layout_matches_oracle(codec, oracle):
+    """ICX_TABLES_GROUPED (one DQT, one DHT segment: 607 / 324-B headers) on
+    the device equals the oracle's grouped layout byte for byte, through the
+    search, the scale loop and the cached path, with sizes compared whole-file
+    against -t (ImageCompressionJpg.java:176) - colour and grey."""
+    rng = np.random.default_rng(41)
+    imgs = []
+    for i in range(8):
+        h, w = int(rng.integers(8, 300)), int(rng.integers(8, 300))
+        im = smooth(h, w, 500 + i) if i % 2 else noise(h, w, 500 + i)
+        imgs.append(im[:, :, 1].copy() if i % 3 == 0 else im)
+    imgs.append(noise(2160, 3840, 23))
+    try:
+        codec.set_table_layout(N.TABLES_GROUPED)
+        oracle.set_table_layout(True)
+        for target, cached in ((4000, None), (30000, [icx.LearnedParams(0.25, 1.0)] * len(imgs)),
+                               (1 << 20, None)):
+            res = codec.fit(imgs, target, 0.25, cached=cached)
+            for k, (img, r) in enumerate(zip(imgs, res)):
+                o = oracle.fit(img, target, 0.25, cached=(0.25, 1.0) if cached else None)
+                assert r["success"] == o["success"], (k, target)
+                if o["success"]:
+                    assert r["data"] == o["data"], (k, target)
+                    hdr = 607 if img.ndim == 3 else 324
+                    assert r["data"][hdr - 14:hdr - 12] == b"\xff\xda" or r["data"][hdr - 10:hdr - 8] == b"\xff\xda"
+    finally:
+        codec.set_table_layout(N.TABLES_SEPARATE)
+        oracle.set_table_layout(False)
+    d = codec.compress_jpg_to_stream(imgs[1], 0.5)
+    assert len(d) == len(oracle.encode(imgs[1], 0.5))  # back to the default layout
+
+
 def test_4k_fixed_quality_cache_path(codec, oracle):
     """BASELINE config 2 semantics: cache hit (0.25, 1.0), -t 1 MiB."""
     imgs = [smooth(2160, 3840, 21), noise(2160, 3840, 22)]
