@@ -149,7 +149,24 @@ def cpu_baseline(frames, n_sample, threads, cores_how="", distinct=320):
                       f"{enc} full encodes, {dt:.2f} s wall"}, sizes
 
 
-def e2e_leg(codec, dev, frames, n_frames, steps, cpu_sample=0, threads=16, small=200):
+def ranks_max(dist, dt):
+    """Max of a per-rank time over the host (gloo) group; dt itself at N = 1."""
+    if not dist:
+        return dt
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
+def rank_sync(dist):
+    """Device drained, then every rank at the same point (bracket of a timed region)."""
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+
+
+def e2e_leg(codec, dev, frames, n_frames, steps, cpu_sample=0, threads=16, small=200, dist=None, world=1):
     """Secondary measurement: the whole per-image hot loop of processImage on
     the device — q95 4:2:0 4K JPEG files resident in HBM -> decode (A11,
     decodeImageWithSubsampling) -> compressJpgWithTargetSize at -t 1 MiB with
@@ -162,9 +179,9 @@ def e2e_leg(codec, dev, frames, n_frames, steps, cpu_sample=0, threads=16, small
     sources is reported beside it (`at_small_batch`): the decoder's
     relaxation tail (the last few re-walk launches, single waves) is a fixed
     latency per call, so a smaller call runs at a lower rate."""
-    line = _e2e_run(codec, dev, frames, n_frames, steps)
+    line = _e2e_run(codec, dev, frames, n_frames, steps, dist, world)
     if small and small < n_frames:
-        line["at_small_batch"] = {k: v for k, v in _e2e_run(codec, dev, frames, small, steps).items()
+        line["at_small_batch"] = {k: v for k, v in _e2e_run(codec, dev, frames, small, steps, dist, world).items()
                                   if k in ("value", "frames", "ms_per_step", "decode_ms_per_step",
                                            "encode_ms_per_step", "decode_mp_s")}
     if cpu_sample:
@@ -185,7 +202,7 @@ def _e2e_sources(codec, dev, frames, n_frames):
     return srcs, lens
 
 
-def _e2e_run(codec, dev, frames, n_frames, steps):
+def _e2e_run(codec, dev, frames, n_frames, steps, dist=None, world=1):
     srcs, lens = _e2e_sources(codec, dev, frames, n_frames)
     px = [torch.empty((H, W, 3), dtype=torch.uint8, device=dev) for _ in range(n_frames)]
     outs = torch.empty((n_frames, TARGET + 1), dtype=torch.uint8, device=dev)
@@ -195,8 +212,9 @@ def _e2e_run(codec, dev, frames, n_frames, steps):
     assert all(s == 0 for s in dec.run())
     fit.run()
     assert all(r["success"] and r["status"] == 0 for r in fit.results())
-    torch.cuda.synchronize()
+    rank_sync(dist)
     td = tf = 0.0
+    t_all = time.perf_counter()
     for _ in range(steps):
         t0 = time.perf_counter()
         dec.run()
@@ -206,11 +224,15 @@ def _e2e_run(codec, dev, frames, n_frames, steps):
         torch.cuda.synchronize()
         td += t1 - t0
         tf += time.perf_counter() - t1
+    rank_sync(dist)
+    # whole job: every rank's frames over the slowest rank's time (the
+    # decode / encode split below is this rank's own)
+    t_all = ranks_max(dist, time.perf_counter() - t_all)
     mp = n_frames * W * H / 1e6
     line = {"metric": "megapixels/sec 4K q95 JPEG bytes in HBM -> device decode -> target-size encode (-t 1MiB, "
                       "q=0.25 cached)",
-            "value": round(mp * steps / (td + tf), 1), "unit": "MP/s", "frames": n_frames, "steps": steps,
-            "distinct_sources": n_frames,
+            "value": round(world * mp * steps / t_all, 1), "unit": "MP/s", "frames": n_frames, "steps": steps,
+            "distinct_sources": n_frames, "n_gpus": world, "frames_per_gpu": n_frames,
             "ms_per_step": round((td + tf) / steps * 1e3, 3), "decode_ms_per_step": round(td / steps * 1e3, 3),
             "encode_ms_per_step": round(tf / steps * 1e3, 3),
             "decode_mp_s": round(mp * steps / td, 1),
@@ -234,33 +256,70 @@ def link_rates(dev, nbytes=1 << 30, reps=5):
     return rates
 
 
-def host_io_leg(codec, frames, n, steps, warmup, cached):
-    """SURVEY §8(d)'s headline definition, PCIe included: decoded BGR frames
-    in pinned host memory -> final JPEG bytes in pinned host memory.  The
-    library uploads sub-batch s+1 and downloads s-1 on their own streams while
-    s computes (icx_runtime.cpp run_batch, prefetch)."""
-    dev = frames[0].device
-    link = link_rates(dev)
-    hf = [f.cpu().pin_memory() for f in frames[:n]]
-    outs = torch.empty((n, TARGET + 1), dtype=torch.uint8).pin_memory()
-    b = codec.prepare(hf, TARGET, Q0, cached=cached[:n] if cached else None, outputs=[outs[i] for i in range(n)])
+def host_frames(frames, n):
+    """The first n frames copied to pinned host memory (the host-fed legs)."""
+    return [f.cpu().pin_memory() for f in frames[:n]]
+
+
+def _timed_host_batch(b, steps, warmup, dist):
+    """Warm-up, then `steps` runs of a prepared host-buffer batch bracketed by
+    barriers; (per-step seconds, max over ranks), results."""
     for _ in range(max(1, warmup)):
         b.run()
     res = b.results()
-    assert all(r["success"] and r["status"] == 0 for r in res), "host-io leg: frames failed"
+    assert all(r["success"] and r["status"] == 0 for r in res), "host-fed leg: frames failed"
+    rank_sync(dist)
     t0 = time.perf_counter()
     for _ in range(steps):
         b.run()
-    dt = (time.perf_counter() - t0) / steps
+    rank_sync(dist)
+    return ranks_max(dist, time.perf_counter() - t0) / steps, res
+
+
+def host_io_leg(codec, frames, hf, steps, warmup, cached, dist=None, world=1):
+    """SURVEY §8(d)'s headline definition, PCIe included: decoded BGR frames
+    in pinned host memory -> final JPEG bytes in pinned host memory.  The
+    library uploads sub-batch s+1 and downloads s-1 on their own streams while
+    s computes (icx_runtime.cpp run_batch, prefetch).  At N > 1 every rank
+    runs it at once (one process per GPU, each over its own link, sharing the
+    host's memory), timed between barriers, max over ranks."""
+    dev = frames[0].device
+    n = len(hf)
+    link = link_rates(dev)
+    outs = torch.empty((n, TARGET + 1), dtype=torch.uint8).pin_memory()
+    b = codec.prepare(hf, TARGET, Q0, cached=cached[:n] if cached else None, outputs=[outs[i] for i in range(n)])
+    dt, res = _timed_host_batch(b, steps, warmup, dist)
     up = sum(f.numel() for f in hf)
     down = sum(r["out_len"] for r in res)
     h2d = up / dt / 1e9
     return {"metric": "megapixels/sec JPEG encode, pinned host BGR in -> host JPEG bytes out (PCIe included)",
-            "value": round(n * W * H / 1e6 / dt, 1), "unit": "MP/s", "frames": n, "steps": steps,
-            "ms_per_step": round(dt * 1e3, 3),
-            "h2d_GBps": round(h2d, 2), "d2h_GBps": round(down / dt / 1e9, 2),
+            "value": round(world * n * W * H / 1e6 / dt, 1), "unit": "MP/s", "n_gpus": world, "frames_per_gpu": n,
+            "steps": steps, "ms_per_step": round(dt * 1e3, 3),
+            "h2d_GBps_per_gpu": round(h2d, 2), "d2h_GBps_per_gpu": round(down / dt / 1e9, 2),
             "link_h2d_GBps": round(link["h2d"], 2), "link_d2h_GBps": round(link["d2h"], 2),
             "h2d_frac_of_link": round(h2d / link["h2d"], 4)}
+
+
+def pool_leg(devices, hf, steps, warmup, cached, dist=None, world=1):
+    """icx_pool_compress_jpg_batch over `devices` (one process driving a
+    device list from one host: the JVM shape of CompressionBatch.java:64-88,
+    the only multi-GPU mode that keeps one learned cache, :71).  The same
+    pinned host frames as host_io, split by the pool into per-device shares
+    (LPT by pixels) run on one host thread per device.  At N > 1 each rank
+    runs its own pool (over its own devices) at once."""
+    n = len(hf)
+    pool = icx.Pool(devices)
+    try:
+        outs = torch.empty((n, TARGET + 1), dtype=torch.uint8).pin_memory()
+        b = pool.prepare(hf, TARGET, Q0, cached=cached[:n] if cached else None,
+                         outputs=[outs[i] for i in range(n)])
+        dt, res = _timed_host_batch(b, steps, warmup, dist)
+    finally:
+        pool.close()
+    return {"metric": "megapixels/sec JPEG encode through icx_pool (pinned host BGR in -> host JPEG bytes out)",
+            "value": round(world * n * W * H / 1e6 / dt, 1), "unit": "MP/s", "devices_per_process": devices,
+            "contexts": len(devices), "n_gpus": world, "frames_per_process": n, "steps": steps,
+            "ms_per_step": round(dt * 1e3, 3)}
 
 
 def e2e_cpu_baseline(srcs, n_sample, threads):
@@ -298,8 +357,13 @@ def main():
     ap.add_argument("--e2e", type=int, default=1000,
                     help="frames (distinct sources) of the decode+encode leg (0 = skip; default: configs[1]'s "
                          "1000, with the first 200 timed beside them)")
-    ap.add_argument("--host-io-frames", type=int, default=1000,
-                    help="frames of the PCIe-inclusive leg (pinned host in/out; 0 = skip; default: configs[1]'s 1000)")
+    ap.add_argument("--host-io-frames", type=int, default=-1,
+                    help="frames per GPU of the PCIe-inclusive legs (host_io, pool; pinned host in/out; 0 = skip; "
+                         "default: configs[1]'s 1000 at N = 1, max(200, 2000 / N) at N > 1 to bound the pinned "
+                         "host memory of a node)")
+    ap.add_argument("--pool-devices", default="",
+                    help="devices of the icx_pool leg, comma-separated (default: this rank's GPU twice: two "
+                         "contexts, the JVM-shaped host on one GPU; 'none' = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
     ap.add_argument("--target", type=int, default=TARGET, help="-t bytes (default 1 MiB)")
@@ -412,15 +476,25 @@ def main():
                         **({"algo_bytes": int(bytes_of[k])} if k in bytes_of else {})}
                     for k, v in kstats.items()},
     }
-    if rank == 0 and world == 1 and args.host_io_frames and not args.host_io:
+    # the host-fed legs and e2e run on every rank (each over its own link and
+    # GPU, together), timed between barriers, max over ranks
+    n_host = args.host_io_frames if args.host_io_frames >= 0 else (1000 if world == 1 else max(200, 2000 // world))
+    n_host = min(n_host, args.images)
+    if n_host and not args.host_io:
         batch = None
-        line["host_io"] = host_io_leg(codec, frames, min(args.host_io_frames, args.images), args.steps,
-                                      args.warmup, cached)
+        hf = host_frames(frames, n_host)
+        line["host_io"] = host_io_leg(codec, frames, hf, args.steps, args.warmup, cached, dist, world)
+        if args.pool_devices != "none":
+            devs = [int(d) for d in args.pool_devices.split(",")] if args.pool_devices else [local, local]
+            line["pool"] = pool_leg(devs, hf, args.steps, args.warmup, cached, dist, world)
+            line["pool"]["vs_host_io"] = round(line["pool"]["value"] / line["host_io"]["value"], 3)
+        hf = None
     cores, cores_how = host_cores()
-    if rank == 0 and world == 1 and args.e2e and not args.host_io:
+    if args.e2e and not args.host_io:
         batch = None
         line["e2e"] = e2e_leg(codec, dev, frames, min(args.e2e, args.images), args.steps,
-                              cpu_sample=0 if args.no_cpu_baseline else max(64, 4 * cores), threads=cores)
+                              cpu_sample=0 if (args.no_cpu_baseline or rank) else max(64, 4 * cores), threads=cores,
+                              dist=dist, world=world)
     if rank == 0 and not args.no_cpu_baseline:
         # rank 0 only, after the timed region (the other ranks wait at the
         # final barrier); at N > 1 the line still carries it

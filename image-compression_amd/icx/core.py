@@ -707,7 +707,8 @@ class PreparedBatch:
             j.cap = buf.numel() if hasattr(buf, "numel") else buf.nbytes
 
     def run(self):
-        st = self.codec._lib.icx_compress_jpg_batch(self.codec._ctx, self.jobs, self.n)
+        # icx_compress_jpg_batch, or icx_pool_compress_jpg_batch for a Pool
+        st = self.codec._batch_call("compress_jpg", self.jobs, self.n)
         self.codec._check(st, "icx_compress_jpg_batch")
         return self
 
@@ -740,6 +741,6 @@ class PreparedDecode:
 
     def run(self):
         with self.codec._lock:
-            st = self.codec._lib.icx_decode_jpg_batch(self.codec._ctx, self.jobs, self.n)
+            st = self.codec._batch_call("decode_jpg", self.jobs, self.n)
         self.codec._check(st, "icx_decode_jpg_batch")
         return [self.jobs[i].status for i in range(self.n)]

@@ -100,3 +100,39 @@ def test_two_rank_shards_balance_skewed_sizes(tmp_path):
     b0, b1 = res[0][2], res[1][2]
     assert max(b0, b1) <= 1.10 * min(b0, b1), (b0, b1)
     assert res[0][3:] == res[1][3:] == (12, 12)
+
+
+def _timing_worker(rank, world, port, q):
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bench.rank_sync(dist)
+    t0 = time.perf_counter()
+    time.sleep(0.05 + 0.25 * rank)  # rank 1 is the slow one
+    bench.rank_sync(dist)
+    q.put((rank, time.perf_counter() - t0, bench.ranks_max(dist, 0.1 * (rank + 1))))
+    dist.destroy_process_group()
+
+
+def test_two_rank_leg_timing_is_max_over_ranks():
+    """bench.py's host-fed legs (host_io, pool, e2e) run on every rank at
+    N > 1: the timed region is bracketed by barriers (both ranks see the slow
+    rank's time) and the reported time is the max over ranks (gloo)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_timing_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in ps)
+    for rank, wall, mx in got:
+        assert wall >= 0.29, (rank, wall)  # the barrier waits for rank 1's 0.3 s
+        assert abs(mx - 0.2) < 1e-9
