@@ -176,6 +176,10 @@ struct icx_ctx {
     std::map<std::string, icx::KStat> stats;
     size_t budget = 0;  // device workspace budget per sub-batch
     int table_layout = 0;  // ICX_TABLES_SEPARATE / ICX_TABLES_GROUPED (icx_set_table_layout)
+    // inverse colour maps of the default TYPE_BYTE_INDEXED [0] / TYPE_BYTE_BINARY
+    // [1] maps (32x32x32, device), built at the first palette resize
+    uint8_t* d_inv[2] = {nullptr, nullptr};
+    int inv_prims[2] = {0, 0};
     DevPool pool;
     DevPool hpool;  // pinned host buffers (hpool.host = true)
     // Host-buffer batches: inputs are uploaded (io_up) into one of two staging

@@ -34,7 +34,13 @@
 
 namespace icx {
 
-constexpr int CHUNK_BLOCKS = 256;        // scan blocks per Huffman chunk (one workgroup)
+// k_huff: one workgroup (256 threads, one per block) per chunk of 256 scan
+// blocks.  (Round 4 measured one wave per 64-block chunk, four chunks per
+// workgroup sharing the coding tables, no workgroup barrier after the table
+// load: k_huff +2...5 %, step +7 % with the 4x chunk count in k_scan/k_stuff;
+// DESIGN.md §9.)
+constexpr int CHUNK_BLOCKS = 256;  // scan blocks per Huffman chunk
+constexpr int HUFF_THREADS = CHUNK_BLOCKS;
 constexpr int MAX_BLOCK_BITS = 1664;     // >= 22 (DC) + 63 * 26 (AC) bits, multiple of 32
 constexpr int BLOCK_WORDS = MAX_BLOCK_BITS / 32;               // 52
 constexpr int CHUNK_WORDS = CHUNK_BLOCKS * BLOCK_WORDS;        // 13312 words = 52 KiB

@@ -8,7 +8,7 @@ namespace icx {
 
 hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat[64],
                             const uint32_t dc[2][16], const uint32_t ac[2][256],
-                            const uint8_t hdr[4][HDR_COLOR]);
+                            const uint8_t hdr[4][HDR_COLOR], const int8_t dith[3][64]);
 
 // kind: 0 = BGR24, 1 = RGB24, 2 = GRAY8
 // ImgState::list_entries of a plan's images after their FDCT (byte accounting)
@@ -33,10 +33,16 @@ struct ResizeArgs {
     int32_t sw, sh, sstride, fmt;
     int32_t dw, dh, dstride, tiles_x;
     int64_t x0l, dxl, y0l, dyl;  // inverse scale (32.32) and the first pixel centre's source position
+    // ICX_INDEXED8 / ICX_BINARY1: the source's colour map (device, 256 entries)
+    // and the inverse map of the destination's default one (device, 32x32x32)
+    const uint32_t* pal = nullptr;
+    const uint8_t* inv = nullptr;
+    int32_t prims = 0;  // the destination map represents the primaries (no dither for them)
 };
 ResizeArgs resize_args(const uint8_t* src, int sw, int sh, int sstride, int fmt, uint8_t* dst, int dw, int dh,
                        int dstride);
 int64_t resize_tiles(int dw, int dh);
+void launch_resize_one(const ResizeArgs& a, hipStream_t st);
 void launch_resize_batch(int fmt, const ResizeArgs* descs, const int64_t* prefix, int m, int64_t tiles,
                          int64_t uniform, hipStream_t st);
 

@@ -1093,6 +1093,13 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
     if (last != 63) sink.put(ac[0].x, (int)ac[0].y);  // EOB
 }
 
+#ifndef ICX_HUFF_ZERO16
+#define ICX_HUFF_ZERO16 1  // zero the assembly LDS with 16-B stores (-0.9 % huff, ab_r3zp_huff_zero16.txt)
+#endif
+#ifndef ICX_HUFF_WGS
+#define ICX_HUFF_WGS 8  // workgroups per CU k_huff is compiled for (8: <= 64 VGPRs)
+#endif
+
 // One workgroup = one chunk of CHUNK_BLOCKS scan blocks; one thread = one
 // 8x8 block (encode_one_block, jchuff.c), run once per trial:
 //   1. quantise + Huffman-code the thread's block straight into its LDS slot
@@ -1105,13 +1112,7 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
 //   4. gather: every 32-bit word of the chunk stream is assembled by the
 //      thread whose block holds the word's first bit (reading the following
 //      blocks' slots as needed) and stored once to scratch[cur].
-#ifndef ICX_HUFF_ZERO16
-#define ICX_HUFF_ZERO16 1  // zero the assembly LDS with 16-B stores (-0.9 % huff, ab_r3zp_huff_zero16.txt)
-#endif
-#ifndef ICX_HUFF_WGS
-#define ICX_HUFF_WGS 8  // workgroups per CU k_huff is compiled for (8: <= 64 VGPRs)
-#endif
-__global__ __launch_bounds__(CHUNK_BLOCKS, ICX_HUFF_WGS) void k_huff(const ImgDesc* __restrict__ descs,
+__global__ __launch_bounds__(HUFF_THREADS, ICX_HUFF_WGS) void k_huff(const ImgDesc* __restrict__ descs,
                                                        const ImgState* __restrict__ states,
                                                        const QNode* __restrict__ nodes,
                                                        const int32_t* __restrict__ ids,
@@ -1433,6 +1434,42 @@ __device__ __forceinline__ void decide_trial(const ImgDesc& D, ImgState& S, cons
     S.active = next >= 0;
 }
 
+// Exclusive scan of `n` per-chunk counts by one 1024-thread workgroup: every
+// thread sums a run of consecutive chunks (one pass whatever n is: an 8K frame
+// has ~3000 chunks), a 64-bit wave scan and the wave totals place the
+// runs, then every thread writes its run's offsets.  Returns the total to
+// every thread.
+template <class Get, class Put>
+__device__ __forceinline__ uint64_t wg_exclusive_scan(int n, Get get, Put put, uint64_t (&s_w)[16])
+{
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int per = (n + 1023) >> 10;
+    const int i0 = min(t * per, n), i1 = min(i0 + per, n);
+    uint64_t sum = 0;
+    for (int i = i0; i < i1; i++) sum += get(i);
+    uint64_t x = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    uint64_t base = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        if (k < wv) base += s_w[k];
+        total += s_w[k];
+    }
+    base += x - sum;
+    for (int i = i0; i < i1; i++) {
+        const uint64_t v = get(i);
+        put(i, base);
+        base += v;
+    }
+    return total;
+}
+
 // One workgroup per image: exclusive scan of the chunk bit counts, then each
 // chunk's 0xFF count: its alignment bin chunk_ffa[(8 - off%8) % 8] plus the
 // byte that starts in the chunk and ends in the next one (or in the padding).
@@ -1441,30 +1478,17 @@ __global__ __launch_bounds__(1024) void k_scan(const ImgDesc* __restrict__ descs
                                                int m)
 {
     __shared__ uint64_t s_w[16];
-    __shared__ uint64_t s_base;
     const int img = ids ? ids[blockIdx.x] : (int)blockIdx.x;
     ImgState& S = states[img];
     if (!S.active) return;
     const ImgDesc& D = descs[img];
     const int cur = S.cur;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    if (t == 0) s_base = 0;
-    __syncthreads();
-    for (int base = 0; base < D.nchunks; base += 1024) {
-        const int i = base + t;
-        // a chunk holds < 2^19 bits, 64 of them < 2^32: the wave scan is 32-bit
-        const uint64_t v = i < D.nchunks ? D.chunk_bits[cur][i] : 0;
-        const uint64_t x = (uint32_t)wave_incl_scan((int)v);
-        if (lane == 63) s_w[wv] = x;
-        __syncthreads();
-        uint64_t wbase = s_base;
-        for (int k = 0; k < wv; k++) wbase += s_w[k];
-        if (i < D.nchunks) D.chunk_off[cur][i] = wbase + x - v;
-        __syncthreads();
-        if (t == 1023) s_base = wbase + x;
-        __syncthreads();
-    }
-    if (t == 0) D.chunk_off[cur][D.nchunks] = s_base;
+    const GAS uint32_t* bits = gp(D.chunk_bits[cur]);
+    GAS uint64_t* offw = gp(D.chunk_off[cur]);
+    const uint64_t total = wg_exclusive_scan(
+        D.nchunks, [&](int i) -> uint64_t { return bits[i]; }, [&](int i, uint64_t o) { offw[i] = o; }, s_w);
+    if (t == 0) offw[D.nchunks] = total;
     __syncthreads();
     const GAS uint64_t* off = gp(D.chunk_off[cur]);
     const GAS uint32_t* ffa = gp(D.chunk_ffa[cur]);
@@ -1486,7 +1510,7 @@ __global__ __launch_bounds__(1024) void k_scan(const ImgDesc* __restrict__ descs
     if (t == 0) {
         uint64_t ff = 0;
         for (int k = 0; k < 16; k++) ff += s_w[k];
-        decide_trial(D, S, nodes, s_base, (uint32_t)ff);
+        decide_trial(D, S, nodes, total, (uint32_t)ff);
     }
 }
 
@@ -1496,31 +1520,18 @@ __global__ __launch_bounds__(1024) void k_ffscan(const ImgDesc* __restrict__ des
                                                  const int32_t* __restrict__ ids, int m)
 {
     __shared__ uint64_t s_w[16];
-    __shared__ uint64_t s_base;
     const int img = ids ? ids[blockIdx.x] : (int)blockIdx.x;
     ImgState& S = states[img];
     if (S.best_node < 0) return;
     const ImgDesc& D = descs[img];
     const int buf = S.best_buf;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    if (t == 0) s_base = 0;
-    __syncthreads();
-    for (int base = 0; base < D.nchunks; base += 1024) {
-        const int i = base + t;
-        const uint64_t v = i < D.nchunks ? D.chunk_ff[buf][i] : 0;  // < 2^16 per chunk
-        const uint64_t x = (uint32_t)wave_incl_scan((int)v);
-        if (lane == 63) s_w[wv] = x;
-        __syncthreads();
-        uint64_t wbase = s_base;
-        for (int k = 0; k < wv; k++) wbase += s_w[k];
-        if (i < D.nchunks) D.chunk_ffoff[i] = wbase + x - v;
-        __syncthreads();
-        if (t == 1023) s_base = wbase + x;
-        __syncthreads();
-    }
-    if (t == 0) {
+    const GAS uint32_t* ff = gp(D.chunk_ff[buf]);
+    GAS uint64_t* ffoff = gp(D.chunk_ffoff);
+    const uint64_t total = wg_exclusive_scan(
+        D.nchunks, [&](int i) -> uint64_t { return ff[i]; }, [&](int i, uint64_t o) { ffoff[i] = o; }, s_w);
+    if (threadIdx.x == 0) {
         const uint64_t nbytes = (D.chunk_off[buf][D.nchunks] + 7) >> 3;
-        const int64_t len = (int64_t)D.hdr_len + (int64_t)nbytes + (int64_t)s_base + 2;
+        const int64_t len = (int64_t)D.hdr_len + (int64_t)nbytes + (int64_t)total + 2;
         S.out_len = len;
         S.status = (uint64_t)len > D.cap ? 4 : 0;
     }
@@ -1699,8 +1710,9 @@ __device__ __forceinline__ uint32_t mul8(uint32_t a, uint32_t c)  // AlphaMath.c
     return ((c * (a * 0x010101u) + (1u << 23)) >> 24) & 0xffu;
 }
 
+// the four taps fetched as IntArgbPre and interpolated: v[b] per byte b
 template <int AB, bool OPAQUE>
-__device__ __forceinline__ uint32_t bilerp4(const uint32_t (&p)[4], int xf, int yf)
+__device__ __forceinline__ void bilerp4_pre(const uint32_t (&p)[4], int xf, int yf, int (&v)[4])
 {
     uint32_t pre[4][4];
 #pragma unroll
@@ -1709,9 +1721,15 @@ __device__ __forceinline__ uint32_t bilerp4(const uint32_t (&p)[4], int xf, int 
 #pragma unroll
         for (int b = 0; b < 4; b++) pre[s][b] = b == AB ? al : mul8(al, (p[s] >> (8 * b)) & 255u);
     }
-    int v[4];
 #pragma unroll
     for (int b = 0; b < 4; b++) v[b] = bilerp(pre[0][b], pre[1][b], pre[2][b], pre[3][b], xf, yf);
+}
+
+template <int AB, bool OPAQUE>
+__device__ __forceinline__ uint32_t bilerp4(const uint32_t (&p)[4], int xf, int yf)
+{
+    int v[4];
+    bilerp4_pre<AB, OPAQUE>(p, xf, yf, v);
     const uint32_t al = (uint32_t)v[AB];
     uint32_t out = 0;
     if (OPAQUE) {
@@ -1761,14 +1779,52 @@ __device__ __forceinline__ uint32_t ldx(const uint8_t* p)
     else return *(const GAS T*)p;
 }
 
+// Palette rasters (IDX 1: TYPE_BYTE_INDEXED, 2: TYPE_BYTE_BINARY; the source
+// holds one colour-map index per byte): the taps are fetched through the
+// source's map as IntArgbPre (CopyByteIndexedToIntArgbPre: mul8 premultiply)
+// and interpolated as the four-byte formats are; the alpha mask blit
+// (SrcOver) onto the new image - its pixel 0, opaque black in both default
+// maps - leaves the premultiplied colour at alpha 255; the store picks the
+// destination index through the inverse colour map (32x32x32 cells), after
+// the 8x8 ordered dither errors at (x & 7, y & 7) for ByteIndexed (skipped
+// when r, g, b are each 0 or 255 and the map represents the primaries; the
+// components clamped to 0..255).  ByteBinary stores have no dither.
+__constant__ int8_t c_dith[3][64];  // make_dither_arrays: red, green, blue errors [(y & 7) * 8 + (x & 7)]
+
+template <int IDX>
+__device__ __forceinline__ uint8_t store_indexed(const ResizeArgs& a, const int (&v)[4], int dx, int dy)
+{
+    int r = v[2], g = v[1], b = v[0];  // bytes B, G, R, A of 0xAARRGGBB
+    if (IDX == 1) {
+        const bool prim = a.prims && (r == 0 || r == 255) && (g == 0 || g == 255) && (b == 0 || b == 255);
+        if (!prim) {
+            const int e = ((dy & 7) << 3) | (dx & 7);
+            r += c_dith[0][e];
+            g += c_dith[1][e];
+            b += c_dith[2][e];
+        }
+        r = min(max(r, 0), 255);
+        g = min(max(g, 0), 255);
+        b = min(max(b, 0), 255);
+    }
+    return gp(a.inv)[((r >> 3) << 10) | ((g >> 3) << 5) | (b >> 3)];
+}
+
 // One destination pixel from the rows ra / rb (addresses of source pixel 0
 // of rows ya / yb: global memory, or LDS rebased so that the same x indexes
 // it), stored at o.
-template <int BPP, int AB, bool OPQ, bool L>
+template <int BPP, int AB, bool OPQ, bool L, int IDX = 0>
 __device__ __forceinline__ void resize_px(const uint8_t* ra, const uint8_t* rb, int xa, int xb, int xf, int yf,
-                                          uint8_t* o)
+                                          uint8_t* o, const ResizeArgs& a, int dx, int dy)
 {
-    if constexpr (BPP == 4) {
+    if constexpr (IDX != 0) {
+        const GAS uint32_t* pal = gp(a.pal);
+        const uint32_t p[4] = {pal[ldx<uint8_t, L>(ra + xa)], pal[ldx<uint8_t, L>(ra + xb)],
+                               pal[ldx<uint8_t, L>(rb + xa)], pal[ldx<uint8_t, L>(rb + xb)]};
+        int v[4];
+        bilerp4_pre<3, false>(p, xf, yf, v);
+        *(GAS uint8_t*)o = store_indexed<IDX>(a, v, dx, dy);
+    } else if constexpr (BPP == 4) {
         const uint32_t p[4] = {ldx<uint32_t, L>(ra + 4 * xa), ldx<uint32_t, L>(ra + 4 * xb),
                                ldx<uint32_t, L>(rb + 4 * xa), ldx<uint32_t, L>(rb + 4 * xb)};
         *(GAS uint32_t*)o = bilerp4<AB, OPQ>(p, xf, yf);
@@ -1785,7 +1841,7 @@ __device__ __forceinline__ void resize_px(const uint8_t* ra, const uint8_t* rb, 
     }
 }
 
-template <int BPP, int AB, bool OPQ>
+template <int BPP, int AB, bool OPQ, int IDX = 0>
 __global__ __launch_bounds__(256) void k_resize(ResizeArgs one, const ResizeArgs* __restrict__ descs,
                                                 const int64_t* __restrict__ prefix, int m)
 {
@@ -1846,8 +1902,8 @@ __global__ __launch_bounds__(256) void k_resize(ResizeArgs one, const ResizeArgs
                                       (uint32_t)(bx0 * BPP)) & 15u;
                 return &lds[(y - by0) * lstr + mis] - (ptrdiff_t)bx0 * BPP;
             };
-            resize_px<BPP, AB, OPQ, true>(lrow(ya), lrow(yb), xa, xb, xf, yf,
-                                    a.dst + (size_t)dy * a.dstride + (size_t)dx * BPP);
+            resize_px<BPP, AB, OPQ, true, IDX>(lrow(ya), lrow(yb), xa, xb, xf, yf,
+                                               a.dst + (size_t)dy * a.dstride + (size_t)dx * BPP, a, dx, dy);
         }
     } else {
         if (dx > dxe) return;
@@ -1856,8 +1912,9 @@ __global__ __launch_bounds__(256) void k_resize(ResizeArgs one, const ResizeArgs
             if (dy > dye) break;
             int ya, yb, yf;
             tap_y(a, dy, ya, yb, yf);
-            resize_px<BPP, AB, OPQ, false>(a.src + (size_t)ya * a.sstride, a.src + (size_t)yb * a.sstride, xa, xb,
-                                           xf, yf, a.dst + (size_t)dy * a.dstride + (size_t)dx * BPP);
+            resize_px<BPP, AB, OPQ, false, IDX>(a.src + (size_t)ya * a.sstride, a.src + (size_t)yb * a.sstride, xa,
+                                                xb, xf, yf, a.dst + (size_t)dy * a.dstride + (size_t)dx * BPP, a,
+                                                dx, dy);
         }
     }
 }
@@ -1865,9 +1922,10 @@ __global__ __launch_bounds__(256) void k_resize(ResizeArgs one, const ResizeArgs
 // =================================================================== host side
 hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat[64],
                             const uint32_t dc[2][16], const uint32_t ac[2][256],
-                            const uint8_t hdr[4][HDR_COLOR])
+                            const uint8_t hdr[4][HDR_COLOR], const int8_t dith[3][64])
 {
     hipError_t e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_dith), dith, 3 * 64))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_nat_to_zz), nat_to_zz, 64))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_zz_to_nat), zz_to_nat, 64))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_dc), dc, sizeof(uint32_t) * 2 * 16))) return e;
@@ -1924,12 +1982,12 @@ void launch_list_count(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t
     ICX_LAUNCH(k_list_count, dim3(p.m), dim3(1024), 0, st, d, s, plan_ids(p), p.m);
 }
 
-void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, bool rev,
+void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t wgs, bool rev,
                  hipStream_t st)
 {
-    if (chunks <= 0) return;
-    const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3((unsigned)p.uniform, (unsigned)p.m) : dim3((unsigned)chunks);
-    ICX_LAUNCH(k_huff, grid, dim3(CHUNK_BLOCKS), 0, st, d, s, n, plan_ids(p), p.prefix, p.m, rev ? 1 : 0);
+    if (wgs <= 0) return;
+    const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3((unsigned)p.uniform, (unsigned)p.m) : dim3((unsigned)wgs);
+    ICX_LAUNCH(k_huff, grid, dim3(HUFF_THREADS), 0, st, d, s, n, plan_ids(p), p.prefix, p.m, rev ? 1 : 0);
 }
 
 void launch_scan(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, hipStream_t st)
@@ -1977,6 +2035,8 @@ static void launch_resize_fmt(int fmt, const ResizeArgs& one, const ResizeArgs* 
     switch (fmt) {
     case ICX_GRAY8: ICX_LAUNCH((k_resize<1, 0, true>), grid, dim3(256), 0, st, one, descs, prefix, m); break;
     case ICX_GRAY16: ICX_LAUNCH((k_resize<2, 0, true>), grid, dim3(256), 0, st, one, descs, prefix, m); break;
+    case ICX_INDEXED8: ICX_LAUNCH((k_resize<1, 0, false, 1>), grid, dim3(256), 0, st, one, descs, prefix, m); break;
+    case ICX_BINARY1: ICX_LAUNCH((k_resize<1, 0, false, 2>), grid, dim3(256), 0, st, one, descs, prefix, m); break;
     case ICX_XRGB32: ICX_LAUNCH((k_resize<4, 3, true>), grid, dim3(256), 0, st, one, descs, prefix, m); break;
     case ICX_ARGB32:
     case ICX_RGBA32: ICX_LAUNCH((k_resize<4, 3, false>), grid, dim3(256), 0, st, one, descs, prefix, m); break;
@@ -1988,8 +2048,12 @@ static void launch_resize_fmt(int fmt, const ResizeArgs& one, const ResizeArgs* 
 void launch_resize(const uint8_t* src, int sw, int sh, int sstride, int fmt, uint8_t* dst, int dw, int dh,
                    int dstride, hipStream_t st)
 {
-    const ResizeArgs a = resize_args(src, sw, sh, sstride, fmt, dst, dw, dh, dstride);
-    launch_resize_fmt(fmt, a, nullptr, nullptr, 1, dim3((unsigned)resize_tiles(dw, dh)), st);
+    launch_resize_one(resize_args(src, sw, sh, sstride, fmt, dst, dw, dh, dstride), st);
+}
+
+void launch_resize_one(const ResizeArgs& a, hipStream_t st)
+{
+    launch_resize_fmt(a.fmt, a, nullptr, nullptr, 1, dim3((unsigned)resize_tiles(a.dw, a.dh)), st);
 }
 
 void launch_resize_batch(int fmt, const ResizeArgs* descs, const int64_t* prefix, int m, int64_t tiles,

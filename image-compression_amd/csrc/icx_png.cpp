@@ -21,7 +21,15 @@
 //
 // Output colour type follows the raster: GRAY8 -> 0 (grey, 8 bits), GRAY16
 // -> 0 (grey, 16 bits, TYPE_USHORT_GRAY), BGR24 / RGB24 / XRGB32 -> 2 (RGB),
-// ARGB32 / ABGR32 / RGBA32 -> 6 (RGBA), no interlace.  Rows are converted,
+// ARGB32 / ABGR32 / RGBA32 -> 6 (RGBA), no interlace.  Palette rasters
+// (INDEXED8: TYPE_BYTE_INDEXED, 8 bits; BINARY1: TYPE_BYTE_BINARY, 1/2/4 bits
+// by map size) follow PNGMetadata.initialize for an IndexColorModel: a map
+// that is the grey ramp i * 255 / (2^depth - 1) becomes grey (colour type 0,
+// or 4 with alpha at 8 bits), anything else a palette (3) with PLTE = the
+// whole map and tRNS = its alphas when it has any; RowFilter uses filter 0
+// for every palette row.  The new images of ImageTools.resizeImage carry the
+// default maps: INDEXED8 -> an 8-bit palette PNG of the 6x6x6 cube + grey
+// ramp, BINARY1 -> a 1-bit grey PNG.  Rows are converted,
 // filtered and deflated one at a time (three row buffers), straight into the
 // caller's buffer: no image-sized temporary.  The caller's thread does the
 // work; ctypes releases the GIL, so the batch driver's writer pool runs one
@@ -37,18 +45,79 @@
 
 namespace {
 
+// How a palette raster is written (PNGMetadata.initialize for an IndexColorModel).
+struct PalOut {
+    int depth = 8;     // bits per sample
+    int ctype = 3;     // 0 grey, 4 grey + alpha, 3 palette
+    bool alpha = false;
+};
+
+PalOut pal_out(const icx_image* img)
+{
+    PalOut o;
+    const int n = img->palette_len;
+    if (img->fmt == ICX_BINARY1) o.depth = n <= 2 ? 1 : n <= 4 ? 2 : 4;
+    const int scale = 255 / ((1 << o.depth) - 1);
+    bool grey = true;
+    for (int i = 0; i < n; i++) {
+        const uint32_t c = img->palette[i];
+        const uint32_t r = c >> 16 & 255, g = c >> 8 & 255, b = c & 255;
+        if (r != (uint32_t)(i * scale & 255) || r != g || r != b) grey = false;
+        if ((c >> 24) != 255) o.alpha = true;
+    }
+    o.ctype = grey && o.alpha && o.depth == 8 ? 4 : grey && !o.alpha ? 0 : 3;
+    return o;
+}
+
 // Bytes per pixel of the PNG row (RowFilter's bytesPerPixel) and of the source.
 int png_bpp(int fmt)
 {
     switch (fmt) {
-    case ICX_GRAY8: return 1;
+    case ICX_GRAY8: case ICX_INDEXED8: case ICX_BINARY1: return 1;
     case ICX_GRAY16: return 2;
     case ICX_BGR24: case ICX_RGB24: case ICX_XRGB32: return 3;
     default: return 4;
     }
 }
 
-int src_bpp(int fmt) { return fmt == ICX_GRAY8 ? 1 : fmt == ICX_GRAY16 ? 2 : fmt <= ICX_RGB24 ? 3 : 4; }
+int src_bpp(int fmt)
+{
+    return fmt == ICX_GRAY8 || fmt == ICX_INDEXED8 || fmt == ICX_BINARY1 ? 1 : fmt == ICX_GRAY16 ? 2
+                                                                        : fmt <= ICX_RGB24 ? 3 : 4;
+}
+
+// Bytes of one PNG row (without the filter byte).
+size_t png_row_bytes(const icx_image* img)
+{
+    if (img->fmt == ICX_INDEXED8 || img->fmt == ICX_BINARY1) {
+        const PalOut o = pal_out(img);
+        return o.ctype == 4 ? 2 * (size_t)img->width : ((size_t)img->width * o.depth + 7) / 8;
+    }
+    return (size_t)img->width * png_bpp(img->fmt);
+}
+
+// A palette row -> PNG samples: indices packed MSB first at `depth` bits,
+// grey levels (the ramp's index is the level) or grey + alpha pairs.
+void convert_pal_row(const uint8_t* s, const icx_image* img, const PalOut& o, uint8_t* d)
+{
+    const int w = img->width;
+    if (o.ctype == 4) {
+        for (int x = 0; x < w; x++) {
+            const uint32_t c = img->palette[s[x] < img->palette_len ? s[x] : 0];
+            d[2 * x] = (uint8_t)(c & 255);
+            d[2 * x + 1] = (uint8_t)(c >> 24);
+        }
+        return;
+    }
+    if (o.depth == 8) {
+        memcpy(d, s, (size_t)w);
+        return;
+    }
+    memset(d, 0, ((size_t)w * o.depth + 7) / 8);
+    const int per = 8 / o.depth;
+    for (int x = 0; x < w; x++)
+        d[x / per] |= (uint8_t)((s[x] & ((1 << o.depth) - 1)) << (8 - o.depth * (x % per + 1)));
+}
 
 // Source row -> PNG sample order (R, G, B[, A] or grey).
 void convert_row(const uint8_t* s, int w, int fmt, uint8_t* d)
@@ -144,16 +213,19 @@ constexpr int kDefaultLevel = 4; // PNGImageWriter.DEFAULT_COMPRESSION_LEVEL
 size_t icx_png_bound(const icx_image* img)
 {
     if (!img || img->width <= 0 || img->height <= 0) return 0;
-    const size_t raw = (size_t)img->height * ((size_t)img->width * png_bpp(img->fmt) + 1);
+    if ((img->fmt == ICX_INDEXED8 || img->fmt == ICX_BINARY1) && (!img->palette || img->palette_len < 1 ||
+                                                                  img->palette_len > 256))
+        return 0;
+    const size_t raw = (size_t)img->height * (png_row_bytes(img) + 1);
     if (raw > kMaxRaw) return 0;
     const size_t z = (size_t)compressBound((uLong)raw);
-    return 8 + 25 + z + 12 * (z / kIdat + 1) + 12 + 64;
+    return 8 + 25 + z + 12 * (z / kIdat + 1) + 12 + 64 + 12 + 3 * 256 + 12 + 256;  // + PLTE, tRNS
 }
 
 icx_status icx_png_encode(const icx_image* img, int32_t level, uint8_t* out, size_t cap, size_t* out_len)
 {
     if (!img || !img->px || !out || !out_len) return ICX_E_NULL;
-    if (img->width <= 0 || img->height <= 0 || img->fmt < ICX_BGR24 || img->fmt > ICX_GRAY16 ||
+    if (img->width <= 0 || img->height <= 0 || img->fmt < ICX_BGR24 || img->fmt > ICX_BINARY1 ||
         img->stride < img->width * src_bpp(img->fmt) || level < -1 || level > 9)
         return ICX_E_INVALID;
     if (icx::is_device_ptr(img->px)) return ICX_E_INVALID;  // host rows only
@@ -161,18 +233,34 @@ icx_status icx_png_encode(const icx_image* img, int32_t level, uint8_t* out, siz
     if (need == 0) return ICX_E_UNSUPPORTED;  // over kMaxRaw
     *out_len = need;
     if (cap < need) return ICX_E_BUFFER;
-    const int bpp = png_bpp(img->fmt);
-    const int n = img->width * bpp;
+    const bool pal = img->fmt == ICX_INDEXED8 || img->fmt == ICX_BINARY1;
+    const PalOut po = pal ? pal_out(img) : PalOut{};
+    const int bpp = pal && po.ctype == 4 ? 2 : png_bpp(img->fmt);
+    const int n = (int)png_row_bytes(img);
     static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
     memcpy(out, sig, 8);
     size_t pos = 8;
     uint8_t* ih = out + pos + 8;
     put32(ih, (uint32_t)img->width);
     put32(ih + 4, (uint32_t)img->height);
-    ih[8] = img->fmt == ICX_GRAY16 ? 16 : 8;                  // bit depth
-    ih[9] = (uint8_t)(bpp <= 2 ? 0 : bpp == 3 ? 2 : 6);      // colour type
+    ih[8] = pal ? (uint8_t)po.depth : img->fmt == ICX_GRAY16 ? 16 : 8;                // bit depth
+    ih[9] = pal ? (uint8_t)po.ctype : (uint8_t)(bpp <= 2 ? 0 : bpp == 3 ? 2 : 6);    // colour type
     ih[10] = ih[11] = ih[12] = 0;                             // deflate, adaptive filtering, no interlace
     pos += close_chunk(out + pos, "IHDR", 13);
+    if (pal && po.ctype == 3) {  // PLTE = the whole map, tRNS = its alphas
+        uint8_t* p = out + pos + 8;
+        for (int i = 0; i < img->palette_len; i++) {
+            p[3 * i] = (uint8_t)(img->palette[i] >> 16);
+            p[3 * i + 1] = (uint8_t)(img->palette[i] >> 8);
+            p[3 * i + 2] = (uint8_t)img->palette[i];
+        }
+        pos += close_chunk(out + pos, "PLTE", 3 * (size_t)img->palette_len);
+        if (po.alpha) {
+            p = out + pos + 8;
+            for (int i = 0; i < img->palette_len; i++) p[i] = (uint8_t)(img->palette[i] >> 24);
+            pos += close_chunk(out + pos, "tRNS", (size_t)img->palette_len);
+        }
+    }
 
     z_stream z{};
     if (deflateInit(&z, level < 0 ? kDefaultLevel : level) != Z_OK) return ICX_E_NOMEM;
@@ -191,8 +279,14 @@ icx_status icx_png_encode(const icx_image* img, int32_t level, uint8_t* out, siz
     int zr = Z_OK;
     bool finished = false;
     for (int y = 0; y < img->height && zr == Z_OK; y++) {
-        convert_row(img->px + (size_t)y * img->stride, img->width, img->fmt, cur);
-        filter_row(cur, prev, n, bpp, filt);
+        if (pal) convert_pal_row(img->px + (size_t)y * img->stride, img, po, cur);
+        else convert_row(img->px + (size_t)y * img->stride, img->width, img->fmt, cur);
+        if (pal && po.ctype == 3) {  // RowFilter: "Use type 0 for palette images"
+            filt[0] = 0;
+            memcpy(filt + 1, cur, (size_t)n);
+        } else {
+            filter_row(cur, prev, n, bpp, filt);
+        }
         z.next_in = filt;
         z.avail_in = (uInt)n + 1;
         const int flush = y + 1 == img->height ? Z_FINISH : Z_NO_FLUSH;

@@ -143,7 +143,107 @@ int build_tree(float lo, float hi, int iter, std::vector<QNode>& nodes, int& dep
 }
 
 // bytes per pixel of a raster (GRAY16: one 2-byte sample)
-int channels(int fmt) { return fmt == ICX_GRAY8 ? 1 : fmt == ICX_GRAY16 ? 2 : fmt <= ICX_RGB24 ? 3 : 4; }
+int channels(int fmt)
+{
+    return fmt == ICX_GRAY8 || fmt == ICX_INDEXED8 || fmt == ICX_BINARY1 ? 1 : fmt == ICX_GRAY16 ? 2
+                                                                        : fmt <= ICX_RGB24 ? 3 : 4;
+}
+
+bool is_palette(int fmt) { return fmt == ICX_INDEXED8 || fmt == ICX_BINARY1; }
+
+// --- default colour maps of the palette types (BufferedImage.java's
+// TYPE_BYTE_INDEXED / TYPE_BYTE_BINARY constructors) and what Java2D derives
+// from a map for storing into it (OpenJDK java.desktop; no JDK here to pin
+// them, parity unpinned: DESIGN.md §11)
+int default_palette(bool binary, uint32_t* pal)
+{
+    if (binary) {  // IndexColorModel(1, 2, {0, 0xff} x 3)
+        pal[0] = 0xff000000u;
+        pal[1] = 0xffffffffu;
+        return 2;
+    }
+    int n = 0;  // 6x6x6 cube (r outer), then a grey ramp from 18 in steps of 256 / 40
+    for (int r = 0; r <= 255; r += 51)
+        for (int g = 0; g <= 255; g += 51)
+            for (int b = 0; b <= 255; b += 51) pal[n++] = 0xff000000u | (uint32_t)r << 16 | (uint32_t)g << 8 | (uint32_t)b;
+    const int step = 256 / (256 - n);
+    for (int v = 3 * step; n < 256; n++, v += step) pal[n] = 0xff000000u | (uint32_t)v * 0x010101u;
+    return 256;
+}
+
+// initCubemap (32 cells per axis): the map's entries seed a 15-bit RGB cube
+// in the order 0, n-1, 1, n-2, ...; then breadth first, level by level, every
+// cell of the previous level claims its unclaimed neighbours (+r, -r, +g, -g,
+// +b, -b) for its entry - an L1 flood fill in which the first claim wins.
+std::vector<uint8_t> inverse_cube(const uint32_t* pal, int n)
+{
+    std::vector<uint8_t> cube(32768, 0);
+    std::vector<uint8_t> claimed(32768, 0);
+    std::vector<std::pair<uint16_t, uint8_t>> level, next;
+    auto claim = [&](std::vector<std::pair<uint16_t, uint8_t>>& to, int cell, int idx) {
+        if (claimed[cell]) return;
+        claimed[cell] = 1;
+        cube[cell] = (uint8_t)idx;
+        to.emplace_back((uint16_t)cell, (uint8_t)idx);
+    };
+    auto cell_of = [](uint32_t c) { return (int)((c >> 9 & 0x7c00) | (c >> 6 & 0x03e0) | (c >> 3 & 0x001f)); };
+    for (int i = 0; i < (n + 1) / 2; i++) {
+        claim(level, cell_of(pal[i]), i);
+        claim(level, cell_of(pal[n - 1 - i]), n - 1 - i);
+    }
+    static const int kMask[3] = {0x7c00, 0x03e0, 0x001f}, kStep[3] = {0x0400, 0x0020, 0x0001};
+    while (!level.empty()) {
+        next.clear();
+        for (const auto& e : level)
+            for (int a = 0; a < 3; a++) {
+                if ((e.first & kMask[a]) + kStep[a] <= kMask[a]) claim(next, e.first + kStep[a], e.second);
+                if ((e.first & kMask[a]) >= kStep[a]) claim(next, e.first - kStep[a], e.second);
+            }
+        level.swap(next);
+    }
+    return cube;
+}
+
+// calculatePrimaryColorsApproximation: the eight corner cells hold colours
+// within 5 of their corners' primaries
+bool represents_primaries(const uint32_t* pal, const std::vector<uint8_t>& cube)
+{
+    for (int c = 0; c < 8; c++) {
+        const int r = c & 4 ? 31 : 0, g = c & 2 ? 31 : 0, b = c & 1 ? 31 : 0;
+        const uint32_t p = pal[cube[(r << 10) | (g << 5) | b]];
+        const int want[3] = {r ? 255 : 0, g ? 255 : 0, b ? 255 : 0};
+        const int got[3] = {(int)(p >> 16 & 255), (int)(p >> 8 & 255), (int)(p & 255)};
+        for (int k = 0; k < 3; k++)
+            if (std::abs(got[k] - want[k]) > 5) return false;
+    }
+    return true;
+}
+
+// make_dither_arrays(256): the 8x8 recursive ordered-dither matrix scaled to
+// [-e/2, e - e/2) with e = (int)(256 / cbrt(256)) = 40; green mirrored
+// left-right, blue top-bottom
+void dither_tables(int8_t (&d)[3][64])
+{
+    const int e = (int)(256 / std::pow(256.0, 1.0 / 3.0)), lo = -e / 2, hi = e - e / 2;
+    int m[8][8];
+    m[0][0] = 0;
+    for (int k = 1; k < 8; k <<= 1)
+        for (int i = 0; i < k; i++)
+            for (int j = 0; j < k; j++) {
+                const int v = m[i][j] * 4;
+                m[i][j] = v;
+                m[i + k][j + k] = v + 1;
+                m[i][j + k] = v + 2;
+                m[i + k][j] = v + 3;
+            }
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) {
+            const auto at = [&](int yy, int xx) { return (int8_t)(m[yy][xx] * (hi - lo) / 64 + lo); };
+            d[0][y * 8 + x] = at(y, x);
+            d[1][y * 8 + x] = at(y, 7 - x);
+            d[2][y * 8 + x] = at(7 - y, x);
+        }
+}
 
 void geometry(ImgDesc& d, int w, int h, int fmt, int layout = ICX_TABLES_SEPARATE)
 {
@@ -457,7 +557,10 @@ icx_status validate(const icx_image* img)
 {
     if (!img || !img->px) return ICX_E_NULL;
     if (img->width <= 0 || img->height <= 0 || img->width > 65535 || img->height > 65535) return ICX_E_INVALID;
-    if (img->fmt < ICX_BGR24 || img->fmt > ICX_GRAY16) return ICX_E_INVALID;
+    if (img->fmt < ICX_BGR24 || img->fmt > ICX_BINARY1) return ICX_E_INVALID;
+    if (is_palette(img->fmt) && (!img->palette || img->palette_len < 1 ||
+                                 img->palette_len > (img->fmt == ICX_BINARY1 ? 16 : 256)))
+        return ICX_E_INVALID;
     if (img->stride < img->width * channels(img->fmt)) return ICX_E_INVALID;
     if (channels(img->fmt) == 4 && (((uintptr_t)img->px | (uintptr_t)img->stride) & 3)) return ICX_E_INVALID;
     if (channels(img->fmt) == 2 && (((uintptr_t)img->px | (uintptr_t)img->stride) & 1)) return ICX_E_INVALID;
@@ -983,16 +1086,28 @@ icx_status icx_create(int device, icx_ctx** out)
         delete c;
         return ICX_E_DEVICE;
     }
-    // constant tables: zig-zag, Huffman codes, marker templates
-    static std::once_flag once;
-    static hipError_t up = hipSuccess;
-    std::call_once(once, [] {
+    // constant tables: zig-zag, Huffman codes, marker templates, dither
+    // errors - built once, uploaded once per DEVICE (__constant__ symbols
+    // live on every device: a pool over several GPUs needs them on each)
+    struct Consts {
         uint8_t nat2zz[64], zz2nat[64];
+        uint32_t dc[2][16] = {}, ac[2][256] = {};
+        uint8_t hdr[4][HDR_COLOR] = {};
+        int8_t dith[3][64];
+    };
+    static std::once_flag once;
+    static Consts K;
+    static std::mutex up_mu;
+    static std::vector<int> up_done;
+    std::call_once(once, [] {
+        uint8_t* nat2zz = K.nat2zz;
+        uint8_t* zz2nat = K.zz2nat;
         for (int k = 0; k < 64; k++) {
             zz2nat[k] = kZigzag[k];
             nat2zz[kZigzag[k]] = (uint8_t)k;
         }
-        uint32_t dc[2][16] = {}, ac[2][256] = {};
+        auto& dc = K.dc;
+        auto& ac = K.ac;
         auto derive = [](const uint8_t* bits, const uint8_t* vals, uint32_t* tbl) {
             unsigned code = 0;
             int k = 0;
@@ -1005,7 +1120,7 @@ icx_status icx_create(int device, icx_ctx** out)
         derive(kDcChrBits, kDcVals, dc[1]);
         derive(kAcLumBits, kAcLumVals, ac[0]);
         derive(kAcChrBits, kAcChrVals, ac[1]);
-        uint8_t hdr[4][HDR_COLOR] = {};
+        auto& hdr = K.hdr;
         for (int g = 0; g < 4; g++) {
             const int nc = (g & 1) ? 3 : 1;
             const bool grouped = g >= 2;  // ICX_TABLES_GROUPED: one DQT and one DHT segment
@@ -1053,8 +1168,16 @@ icx_status icx_create(int device, icx_ctx** out)
                                           : (grouped ? HDR_GRAY_GROUPED : HDR_GRAY))) abort();
             memcpy(hdr[g], h.data(), h.size());
         }
-        up = upload_constants(nat2zz, zz2nat, dc, ac, hdr);
+        dither_tables(K.dith);
     });
+    hipError_t up = hipSuccess;
+    {
+        std::lock_guard<std::mutex> lk(up_mu);
+        if (std::find(up_done.begin(), up_done.end(), device) == up_done.end()) {
+            up = upload_constants(K.nat2zz, K.zz2nat, K.dc, K.ac, K.hdr, K.dith);
+            if (up == hipSuccess) up_done.push_back(device);
+        }
+    }
     if (up != hipSuccess) {
         hipStreamDestroy(c->stream);
         delete c;
@@ -1082,6 +1205,8 @@ void icx_destroy(icx_ctx* ctx)
     hipStreamSynchronize(ctx->stream);
     for (auto& p : ctx->pending) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
     for (auto e : ctx->evpool) hipEventDestroy(e);
+    for (auto p : ctx->d_inv)
+        if (p) hipFree(p);
     hipStreamDestroy(ctx->stream);
     if (ctx->dec_aux) {
         hipStreamSynchronize(ctx->dec_aux);
@@ -1139,6 +1264,27 @@ void icx_scaled_dims(int32_t width, int32_t height, double scale, int32_t* out_w
 }
 
 int32_t icx_jpeg_header_size(int32_t fmt) { return fmt == ICX_GRAY8 ? HDR_GRAY : HDR_COLOR; }
+
+int32_t icx_default_palette(int32_t binary, uint32_t pal[256])
+{
+    if (!pal) return 0;
+    return default_palette(binary != 0, pal);
+}
+
+void icx_inverse_colour_map(const uint32_t* pal, int32_t n, uint8_t cube[32768])
+{
+    if (!pal || !cube || n < 1 || n > 256) return;
+    const std::vector<uint8_t> c = inverse_cube(pal, n);
+    memcpy(cube, c.data(), c.size());
+}
+
+void icx_dither_tables(int8_t err[3][64])
+{
+    if (!err) return;
+    int8_t d[3][64];
+    dither_tables(d);
+    memcpy(err, d, sizeof(d));
+}
 
 int32_t icx_jpeg_header_size_layout(int32_t fmt, int32_t layout)
 {
@@ -1246,6 +1392,32 @@ static int64_t touched(int sw, int dw, int64_t x0l, int64_t dxl)
     return n;
 }
 
+// A palette raster's resize arguments: its colour map (padded to 256 entries
+// with opaque black) copied into the workspace, and the inverse map of the
+// destination type's default map (built and uploaded at first use).
+static hipError_t palette_args(icx_ctx* c, const icx_image& img, ResizeArgs& a)
+{
+    if (!is_palette(img.fmt)) return hipSuccess;
+    const int b = img.fmt == ICX_BINARY1;
+    hipError_t e = hipSuccess;
+    if (!c->d_inv[b]) {
+        uint32_t pal[256];
+        const int n = default_palette(b, pal);
+        const std::vector<uint8_t> cube = inverse_cube(pal, n);
+        c->inv_prims[b] = represents_primaries(pal, cube);
+        if ((e = hipMalloc(&c->d_inv[b], cube.size())) != hipSuccess) return e;
+        if ((e = hipMemcpy(c->d_inv[b], cube.data(), cube.size(), hipMemcpyHostToDevice)) != hipSuccess) return e;
+    }
+    uint32_t pal[256];
+    for (int i = 0; i < 256; i++) pal[i] = i < img.palette_len ? img.palette[i] : 0xff000000u;
+    uint32_t* dp = (uint32_t*)c->dev.take(sizeof(pal));
+    if ((e = hipMemcpy(dp, pal, sizeof(pal), hipMemcpyHostToDevice)) != hipSuccess) return e;
+    a.pal = dp;
+    a.inv = c->d_inv[b];
+    a.prims = c->inv_prims[b];
+    return hipSuccess;
+}
+
 icx_status icx_resize_bilinear(icx_ctx* ctx, const icx_image* src, uint8_t* dst, int32_t dst_w, int32_t dst_h,
                                int32_t dst_stride)
 {
@@ -1257,7 +1429,7 @@ icx_status icx_resize_bilinear(icx_ctx* ctx, const icx_image* src, uint8_t* dst,
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     hipSetDevice(ctx->device);
     const bool din = is_device_ptr(src->px), dout = is_device_ptr(dst);
-    size_t need = 1 << 20;
+    size_t need = (1 << 20) + 2048;
     if (!din) need += (size_t)src->width * nch * src->height + 256;
     if (!dout) need += (size_t)dst_stride * dst_h + 256;
     hipError_t e = ctx->dev.reserve(need);
@@ -1275,14 +1447,14 @@ icx_status icx_resize_bilinear(icx_ctx* ctx, const icx_image* src, uint8_t* dst,
     }
     uint8_t* d = dout ? dst : (uint8_t*)ctx->dev.take((size_t)dst_stride * dst_h);
     {
-        if (ctx->prof) {
-            const ResizeArgs a = resize_args(s, src->width, src->height, sstride, src->fmt, d, dst_w, dst_h, dst_stride);
+        ResizeArgs a = resize_args(s, src->width, src->height, sstride, src->fmt, d, dst_w, dst_h, dst_stride);
+        if ((e = palette_args(ctx, *src, a)) != hipSuccess) return hip_fail(ctx, e, "resize palette");
+        if (ctx->prof)
             ctx->stats["resize.bytes"].units += (touched(src->width, dst_w, a.x0l, a.dxl) *
                                                      touched(src->height, dst_h, a.y0l, a.dyl) +
                                                  (int64_t)dst_w * dst_h) * nch;
-        }
         Timed tm(ctx, "resize", (int64_t)dst_w * dst_h, true);
-        launch_resize(s, src->width, src->height, sstride, src->fmt, d, dst_w, dst_h, dst_stride, ctx->stream);
+        launch_resize_one(a, ctx->stream);
     }
     if (!dout) {
         e = hipMemcpyAsync(dst, d, (size_t)dst_stride * dst_h, hipMemcpyDeviceToHost, ctx->stream);
@@ -1374,7 +1546,7 @@ icx_status icx_png_fit_batch(icx_ctx* ctx, icx_png_fit_job* jobs, int32_t n)
         while (pos < todo.size() && jobs[todo[pos]].src.fmt == fmt) {
             const icx_png_fit_job& j = jobs[todo[pos]];
             const size_t nch = channels(fmt);
-            size_t per = 4096;
+            size_t per = 4096 + 2048;
             if (!is_device_ptr(j.src.px)) per += (size_t)j.src.width * j.src.height * nch + 256;
             if (!is_device_ptr(j.dst)) per += (size_t)j.out_w * j.out_h * nch + 256;
             if (!grp.empty() && need + per > ctx->budget) break;
@@ -1408,6 +1580,7 @@ icx_status icx_png_fit_batch(icx_ctx* ctx, icx_png_fit_job* jobs, int32_t n)
             uint8_t* dp = j.dst;
             if (!is_device_ptr(dp)) dp = dl[k] = (uint8_t*)ctx->dev.take((size_t)j.out_w * j.out_h * nch);
             args[k] = resize_args(sp, j.src.width, j.src.height, sstride, fmt, dp, j.out_w, j.out_h, j.out_w * nch);
+            if (e == hipSuccess) e = palette_args(ctx, j.src, args[k]);
             const int64_t tiles = resize_tiles(j.out_w, j.out_h);
             prefix[k + 1] = prefix[k] + tiles;
             uniform = uniform < 0 || uniform == tiles ? tiles : 0;

@@ -14,8 +14,10 @@ LIB_PATH = os.environ.get("ICX_LIB") or os.path.join(os.path.dirname(_HERE), "li
 OK, E_INVALID, E_NOMEM, E_DEVICE, E_BUFFER, E_UNSUPPORTED, E_CORRUPT, E_NULL = range(8)
 # icx_fmt (XRGB32/ARGB32: TYPE_INT_RGB/ARGB int rasters, ABGR32: TYPE_4BYTE_ABGR, RGBA32: PNG order,
 # GRAY16: TYPE_USHORT_GRAY, uint16 samples)
-BGR24, RGB24, GRAY8, XRGB32, ARGB32, ABGR32, RGBA32, GRAY16 = range(8)
-CHANNELS = {BGR24: 3, RGB24: 3, GRAY8: 1, XRGB32: 4, ARGB32: 4, ABGR32: 4, RGBA32: 4, GRAY16: 1}
+# INDEXED8 / BINARY1: TYPE_BYTE_INDEXED / TYPE_BYTE_BINARY, one colour-map index per byte + Image.palette
+BGR24, RGB24, GRAY8, XRGB32, ARGB32, ABGR32, RGBA32, GRAY16, INDEXED8, BINARY1 = range(10)
+CHANNELS = {BGR24: 3, RGB24: 3, GRAY8: 1, XRGB32: 4, ARGB32: 4, ABGR32: 4, RGBA32: 4, GRAY16: 1, INDEXED8: 1,
+            BINARY1: 1}
 BYTES_PER_PX = {**CHANNELS, GRAY16: 2}
 # icx_set_table_layout: one DQT/DHT segment per table (623 B header) / all in one (607 B)
 TABLES_SEPARATE, TABLES_GROUPED = 0, 1
@@ -23,7 +25,8 @@ TABLES_SEPARATE, TABLES_GROUPED = 0, 1
 EXPORTS = [
     "icx_abi_version", "icx_create", "icx_destroy", "icx_status_string", "icx_last_error",
     "icx_quality_tables", "icx_create_key", "icx_subsampling_factor", "icx_scaled_dims",
-    "icx_jpeg_header_size", "icx_jpeg_header_size_layout", "icx_set_table_layout", "icx_compress_jpg_to_stream", "icx_find_best_quality",
+    "icx_jpeg_header_size", "icx_jpeg_header_size_layout", "icx_default_palette", "icx_inverse_colour_map",
+    "icx_dither_tables", "icx_set_table_layout", "icx_compress_jpg_to_stream", "icx_find_best_quality",
     "icx_compress_jpg_with_target_size", "icx_compress_jpg_batch", "icx_resize_image",
     "icx_resize_bilinear", "icx_png_fit", "icx_num_blocks", "icx_debug_fdct",
     "icx_profile_enable", "icx_profile_reset", "icx_profile_query",
@@ -48,7 +51,8 @@ class IcxError(RuntimeError):
 
 class Image(ctypes.Structure):
     _fields_ = [("px", ctypes.c_void_p), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
-                ("stride", ctypes.c_int32), ("fmt", ctypes.c_int32)]
+                ("stride", ctypes.c_int32), ("fmt", ctypes.c_int32),
+                ("palette", ctypes.c_void_p), ("palette_len", ctypes.c_int32)]
 
 
 class LearnedParams(ctypes.Structure):
@@ -112,6 +116,9 @@ def load():
         "icx_scaled_dims": (None, [c.c_int32, c.c_int32, c.c_double, P(c.c_int32), P(c.c_int32)]),
         "icx_jpeg_header_size": (c.c_int32, [c.c_int32]),
         "icx_jpeg_header_size_layout": (c.c_int32, [c.c_int32, c.c_int32]),
+        "icx_default_palette": (c.c_int32, [c.c_int32, P(c.c_uint32)]),
+        "icx_inverse_colour_map": (None, [c.c_void_p, c.c_int32, c.c_void_p]),
+        "icx_dither_tables": (None, [c.c_void_p]),
         "icx_set_table_layout": (c.c_int, [c.c_void_p, c.c_int32]),
         "icx_compress_jpg_to_stream": (c.c_int, [c.c_void_p, P(Image), c.c_float, c.c_void_p, c.c_size_t,
                                                  P(c.c_size_t)]),

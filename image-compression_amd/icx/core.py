@@ -91,10 +91,59 @@ def create_key(image, file_size) -> SimilarityKey:
     return SimilarityKey(w // 100, h // 100, int(file_size) // 102400)
 
 
+class IndexedImage:
+    """A TYPE_BYTE_INDEXED (fmt INDEXED8) or TYPE_BYTE_BINARY (BINARY1) raster:
+    one colour-map index per byte (`indices`, (H, W) uint8; a 1/2/4-bit raster
+    unpacked) and its IndexColorModel (`palette`, 0xAARRGGBB uint32).  How the
+    JDK's PNG reader returns palette PNGs and 1/2/4-bit grey PNGs; the resize
+    keeps the type with the type's DEFAULT map (ImageTools.java:12-17)."""
+
+    def __init__(self, indices, palette, fmt):
+        self.indices = np.ascontiguousarray(indices, dtype=np.uint8)
+        self.palette = np.ascontiguousarray(palette, dtype=np.uint32)
+        if fmt not in (N.INDEXED8, N.BINARY1) or self.indices.ndim != 2:
+            raise ValueError("IndexedImage: (H, W) indices, fmt INDEXED8 or BINARY1")
+        if not 1 <= len(self.palette) <= (16 if fmt == N.BINARY1 else 256):
+            raise ValueError("IndexedImage: palette size")
+        self.fmt = fmt
+
+    @property
+    def shape(self):
+        return self.indices.shape
+
+    @property
+    def ndim(self):
+        return 2
+
+    @property
+    def dtype(self):
+        return self.indices.dtype
+
+    def colours(self) -> np.ndarray:
+        """(H, W, 4) bytes A, R, G, B per pixel (the map applied)."""
+        p = self.palette[np.minimum(self.indices, len(self.palette) - 1)]
+        return np.stack([(p >> s & 255).astype(np.uint8) for s in (24, 16, 8, 0)], -1)
+
+    @classmethod
+    def default(cls, fmt, height, width):
+        """An all-zero raster of `new BufferedImage(width, height, type)`."""
+        return cls(np.zeros((height, width), np.uint8), default_palette(fmt == N.BINARY1), fmt)
+
+
+def default_palette(binary: bool) -> np.ndarray:
+    """The colour map of a new TYPE_BYTE_INDEXED (256 entries: 6x6x6 cube +
+    grey ramp) or TYPE_BYTE_BINARY (black, white) BufferedImage."""
+    pal = (ctypes.c_uint32 * 256)()
+    n = N.load().icx_default_palette(1 if binary else 0, pal)
+    return np.array(pal[:n], dtype=np.uint32)
+
+
 def _fmt_of(img):
     """The BufferedImage type of an array: (H, W) grey = TYPE_BYTE_GRAY,
     (H, W, 3) = TYPE_3BYTE_BGR, (H, W, 4) = TYPE_4BYTE_ABGR (bytes A, B, G, R:
     how ImageIO reads an RGBA PNG).  Other layouts: pass fmt explicitly."""
+    if isinstance(img, IndexedImage):
+        return img.fmt
     if img.ndim == 2 and str(getattr(img, "dtype", "")) in ("uint16", "torch.uint16", "torch.int16"):
         return N.GRAY16  # TYPE_USHORT_GRAY
     if img.ndim == 2 or (img.ndim == 3 and img.shape[2] == 1):
@@ -113,6 +162,18 @@ def _out_shape(h, w, fmt):
 
 def _out_dtype(fmt):
     return np.uint16 if fmt == N.GRAY16 else np.uint8
+
+
+def _new_raster(h, w, fmt):
+    """The destination of a resize: an array of the source's type, or for a
+    palette type a new raster with that type's default colour map."""
+    if fmt in (N.INDEXED8, N.BINARY1):
+        return IndexedImage(np.empty((h, w), np.uint8), default_palette(fmt == N.BINARY1), fmt)
+    return np.empty(_out_shape(h, w, fmt), _out_dtype(fmt))
+
+
+def _pixels(raster):
+    return raster.indices if isinstance(raster, IndexedImage) else raster
 
 
 class DeviceImage:
@@ -221,6 +282,13 @@ def _image_struct(img, fmt=None):
         fmt = _fmt_of(img)
     h, w = int(img.shape[0]), int(img.shape[1])
     bpp = N.BYTES_PER_PX[fmt]
+    if isinstance(img, IndexedImage):
+        if fmt != img.fmt:
+            raise ValueError("an IndexedImage keeps its own format")
+        return N.Image(img.indices.ctypes.data, w, h, img.indices.strides[0], fmt, img.palette.ctypes.data,
+                       len(img.palette)), img
+    if fmt in (N.INDEXED8, N.BINARY1):
+        raise ValueError("palette formats need an IndexedImage (indices + colour map)")
     if getattr(img, "icx_device", False):
         return N.Image(img.data_ptr(), w, h, w * bpp, fmt), img
     if isinstance(img, np.ndarray):
@@ -287,19 +355,21 @@ class Codec:
         w = ctypes.c_int32()
         h = ctypes.c_int32()
         self._lib.icx_scaled_dims(img.width, img.height, float(scale), ctypes.byref(w), ctypes.byref(h))
-        out = np.empty(_out_shape(h.value, w.value, img.fmt), _out_dtype(img.fmt))
+        res = _new_raster(h.value, w.value, img.fmt)
+        out = _pixels(res)
         st = self._lib.icx_resize_image(self._ctx, ctypes.byref(img), float(scale), out.ctypes.data, out.nbytes,
                                         ctypes.byref(w), ctypes.byref(h))
         self._check(st, "icx_resize_image")
-        return out
+        return res
 
     def resize_to(self, original_image, width: int, height: int, fmt=None) -> np.ndarray:
         img, keep = _image_struct(original_image, fmt)
-        out = np.empty(_out_shape(height, width, img.fmt), _out_dtype(img.fmt))
+        res = _new_raster(height, width, img.fmt)
+        out = _pixels(res)
         st = self._lib.icx_resize_bilinear(self._ctx, ctypes.byref(img), out.ctypes.data, width, height,
                                            width * N.BYTES_PER_PX[img.fmt])
         self._check(st, "icx_resize_bilinear")
-        return out
+        return res
 
     # -------------------------------------------------------------- A4
     def compress_jpg_to_stream(self, image, quality: float) -> bytes:
@@ -452,8 +522,8 @@ class Codec:
                 continue
             dw, dh = scaled_dims(img.width, img.height,
                                  min(params.min_width / img.width, params.min_height / img.height))
-            outs[i] = np.empty(_out_shape(dh, dw, img.fmt), _out_dtype(img.fmt))
-            j.dst, j.cap = outs[i].ctypes.data, outs[i].nbytes
+            outs[i] = _new_raster(dh, dw, img.fmt)
+            j.dst, j.cap = _pixels(outs[i]).ctypes.data, _pixels(outs[i]).nbytes
         with self._lock:
             st = self._batch_call("png_fit", jobs, n)
         self._check(st, "icx_png_fit_batch")

@@ -79,21 +79,78 @@ def format_file_size(size: int) -> str:
     return f"{size / 1024 ** g:,.1f}".rstrip("0").rstrip(".") + " " + units[g]
 
 
-def _to_array(im):
+def png_palette_info(path):
+    """(bit depth, colour type, PLTE entries as 0xRRGGBB, tRNS bytes or None)
+    of a PNG file, from its chunks before the first IDAT; None if not a PNG."""
+    import struct
+    with open(path, "rb") as f:
+        if f.read(8) != b"\x89PNG\r\n\x1a\n":
+            return None
+        depth = ctype = None
+        plte, trns = [], None
+        while True:
+            head = f.read(8)
+            if len(head) < 8:
+                break
+            n, tag = struct.unpack(">I4s", head)
+            if tag == b"IDAT" or tag == b"IEND":
+                break
+            body = f.read(n)
+            f.read(4)
+            if tag == b"IHDR":
+                depth, ctype = body[8], body[9]
+            elif tag == b"PLTE":
+                plte = [(body[3 * i] << 16) | (body[3 * i + 1] << 8) | body[3 * i + 2] for i in range(n // 3)]
+            elif tag == b"tRNS":
+                trns = body
+    return depth, ctype, plte, trns
+
+
+def _indexed_raster(im, path):
+    """The JDK PNG reader's raster for a palette PNG (colour type 3) or a
+    1/2/4-bit grey PNG, else None (PNGImageReader.getImageTypes):
+      - palette, 8 bits -> TYPE_BYTE_INDEXED; 1/2/4 bits -> TYPE_BYTE_BINARY;
+        the IndexColorModel is PLTE padded to 2^depth entries with its last
+        entry, alphas = tRNS padded with 255 (none without tRNS);
+      - grey 1/2/4 bits -> TYPE_BYTE_BINARY with the ramp i * 255 / (2^depth - 1)."""
+    from .core import IndexedImage
+    info = png_palette_info(path)
+    if info is None:
+        return None
+    depth, ctype, plte, trns = info
+    if ctype == 3 and plte:
+        n = 1 << depth
+        rgb = [plte[i] if i < len(plte) else plte[-1] for i in range(n)]
+        alpha = [trns[i] if trns is not None and i < len(trns) else 255 for i in range(n)]
+        pal = np.array([(a << 24) | c for a, c in zip(alpha, rgb)], np.uint32)
+        idx = np.asarray(im.convert("P") if im.mode != "P" else im, dtype=np.uint8)
+        return IndexedImage(idx, pal, N.INDEXED8 if depth == 8 else N.BINARY1)
+    if ctype == 0 and depth in (1, 2, 4):
+        n = 1 << depth
+        pal = np.array([0xff000000 | (i * 255 // (n - 1)) * 0x010101 for i in range(n)], np.uint32)
+        grey = np.asarray(im.convert("L") if im.mode == "1" else im, dtype=np.uint8)
+        return IndexedImage((grey.astype(np.uint16) * (n - 1) // 255).astype(np.uint8), pal, N.BINARY1)
+    return None
+
+
+def _to_array(im, path=None):
     """Decoded raster as the BufferedImage type the JDK reader returns:
     TYPE_BYTE_GRAY (H, W), TYPE_USHORT_GRAY (H, W) uint16 for a 16-bit grey
     PNG, TYPE_3BYTE_BGR (H, W, 3) or, with an alpha channel, TYPE_4BYTE_ABGR
-    (H, W, 4) - ImageTools.resizeImage keeps that type and the PNG is written
-    back with it (ImageTools.java:12-15)."""
+    (H, W, 4), and for palette PNGs and 1/2/4-bit grey PNGs an IndexedImage
+    (TYPE_BYTE_INDEXED / TYPE_BYTE_BINARY) - ImageTools.resizeImage keeps that
+    type and the PNG is written back with it (ImageTools.java:12-15)."""
+    if path is not None and im.format == "PNG":
+        r = _indexed_raster(im, path)
+        if r is not None:  # TYPE_BYTE_INDEXED / TYPE_BYTE_BINARY (kept by ImageTools, DESIGN.md §11)
+            return r
     mode = im.mode
     if mode == "L":
         return np.asarray(im, dtype=np.uint8)
     if mode in ("I;16", "I;16B", "I;16L") or (mode == "I" and im.format == "PNG"):
         # 16-bit grey PNG (Pillow: I;16, or I in older versions): TYPE_USHORT_GRAY
         return np.ascontiguousarray(np.asarray(im).astype(np.uint16))
-    if mode in ("I", "F", "1"):
-        # 1-bit PNGs are TYPE_BYTE_BINARY in the JDK (re-thresholded by Java2D
-        # after the resize); here 8-bit grey, an approximation (DESIGN.md §11)
+    if mode in ("I", "F", "1"):  # (a 1-bit PNG is an IndexedImage, above)
         return np.asarray(im.convert("L"), dtype=np.uint8)
     if mode in ("LA", "PA"):
         # grey+alpha is TYPE_CUSTOM there, drawn into TYPE_INT_ARGB: RGBA out
@@ -101,12 +158,7 @@ def _to_array(im):
         mode, im = "RGBA", im.convert("RGBA")
     if mode == "RGBA":
         return np.ascontiguousarray(np.asarray(im, dtype=np.uint8)[:, :, ::-1])  # TYPE_4BYTE_ABGR
-    if mode != "RGB":
-        # CMYK, and palette PNGs with or without tRNS: the JDK reads a palette
-        # PNG as TYPE_BYTE_INDEXED (TYPE_BYTE_BINARY below 8 bits) and
-        # ImageTools keeps that type, so Java2D re-quantises the resized pixels
-        # to the default colour-cube palette of a new TYPE_BYTE_INDEXED image,
-        # whose transparency is lost.  Here: RGB, an approximation
+    if mode != "RGB":  # CMYK, and palette images of other formats (GIF, BMP: not the PNG path)
         im = im.convert("RGB")
     rgb = np.asarray(im, dtype=np.uint8)
     return np.ascontiguousarray(rgb[:, :, ::-1])  # TYPE_3BYTE_BGR
@@ -169,10 +221,14 @@ def decode_image_with_subsampling(input_path, params: CompressionParams, file_si
                       params.min_width, params.min_height)
             return None
         s = subsampling_factor(width, height)
-        arr = _to_array(im)
+        arr = _to_array(im, input_path)
     if s > 1:  # ImageReadParam.setSourceSubsampling(s, s, 0, 0): keep pixels (x*s, y*s)
         log.debug("%s - 對圖片應用二次取樣，比率: %d", os.path.basename(str(input_path)), s)
-        arr = np.ascontiguousarray(arr[::s, ::s])
+        from .core import IndexedImage
+        if isinstance(arr, IndexedImage):
+            arr = IndexedImage(arr.indices[::s, ::s], arr.palette, arr.fmt)
+        else:
+            arr = np.ascontiguousarray(arr[::s, ::s])
     return DecodedImage(arr, fmt, width, height, s)
 
 

@@ -18,11 +18,13 @@ from . import _native as N
 
 def encode_png(img, fmt=None, level: int = -1) -> bytes:
     """img: host (H, W) grey, (H, W, 3) BGR or (H, W, 4) ABGR uint8 array,
-    (H, W) uint16 grey (TYPE_USHORT_GRAY, a 16-bit PNG), or another icx_fmt
+    (H, W) uint16 grey (TYPE_USHORT_GRAY, a 16-bit PNG), an IndexedImage
+    (TYPE_BYTE_INDEXED / TYPE_BYTE_BINARY: a palette or 1-bit grey PNG, as
+    PNGMetadata.initialize picks for its colour map), or another icx_fmt
     given explicitly -> PNG file bytes.  level -1 = PNGImageWriter's default."""
-    from .core import _image_struct
+    from .core import IndexedImage, _image_struct
     lib = N.load()
-    im, keep = _image_struct(np.ascontiguousarray(img), fmt)
+    im, keep = _image_struct(img if isinstance(img, IndexedImage) else np.ascontiguousarray(img), fmt)
     cap = lib.icx_png_bound(ctypes.byref(im))
     if cap == 0:
         raise N.IcxError(N.E_UNSUPPORTED, "image too large for one IDAT chunk")

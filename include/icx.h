@@ -34,7 +34,7 @@ extern "C" {
 #endif
 
 #define ICX_ABI_VERSION 4  /* 2: four-byte pixel formats, icx_png_encode; 3: ICX_GRAY16, icx_png_fit_batch;
-                              4: icx_set_table_layout */
+                              4: icx_set_table_layout, ICX_INDEXED8 / ICX_BINARY1 (icx_image.palette) */
 
 typedef struct icx_ctx icx_ctx;
 
@@ -65,7 +65,15 @@ typedef enum icx_status {
  * native-endian uint16 samples, rows and px 2-byte aligned; resize / PNG
  * entry points only.  Java2D's bilinear loops carry it through 8-bit
  * IntArgbPre (UshortGray.h: the high byte in, gray * 257 out), and so does
- * icx_resize_image; icx_png_encode writes it as a 16-bit grey PNG. */
+ * icx_resize_image; icx_png_encode writes it as a 16-bit grey PNG.
+ * ICX_INDEXED8 is TYPE_BYTE_INDEXED (an 8-bit palette PNG as the JDK reads
+ * it) and ICX_BINARY1 TYPE_BYTE_BINARY (a 1/2/4-bit palette or grey PNG):
+ * one colour-map index per byte (a packed raster unpacked), the colour map in
+ * icx_image.palette (0xAARRGGBB, palette_len entries; <= 256, <= 16 for
+ * BINARY1).  ImageTools.resizeImage keeps the type, so the resized image gets
+ * Java2D's DEFAULT map of a new BufferedImage of that type (INDEXED8: the
+ * 6x6x6 cube + grey ramp of icx_default_palette, dithered; BINARY1: black /
+ * white): resize and PNG entry points only. */
 typedef enum icx_fmt {
     ICX_BGR24 = 0,
     ICX_RGB24 = 1,
@@ -74,7 +82,9 @@ typedef enum icx_fmt {
     ICX_ARGB32 = 4,
     ICX_ABGR32 = 5,
     ICX_RGBA32 = 6,
-    ICX_GRAY16 = 7
+    ICX_GRAY16 = 7,
+    ICX_INDEXED8 = 8,
+    ICX_BINARY1 = 9
 } icx_fmt;
 
 /* A decoded image (BufferedImage).  stride in bytes. */
@@ -84,7 +94,20 @@ typedef struct icx_image {
     int32_t height;
     int32_t stride;
     int32_t fmt; /* icx_fmt */
+    const uint32_t* palette; /* ICX_INDEXED8 / ICX_BINARY1: host colour map (0xAARRGGBB), else ignored */
+    int32_t palette_len;
 } icx_image;
+
+/* The colour map of `new BufferedImage(w, h, TYPE_BYTE_INDEXED)` (binary = 0:
+ * 256 entries) or TYPE_BYTE_BINARY (binary = 1: 2 entries); returns the
+ * entry count. */
+int32_t icx_default_palette(int32_t binary, uint32_t pal[256]);
+/* What Java2D derives from a colour map for storing into it: the inverse map
+ * of 32x32x32 cells (AWT initCubemap, index = (r>>3)<<10 | (g>>3)<<5 | b>>3)
+ * and the ordered-dither error tables of a 256-entry map
+ * (make_dither_arrays: red, green, blue, [(y & 7) * 8 + (x & 7)]). */
+void icx_inverse_colour_map(const uint32_t* pal, int32_t n, uint8_t cube[32768]);
+void icx_dither_tables(int8_t err[3][64]);
 
 /* learn/LearnedParams.java:8  record LearnedParams(float quality, double scale) */
 typedef struct icx_learned_params {

@@ -844,6 +844,203 @@ int oracle_resize(const uint8_t* src, int sw, int sh, int sstride, int fmt, uint
 }
 
 /* ------------------------------------------------------------------ */
+/* A12, palette rasters (ImageTools.java:12-17 keeps TYPE_BYTE_INDEXED / */
+/* TYPE_BYTE_BINARY, so `new BufferedImage(nw, nh, type)` gets Java2D's   */
+/* DEFAULT colour map, not the source's).  Restated from the published    */
+/* OpenJDK java.desktop sources, no JDK here to pin them (parity unpinned):*/
+/*  - BufferedImage(TYPE_BYTE_INDEXED): a 6x6x6 cube at 0, 51, ..., 255   */
+/*    (r outer, b inner), then a grey ramp 18, 24, ..., 252 (256/40 = 6); */
+/*    TYPE_BYTE_BINARY: {black, white}, 1 bit.                            */
+/*  - the source is fetched as IntArgbPre through its own colour map      */
+/*    (CopyByteIndexedToIntArgbPre: alpha 0 -> 0, else mul8 premultiply), */
+/*    the taps interpolated as for the four-byte formats, and the alpha   */
+/*    mask blit (SrcOver) composes onto the new image's pixel 0 = opaque  */
+/*    black: the result is the premultiplied colour, alpha 255;           */
+/*  - ByteIndexed store (StoreByteIndexedFrom3ByteRgb): unless r, g, b are */
+/*    each 0 or 255 and the map "represents primaries", the 8x8 ordered   */
+/*    dither errors (make_dither_arrays: make_sgn_ordered_dither_array    */
+/*    over [-20, 20) for a 256-entry map, green mirrored horizontally,    */
+/*    blue vertically) are added at (x & 7, y & 7), components clamped,   */
+/*    then the inverse colour map of 32x32x32 cells (initCubemap: an L1   */
+/*    flood fill from the map's entries, inserted 0, n-1, 1, n-2, ...,    */
+/*    level by level, first claim wins) gives the index;                  */
+/*  - ByteBinary1Bit store: the inverse map alone, no dither.             */
+/* ------------------------------------------------------------------ */
+void oracle_default_palette(int binary, uint32_t pal[256], int* n)
+{
+    if (binary) {
+        pal[0] = 0xff000000u;
+        pal[1] = 0xffffffffu;
+        *n = 2;
+        return;
+    }
+    int i = 0;
+    for (int r = 0; r < 256; r += 51)
+        for (int g = 0; g < 256; g += 51)
+            for (int b = 0; b < 256; b += 51) pal[i++] = 0xff000000u | (uint32_t)(r << 16) | (uint32_t)(g << 8) | (uint32_t)b;
+    const int incr = 256 / (256 - i);
+    for (int gray = incr * 3; i < 256; i++, gray += incr)
+        pal[i] = 0xff000000u | (uint32_t)(gray << 16) | (uint32_t)(gray << 8) | (uint32_t)gray;
+    *n = 256;
+}
+
+static int cube_insert(uint8_t* used, uint8_t* lut, uint16_t* list, uint8_t* idx, int n, int rgb, int index)
+{
+    if (used[rgb]) return n;
+    used[rgb] = 1;
+    lut[rgb] = (uint8_t)index;
+    list[n] = (uint16_t)rgb;
+    idx[n] = (uint8_t)index;
+    return n + 1;
+}
+
+void oracle_inverse_cube(const uint32_t* cmap, int n, uint8_t cube[32768])
+{
+    uint8_t* used = (uint8_t*)calloc(32768, 1);
+    uint16_t* cur = (uint16_t*)malloc(32768 * 2 * sizeof(uint16_t));
+    uint8_t* cidx = (uint8_t*)malloc(32768 * 2);
+    uint16_t* nxt = cur + 32768;
+    uint8_t* nidx = cidx + 32768;
+    int nc = 0;
+    const int mid = (n >> 1) + (n & 1);
+    for (int i = 0; i < mid; i++) {
+        const int k[2] = {i, n - i - 1};
+        for (int e = 0; e < 2; e++) {
+            const uint32_t px = cmap[k[e]];
+            const int rgb = (int)(((px & 0x00f80000u) >> 9) | ((px & 0x0000f800u) >> 6) | ((px & 0xf8u) >> 3));
+            nc = cube_insert(used, cube, cur, cidx, nc, rgb, k[e]);
+        }
+    }
+    static const int mask[3] = {0x7c00, 0x03e0, 0x001f}, delta[3] = {0x0400, 0x0020, 0x0001};
+    while (nc) {
+        int nn = 0;
+        for (int i = 0; i < nc; i++) {
+            const int rgb = cur[i], index = cidx[i];
+            for (int a = 0; a < 3; a++) {
+                if ((rgb & mask[a]) + delta[a] <= mask[a]) nn = cube_insert(used, cube, nxt, nidx, nn, rgb + delta[a], index);
+                if ((rgb & mask[a]) >= delta[a]) nn = cube_insert(used, cube, nxt, nidx, nn, rgb - delta[a], index);
+            }
+        }
+        memcpy(cur, nxt, (size_t)nn * sizeof(uint16_t));
+        memcpy(cidx, nidx, (size_t)nn);
+        nc = nn;
+    }
+    free(used);
+    free(cur);
+    free(cidx);
+}
+
+/* the three 8x8 dither error tables, [(y & 7) * 8 + (x & 7)] */
+void oracle_dither_tables(int cmapsize, int8_t red[64], int8_t green[64], int8_t blue[64])
+{
+    const int e = (int)(256 / pow(cmapsize, 1.0 / 3.0));
+    const int lo = -e / 2, hi = e - e / 2;
+    int oda[64];
+    oda[0] = 0;
+    for (int k = 1; k < 8; k *= 2)
+        for (int i = 0; i < k; i++)
+            for (int j = 0; j < k; j++) {
+                oda[i * 8 + j] = oda[i * 8 + j] * 4;
+                oda[(i + k) * 8 + (j + k)] = oda[i * 8 + j] + 1;
+                oda[i * 8 + (j + k)] = oda[i * 8 + j] + 2;
+                oda[(i + k) * 8 + j] = oda[i * 8 + j] + 3;
+            }
+    for (int i = 0; i < 64; i++) red[i] = green[i] = blue[i] = (int8_t)(oda[i] * (hi - lo) / 64 + lo);
+    for (int i = 0; i < 8; i++)
+        for (int j = 0; j < 4; j++) {
+            int8_t t = green[i * 8 + j];
+            green[i * 8 + j] = green[i * 8 + 7 - j];
+            green[i * 8 + 7 - j] = t;
+            t = blue[j * 8 + i];
+            blue[j * 8 + i] = blue[(7 - j) * 8 + i];
+            blue[(7 - j) * 8 + i] = t;
+        }
+}
+
+/* BufImgSurfaceData.c calculatePrimaryColorsApproximation: every corner cell
+ * of the inverse map holds a colour within 5 of that corner's primary */
+static int represents_primaries(const uint32_t* cmap, const uint8_t* cube)
+{
+    for (int i = 0; i < 32; i += 31)
+        for (int j = 0; j < 32; j += 31)
+            for (int k = 0; k < 32; k += 31) {
+                const uint32_t c = cmap[cube[(i << 10) | (j << 5) | k]];
+                const int r = (c >> 16) & 255, g = (c >> 8) & 255, b = c & 255;
+                const int er = i ? 255 : 0, eg = j ? 255 : 0, eb = k ? 255 : 0;
+                if (abs(r - er) > 5 || abs(g - eg) > 5 || abs(b - eb) > 5) return 0;
+            }
+    return 1;
+}
+
+static inline int clamp_byte(int c) { return (c >> 8) ? (~(c >> 31)) & 255 : c; }
+
+int oracle_resize_indexed(const uint8_t* src, int sw, int sh, int sstride, const uint32_t* pal, int binary,
+                          uint8_t* dst, int dw, int dh, int dstride)
+{
+    if (sw <= 0 || sh <= 0 || dw <= 0 || dh <= 0 || !src || !dst || !pal) return 1;
+    uint32_t dpal[256];
+    int dn;
+    oracle_default_palette(binary, dpal, &dn);
+    uint8_t* cube = (uint8_t*)malloc(32768);
+    if (!cube) return 2;
+    oracle_inverse_cube(dpal, dn, cube);
+    int8_t er[64], eg[64], eb[64];
+    oracle_dither_tables(256, er, eg, eb);
+    const int prims = represents_primaries(dpal, cube);
+    double ix = 1.0 / ((double)dw / sw), iy = 1.0 / ((double)dh / sh);
+    int64_t dxl = dbl_to_long(ix), dyl = dbl_to_long(iy);
+    int64_t x0l = dbl_to_long(0.5 * ix), y0l = dbl_to_long(0.5 * iy);
+    const int64_t half = (int64_t)1 << 31;
+    for (int dy = 0; dy < dh; dy++) {
+        int64_t yl = y0l + (int64_t)dy * dyl - half;
+        int yw = (int)(yl >> 32), yf = (int)((uint32_t)yl >> 24), ya, yb;
+        if (yw < 0) ya = yb = 0;
+        else if (yw + 1 >= sh) ya = yb = yw;
+        else { ya = yw; yb = yw + 1; }
+        for (int dx = 0; dx < dw; dx++) {
+            int64_t xl = x0l + (int64_t)dx * dxl - half;
+            int xw = (int)(xl >> 32), xf = (int)((uint32_t)xl >> 24), xa, xb;
+            if (xw < 0) xa = xb = 0;
+            else if (xw + 1 >= sw) xa = xb = xw;
+            else { xa = xw; xb = xw + 1; }
+            const uint32_t q[4] = {pal[src[(size_t)ya * sstride + xa]], pal[src[(size_t)ya * sstride + xb]],
+                                   pal[src[(size_t)yb * sstride + xa]], pal[src[(size_t)yb * sstride + xb]]};
+            int pre[4][4];  /* [tap][b, g, r, a] */
+            for (int s = 0; s < 4; s++) {
+                const int a = (int)(q[s] >> 24);
+                for (int b = 0; b < 3; b++) pre[s][b] = mul8(a, (int)(q[s] >> (8 * b)) & 255);
+                pre[s][3] = a;
+            }
+            int v[3];
+            for (int b = 0; b < 3; b++) {
+                int top = (pre[0][b] << 8) + (pre[1][b] - pre[0][b]) * xf;
+                int bot = (pre[2][b] << 8) + (pre[3][b] - pre[2][b]) * xf;
+                v[b] = (((top << 8) + (bot - top) * yf) + (1 << 15)) >> 16;
+            }
+            /* SrcOver onto opaque black: the premultiplied colour */
+            int r = v[2], g = v[1], b = v[0];
+            if (!binary) {
+                const int prim = (r == 0 || r == 255) && (g == 0 || g == 255) && (b == 0 || b == 255) && prims;
+                if (!prim) {
+                    const int e = (dy & 7) * 8 + (dx & 7);
+                    r += er[e];
+                    g += eg[e];
+                    b += eb[e];
+                }
+                if ((r | g | b) >> 8) {
+                    r = clamp_byte(r);
+                    g = clamp_byte(g);
+                    b = clamp_byte(b);
+                }
+            }
+            dst[(size_t)dy * dstride + dx] = cube[((r >> 3) << 10) | ((g >> 3) << 5) | (b >> 3)];
+        }
+    }
+    free(cube);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
 /* A2 + A4: compressJpgWithTargetSize / tryCachedParams                */
 /* ------------------------------------------------------------------ */
 int oracle_compress_jpg_with_target_size(const uint8_t* px, int w, int h, int stride, int fmt,

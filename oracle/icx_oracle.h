@@ -67,6 +67,18 @@ float oracle_find_best_quality(const uint8_t* px, int w, int h, int stride, int 
 /* A12: bilinear resize (Java2D TransformHelper fixed-point semantics). */
 int oracle_resize(const uint8_t* src, int sw, int sh, int sstride, int fmt,
                   uint8_t* dst, int dw, int dh, int dstride);
+/* A12 for TYPE_BYTE_INDEXED / TYPE_BYTE_BINARY sources: src = one palette
+ * index per byte (a 1/2/4-bit raster unpacked), pal = its colour map
+ * (0xAARRGGBB).  dst = one index per byte into the DEFAULT map of a new
+ * BufferedImage of that type (oracle_default_palette: binary 0 -> the 6x6x6
+ * cube + grey ramp, 1 -> black/white), dithered as Java2D's ByteIndexed
+ * store does (binary: no dither).  Parity unpinned (no JDK). */
+int oracle_resize_indexed(const uint8_t* src, int sw, int sh, int sstride, const uint32_t* pal, int binary,
+                          uint8_t* dst, int dw, int dh, int dstride);
+void oracle_default_palette(int binary, uint32_t pal[256], int* n);
+void oracle_inverse_cube(const uint32_t* cmap, int n, uint8_t cube[32768]);
+void oracle_dither_tables(int cmapsize, int8_t red[64], int8_t green[64], int8_t blue[64]);
+
 /* (int)(w*scale) clamped to >= 1, per ImageTools.java:8-9 */
 void oracle_scaled_dims(int w, int h, double scale, int* dw, int* dh);
 

@@ -59,6 +59,11 @@ class Oracle:
         L.oracle_jpeg_decode.argtypes = [c.c_void_p, c.c_size_t, c.c_int, c.c_void_p, c.c_size_t, P(c.c_int),
                                          P(c.c_int), P(c.c_int)]
         L.oracle_set_table_layout.argtypes = [c.c_int]
+        L.oracle_resize_indexed.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_void_p,
+                                            c.c_int, c.c_int, c.c_int]
+        L.oracle_default_palette.argtypes = [c.c_int, c.c_void_p, P(c.c_int)]
+        L.oracle_inverse_cube.argtypes = [c.c_void_p, c.c_int, c.c_void_p]
+        L.oracle_dither_tables.argtypes = [c.c_int, c.c_void_p, c.c_void_p, c.c_void_p]
         self.L = L
 
     def set_table_layout(self, grouped):
@@ -117,6 +122,26 @@ class Oracle:
         out = np.empty((dh, dw, nch) if nch > 1 else (dh, dw), img.dtype)
         self.L.oracle_resize(img.ctypes.data, w, h, img.strides[0], fmt, out.ctypes.data, dw, dh,
                              dw * nch * img.itemsize)
+        return out
+
+    def default_palette(self, binary):
+        pal = np.zeros(256, np.uint32)
+        n = ctypes.c_int()
+        self.L.oracle_default_palette(1 if binary else 0, pal.ctypes.data, ctypes.byref(n))
+        return pal[:n.value].copy()
+
+    def resize_indexed(self, indices, palette, binary, dw, dh):
+        """TYPE_BYTE_INDEXED (binary 0) / TYPE_BYTE_BINARY (1) resize: source
+        indices + colour map -> indices into the type's default map."""
+        src = np.ascontiguousarray(indices, np.uint8)
+        pal = np.full(256, 0xff000000, np.uint32)
+        p = np.asarray(palette, np.uint32)
+        pal[:len(p)] = p
+        out = np.empty((dh, dw), np.uint8)
+        h, w = src.shape
+        rc = self.L.oracle_resize_indexed(src.ctypes.data, w, h, src.strides[0], pal.ctypes.data, 1 if binary else 0,
+                                          out.ctypes.data, dw, dh, dw)
+        assert rc == 0, rc
         return out
 
     def fit(self, img, target, q0, cached=None):

@@ -3,7 +3,8 @@ only: lets the host-side batch/cache/sharding logic run in CPU-only CI; the
 product package never uses it."""
 import numpy as np
 
-from icx.core import LearnedParams, image_dims
+from icx import _native as N
+from icx.core import IndexedImage, LearnedParams, default_palette, image_dims
 from tests.oracle_ffi import Oracle
 
 
@@ -42,6 +43,10 @@ class OracleCodec:
             return None
         s = min(params.min_width / w, params.min_height / h)
         dw, dh = self.o.scaled_dims(w, h, s)
+        if isinstance(img, IndexedImage):  # the type kept, with its default colour map
+            binary = img.fmt == N.BINARY1
+            return IndexedImage(self.o.resize_indexed(img.indices, img.palette, binary, dw, dh),
+                                default_palette(binary), img.fmt)
         return self.o.resize(img, dw, dh)  # (H, W, 4) = ABGR, as icx.core._fmt_of
 
     def png_fit_batch(self, images, params):

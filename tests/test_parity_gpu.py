@@ -539,3 +539,45 @@ def test_pool_splits_batches_across_contexts(codec, oracle):
         assert lib.icx_pool_size(pool._pool) == 2
     finally:
         pool.close()
+
+
+def test_palette_resize_matches_restatement(codec, oracle):
+    """TYPE_BYTE_INDEXED / TYPE_BYTE_BINARY rasters (palette PNGs, 1/2/4-bit
+    PNGs) through k_resize: the source's colour map to IntArgbPre, bilinear,
+    SrcOver onto the new image's black, then the default map's inverse cube
+    (dithered for ByteIndexed) - bit-exact against the oracle's restatement,
+    single images and a batched group mixed with other formats, staged and
+    direct tiles.  Parity unpinned vs Java2D (no JDK here; ImageTools.java:12-17)."""
+    from icx.core import IndexedImage
+    rng = np.random.default_rng(77)
+    pal8 = (rng.integers(0, 1 << 24, 256) | (rng.integers(0, 256, 256) << 24)).astype(np.uint32)
+    pal8[:200] |= 0xff000000  # mostly opaque, some translucent / transparent entries
+    cases = []
+    for (h, w) in ((300, 517), (96, 64), (1080, 1920), (37, 1501)):
+        cases.append(IndexedImage(rng.integers(0, 256, (h, w)).astype(np.uint8), pal8, N.INDEXED8))
+        smooth_idx = (np.add.outer(np.arange(h) // 7, np.arange(w) // 5) % 216).astype(np.uint8)
+        cases.append(IndexedImage(smooth_idx, icx.default_palette(False), N.INDEXED8))
+        n = 16
+        pal4 = (0xff000000 | rng.integers(0, 1 << 24, n)).astype(np.uint32)
+        cases.append(IndexedImage(rng.integers(0, n, (h, w)).astype(np.uint8), pal4, N.BINARY1))
+        cases.append(IndexedImage(rng.integers(0, 2, (h, w)).astype(np.uint8), icx.default_palette(True),
+                                  N.BINARY1))
+    for im in cases:
+        for scale in (0.5, 0.37, 0.13):
+            got = codec.resize_image(im, scale)
+            dw, dh = got.shape[1], got.shape[0]
+            want = oracle.resize_indexed(im.indices, im.palette, im.fmt == N.BINARY1, dw, dh)
+            assert isinstance(got, IndexedImage) and got.fmt == im.fmt
+            assert np.array_equal(got.palette, icx.default_palette(im.fmt == N.BINARY1))
+            assert np.array_equal(got.indices, want), (im.shape, im.fmt, scale)
+    params = icx.CompressionParams(0.25, 1 << 20, 200, 150, 1 << 20)
+    mixed = cases + [smooth(300, 517, 5), noise(96, 640, 6)[:, :, 1].copy()]
+    res = codec.png_fit_batch(mixed, params)
+    for im, r in zip(mixed, res):
+        if r is None:
+            continue
+        if isinstance(im, IndexedImage):
+            want = oracle.resize_indexed(im.indices, im.palette, im.fmt == N.BINARY1, r.shape[1], r.shape[0])
+            assert np.array_equal(r.indices, want), (im.shape, im.fmt)
+        else:
+            assert np.array_equal(r, oracle.resize(im, r.shape[1], r.shape[0]))

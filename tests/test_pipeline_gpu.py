@@ -35,6 +35,12 @@ def _make_inputs(d):
     p = d / "pic.png"
     Image.fromarray(smooth(500, 700, 5)[:, :, ::-1]).save(p)
     files.append(str(p))
+    # palette and 1-bit PNGs: TYPE_BYTE_INDEXED / TYPE_BYTE_BINARY kept (IndexedImage)
+    pal = Image.fromarray(smooth(420, 640, 7)[:, :, ::-1]).quantize(200)
+    pal.save(d / "pal.png", transparency=0)
+    files.append(str(d / "pal.png"))
+    Image.fromarray(noise(400, 600, 8)[:, :, 0]).convert("1").save(d / "bits.png")
+    files.append(str(d / "bits.png"))
     files.append(str(d / "missing.jpg"))
     lst = d / "list.txt"
     lst.write_text("\n".join(files))
