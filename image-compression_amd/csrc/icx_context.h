@@ -182,6 +182,9 @@ struct icx_ctx {
     int inv_prims[2] = {0, 0};
     DevPool pool;
     DevPool hpool;  // pinned host buffers (hpool.host = true)
+    // the pools' own lock: host threads reading files into pinned buffers must
+    // not wait for a batch call, which holds `mu` for its whole run
+    std::mutex pool_mu;
     // Host-buffer batches: inputs are uploaded (io_up) into one of two staging
     // arenas while the previous sub-batch computes, outputs leave (io_down)
     // while the next one computes; created on first use.

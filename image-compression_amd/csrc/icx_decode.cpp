@@ -776,18 +776,27 @@ icx_status pool_alloc(icx_ctx* ctx, DevPool& P, size_t bytes, void** ptr)
 {
     if (!ctx || !ptr) return ICX_E_NULL;
     *ptr = nullptr;
-    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     const size_t c = DevPool::cls(bytes);
-    auto f = P.free_.find(c);
-    if (f != P.free_.end() && !f->second.empty()) {
-        *ptr = f->second.back();
-        f->second.pop_back();
-        P.cached -= c;
-    } else {
-        hipError_t e = hipSetDevice(ctx->device);
-        if (e == hipSuccess) e = P.host ? hipHostMalloc(ptr, c, hipHostMallocPortable) : hipMalloc(ptr, c);
-        if (e != hipSuccess) return hip_fail(ctx, e, P.host ? "hipHostMalloc" : "hipMalloc");
+    {
+        std::lock_guard<std::mutex> lk(ctx->pool_mu);
+        auto f = P.free_.find(c);
+        if (f != P.free_.end() && !f->second.empty()) {
+            *ptr = f->second.back();
+            f->second.pop_back();
+            P.cached -= c;
+            P.live_[*ptr] = c;
+            return ICX_OK;
+        }
     }
+    // a new buffer: allocated outside every lock (a pinned allocation of a few
+    // MB takes milliseconds; other threads keep taking cached buffers)
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = P.host ? hipHostMalloc(ptr, c, hipHostMallocPortable) : hipMalloc(ptr, c);
+    if (e != hipSuccess) {
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);  // (no pool lock held: no lock-order inversion)
+        return hip_fail(ctx, e, P.host ? "hipHostMalloc" : "hipMalloc");
+    }
+    std::lock_guard<std::mutex> lk(ctx->pool_mu);
     P.live_[*ptr] = c;
     return ICX_OK;
 }
@@ -796,24 +805,34 @@ icx_status pool_free(icx_ctx* ctx, DevPool& P, void* ptr)
 {
     if (!ctx) return ICX_E_NULL;
     if (!ptr) return ICX_OK;
-    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
-    auto l = P.live_.find(ptr);
-    if (l == P.live_.end()) return fail(ctx, ICX_E_INVALID, "free of a buffer this context did not allocate");
-    const size_t c = l->second;
-    P.live_.erase(l);
-    // A recycled buffer's next use is a copy or launch on this context's
-    // stream, ordered after every launch that used it before, so recycling
-    // needs no synchronisation.  (Host buffers: every call that reads one
-    // synchronises before returning.)
-    if (P.cached + c <= P.limit) {
-        P.free_[c].push_back(ptr);
-        P.cached += c;
-        return ICX_OK;
+    size_t c = 0;
+    {
+        std::lock_guard<std::mutex> lk(ctx->pool_mu);
+        auto l = P.live_.find(ptr);
+        if (l != P.live_.end()) {
+            c = l->second;
+            P.live_.erase(l);
+            // A recycled buffer's next use is a copy or launch on this context's
+            // stream, ordered after every launch that used it before, so recycling
+            // needs no synchronisation.  (Host buffers: every call that reads one
+            // synchronises before returning.)
+            if (P.cached + c <= P.limit) {
+                P.free_[c].push_back(ptr);
+                P.cached += c;
+                return ICX_OK;
+            }
+        }
+    }
+    if (!c) {
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        return fail(ctx, ICX_E_INVALID, "free of a buffer this context did not allocate");
     }
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e == hipSuccess) e = P.host ? hipHostFree(ptr) : hipFree(ptr);
-    return e == hipSuccess ? ICX_OK : hip_fail(ctx, e, "free");
+    if (e == hipSuccess) return ICX_OK;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    return hip_fail(ctx, e, "free");
 }
 }  // namespace
 

@@ -3,7 +3,7 @@ defaults, plus GPU placement flags.
 
   python -m icx -f list.txt -o outdir [-q 0.25] [-s 1048576] [-w 1920] [-i 1920]
                 [-t 1048576] [--timeOut 24] [--cache-db image-compression-cache]
-                [--devices 0,1] [--group 16] [--decode-threads N]
+                [--devices 0,1] [--group 64] [--decode-threads N]
 
 Multi-GPU: either one process driving several devices (--devices, one worker
 thread per GPU sharing one L1 cache), or one process per GPU under torchrun
@@ -35,7 +35,7 @@ def build_parser():
     p.add_argument("--timeOut", type=float, default=24)
     p.add_argument("--cache-db", default="image-compression-cache")
     p.add_argument("--devices", default=None, help="GPU ordinals for this process, e.g. 0,1 (default: LOCAL_RANK or 0)")
-    p.add_argument("--group", type=int, default=16, help="JPEGs per device batch")
+    p.add_argument("--group", type=int, default=64, help="JPEGs (or PNGs) per device batch")
     p.add_argument("--decode-threads", type=int, default=None)
     p.add_argument("-V", "--version", action="version", version="1.0")
     return p

@@ -44,6 +44,49 @@ from .core import (CompressionParams, CompressionReport, CompressionResult, crea
 
 log = logging.getLogger("icx.pipeline")
 
+
+class StageTimes:
+    """Seconds spent per stage of a CompressionBatch run, summed over the
+    threads doing it (thread-seconds): where the host time of the files ->
+    files path goes.  Stages: stat, read (file bytes into
+    pinned memory), parse (JPEG header), host_decode (Pillow: PNG and files
+    the device decoder refuses), queue_wait (a GPU worker idle for work),
+    gpu_decode / gpu_fit / gpu_png (the batched device calls, wall time of
+    the calling worker), write (JPEG file writes), png_write (filter + deflate
+    + write)."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self.seconds = {}
+        self.calls = {}
+
+    def add(self, name, dt):
+        with self._lock:
+            self.seconds[name] = self.seconds.get(name, 0.0) + dt
+            self.calls[name] = self.calls.get(name, 0) + 1
+
+    def as_dict(self):
+        with self._lock:
+            return {k: {"seconds": round(v, 4), "calls": self.calls[k]} for k, v in sorted(self.seconds.items())}
+
+
+_stages: Optional[StageTimes] = None  # set while a CompressionBatch with stage_times runs
+
+
+class _span:
+    __slots__ = ("name", "t0")
+
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        self.t0 = time.perf_counter() if _stages is not None else 0.0
+
+    def __exit__(self, *exc):
+        if _stages is not None:
+            _stages.add(self.name, time.perf_counter() - self.t0)
+        return False
+
 # Pillow format -> javax.imageio reader SPI getFormatNames()[0].toLowerCase()
 # (formats the JDK can read; anything else has no reader: readers.hasNext() == false)
 IMAGEIO_FORMATS = {"JPEG": "jpeg", "PNG": "png", "GIF": "gif", "BMP": "bmp", "TIFF": "tif", "WBMP": "wbmp"}
@@ -168,15 +211,17 @@ def _device_jpeg(input_path, params: CompressionParams, reader=None):
     """The file bytes (read by `reader`: into pinned host memory when the codec
     provides it) and header of a JPEG the device decoder supports, else None."""
     from .core import jpeg_info
-    if reader is None:
-        with open(input_path, "rb") as f:
-            data = f.read()
-    else:
-        data = reader(input_path)
+    with _span("read"):
+        if reader is None:
+            with open(input_path, "rb") as f:
+                data = f.read()
+        else:
+            data = reader(input_path)
     head = data[:2] if isinstance(data, bytes) else bytes(data[:2])
     if head != b"\xff\xd8":
         return None
-    st, w, h, _ = jpeg_info(data if isinstance(data, bytes) else data.array)
+    with _span("parse"):
+        st, w, h, _ = jpeg_info(data if isinstance(data, bytes) else data.array)
     if st != N.OK:
         return None
     if w <= params.min_width or h <= params.min_height:  # ImageCompression.java:131
@@ -206,7 +251,8 @@ def decode_image_with_subsampling(input_path, params: CompressionParams, file_si
         if d is not None:
             return d
     try:
-        im = Image.open(input_path)
+        with _span("host_decode"):
+            im = Image.open(input_path)
     except (Image.UnidentifiedImageError, ValueError):
         log.warning("%s - 找不到對應的圖片讀取器，跳過", input_path)
         return None
@@ -221,7 +267,8 @@ def decode_image_with_subsampling(input_path, params: CompressionParams, file_si
                       params.min_width, params.min_height)
             return None
         s = subsampling_factor(width, height)
-        arr = _to_array(im, input_path)
+        with _span("host_decode"):
+            arr = _to_array(im, input_path)
     if s > 1:  # ImageReadParam.setSourceSubsampling(s, s, 0, 0): keep pixels (x*s, y*s)
         log.debug("%s - 對圖片應用二次取樣，比率: %d", os.path.basename(str(input_path)), s)
         from .core import IndexedImage
@@ -246,7 +293,9 @@ def _prepare(index, path, output_dir, params, device_jpeg=False) -> _Item:
     """processImage up to and including the decode (ImageCompression.java:53-76)."""
     it = _Item(index, path)
     try:
-        if not os.path.exists(path) or not os.access(path, os.R_OK):
+        with _span("stat"):
+            ok = os.path.exists(path) and os.access(path, os.R_OK)
+        if not ok:
             log.warning("%s - 檔案不存在或不可讀，跳過", path)
             it.report = CompressionReport(CompressionResult.SKIPPED_NOT_FOUND, 0, 0)
             return it
@@ -346,8 +395,9 @@ def decode_group(codec, items: List[_Item]):
 
 def _jpeg_write(it: _Item, data: bytes, success: bool):
     try:
-        with open(it.output, "wb") as f:
-            f.write(data)
+        with _span("write"):
+            with open(it.output, "wb") as f:
+                f.write(data)
         _finish(it, success)
     except Exception as e:
         _fail(it, e)
@@ -357,7 +407,8 @@ def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, ca
     """compressJpgWithTargetSize for a group of decoded JPEGs in one device batch
     (file writes on `writer`, a host thread pool, when given)."""
     try:
-        decode_group(codec, items)
+        with _span("gpu_decode"):
+            decode_group(codec, items)
     except Exception as e:  # context-level failure: every image of the group fails alike
         for it in items:
             _fail(it, e)
@@ -369,8 +420,9 @@ def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, ca
     with cache.lock:
         cached = [cache.get(k) for k in keys]
     try:
-        res = codec.fit([it.decoded.image for it in items], params.target_max_size_bytes, params.quality,
-                        cached=cached)
+        with _span("gpu_fit"):
+            res = codec.fit([it.decoded.image for it in items], params.target_max_size_bytes, params.quality,
+                            cached=cached)
     except Exception as e:  # context-level failure: every image of the group fails alike
         for it in items:
             _fail(it, e)
@@ -399,7 +451,8 @@ def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, ca
 def _png_write(it: _Item, resized):
     try:
         from .pngio import write_png
-        write_png(it.output, resized)
+        with _span("png_write"):
+            write_png(it.output, resized)
         _finish(it, True)
     except Exception as e:
         _fail(it, e)
@@ -432,7 +485,8 @@ def compress_png_group(codec, items: List[_Item], params: CompressionParams, wri
             compress_png_item(codec, it, params, writer)
         return
     try:
-        res = codec.png_fit_batch([it.decoded.image for it in items], params)
+        with _span("gpu_png"):
+            res = codec.png_fit_batch([it.decoded.image for it in items], params)
     except Exception:  # a bad image fails alone: redo the group one by one
         for it in items:
             compress_png_item(codec, it, params, writer)
@@ -479,6 +533,7 @@ class BatchReport:
     cache_size: int = 0
     seconds: float = 0.0
     megapixels: float = 0.0
+    stages: dict = field(default_factory=dict)  # StageTimes.as_dict() when the batch recorded them
 
     @property
     def success(self):
@@ -585,9 +640,9 @@ class CompressionBatch:
     each); they share one L1 learned cache (the reference's ConcurrentHashMap)."""
 
     def __init__(self, file_list_path, save_dir, params: CompressionParams, time_out_hr: float = 24,
-                 h2_cache_path="image-compression-cache", codecs=None, group_size: int = 16,
+                 h2_cache_path="image-compression-cache", codecs=None, group_size: int = 64,
                  decode_threads: Optional[int] = None, rank: int = 0, world: int = 1,
-                 device_decode: Optional[bool] = None):
+                 device_decode: Optional[bool] = None, stage_times: bool = False):
         self.file_list_path = file_list_path
         self.save_dir = save_dir
         self.params = params
@@ -597,6 +652,7 @@ class CompressionBatch:
         self.group_size = max(1, group_size)
         self.decode_threads = decode_threads or host_cores()[0]
         self.rank, self.world = rank, world
+        self.stage_times = StageTimes() if stage_times else None
         # JPEG decode on the GPU when every codec can (the default for icx.Codec)
         if device_decode is None:
             device_decode = bool(self.codecs) and all(hasattr(c, "decode_jpg_batch") for c in self.codecs)
@@ -615,6 +671,8 @@ class CompressionBatch:
         elif not hasattr(cache, "lock"):
             cache = LockedDict(cache)
         rep = BatchReport()
+        global _stages
+        _stages = self.stage_times
         t0 = time.perf_counter()
         try:
             if mgr is not None:  # CompressionBatch.java:49-52 (inside the try: a schema error ends the batch)
@@ -633,7 +691,10 @@ class CompressionBatch:
         except sqlite3.Error:  # CompressionBatch.java:134-139: logged, the batch ends
             log.exception("執行批次壓縮時發生未預期錯誤")
         finally:
+            _stages = None
             rep.seconds = time.perf_counter() - t0
+            if self.stage_times is not None:
+                rep.stages = self.stage_times.as_dict()
             rep.cache_size = len(cache) if cache is not None else 0
             if mgr is not None:
                 if cache is not None:
@@ -652,7 +713,8 @@ class CompressionBatch:
 
         def gpu_worker(codec):
             while True:
-                grp = work.get()
+                with _span("queue_wait"):
+                    grp = work.get()
                 if grp is None:
                     return
                 kind, its = grp

@@ -10,7 +10,10 @@ host threads), written to a scratch directory first (not timed).  Runs the
 batch twice with the same cache DB: run 1 learns (full search), run 2 is the
 warm-cache run (C5's timing rule).  Per run: wall time, and the device time
 of each kernel family (HIP events) - the rest is host work (file reads,
-header parses, PNG decode and deflate, file writes) not hidden behind it.
+header parses, PNG decode and deflate, file writes) not hidden behind it -
+and the thread-seconds of every pipeline stage (pipeline.StageTimes).
+--procs N runs N processes at once on the same GPU(s), each over its share of
+the list (warm cache), to tell a per-process bound from the box's own.
 Prints one JSON line."""
 import argparse
 import io
@@ -36,6 +39,8 @@ def main():
     ap.add_argument("--dir", default=None)
     ap.add_argument("--png", type=int, default=0, help="4K PNG files added to the list (configs[4] mix)")
     ap.add_argument("--devices", default="0", help="GPUs driven by this process (one worker each)")
+    ap.add_argument("--procs", type=int, default=1, help="processes sharing the list (warm-cache run only)")
+    ap.add_argument("--decode-threads", type=int, default=0, help="host reader threads (0: every usable core)")
     a = ap.parse_args()
     from PIL import Image
 
@@ -73,6 +78,11 @@ def main():
     with open(lst, "w") as f:
         f.write("\n".join(paths))
     params = CompressionParams(0.25, 1 << 20, 1920, 1920, 1 << 20)  # Execute.java defaults
+    if a.procs > 1:
+        multi_process(a, work, lst, params, blobs, png_blobs)
+        if not a.dir:
+            shutil.rmtree(work, ignore_errors=True)
+        return
     codecs = [icx.Codec(int(d)) for d in a.devices.split(",")]
     kernels = ("dec_unstuff", "dec_init", "dec_sync", "dec_sync_r1", "dec_sync_r2", "dec_sync_r3", "dec_write",
                "dec_dc", "dec_idct", "dec_color", "fdct", "huff", "scan", "ffscan", "stuff", "resize")
@@ -84,7 +94,8 @@ def main():
             c.profile_reset()
         t0 = time.perf_counter()
         rep = pipeline.CompressionBatch(lst, out, params, 1, os.path.join(work, "cache"), codecs=codecs,
-                                        group_size=a.group).execute()
+                                        group_size=a.group, decode_threads=a.decode_threads or None,
+                                        stage_times=True).execute()
         dt = time.perf_counter() - t0
         dev = {}
         for c in codecs:
@@ -98,7 +109,8 @@ def main():
                      "success": rep.success, "failed": rep.failed, "skipped": rep.skipped,
                      "in_bytes": rep.original_size, "out_bytes": rep.compressed_size,
                      "device_ms": dev, "device_ms_total": round(sum(dev.values()), 1),
-                     "host_threads": pipeline.host_cores()[0]})
+                     "host_threads": a.decode_threads or pipeline.host_cores()[0], "stages": rep.stages,
+                     "file_read_GBps": round(rep.original_size / dt / 1e9, 2)})
     for c in codecs:
         c.close()
     print(json.dumps({"metric": "CompressionBatch end-to-end (files -> files), 4K q95 JPEG" +
@@ -109,6 +121,54 @@ def main():
                       "runs": runs}))
     if not a.dir:
         shutil.rmtree(work, ignore_errors=True)
+
+
+def _proc(k, n, lst, work, params, group, devices, threads, barrier, q):
+    """One process of --procs: its share of the list, learning run untimed,
+    the warm-cache run started with the others (barrier)."""
+    import icx
+    from icx import pipeline
+    lines = open(lst).read().split("\n")
+    mine = os.path.join(work, f"list{k}.txt")
+    with open(mine, "w") as f:
+        f.write("\n".join(lines[k::n]))
+    codecs = [icx.Codec(int(d)) for d in devices.split(",")]
+    cache = os.path.join(work, f"cache{k}")
+    pipeline.CompressionBatch(mine, os.path.join(work, f"o{k}a"), params, 1, cache, codecs=codecs,
+                              group_size=group, decode_threads=threads).execute()
+    barrier.wait()
+    t0 = time.perf_counter()
+    rep = pipeline.CompressionBatch(mine, os.path.join(work, f"o{k}b"), params, 1, cache, codecs=codecs,
+                                    group_size=group, decode_threads=threads, stage_times=True).execute()
+    dt = time.perf_counter() - t0
+    for c in codecs:
+        c.close()
+    q.put({"proc": k, "files": rep.total, "success": rep.success, "seconds": round(dt, 3),
+           "in_bytes": rep.original_size, "stages": rep.stages})
+
+
+def multi_process(a, work, lst, params, blobs, png_blobs):
+    import multiprocessing as mp
+    from icx import pipeline
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    barrier = ctx.Barrier(a.procs)
+    threads = a.decode_threads or max(1, pipeline.host_cores()[0] // a.procs)
+    ps = [ctx.Process(target=_proc, args=(k, a.procs, lst, work, params, a.group, a.devices, threads, barrier, q))
+          for k in range(a.procs)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=900) for _ in ps), key=lambda r: r["proc"])
+    for p in ps:
+        p.join(60)
+    wall = max(r["seconds"] for r in res)
+    files = sum(r["files"] for r in res)
+    print(json.dumps({"metric": f"CompressionBatch end-to-end, {a.procs} processes on devices {a.devices} "
+                                "(warm cache), 4K q95 JPEG" + (" + 4K PNG" if a.png else ""),
+                      "files": files, "procs": a.procs, "threads_per_proc": threads, "group_size": a.group,
+                      "seconds": wall, "images_per_s": round(files / wall, 1),
+                      "file_read_GBps": round(sum(r["in_bytes"] for r in res) / wall / 1e9, 2),
+                      "mean_src_bytes": int(np.mean([len(b) for b in blobs])), "per_proc": res}))
 
 
 if __name__ == "__main__":
