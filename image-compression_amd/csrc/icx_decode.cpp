@@ -358,6 +358,7 @@ icx_status run_progressive(icx_ctx* c, std::vector<DecItem>& items, int16_t* coe
 icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out, size_t coef_cap)
 {
     std::lock_guard<std::recursive_mutex> lk(c->mu);
+    HostSpan call{c, "host.call_decode"};  // the whole call, wall time (profiling)
     hipError_t he = hipSetDevice(c->device);
     if (he != hipSuccess) return hip_fail(c, he, "hipSetDevice");
     std::vector<DecItem> items, prog;

@@ -573,6 +573,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
                      ImgState* search_out = nullptr)
 {
     std::lock_guard<std::recursive_mutex> lk(c->mu);
+    HostSpan call{c, "host.call_fit"};  // the whole call, wall time (profiling)
     hipError_t he = hipSetDevice(c->device);
     if (he != hipSuccess) return hip_fail(c, he, "hipSetDevice");
     std::vector<int> order;

@@ -393,14 +393,19 @@ def decode_group(codec, items: List[_Item]):
             _fail(it, e)
 
 
-def _jpeg_write(it: _Item, data: bytes, success: bool):
+def _jpeg_write(it: _Item, data, success: bool, n=None):
+    """Write a JPEG file: bytes, or the first n bytes of a PinnedBuffer, which
+    goes back to the pool afterwards."""
     try:
         with _span("write"):
             with open(it.output, "wb") as f:
-                f.write(data)
+                f.write(data if n is None else memoryview(data.array)[:n])
         _finish(it, success)
     except Exception as e:
         _fail(it, e)
+    finally:
+        if n is not None:
+            data.free()
 
 
 def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, cache, writer=None):
@@ -419,11 +424,27 @@ def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, ca
     keys = [create_key(it.decoded.image, it.original_size) for it in items]
     with cache.lock:
         cached = [cache.get(k) for k in keys]
+    # the files land in pinned host buffers (a DMA each, no staging copy); the
+    # writer pool writes them from there and hands them back
+    outs = None
+    if hasattr(codec, "_ctx"):
+        from .core import PinnedBuffer
+        # (a fitting file is <= -t; and no baseline JPEG reaches 10 bytes a pixel)
+        outs = [PinnedBuffer(codec, min(params.target_max_size_bytes + 1,
+                                        10 * it.decoded.image.shape[0] * it.decoded.image.shape[1] + 65536))
+                for it in items]
     try:
         with _span("gpu_fit"):
             res = codec.fit([it.decoded.image for it in items], params.target_max_size_bytes, params.quality,
-                            cached=cached)
+                            cached=cached, outputs=[o.array for o in outs] if outs else None)
+            if outs:
+                for r, o in zip(res, outs):
+                    r["data"] = o if r["success"] and r["status"] == N.OK else None
+                    if r["data"] is None:
+                        o.free()
     except Exception as e:  # context-level failure: every image of the group fails alike
+        for o in outs or ():
+            o.free()
         for it in items:
             _fail(it, e)
         return
@@ -438,11 +459,12 @@ def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, ca
                     with cache.lock:
                         cache[key] = r["learned"]
                 it.decoded = None  # the frame's HBM buffer goes back to the pool now
+                pinned = not isinstance(r["data"], (bytes, bytearray))
                 if writer is not None:
-                    writer.submit(_jpeg_write, it, r["data"], True)
+                    writer.submit(_jpeg_write, it, r["data"], True, r["out_len"] if pinned else None)
                     continue
-                with open(it.output, "wb") as f:
-                    f.write(r["data"])
+                _jpeg_write(it, r["data"], True, r["out_len"] if pinned else None)
+                continue
             _finish(it, r["success"])
         except Exception as e:
             _fail(it, e)

@@ -97,18 +97,24 @@ def main():
                                         group_size=a.group, decode_threads=a.decode_threads or None,
                                         stage_times=True).execute()
         dt = time.perf_counter() - t0
-        dev = {}
+        dev, host = {}, {}
         for c in codecs:
             c.profile(False)
             for k in kernels:
                 ms = c.profile_query(k)["ms"]
                 if ms:
                     dev[k] = round(dev.get(k, 0.0) + ms, 2)
+            for k in ("host.call_decode", "host.call_fit", "host.dec_headers", "host.dec_setup", "host.sync",
+                      "host.results"):
+                q = c.profile_query(k)
+                if q["launches"]:
+                    host[k] = {"ms": round(host.get(k, {}).get("ms", 0.0) + q["ms"], 2),
+                               "calls": host.get(k, {}).get("calls", 0) + q["launches"]}
         runs.append({"run": "learn" if r == 0 else "warm cache", "seconds": round(dt, 3),
                      "images_per_s": round(rep.total / dt, 1), "mp_per_s": round(rep.megapixels / dt, 1),
                      "success": rep.success, "failed": rep.failed, "skipped": rep.skipped,
                      "in_bytes": rep.original_size, "out_bytes": rep.compressed_size,
-                     "device_ms": dev, "device_ms_total": round(sum(dev.values()), 1),
+                     "device_ms": dev, "device_ms_total": round(sum(dev.values()), 1), "library_host_spans": host,
                      "host_threads": a.decode_threads or pipeline.host_cores()[0], "stages": rep.stages,
                      "file_read_GBps": round(rep.original_size / dt / 1e9, 2)})
     for c in codecs:
