@@ -10,6 +10,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -144,11 +145,22 @@ struct DevPool {
         return c;
     }
     bool host = false;  // pinned host pool (hipHostMalloc) instead of device memory
+    // pinned buffers below kSlabMax are carved from slabs of >= kSlab bytes:
+    // one hipHostMalloc per slab (a pinned allocation costs milliseconds and
+    // the runtime serialises them: a batch's first run read files at 2 GB/s
+    // with one allocation per file); carved buffers always return to the free
+    // lists, the slabs are released with the pool
+    static constexpr size_t kSlab = (size_t)64 << 20, kSlabMax = (size_t)16 << 20;
+    std::vector<void*> slabs;
+    std::set<void*> carved;
     ~DevPool()
     {
         for (auto& kv : free_)
-            for (void* p : kv.second) (void)(host ? hipHostFree(p) : hipFree(p));
-        for (auto& kv : live_) (void)(host ? hipHostFree(kv.first) : hipFree(kv.first));
+            for (void* p : kv.second)
+                if (!carved.count(p)) (void)(host ? hipHostFree(p) : hipFree(p));
+        for (auto& kv : live_)
+            if (!carved.count(kv.first)) (void)(host ? hipHostFree(kv.first) : hipFree(kv.first));
+        for (void* s : slabs) (void)hipHostFree(s);
     }
 };
 

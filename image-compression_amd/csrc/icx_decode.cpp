@@ -789,15 +789,28 @@ icx_status pool_alloc(icx_ctx* ctx, DevPool& P, size_t bytes, void** ptr)
             return ICX_OK;
         }
     }
-    // a new buffer: allocated outside every lock (a pinned allocation of a few
-    // MB takes milliseconds; other threads keep taking cached buffers)
+    // a new buffer (or slab): allocated outside every lock (a pinned
+    // allocation takes milliseconds; other threads keep taking cached buffers)
+    const bool slab = P.host && c <= DevPool::kSlabMax;
+    const size_t bytes_new = slab ? std::max(c, DevPool::kSlab) : c;
     hipError_t e = hipSetDevice(ctx->device);
-    if (e == hipSuccess) e = P.host ? hipHostMalloc(ptr, c, hipHostMallocPortable) : hipMalloc(ptr, c);
+    if (e == hipSuccess) e = P.host ? hipHostMalloc(ptr, bytes_new, hipHostMallocPortable) : hipMalloc(ptr, bytes_new);
     if (e != hipSuccess) {
         std::lock_guard<std::recursive_mutex> lk(ctx->mu);  // (no pool lock held: no lock-order inversion)
         return hip_fail(ctx, e, P.host ? "hipHostMalloc" : "hipMalloc");
     }
     std::lock_guard<std::mutex> lk(ctx->pool_mu);
+    if (slab) {  // the first piece is this call's, the rest go to the free list
+        P.slabs.push_back(*ptr);
+        for (size_t o = 0; o < bytes_new; o += c) {
+            void* p = (char*)*ptr + o;
+            P.carved.insert(p);
+            if (o) {
+                P.free_[c].push_back(p);
+                P.cached += c;
+            }
+        }
+    }
     P.live_[*ptr] = c;
     return ICX_OK;
 }
@@ -817,7 +830,7 @@ icx_status pool_free(icx_ctx* ctx, DevPool& P, void* ptr)
             // stream, ordered after every launch that used it before, so recycling
             // needs no synchronisation.  (Host buffers: every call that reads one
             // synchronises before returning.)
-            if (P.cached + c <= P.limit) {
+            if (P.cached + c <= P.limit || P.carved.count(ptr)) {
                 P.free_[c].push_back(ptr);
                 P.cached += c;
                 return ICX_OK;

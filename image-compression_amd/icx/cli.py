@@ -3,10 +3,14 @@ defaults, plus GPU placement flags.
 
   python -m icx -f list.txt -o outdir [-q 0.25] [-s 1048576] [-w 1920] [-i 1920]
                 [-t 1048576] [--timeOut 24] [--cache-db image-compression-cache]
-                [--devices 0,1] [--group 64] [--decode-threads N]
+                [--devices 0,1] [--workers-per-device 2] [--group 64] [--decode-threads N]
 
-Multi-GPU: either one process driving several devices (--devices, one worker
-thread per GPU sharing one L1 cache), or one process per GPU under torchrun
+Each device gets --workers-per-device GPU worker threads, each with its own
+libicx context, so one group's host work (file bytes to the decoder, results
+to the writers) overlaps another group's kernels: files -> files JPEG on one
+MI355X, 1491 files/s with one worker, 2199 with two.
+Multi-GPU: either one process driving several devices (--devices, worker
+threads per GPU sharing one L1 cache), or one process per GPU under torchrun
 (RANK/WORLD_SIZE/LOCAL_RANK): the file list is sharded by file size
 (longest-processing-time first, pipeline.shard), result
 counters are summed and the learned-cache entries merged on rank 0, which
@@ -35,6 +39,8 @@ def build_parser():
     p.add_argument("--timeOut", type=float, default=24)
     p.add_argument("--cache-db", default="image-compression-cache")
     p.add_argument("--devices", default=None, help="GPU ordinals for this process, e.g. 0,1 (default: LOCAL_RANK or 0)")
+    p.add_argument("--workers-per-device", type=int, default=2,
+                   help="GPU worker threads (libicx contexts) per device")
     p.add_argument("--group", type=int, default=64, help="JPEGs (or PNGs) per device batch")
     p.add_argument("--decode-threads", type=int, default=None)
     p.add_argument("-V", "--version", action="version", version="1.0")
@@ -63,7 +69,7 @@ def main(argv=None) -> int:
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-    codecs = [Codec(d) for d in devices]
+    codecs = [Codec(d) for d in devices for _ in range(max(1, a.workers_per_device))]
     batch = CompressionBatch(a.file_list, a.output_dir, params, a.timeOut, a.cache_db, codecs=codecs,
                              group_size=a.group, decode_threads=a.decode_threads, rank=rank, world=world)
     if dist is None:

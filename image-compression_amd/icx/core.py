@@ -534,13 +534,14 @@ class Codec:
         return res
 
     # -------------------------------------------------------------- A11 decode
-    def decode_jpg_batch(self, datas, subsampling: int = 0, device_out: bool = False):
+    def decode_jpg_batch(self, datas, subsampling: int = 0, device_out: bool = False, infos=None):
         """Decode JPEG files (bytes / uint8 arrays / DeviceImage / CUDA uint8
         tensors) on the GPU: decodeImageWithSubsampling's read
         (ImageCompression.java:113-155).  subsampling 0 = the reference's
         rule.  Returns one (status, image) per file; image is (H, W, 3) BGR or
         (H, W) grey, a DeviceImage when device_out (it stays in HBM for the
-        encoder), else numpy."""
+        encoder), else numpy.  infos: the files' icx_jpeg_info results when the
+        caller has them (the batch driver parsed every header already)."""
         n = len(datas)
         jobs = (N.DecodeJob * n)()
         keep, outs = [], [None] * n
@@ -558,7 +559,7 @@ class Codec:
                 keep.append(a)
                 jobs[i].data, jobs[i].len = a.ctypes.data, a.nbytes
             jobs[i].subsampling = int(subsampling)
-            info = jpeg_info(_host_header(d))
+            info = infos[i] if infos is not None else jpeg_info(_host_header(d))
             if info[0] == N.OK:
                 _, w, h, nc = info
                 s = subsampling if subsampling > 0 else subsampling_factor(w, h)
@@ -667,10 +668,10 @@ class Pool(Codec):
             st = self._lib.icx_set_table_layout(self._lib.icx_pool_context(self._pool, i), int(layout))
             self._check(st, "icx_set_table_layout")
 
-    def decode_jpg_batch(self, datas, subsampling: int = 0, device_out: bool = False):
+    def decode_jpg_batch(self, datas, subsampling: int = 0, device_out: bool = False, infos=None):
         if device_out:
             raise ValueError("a Pool decodes into host memory; use one device's Codec for device_out")
-        return super().decode_jpg_batch(datas, subsampling, False)
+        return super().decode_jpg_batch(datas, subsampling, False, infos)
 
 
 def jpeg_info(data):

@@ -104,6 +104,7 @@ class DecodedImage:
     height: int
     subsampling: int
     data: Optional[bytes] = None
+    ncomp: int = 3  # components of a JPEG left to the device decoder (its header, parsed once)
 
     @property
     def decoded_dims(self):
@@ -221,7 +222,7 @@ def _device_jpeg(input_path, params: CompressionParams, reader=None):
     if head != b"\xff\xd8":
         return None
     with _span("parse"):
-        st, w, h, _ = jpeg_info(data if isinstance(data, bytes) else data.array)
+        st, w, h, nc = jpeg_info(data if isinstance(data, bytes) else data.array)
     if st != N.OK:
         return None
     if w <= params.min_width or h <= params.min_height:  # ImageCompression.java:131
@@ -231,7 +232,7 @@ def _device_jpeg(input_path, params: CompressionParams, reader=None):
     s = subsampling_factor(w, h)
     if s > 1:
         log.debug("%s - 對圖片應用二次取樣，比率: %d", os.path.basename(str(input_path)), s)
-    return DecodedImage(None, "jpeg", w, h, s, data)
+    return DecodedImage(None, "jpeg", w, h, s, data, nc)
 
 
 def decode_image_with_subsampling(input_path, params: CompressionParams, file_size: int,
@@ -373,8 +374,11 @@ def decode_group(codec, items: List[_Item]):
         return
     # a codec that decodes into host memory only (icx.Pool: its images may
     # land on any of its devices) hands back numpy frames, which its fit uploads
+    kw = {}
+    if hasattr(codec, "_ctx"):  # (icx.Codec / Pool: the headers were parsed by _device_jpeg)
+        kw["infos"] = [(N.OK, it.decoded.width, it.decoded.height, it.decoded.ncomp) for it in todo]
     res = codec.decode_jpg_batch([it.decoded.data for it in todo], subsampling=0,
-                                 device_out=getattr(codec, "supports_device_out", True))
+                                 device_out=getattr(codec, "supports_device_out", True), **kw)
     for it, (st, img) in zip(todo, res):
         it.decoded.data = None
         if st == N.OK:
