@@ -8,7 +8,7 @@ defaults, plus GPU placement flags.
 Each device gets --workers-per-device GPU worker threads, each with its own
 libicx context, so one group's host work (file bytes to the decoder, results
 to the writers) overlaps another group's kernels: files -> files JPEG on one
-MI355X, 1491 files/s with one worker, 2199 with two.
+MI355X, 1830 files/s with one worker, 2422 with two.
 Multi-GPU: either one process driving several devices (--devices, worker
 threads per GPU sharing one L1 cache), or one process per GPU under torchrun
 (RANK/WORLD_SIZE/LOCAL_RANK): the file list is sharded by file size
