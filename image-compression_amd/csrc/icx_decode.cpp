@@ -320,9 +320,9 @@ icx_status run_progressive(icx_ctx* c, std::vector<DecItem>& items, int16_t* coe
             d.tab = d_tab + k;
             const int64_t nmcu = (int64_t)d.mcux * d.mcuy;
             ids.push_back(k);
-            cnt_blk.push_back(d.fuse420 ? (2 * nmcu + 31) / 32 : (d.nblocks + 31) / 32);
+            cnt_blk.push_back(dec_idct_items(d.fuse420 ? (2 * nmcu + 31) / 32 : (d.nblocks + 31) / 32));
             cnt_px.push_back(d.fuse420 ? 0 : ((int64_t)d.oh * ((d.ow + 3) / 4) + 255) / 256);
-            cnt_rows.push_back(d.fuse420 ? (int64_t)d.mcuy * ((d.mcux + 7) / 8) : 0);
+            cnt_rows.push_back(d.fuse420 ? (int64_t)dec_lc_items(d.mcux, d.mcuy) : 0);
             tpx += (int64_t)d.w * d.h;
         }
         if (coef_out || ids.empty()) continue;
@@ -428,7 +428,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             it.ent_cap = (size_t)scan_len + (size_t)(DEC_PAD - 2) * d.nseg_max + DEC_TAIL + 64 + 4 * DEC_WIN;
             it.ntiles = (scan_len + DEC_TILE - 1) / DEC_TILE;
             it.nblocks = d.nblocks;
-            size_t per = align_up(scan_len + 64, 256) + align_up(it.ent_cap, 256) + it.ntiles * 8 + 512 +
+            size_t per = (it.dev_in ? 0 : align_up(scan_len, 256)) + align_up(it.ent_cap, 256) + it.ntiles * 8 + 512 +
                          (size_t)d.nseg_max * 4 + (size_t)d.nblocks * (128 + 4) + sizeof(DecTab) + 4096;
             for (int k = 0; k < 3; k++) per += align_up((size_t)d.pw[k] * d.ph[k], 256);
             per += (size_t)(it.ent_cap * 8 / 2048 + 2) * (8 + 2 + 4 + 4);  // subsequence arrays at S >= 2048
@@ -445,8 +445,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         const uint32_t S = pick_sub_bits(bits);
         // every small argument array of the sub-batch travels in one packed upload
         const size_t up = Uploader::need<DecTab>(m) + Uploader::need<DecDesc>(m) + Uploader::need<DecState>(m) +
-                          Uploader::need<int32_t>(m) + Uploader::need<StageJob>(m) +
-                          3 * Uploader::need<int64_t>(m + 1) +
+                          Uploader::need<int32_t>(m) + 2 * Uploader::need<int64_t>(m + 1) +
                           // the decode tails (subsets settled at one check): ids and 4 plans each; each
                           // image is in one tail, so at most m + 1 tails of 36 B per image + alignment
                           36 * (size_t)m + (size_t)(m + 1) * (64 + 4 * 72);
@@ -485,11 +484,8 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         }
         DecTab* h_tab;
         DecTab* d_tab = U.alloc<DecTab>(uniq.size(), &h_tab);
-        StageJob* h_stage;
-        const StageJob* d_stage = U.alloc<StageJob>(m, &h_stage);
         if (U.overflow) return fail(c, ICX_E_NOMEM, "upload staging exhausted");
         std::vector<DecState> states(m);
-        std::vector<int64_t> cnt_stage(m);
         std::vector<char> tab_ok(uniq.size(), 0);
         int64_t max_nsub = 0;
         for (int k = 0; k < m; k++) {
@@ -507,13 +503,12 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             const int64_t scan_len = (int64_t)(it.job->len - it.J.scan_off);
             d.scan_len = scan_len;
             d.ntiles = (int32_t)it.ntiles;
-            // the scan copy: 16-B aligned, zero-padded by 64 bytes (k_unstuff_* read past the end)
-            const int64_t padded = (int64_t)align_up(scan_len + 64, 16);
-            uint8_t* scan = (uint8_t*)c->dev.take(align_up(scan_len + 64, 256));
+            // k_unstuff_* read the stuffed scan at any alignment and never past
+            // scan_len's 16-B chunk: a device file is read where it lies, a host
+            // file takes one DMA (pageable: via pinned staging)
             const uint8_t* src = it.job->data + it.J.scan_off;
-            if (it.dev_in) {  // device file: k_stage copies and pads
-                h_stage[k] = StageJob{src, scan, scan_len, padded};
-            } else {  // host file: one DMA (pageable: via pinned staging), k_stage pads the tail in place
+            if (!it.dev_in) {
+                uint8_t* scan = (uint8_t*)c->dev.take(align_up(scan_len, 256));
                 if (!is_pinned_ptr(it.job->data)) {
                     uint8_t* h = (uint8_t*)c->host.take(scan_len);
                     if (h) {
@@ -523,11 +518,9 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
                 }
                 e = hipMemcpyAsync(scan, src, scan_len, hipMemcpyHostToDevice, c->stream);
                 if (e != hipSuccess) return hip_fail(c, e, "scan upload");
-                const int64_t t0 = scan_len & ~(int64_t)15;
-                h_stage[k] = StageJob{scan + t0, scan + t0, scan_len - t0, padded - t0};
+                src = scan;
             }
-            cnt_stage[k] = (h_stage[k].dst_len + STAGE_TILE - 1) / STAGE_TILE;
-            d.scan = scan;
+            d.scan = src;
             d.ent = (uint8_t*)c->dev.take(align_up(it.ent_cap, 256));
             d.ent_cap = (int64_t)it.ent_cap;
             d.tile_cnt = (uint32_t*)c->dev.take(it.ntiles * 4 + 4);
@@ -567,27 +560,25 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         std::vector<int64_t> cnt_tiles(m), cnt_subs(m), cnt_pieces(m), cnt_blk(m), cnt_px(m), cnt_rows(m);
         int64_t stuffed = 0;
         for (int k = 0; k < m; k++) {
-            cnt_tiles[k] = sub[k]->ntiles;
+            cnt_tiles[k] = (sub[k]->ntiles + DEC_UNSTUFF_TILES - 1) / DEC_UNSTUFF_TILES;  // k_unstuff_count / _scatter
             cnt_subs[k] = (desc[k].nsub_max + 1 + 255) / 256;
             cnt_pieces[k] = ((int64_t)(desc[k].nsub_max + 1) * dec_pieces(S) + 255) / 256;  // k_dec_write
             // colour: luma IDCT fused with upsampling + conversion for s == 1 4:2:0 fancy (chroma
             // blocks alone go through k_dec_idct), the per-pixel gather kernel otherwise
             const DecDesc& q = desc[k];
             const int64_t nmcu = (int64_t)q.mcux * q.mcuy;
-            cnt_blk[k] = q.fuse420 ? (2 * nmcu + 31) / 32 : (q.nblocks + 31) / 32;
+            cnt_blk[k] = dec_idct_items(q.fuse420 ? (2 * nmcu + 31) / 32 : (q.nblocks + 31) / 32);
             cnt_px[k] = q.fuse420 ? 0 : ((int64_t)q.oh * ((q.ow + 3) / 4) + 255) / 256;
-            cnt_rows[k] = q.fuse420 ? (int64_t)q.mcuy * ((q.mcux + 7) / 8) : 0;
+            cnt_rows[k] = q.fuse420 ? (int64_t)dec_lc_items(q.mcux, q.mcuy) : 0;
             stuffed += desc[k].scan_len;
         }
         // plans of the whole sub-batch; the pixel stages get theirs per tail
-        const WPlan Pg = plan_of(U, cnt_stage, d_ids), Pt = plan_of(U, cnt_tiles, d_ids),
-                    Ps = plan_of(U, cnt_subs, d_ids);
+        const WPlan Pt = plan_of(U, cnt_tiles, d_ids), Ps = plan_of(U, cnt_subs, d_ids);
         icx_status st = U.flush();
         if (st) return st;
         e = hipMemsetAsync(d_changed, 0, (size_t)max_it * 4, c->stream);
         if (e == hipSuccess) e = hipMemsetAsync(d_wlcnt, 0, (size_t)m * max_it * 4, c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "counter clear");
-        launch_stage(d_stage, Pg.p, Pg.total, c->stream);
         {
             Timed tm(c, "dec_unstuff", stuffed);
             launch_unstuff(d_desc, d_state, Pt.p, Pt.total, d_ids, m, S, c->stream);

@@ -30,6 +30,7 @@
 // Everything here is __host__ __device__ so tests/dec_emu.cpp can run the same
 // state machine serially on the CPU.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __HIPCC__
@@ -43,7 +44,8 @@ namespace icx {
 
 constexpr int DEC_SUB_BITS = 1024;   // bits per subsequence (one thread)
 constexpr int DEC_LUT_BITS = 10;     // Huffman fast-lookup width
-constexpr int DEC_TILE = 4096;       // stuffed bytes per unstuff workgroup (256 x 16)
+constexpr int DEC_TILE = 4096;       // stuffed bytes per unstuff tile (256 threads x 16)
+constexpr int DEC_UNSTUFF_TILES = 4; // consecutive tiles per k_unstuff_count / k_unstuff_scatter workgroup
 constexpr int DEC_PAD = 8;           // 0xFF bytes standing in for each RSTn marker
 constexpr int DEC_TAIL = 16;         // 0xFF bytes after the last interval
 constexpr uint32_t DEC_END = 0xFFFFFFFFu;
@@ -144,6 +146,25 @@ ICX_HD int dec_walk_mcu(int ncomp, int nbmcu, const int* td, const int* ta)
 {
     if (ncomp != 3) return nbmcu;
     return td[0] == td[1] && td[0] == td[2] && ta[0] == ta[1] && ta[0] == ta[2] ? 1 : nbmcu;
+}
+
+// the IDCT kernels load a dequantisation row as one 16-byte load
+static_assert(offsetof(DecTab, qt) % 16 == 0 && sizeof(DecTab) % 16 == 0, "DecTab.qt rows 16-byte aligned");
+
+// k_dec_idct work items per image: tiles of 32 blocks (nblk_tiles),
+// DEC_IDCT_TILES consecutive tiles per workgroup.
+constexpr int DEC_IDCT_TILES = 4;
+ICX_HD long long dec_idct_items(long long nblk_tiles)
+{
+    return (nblk_tiles + DEC_IDCT_TILES - 1) / DEC_IDCT_TILES;
+}
+
+// k_dec_luma_color_420 work items per image: tiles of one MCU row x 8 MCUs,
+// DEC_LC_TILES consecutive tiles per workgroup.
+constexpr int DEC_LC_TILES = 4;
+ICX_HD long long dec_lc_items(int mcux, int mcuy)
+{
+    return ((long long)mcuy * ((mcux + 7) / 8) + DEC_LC_TILES - 1) / DEC_LC_TILES;
 }
 
 // One k_stage copy: len bytes from src (any alignment, device memory) to dst

@@ -84,19 +84,44 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint3
     return r;
 }
 
-// 16 stuffed bytes of thread t of tile `tile` (zero beyond scan_len) plus neighbours.
-struct Bytes16 {
-    uint8_t b[16];
-    int prev, next;
+// 16 stuffed bytes at scan offset `base` (< scan_len) as four dwords, with
+// the byte after them; bytes at or past scan_len read as zero.  The scan may
+// start at any byte address - a device-resident file is read where it lies,
+// no staging copy: the two aligned 16-B chunks covering the bytes are loaded
+// (the second only when it holds a scan byte, so no load leaves the file's
+// pages) and the misalignment, uniform over the image, is shifted out.
+struct Scan16 {
+    uint4 v;
+    int next;
 };
-__device__ __forceinline__ void load16(const DecDesc& d, int64_t base, Bytes16& B)
+__device__ __forceinline__ Scan16 scan16(const uint8_t* scan, int64_t scan_len, int64_t base)
 {
-    const uint4 v = *(const uint4*)(d.scan + base);  // scan copy is 16-B aligned and padded
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const uintptr_t p = (uintptr_t)(scan + base), a = p & ~(uintptr_t)15;
+    const uint32_t sh = (uint32_t)(p & 15), q = sh >> 2, b = sh & 3;
+    const bool more = a + 16 < (uintptr_t)(scan + scan_len);
+    const uint4 c0 = *(const uint4*)a;
+    uint4 c1 = *(const uint4*)(more ? a + 16 : a);  // unconditional: no branch and wait around the load
+    if (!more) c1 = make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t x[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    uint32_t y[5];
 #pragma unroll
-    for (int k = 0; k < 16; k++) B.b[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-    B.prev = base > 0 ? d.scan[base - 1] : 0;
-    B.next = d.scan[base + 16];
+    for (int k = 0; k < 5; k++) y[k] = q == 0 ? x[k] : q == 1 ? x[k + 1] : q == 2 ? x[k + 2] : x[k + 3];
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) w[k] = __builtin_amdgcn_alignbyte(y[k + 1], y[k], b);
+    Scan16 r;
+    r.next = (int)((y[4] >> (8 * b)) & 255u);
+    const int64_t rem = scan_len - base;
+    if (rem <= 16) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int64_t nb = rem - 4 * k;  // scan bytes in dword k
+            if (nb < 4) w[k] = nb <= 0 ? 0u : w[k] & ((1u << (8 * nb)) - 1);
+        }
+        r.next = 0;
+    }
+    r.v = make_uint4(w[0], w[1], w[2], w[3]);
+    return r;
 }
 
 }  // namespace
@@ -201,48 +226,71 @@ __device__ __forceinline__ Unstuff16 unstuff16(const ByteClass& c, int prev, int
 // neither 0x00, 0xFF nor an RSTn code.  Bytes from that marker on are dropped
 // by k_unstuff_scan (it recounts the marker's tile and zeroes the tiles after
 // it), so one pass over the stuffed stream finds both.  A thread whose bytes
-// hold no 0xFF (nor follow one) counts them without the per-byte rule.
+// hold no 0xFF (nor follow one) counts them without the per-byte rule.  A
+// workgroup counts DEC_UNSTUFF_TILES consecutive tiles, all their loads
+// issued first (one 4 KiB tile per workgroup left each workgroup a single
+// 16-byte load per thread in flight).
 __global__ void __launch_bounds__(256) k_unstuff_count(const DecDesc* D, DecState* S, Plan p)
 {
-    __shared__ uint32_t sh[2][4];
+    constexpr int U = DEC_UNSTUFF_TILES;
+    __shared__ uint32_t sh[U][4];
     int slot;
-    int64_t tile;
-    if (!plan_slot(p, slot, tile)) return;
+    int64_t item;
+    if (!plan_slot(p, slot, item)) return;
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
-    const int64_t base = tile * DEC_TILE + threadIdx.x * 16;
-    uint32_t nb = 0, nr = 0;
-    if (base < d.scan_len) {
-        const uint4 v = *(const uint4*)(d.scan + base);  // scan copy is 16-B aligned and padded
-        const int prev = base > 0 ? d.scan[base - 1] : 0;
-        if (!any_ff(v, prev)) {
-            nb = (uint32_t)min((int64_t)16, d.scan_len - base);
-        } else {  // branch-free rule over the 16 bytes (SWAR masks)
-            const Unstuff16 u = unstuff16(classify16(v), prev, d.scan[base + 16]);
-            const int64_t rem = d.scan_len - base;  // bytes of this thread below scan_len
-            const uint32_t valid = rem >= 16 ? 0xFFFFu : (1u << rem) - 1;
-            nb = (uint32_t)__popc(u.keep & valid) + DEC_PAD * (uint32_t)__popc(u.rst & valid);
-            nr = (uint32_t)__popc(u.rst & valid);
-            // a marker needs its next byte below scan_len
-            const uint32_t mk = u.mark & (rem - 1 >= 16 ? 0xFFFFu : (1u << (rem - 1)) - 1);
-            if (mk) atomicMin((unsigned long long*)&S[img].end, (unsigned long long)(base + __builtin_ctz(mk)));
-        }
-    }
-    // workgroup sums: wave reduction, then the four wave totals
+    const int64_t len = d.scan_len;
+    const int64_t tile0 = item * U;
+    Scan16 q[U];
+    int prev[U];
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        nb += __shfl_xor(nb, o, 64);
-        nr += __shfl_xor(nr, o, 64);
+    for (int u = 0; u < U; u++) {  // bases past the scan load its last chunk and count nothing
+        const int64_t base = (tile0 + u) * DEC_TILE + threadIdx.x * 16;
+        const int64_t bc = base < len ? base : len - 1;
+        q[u] = scan16(d.scan, len, bc);
+        prev[u] = d.scan[bc > 0 ? bc - 1 : 0];
     }
+    uint32_t cnt[U];  // output bytes (bits 0..19) + RSTn markers << 20 of this thread's 16 bytes
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int64_t base = (tile0 + u) * DEC_TILE + threadIdx.x * 16;
+        const int pv = base > 0 ? prev[u] : 0;
+        uint32_t c = 0;
+        if (base < len) {
+            if (!any_ff(q[u].v, pv)) {
+                c = (uint32_t)min((int64_t)16, len - base);
+            } else {  // branch-free rule over the 16 bytes (SWAR masks)
+                const Unstuff16 x = unstuff16(classify16(q[u].v), pv, q[u].next);
+                const int64_t rem = len - base;  // bytes of this thread below scan_len
+                const uint32_t valid = rem >= 16 ? 0xFFFFu : (1u << rem) - 1;
+                const uint32_t nr = (uint32_t)__popc(x.rst & valid);
+                c = (uint32_t)__popc(x.keep & valid) + DEC_PAD * nr + (nr << 20);
+                // a marker needs its next byte below scan_len
+                const uint32_t mk = x.mark & (rem - 1 >= 16 ? 0xFFFFu : (1u << (rem - 1)) - 1);
+                if (mk) atomicMin((unsigned long long*)&S[img].end, (unsigned long long)(base + __builtin_ctz(mk)));
+            }
+        }
+        cnt[u] = c;
+    }
+    // workgroup sums: wave reductions, then the four wave totals (a tile's
+    // bytes < 2^20, its markers < 2^12)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (lane == 0) {
-        sh[0][w] = nb;
-        sh[1][w] = nr;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        uint32_t c = cnt[u];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+        if (lane == 0) sh[u][w] = c;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        d.tile_cnt[tile] = sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3];
-        d.tile_rst[tile] = sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3];
+    if (threadIdx.x < U) {
+        const int u = threadIdx.x;
+        const int64_t tile = tile0 + u;
+        if (tile < d.ntiles) {
+            const uint32_t c = sh[u][0] + sh[u][1] + sh[u][2] + sh[u][3];
+            d.tile_cnt[tile] = c & 0xFFFFFu;
+            d.tile_rst[tile] = c >> 20;
+        }
     }
 }
 
@@ -267,7 +315,8 @@ __global__ void __launch_bounds__(1024) k_unstuff_scan(const DecDesc* D, DecStat
             const int64_t i = te * DEC_TILE + threadIdx.x * (DEC_TILE / 1024) + k;
             if (i < end) {
                 int rst;
-                nb += (uint32_t)dec_unstuff_rule(i > 0 ? d.scan[i - 1] : 0, d.scan[i], d.scan[i + 1], &rst);
+                nb += (uint32_t)dec_unstuff_rule(i > 0 ? d.scan[i - 1] : 0, d.scan[i],
+                                                 i + 1 < d.scan_len ? d.scan[i + 1] : 0, &rst);
                 nr += (uint32_t)rst;
             }
         }
@@ -319,116 +368,136 @@ __global__ void __launch_bounds__(1024) k_unstuff_scan(const DecDesc* D, DecStat
     }
 }
 
-// Compact one tile: each thread applies the unstuffing rule to its 16 bytes
-// (fully unrolled, no dynamic register indexing) and places its output bytes
-// at its workgroup-local offset in a zeroed LDS copy of the tile's output - a
-// thread without 0xFF bytes as four shifted dwords (the two partial ones ORed
-// in), the others byte by byte - and the workgroup then stores the tile's
-// output as aligned dwords (funnel-shifted out of LDS), the unaligned head and
-// tail bytes by single lanes.
+// Compact DEC_UNSTUFF_TILES consecutive tiles (all their loads issued
+// first), one after the other: each thread applies the unstuffing rule to its
+// 16 bytes (fully unrolled, no dynamic register indexing) and places its
+// output bytes at its workgroup-local offset in a zeroed LDS copy of the
+// tile's output - a thread without 0xFF bytes as four shifted dwords (the two
+// partial ones ORed in), the others byte by byte - and the workgroup then
+// stores the tile's output as aligned dwords (funnel-shifted out of LDS), the
+// unaligned head and tail bytes by single lanes.
 __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const DecState* S, Plan p)
 {
+    constexpr int U = DEC_UNSTUFF_TILES;
     __shared__ uint32_t sh[8];
     __shared__ uint32_t bufw[(DEC_TILE / 2 * DEC_PAD + 64) / 4];  // worst case: an RSTn marker every 2 bytes
     uint8_t* const buf = (uint8_t*)bufw;
     int slot;
-    int64_t tile;
-    if (!plan_slot(p, slot, tile)) return;
+    int64_t item;
+    if (!plan_slot(p, slot, item)) return;
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
-    const int64_t base = tile * DEC_TILE + threadIdx.x * 16;
-    const int64_t end = S[img].end;
-    if (tile * DEC_TILE >= end) return;  // workgroup-uniform: nothing of this tile is data
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    bool plain = false;  // 16 data bytes, no 0xFF among them or before them
-    uint32_t keep = 0, rstm = 0;
-    if (base < end) {
-        v = *(const uint4*)(d.scan + base);
-        const int prev = base > 0 ? d.scan[base - 1] : 0;
-        plain = base + 16 <= end && !any_ff(v, prev);
-        if (!plain) {  // the rule over the 16 bytes as masks (bytes from `end` on drop out)
-            const Unstuff16 u = unstuff16(classify16(v), prev, d.scan[base + 16]);
-            const int64_t rem = end - base;
-            const uint32_t valid = rem >= 16 ? 0xFFFFu : (1u << rem) - 1;
-            keep = u.keep & valid;
-            rstm = u.rst & valid;
-        }
-    }
-    const uint32_t nr = (uint32_t)__popc(rstm);
-    const uint32_t nb = plain ? 16u : (uint32_t)__popc(keep) + DEC_PAD * nr;
-    uint32_t tb, tr;
-    uint32_t ob = block_exscan<256>(nb, sh, tb);
-    uint32_t orr = block_exscan<256>(nr, sh, tr) + d.tile_rst[tile];
-    const uint32_t tile_off = d.tile_cnt[tile];
-    for (uint32_t k = threadIdx.x; k < (tb + 7) / 4; k += 256) bufw[k] = 0;
-    __syncthreads();
-    if (plain) {
-        const uint32_t s8 = (ob & 3) * 8;
-        uint32_t* wp = bufw + (ob >> 2);
-        if (s8 == 0) {
-            wp[0] = v.x; wp[1] = v.y; wp[2] = v.z; wp[3] = v.w;
-        } else {
-            atomicOr(wp, v.x << s8);
-            wp[1] = (v.x >> (32 - s8)) | (v.y << s8);
-            wp[2] = (v.y >> (32 - s8)) | (v.z << s8);
-            wp[3] = (v.z >> (32 - s8)) | (v.w << s8);
-            atomicOr(wp + 4, v.w >> (32 - s8));
-        }
-    } else if (nr == 0 && nb > 0) {
-        // drop the bytes outside `keep` (highest first, so lower positions stay
-        // put: usually one stuffed zero), then OR the nb bytes in at ob
-        uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        uint32_t drop = ~keep & 0xFFFFu;
-        while (drop) {
-            const int k = 31 - __builtin_clz(drop);
-            drop &= ~(1u << k);
-            const int q = k >> 2;
-            const uint32_t low = (1u << (8 * (k & 3))) - 1u;  // bytes of dword q below k
+    const int64_t end = S[img].end, len = d.scan_len;
+    const int64_t tile0 = item * U;
+    if (tile0 * DEC_TILE >= end) return;  // workgroup-uniform: nothing of these tiles is data
+    Scan16 q[U];
+    int prev[U];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t up = j < 3 ? w[j + 1] << 24 : 0u;
-                if (j > q) w[j] = (w[j] >> 8) | up;
-                else if (j == q) w[j] = (w[j] & low) | ((w[j] >> 8) & ~low) | up;
+    for (int u = 0; u < U; u++) {  // bases past the scan load its last chunk and place nothing
+        const int64_t base = (tile0 + u) * DEC_TILE + threadIdx.x * 16;
+        const int64_t bc = base < len ? base : len - 1;
+        q[u] = scan16(d.scan, len, bc);
+        prev[u] = d.scan[bc > 0 ? bc - 1 : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int64_t tile = tile0 + u;
+        // workgroup-uniform; the scan's first barrier also orders the previous
+        // tile's buffer reads before this tile's zeroing
+        if (tile * DEC_TILE >= end) break;
+        const int64_t base = tile * DEC_TILE + threadIdx.x * 16;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        bool plain = false;  // 16 data bytes, no 0xFF among them or before them
+        uint32_t keep = 0, rstm = 0;
+        if (base < end) {
+            v = q[u].v;
+            const int prev_b = base > 0 ? prev[u] : 0;
+            plain = base + 16 <= end && !any_ff(v, prev_b);
+            if (!plain) {  // the rule over the 16 bytes as masks (bytes from `end` on drop out)
+                const Unstuff16 x = unstuff16(classify16(v), prev_b, q[u].next);
+                const int64_t rem = end - base;
+                const uint32_t valid = rem >= 16 ? 0xFFFFu : (1u << rem) - 1;
+                keep = x.keep & valid;
+                rstm = x.rst & valid;
             }
         }
-        const uint32_t s8 = (ob & 3) * 8;
-        uint32_t* wp = bufw + (ob >> 2);
-        atomicOr(wp, w[0] << s8);
+        const uint32_t nr = (uint32_t)__popc(rstm);
+        const uint32_t nb = plain ? 16u : (uint32_t)__popc(keep) + DEC_PAD * nr;
+        uint32_t tot;  // one scan of bytes (bits 0..19) and RSTn markers (<< 20)
+        const uint32_t ex = block_exscan<256>(nb | (nr << 20), sh, tot);
+        const uint32_t tb = tot & 0xFFFFFu;
+        uint32_t ob = ex & 0xFFFFFu;
+        uint32_t orr = (ex >> 20) + d.tile_rst[tile];
+        const uint32_t tile_off = d.tile_cnt[tile];
+        for (uint32_t k = threadIdx.x; k < (tb + 7) / 4; k += 256) bufw[k] = 0;
+        __syncthreads();
+        if (plain) {
+            const uint32_t s8 = (ob & 3) * 8;
+            uint32_t* wp = bufw + (ob >> 2);
+            if (s8 == 0) {
+                wp[0] = v.x; wp[1] = v.y; wp[2] = v.z; wp[3] = v.w;
+            } else {
+                atomicOr(wp, v.x << s8);
+                wp[1] = (v.x >> (32 - s8)) | (v.y << s8);
+                wp[2] = (v.y >> (32 - s8)) | (v.z << s8);
+                wp[3] = (v.z >> (32 - s8)) | (v.w << s8);
+                atomicOr(wp + 4, v.w >> (32 - s8));
+            }
+        } else if (nr == 0 && nb > 0) {
+            // drop the bytes outside `keep` (highest first, so lower positions stay
+            // put: usually one stuffed zero), then OR the nb bytes in at ob
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            uint32_t drop = ~keep & 0xFFFFu;
+            while (drop) {
+                const int k = 31 - __builtin_clz(drop);
+                drop &= ~(1u << k);
+                const int q = k >> 2;
+                const uint32_t low = (1u << (8 * (k & 3))) - 1u;  // bytes of dword q below k
 #pragma unroll
-        for (int j = 1; j < 4; j++) atomicOr(wp + j, (w[j] << s8) | (s8 ? w[j - 1] >> (32 - s8) : 0u));
-        if (s8) atomicOr(wp + 4, w[3] >> (32 - s8));
-    } else if (nr > 0) {  // RSTn codes (restart intervals): byte by byte
-        Bytes16 B;
-        load16(d, base, B);
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t up = j < 3 ? w[j + 1] << 24 : 0u;
+                    if (j > q) w[j] = (w[j] >> 8) | up;
+                    else if (j == q) w[j] = (w[j] & low) | ((w[j] >> 8) & ~low) | up;
+                }
+            }
+            const uint32_t s8 = (ob & 3) * 8;
+            uint32_t* wp = bufw + (ob >> 2);
+            atomicOr(wp, w[0] << s8);
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            if ((rstm >> k) & 1) {
-                for (int q = 0; q < DEC_PAD; q++) buf[ob + q] = 0xFF;
-                ob += DEC_PAD;
-                if (orr + 1 < (uint32_t)d.nseg_max) d.seg[orr + 1] = tile_off + ob;
-                orr++;
-            } else if ((keep >> k) & 1) {
-                buf[ob++] = B.b[k];
+            for (int j = 1; j < 4; j++) atomicOr(wp + j, (w[j] << s8) | (s8 ? w[j - 1] >> (32 - s8) : 0u));
+            if (s8) atomicOr(wp + 4, w[3] >> (32 - s8));
+        } else if (nr > 0) {  // RSTn codes (restart intervals): byte by byte
+            const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                if ((rstm >> k) & 1) {
+                    for (int q = 0; q < DEC_PAD; q++) buf[ob + q] = 0xFF;
+                    ob += DEC_PAD;
+                    if (orr + 1 < (uint32_t)d.nseg_max) d.seg[orr + 1] = tile_off + ob;
+                    orr++;
+                } else if ((keep >> k) & 1) {
+                    buf[ob++] = (uint8_t)(vw[k >> 2] >> (8 * (k & 3)));
+                }
             }
         }
+        __syncthreads();
+        // tile output = global bytes [tile_off, tile_off + tb)
+        const uint32_t head = min((4u - (tile_off & 3u)) & 3u, tb);
+        if (threadIdx.x < head && (int64_t)(tile_off + threadIdx.x) < d.ent_cap)
+            d.ent[tile_off + threadIdx.x] = buf[threadIdx.x];
+        const uint32_t nw = (tb - head) >> 2;         // whole aligned dwords
+        const uint32_t sh8 = head;                    // local byte of the first dword: head + 4k
+        uint32_t* const dstw = (uint32_t*)(d.ent + tile_off + head);  // 4-byte aligned
+        const int64_t cap_w = (d.ent_cap - (int64_t)(tile_off + head)) >> 2;
+        for (uint32_t k = threadIdx.x; k < nw; k += 256) {
+            const uint32_t lb = head + 4 * k;
+            const uint32_t val = __builtin_amdgcn_alignbyte(bufw[(lb >> 2) + 1], bufw[lb >> 2], sh8);
+            if ((int64_t)k < cap_w) dstw[k] = val;
+        }
+        const uint32_t t0 = head + 4 * nw;
+        if (threadIdx.x < tb - t0 && (int64_t)(tile_off + t0 + threadIdx.x) < d.ent_cap)
+            d.ent[tile_off + t0 + threadIdx.x] = buf[t0 + threadIdx.x];
     }
-    __syncthreads();
-    // tile output = global bytes [tile_off, tile_off + tb)
-    const uint32_t head = min((4u - (tile_off & 3u)) & 3u, tb);
-    if (threadIdx.x < head && (int64_t)(tile_off + threadIdx.x) < d.ent_cap)
-        d.ent[tile_off + threadIdx.x] = buf[threadIdx.x];
-    const uint32_t nw = (tb - head) >> 2;         // whole aligned dwords
-    const uint32_t sh8 = head;                    // local byte of the first dword: head + 4k
-    uint32_t* const dstw = (uint32_t*)(d.ent + tile_off + head);  // 4-byte aligned
-    const int64_t cap_w = (d.ent_cap - (int64_t)(tile_off + head)) >> 2;
-    for (uint32_t k = threadIdx.x; k < nw; k += 256) {
-        const uint32_t lb = head + 4 * k;
-        const uint32_t val = __builtin_amdgcn_alignbyte(bufw[(lb >> 2) + 1], bufw[lb >> 2], sh8);
-        if ((int64_t)k < cap_w) dstw[k] = val;
-    }
-    const uint32_t t0 = head + 4 * nw;
-    if (threadIdx.x < tb - t0 && (int64_t)(tile_off + t0 + threadIdx.x) < d.ent_cap)
-        d.ent[tile_off + t0 + threadIdx.x] = buf[t0 + threadIdx.x];
 }
 
 // ------------------------------------------------------------ entropy decode
@@ -847,19 +916,21 @@ __device__ __forceinline__ uint32_t idct_limit(int32_t v)
 
 // jpeg_idct_islow of one block by 8 threads (thread r owns coefficient row r,
 // then column r, then output row r); ws = this block's 8 x 9 LDS workspace.
-// Returns output row r as 8 range-limited samples packed in two dwords.  The
-// caller's 8 threads must all reach the barriers (real == false: no work).
-__device__ __forceinline__ uint2 idct_block_row(const DecDesc& d, int64_t b, int comp, int r, bool real,
-                                                int32_t* ws)
+// q = the block's quantised coefficient row r (natural order), dc = its DC
+// value, qt = dequantisation row r.  Returns output row r as 8 range-limited
+// samples packed in two dwords.  The caller's 8 threads must all reach the
+// barriers (real == false: no work).
+__device__ __forceinline__ uint2 idct_row_of(const uint4& q, int32_t dc, const uint4& qt, int r, bool real,
+                                             int32_t* ws)
 {
     int32_t v[8];
     if (real) {
-        const uint4 q = *(const uint4*)(d.coefs + b * 64 + r * 8);
         const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-        const uint16_t* qt = d.tab->qt[comp] + r * 8;
+        const uint32_t t[4] = {qt.x, qt.y, qt.z, qt.w};
 #pragma unroll
-        for (int c = 0; c < 8; c++) v[c] = (int32_t)(int16_t)(w[c >> 1] >> (16 * (c & 1))) * (int32_t)qt[c];
-        if (r == 0) v[0] = d.dc[b] * (int32_t)qt[0];
+        for (int c = 0; c < 8; c++)
+            v[c] = (int32_t)(int16_t)(w[c >> 1] >> (16 * (c & 1))) * (int32_t)((t[c >> 1] >> (16 * (c & 1))) & 0xFFFFu);
+        if (r == 0) v[0] = dc * (int32_t)(qt.x & 0xFFFFu);
 #pragma unroll
         for (int c = 0; c < 8; c++) ws[r * 9 + c] = v[c];
     }
@@ -886,9 +957,56 @@ __device__ __forceinline__ uint2 idct_block_row(const DecDesc& d, int64_t b, int
     return make_uint2(lo, hi);
 }
 
-// 8 threads per block, 32 blocks per workgroup, one image per workgroup, into
-// the component planes.  fuse420 images: chroma blocks only (their luma IDCT
-// runs inside k_dec_luma_color_420).
+__device__ __forceinline__ uint2 idct_block_row(const DecDesc& d, int64_t b, int comp, int r, bool real,
+                                                int32_t* ws)
+{
+    uint4 q = make_uint4(0u, 0u, 0u, 0u), qt = q;
+    int32_t dc = 0;
+    if (real) {
+        q = *(const uint4*)(d.coefs + b * 64 + r * 8);
+        qt = *(const uint4*)(d.tab->qt[comp] + r * 8);
+        dc = d.dc[b];
+    }
+    return idct_row_of(q, dc, qt, r, real, ws);
+}
+
+// 8 threads per block, 32 blocks per tile, DEC_IDCT_TILES consecutive tiles
+// per workgroup (the next tile's coefficient row, DC value and dequantisation
+// row in registers while the current one transforms), one image per
+// workgroup, into the component planes.  fuse420 images: chroma blocks only
+// (their luma IDCT runs inside k_dec_luma_color_420).
+struct IdctBlk {
+    int64_t b;
+    int comp, bx, by;
+    bool real;
+};
+__device__ __forceinline__ IdctBlk idct_blk(const DecDesc& d, int i)
+{
+    int m, k;
+    if (d.fuse420) {
+        m = i >> 1;
+        k = d.nby + (i & 1);
+    } else {
+        m = i / d.nbmcu;
+        k = i - m * d.nbmcu;
+    }
+    IdctBlk r{(int64_t)m * d.nbmcu + k, 0, 0, 0, false};
+    const bool valid = r.b < d.nblocks;
+    if (valid) {
+        const int mx = m % d.mcux, my = m / d.mcux;
+        if (k < d.nby) {
+            r.bx = mx * d.hs + k % d.hs;
+            r.by = my * d.vs + k / d.hs;
+        } else {
+            r.comp = k - d.nby + 1;
+            r.bx = mx;
+            r.by = my;
+        }
+    }
+    r.real = valid && r.bx * 8 < d.pw[r.comp] && r.by * 8 < d.ph[r.comp];  // dummy blocks: no IDCT (jdcoefct.c)
+    return r;
+}
+
 __global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecState* S, Plan p)
 {
     __shared__ int32_t ws[32][8 * 9];
@@ -899,32 +1017,43 @@ __global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecSta
     const DecDesc& d = D[img];
     if (S[img].status) return;
     const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;
-    const int i = (int)wg * 32 + lb;  // < 2^31: at most 65535^2 * 3 / 64 blocks
-    int m, k;
-    if (d.fuse420) {
-        m = i >> 1;
-        k = d.nby + (i & 1);
-    } else {
-        m = i / d.nbmcu;
-        k = i - m * d.nbmcu;
-    }
-    const int64_t b = (int64_t)m * d.nbmcu + k;
-    const bool valid = b < d.nblocks;
-    int comp = 0, bx = 0, by = 0;
-    if (valid) {
-        const int mx = m % d.mcux, my = m / d.mcux;
-        if (k < d.nby) {
-            bx = mx * d.hs + k % d.hs;
-            by = my * d.vs + k / d.hs;
-        } else {
-            comp = k - d.nby + 1;
-            bx = mx;
-            by = my;
+    const int ntile = (int)(d.fuse420 ? (2 * (int64_t)d.mcux * d.mcuy + 31) / 32 : (d.nblocks + 31) / 32);
+    const ICX_GLOBAL int16_t* const coefs = (const ICX_GLOBAL int16_t*)d.coefs;
+    const ICX_GLOBAL int32_t* const dcs = (const ICX_GLOBAL int32_t*)d.dc;
+    const ICX_GLOBAL uint16_t* const qts = (const ICX_GLOBAL uint16_t*)d.tab->qt[0];
+    ICX_GLOBAL uint8_t* const planes[3] = {(ICX_GLOBAL uint8_t*)d.plane[0], (ICX_GLOBAL uint8_t*)d.plane[1],
+                                           (ICX_GLOBAL uint8_t*)d.plane[2]};
+    const int pw[3] = {d.pw[0], d.pw[1], d.pw[2]};
+    int tile = (int)wg * DEC_IDCT_TILES;
+    if (tile >= ntile) return;
+    // i < 2^31: at most 65535^2 * 3 / 64 blocks
+    IdctBlk cb = idct_blk(d, tile * 32 + lb);
+    const int64_t b0 = cb.b < d.nblocks ? cb.b : 0;
+    uint4 q = *(const ICX_GLOBAL uint4*)(coefs + b0 * 64 + r * 8);
+    int32_t dc = dcs[b0];
+    uint4 qt = *(const ICX_GLOBAL uint4*)(qts + cb.comp * 64 + r * 8);
+    for (int it = 0; it < DEC_IDCT_TILES; it++, tile++) {
+        if (tile >= ntile) break;  // workgroup-uniform
+        IdctBlk nb = cb;
+        uint4 nq = q, nqt = qt;
+        int32_t ndc = dc;
+        if (it + 1 < DEC_IDCT_TILES && tile + 1 < ntile) {
+            nb = idct_blk(d, (tile + 1) * 32 + lb);
+            const int64_t bb = nb.b < d.nblocks ? nb.b : 0;
+            nq = *(const ICX_GLOBAL uint4*)(coefs + bb * 64 + r * 8);
+            ndc = dcs[bb];
+            nqt = *(const ICX_GLOBAL uint4*)(qts + nb.comp * 64 + r * 8);
         }
+        const uint2 row = idct_row_of(q, dc, qt, r, cb.real, ws[lb]);
+        // no barrier before the next tile: a thread's pass 2 reads only its own
+        // workspace row, which only it rewrites, and pass 1 of the next tile
+        // comes after idct_row_of's first barrier
+        if (cb.real) *(ICX_GLOBAL uint2*)(planes[cb.comp] + (int64_t)(cb.by * 8 + r) * pw[cb.comp] + cb.bx * 8) = row;
+        cb = nb;
+        q = nq;
+        qt = nqt;
+        dc = ndc;
     }
-    const bool real = valid && bx * 8 < d.pw[comp] && by * 8 < d.ph[comp];  // dummy blocks: no IDCT (jdcoefct.c)
-    const uint2 row = idct_block_row(d, b, comp, r, real, ws[lb]);
-    if (real) *(uint2*)(d.plane[comp] + (int64_t)(by * 8 + r) * d.pw[comp] + bx * 8) = row;
 }
 
 // ----------------------------------------------------------- colour output
@@ -1004,115 +1133,166 @@ __global__ void __launch_bounds__(256) k_dec_color(const DecDesc* D, const DecSt
 }
 
 // s == 1, 4:2:0 with fancy upsampling (the JDK decode of nearly every photo):
-// one workgroup per MCU row x LC_NM MCUs (16 x 128 output pixels).  The 32
-// luma blocks are inverse-transformed straight into an LDS tile (the luma
-// plane never reaches HBM); chroma rows cy0-1 .. cy0+8 (edge-replicated,
-// jdmainct.c context rows) and columns cx0-4 .. cx0+67 of both chroma planes
-// (written by k_dec_idct) are staged as dwords; each thread then converts a
-// 4 x 2 pixel tile from the 3 x 4 chroma neighbourhood it shares
-// (h2v2_fancy_upsample + ycc_rgb_convert).
-constexpr int LC_NM = 8;
+// a tile is one MCU row x LC_NM MCUs (16 x 128 output pixels).  The 32 luma
+// blocks are inverse-transformed straight into an LDS tile (the luma plane
+// never reaches HBM); chroma rows cy0-1 .. cy0+8 (edge-replicated, jdmainct.c
+// context rows) and columns cx0-4 .. cx0+67 of both chroma planes (written by
+// k_dec_idct) are staged as dwords; each thread then converts a 4 x 2 pixel
+// tile from the 3 x 4 chroma neighbourhood it shares (h2v2_fancy_upsample +
+// ycc_rgb_convert).  A workgroup runs LC_T consecutive tiles with the next
+// tile's coefficient, DC and chroma loads in registers while it transforms
+// and converts the current one, so the HBM reads of a CU's workgroups stay in
+// flight through their barrier phases (one tile per workgroup left each
+// workgroup's loads exposed, then a few microseconds of compute with none).
+constexpr int LC_NM = 8;  // dec_lc_items
 constexpr int LC_W = 16 * LC_NM;      // output columns per tile
 constexpr int LC_CD = LC_W / 8 + 2;   // chroma dwords per staged row
+constexpr int LC_CE = 2 * 10 * LC_CD; // chroma dwords per tile (both planes)
+constexpr int LC_T = DEC_LC_TILES;    // tiles per workgroup
+
+struct LcLoad {
+    uint4 q;         // coefficient row r of this thread's luma block
+    int32_t dc;      // its DC value
+    uint32_t c[2];   // chroma dwords e = t, t + 256 of the tile
+};
+
+// The image's fields the tile loop uses, read once into registers (the
+// loop's byte stores may alias the descriptor as far as the compiler knows,
+// and a reload after each store would wait for the prefetch in flight).
+struct LcImg {
+    const ICX_GLOBAL int16_t* coefs;  // global address space: loads that wait on vmcnt alone
+    const ICX_GLOBAL int32_t* dc;
+    const ICX_GLOBAL uint8_t* plane[2];
+    int pitch[2];
+    int nbmcu, mcux, ch, pwd, tpr;
+};
+
+__device__ __forceinline__ void lc_fetch(const LcImg& g, int item, int t, LcLoad& L)
+{
+    const int my = item / g.tpr, mx0 = (item - my * g.tpr) * LC_NM;
+    const int lb = t >> 3, r = t & 7, k = lb & 3;
+    int mx = mx0 + (lb >> 2);
+    mx = mx < g.mcux ? mx : g.mcux - 1;  // blocks past the last MCU: any loadable block, not transformed
+    const int64_t b = ((int64_t)my * g.mcux + mx) * g.nbmcu + k;
+    L.q = *(const ICX_GLOBAL uint4*)(g.coefs + b * 64 + r * 8);
+    L.dc = g.dc[b];
+    const int cx0 = mx0 * 8, cy0 = my * 8;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        int e = t + 256 * h;
+        e = e < LC_CE ? e : LC_CE - 1;
+        const int comp = e / (10 * LC_CD), rem = e - comp * (10 * LC_CD);
+        const int j = rem / LC_CD, q = rem - j * LC_CD;
+        int rr = cy0 - 1 + j;
+        rr = rr < 0 ? 0 : rr > g.ch - 1 ? g.ch - 1 : rr;
+        int dw = (cx0 >> 2) - 1 + q;
+        dw = dw < 0 ? 0 : dw > g.pwd - 1 ? g.pwd - 1 : dw;  // clamped dwords hold only unused columns
+        L.c[h] = ((const ICX_GLOBAL uint32_t*)(g.plane[comp] + (int64_t)rr * g.pitch[comp]))[dw];
+    }
+}
+
 __global__ void __launch_bounds__(256) k_dec_luma_color_420(const DecDesc* D, const DecState* S, Plan p)
 {
     __shared__ int32_t ws[32][8 * 9];
     __shared__ __attribute__((aligned(16))) uint32_t ly[16][LC_W / 4];
-    __shared__ uint32_t lc[2][10][LC_CD];  // [cb|cr][chroma row cy0-1+j][dword]; byte q <-> column cx0-4+q
+    __shared__ uint32_t lcb[2][LC_CE];  // per tile parity: [cb|cr][chroma row cy0-1+j][dword]; byte q <-> column cx0-4+q
     int slot;
     int64_t wg;
     // the image's state and descriptor fields are read before the exits, so
-    // their loads go out together with the plan's (a chain of dependent loads
-    // otherwise, long against a workgroup's few microseconds of work)
+    // their loads go out together with the plan's
     const bool in = plan_slot(p, slot, wg);
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
-    const int status = S[img].status, mcux = d.mcux, cw = d.cw[1], ch = d.ch[1], pwd = d.pw[1] >> 2;
-    const int pw0 = d.pw[0], ph0 = d.ph[0], nbmcu = d.nbmcu, ow = d.ow, oh = d.oh;
-    const uint8_t* plane1 = d.plane[1];
-    const uint8_t* plane2 = d.plane[2];
-    const int pitch1 = d.pw[1], pitch2 = d.pw[2];
+    const int status = S[img].status, mcux = d.mcux, mcuy = d.mcuy, cw = d.cw[1];
+    const int pw0 = d.pw[0], ph0 = d.ph[0], ow = d.ow, oh = d.oh, ostride = d.ostride;
+    ICX_GLOBAL uint8_t* const out = (ICX_GLOBAL uint8_t*)d.out;
+    const LcImg g{(const ICX_GLOBAL int16_t*)d.coefs, (const ICX_GLOBAL int32_t*)d.dc,
+                  {(const ICX_GLOBAL uint8_t*)d.plane[1], (const ICX_GLOBAL uint8_t*)d.plane[2]}, {d.pw[1], d.pw[2]},
+                  d.nbmcu, mcux, d.ch[1], d.pw[1] >> 2, (mcux + LC_NM - 1) / LC_NM};
+    const ICX_GLOBAL uint16_t* const qtab = (const ICX_GLOBAL uint16_t*)d.tab->qt[0];
     if (!in || status) return;
-    const int tpr = (mcux + LC_NM - 1) / LC_NM;
-    const int item = (int)wg;
-    const int my = item / tpr, mx0 = (item - my * tpr) * LC_NM;
+    const int tpr = g.tpr, ntile = tpr * mcuy;
     const int t = threadIdx.x;
-    // chroma staging first: its loads overlap the luma IDCT
-    const int cx0 = mx0 * 8, cy0 = my * 8;
-    for (int e = t; e < 2 * 10 * LC_CD; e += 256) {
-        const int comp = e / (10 * LC_CD), rem = e - comp * (10 * LC_CD);
-        const int j = rem / LC_CD, q = rem - j * LC_CD;
-        int rr = cy0 - 1 + j;
-        rr = rr < 0 ? 0 : rr > ch - 1 ? ch - 1 : rr;
-        int dw = (cx0 >> 2) - 1 + q;
-        dw = dw < 0 ? 0 : dw > pwd - 1 ? pwd - 1 : dw;  // clamped dwords hold only unused columns
-        lc[comp][j][q] = ((const uint32_t*)((comp ? plane2 : plane1) + (int64_t)rr * (comp ? pitch2 : pitch1)))[dw];
-    }
-    {  // luma: block lb = MCU lb / 4, block k = lb % 4 of it
-        const int lb = t >> 3, r = t & 7, mx = mx0 + (lb >> 2), k = lb & 3;
-        const int bx = mx * 2 + (k & 1), by = my * 2 + (k >> 1);
-        const bool real = mx < mcux && bx * 8 < pw0 && by * 8 < ph0;
-        const int64_t b = ((int64_t)my * mcux + mx) * nbmcu + k;
-        const uint2 row = idct_block_row(d, b, 0, r, real, ws[lb]);
-        *(uint2*)&ly[(k >> 1) * 8 + r][(lb >> 2) * 4 + (k & 1) * 2] = row;
-    }
-    __syncthreads();
-    const int rp = t >> 5, xt = 4 * (t & 31);  // chroma row cy0 + rp -> output rows 2rp, 2rp+1; columns xt..xt+3
-    const int x0 = mx0 * 16;
-    const int n = ow - x0 - xt;
-    const int y0 = my * 16 + 2 * rp;
-    if (n <= 0 || y0 >= oh) return;
-    const int i0 = (x0 + xt) >> 1;       // chroma columns i0, i0 + 1
-    const int li = (xt >> 1) + 4;        // local byte of i0
-    int cv[2][2][4];                     // [comp][top|bottom row][column]
-#pragma unroll
-    for (int comp = 0; comp < 2; comp++) {
-        const uint8_t* c0 = (const uint8_t*)lc[comp][rp];  // rows cy0+rp-1, cy0+rp, cy0+rp+1
-        const uint8_t* c1 = c0 + LC_CD * 4;
-        const uint8_t* c2 = c1 + LC_CD * 4;
-        int cs_t[4], cs_b[4];  // column sums for i0-1 .. i0+2
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int a = c1[li - 1 + k] * 3;
-            cs_t[k] = a + c0[li - 1 + k];
-            cs_b[k] = a + c2[li - 1 + k];
+    int item = (int)wg * LC_T;
+    if (item >= ntile) return;
+    const uint4 qt = *(const ICX_GLOBAL uint4*)(qtab + (t & 7) * 8);
+    LcLoad cur;
+    lc_fetch(g, item, t, cur);
+    for (int it = 0; it < LC_T; it++, item++) {
+        if (item >= ntile) break;  // workgroup-uniform
+        LcLoad nxt = cur;
+        if (it + 1 < LC_T && item + 1 < ntile) lc_fetch(g, item + 1, t, nxt);
+        const int my = item / tpr, mx0 = (item - my * tpr) * LC_NM;
+        uint32_t* lc = lcb[it & 1];  // the previous tile's colour pass may still read the other one
+        lc[t] = cur.c[0];
+        if (t + 256 < LC_CE) lc[t + 256] = cur.c[1];
+        {  // luma: block lb = MCU lb / 4, block k = lb % 4 of it
+            const int lb = t >> 3, r = t & 7, mx = mx0 + (lb >> 2), k = lb & 3;
+            const int bx = mx * 2 + (k & 1), by = my * 2 + (k >> 1);
+            const bool real = mx < mcux && bx * 8 < pw0 && by * 8 < ph0;
+            const uint2 row = idct_row_of(cur.q, cur.dc, qt, r, real, ws[lb]);
+            *(uint2*)&ly[(k >> 1) * 8 + r][(lb >> 2) * 4 + (k & 1) * 2] = row;
         }
+        __syncthreads();
+        const int rp = t >> 5, xt = 4 * (t & 31);  // chroma row cy0 + rp -> output rows 2rp, 2rp+1; columns xt..xt+3
+        const int x0 = mx0 * 16;
+        const int n = ow - x0 - xt;
+        const int y0 = my * 16 + 2 * rp;
+        if (n > 0 && y0 < oh) {
+            const int i0 = (x0 + xt) >> 1;       // chroma columns i0, i0 + 1
+            const int li = (xt >> 1) + 4;        // local byte of i0
+            int cv[2][2][4];                     // [comp][top|bottom row][column]
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int* cs = h ? cs_b : cs_t;
+            for (int comp = 0; comp < 2; comp++) {
+                const uint8_t* c0 = (const uint8_t*)(lc + comp * 10 * LC_CD + rp * LC_CD);  // rows cy0+rp-1 .. +1
+                const uint8_t* c1 = c0 + LC_CD * 4;
+                const uint8_t* c2 = c1 + LC_CD * 4;
+                int cs_t[4], cs_b[4];  // column sums for i0-1 .. i0+2
 #pragma unroll
-            for (int u = 0; u < 2; u++) {  // chroma column i0 + u -> output columns 2u, 2u + 1
-                const int i = i0 + u, c = cs[1 + u];
-                cv[comp][h][2 * u] = i == 0 ? (c * 4 + 8) >> 4 : (c * 3 + cs[u] + 8) >> 4;
-                cv[comp][h][2 * u + 1] = i == cw - 1 ? (c * 4 + 7) >> 4 : (c * 3 + cs[2 + u] + 7) >> 4;
+                for (int k = 0; k < 4; k++) {
+                    const int a = c1[li - 1 + k] * 3;
+                    cs_t[k] = a + c0[li - 1 + k];
+                    cs_b[k] = a + c2[li - 1 + k];
+                }
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int* cs = h ? cs_b : cs_t;
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {  // chroma column i0 + u -> output columns 2u, 2u + 1
+                        const int i = i0 + u, c = cs[1 + u];
+                        cv[comp][h][2 * u] = i == 0 ? (c * 4 + 8) >> 4 : (c * 3 + cs[u] + 8) >> 4;
+                        cv[comp][h][2 * u + 1] = i == cw - 1 ? (c * 4 + 7) >> 4 : (c * 3 + cs[2 + u] + 7) >> 4;
+                    }
+                }
+            }
+            const int m = n < 4 ? n : 4;
+            const int rows = oh - y0 < 2 ? 1 : 2;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {  // unrolled: cv stays in registers
+                if (h >= rows) break;
+                const uint32_t yq = ly[2 * rp + h][xt >> 2];
+                uint32_t w[3] = {0, 0, 0};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int yy = (yq >> (8 * k)) & 255;
+                    const int cb = cv[0][h][k] - 128, cr = cv[1][h][k] - 128;
+                    const uint32_t B = clamp255(yy + ((116130 * cb + 32768) >> 16));
+                    const uint32_t G = clamp255(yy + ((-22554 * cb + 32768 - 46802 * cr) >> 16));
+                    const uint32_t R = clamp255(yy + ((91881 * cr + 32768) >> 16));
+                    const int o = 3 * k;  // byte offset inside the 12-byte group
+                    w[o >> 2] |= B << (8 * (o & 3));
+                    w[(o + 1) >> 2] |= G << (8 * ((o + 1) & 3));
+                    w[(o + 2) >> 2] |= R << (8 * ((o + 2) & 3));
+                }
+                ICX_GLOBAL uint8_t* o = out + (int64_t)(y0 + h) * ostride + (int64_t)(x0 + xt) * 3;
+                if (m == 4 && (((uintptr_t)o) & 3) == 0) {
+                    *(ICX_GLOBAL uint3*)o = make_uint3(w[0], w[1], w[2]);
+                } else {
+                    for (int k = 0; k < 3 * m; k++) o[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+                }
             }
         }
-    }
-    const int m = n < 4 ? n : 4;
-    const int rows = oh - y0 < 2 ? 1 : 2;
-#pragma unroll
-    for (int h = 0; h < 2; h++) {  // unrolled: cv stays in registers
-        if (h >= rows) break;
-        const uint32_t yq = ly[2 * rp + h][xt >> 2];
-        uint32_t w[3] = {0, 0, 0};
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int yy = (yq >> (8 * k)) & 255;
-            const int cb = cv[0][h][k] - 128, cr = cv[1][h][k] - 128;
-            const uint32_t B = clamp255(yy + ((116130 * cb + 32768) >> 16));
-            const uint32_t G = clamp255(yy + ((-22554 * cb + 32768 - 46802 * cr) >> 16));
-            const uint32_t R = clamp255(yy + ((91881 * cr + 32768) >> 16));
-            const int o = 3 * k;  // byte offset inside the 12-byte group
-            w[o >> 2] |= B << (8 * (o & 3));
-            w[(o + 1) >> 2] |= G << (8 * ((o + 1) & 3));
-            w[(o + 2) >> 2] |= R << (8 * ((o + 2) & 3));
-        }
-        uint8_t* o = d.out + (int64_t)(y0 + h) * d.ostride + (int64_t)(x0 + xt) * 3;
-        if (m == 4 && (((uintptr_t)o) & 3) == 0) {
-            *(uint3*)o = make_uint3(w[0], w[1], w[2]);
-        } else {
-            for (int k = 0; k < 3 * m; k++) o[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-        }
+        cur = nxt;
     }
 }
 

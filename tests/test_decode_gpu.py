@@ -188,7 +188,8 @@ def _with_comments(data, sizes):
 def test_decode_device_inputs_unaligned_and_long_headers(codec, dgolden):
     """Device-resident files at every address alignment, and headers longer
     than the first 4 KiB header fetch (re-fetched at 32 KiB, then 256 KiB),
-    in one batch: the k_stage gather/copy paths."""
+    in one batch: the k_stage header gather, and k_unstuff_* reading each
+    file's scan where it lies at any byte alignment (no staging copy)."""
     import torch
     meta, jpgs, pxs = dgolden
     names = ["c130x250_s2_q95", "c66x130_s1_q50", "g47x61_q90", "rst7_130x250_444", "c7x9_s2_q95"]
@@ -205,7 +206,7 @@ def test_decode_device_inputs_unaligned_and_long_headers(codec, dgolden):
     for i, (st, img) in enumerate(res):
         assert st == N.OK, (i, st)
         assert np.array_equal(img, want[i]), i
-    # the same files from pageable host memory (scan tail padded in place on the device)
+    # the same files from pageable host memory (one DMA of each scan, 256-B aligned)
     res = codec.decode_jpg_batch([d.cpu().numpy().tobytes() for d in datas], subsampling=1)
     for i, (st, img) in enumerate(res):
         assert st == N.OK and np.array_equal(img, want[i]), i
