@@ -557,10 +557,11 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         DecState* d_state = U.put(states.data(), m);
         const int32_t* d_ids = U.put(ids.data(), m);
 
-        std::vector<int64_t> cnt_tiles(m), cnt_subs(m), cnt_pieces(m), cnt_blk(m), cnt_px(m), cnt_rows(m);
+        std::vector<int64_t> cnt_tiles(m), cnt_ctiles(m), cnt_subs(m), cnt_pieces(m), cnt_blk(m), cnt_px(m), cnt_rows(m);
         int64_t stuffed = 0;
         for (int k = 0; k < m; k++) {
-            cnt_tiles[k] = (sub[k]->ntiles + DEC_UNSTUFF_TILES - 1) / DEC_UNSTUFF_TILES;  // k_unstuff_count / _scatter
+            cnt_tiles[k] = (sub[k]->ntiles + DEC_SCATTER_TILES - 1) / DEC_SCATTER_TILES;  // k_unstuff_scatter
+            cnt_ctiles[k] = (sub[k]->ntiles + DEC_UNSTUFF_TILES - 1) / DEC_UNSTUFF_TILES;  // k_unstuff_count
             cnt_subs[k] = (desc[k].nsub_max + 1 + 255) / 256;
             cnt_pieces[k] = ((int64_t)(desc[k].nsub_max + 1) * dec_pieces(S) + 255) / 256;  // k_dec_write
             // colour: luma IDCT fused with upsampling + conversion for s == 1 4:2:0 fancy (chroma
@@ -573,7 +574,8 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             stuffed += desc[k].scan_len;
         }
         // plans of the whole sub-batch; the pixel stages get theirs per tail
-        const WPlan Pt = plan_of(U, cnt_tiles, d_ids), Ps = plan_of(U, cnt_subs, d_ids);
+        const WPlan Pt = plan_of(U, cnt_tiles, d_ids), Pc = plan_of(U, cnt_ctiles, d_ids),
+                    Ps = plan_of(U, cnt_subs, d_ids);
         icx_status st = U.flush();
         if (st) return st;
         e = hipMemsetAsync(d_changed, 0, (size_t)max_it * 4, c->stream);
@@ -581,7 +583,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         if (e != hipSuccess) return hip_fail(c, e, "counter clear");
         {
             Timed tm(c, "dec_unstuff", stuffed);
-            launch_unstuff(d_desc, d_state, Pt.p, Pt.total, d_ids, m, S, c->stream);
+            launch_unstuff(d_desc, d_state, Pc.p, Pc.total, Pt.p, Pt.total, d_ids, m, S, c->stream);
         }
         {
             Timed tm(c, "dec_init", stuffed);

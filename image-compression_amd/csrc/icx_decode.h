@@ -45,7 +45,14 @@ namespace icx {
 constexpr int DEC_SUB_BITS = 1024;   // bits per subsequence (one thread)
 constexpr int DEC_LUT_BITS = 10;     // Huffman fast-lookup width
 constexpr int DEC_TILE = 4096;       // stuffed bytes per unstuff tile (256 threads x 16)
-constexpr int DEC_UNSTUFF_TILES = 4; // consecutive tiles per k_unstuff_count / k_unstuff_scatter workgroup
+#ifndef ICX_DEC_UNSTUFF_TILES
+#define ICX_DEC_UNSTUFF_TILES 4
+#endif
+#ifndef ICX_DEC_SCATTER_TILES
+#define ICX_DEC_SCATTER_TILES 1
+#endif
+constexpr int DEC_UNSTUFF_TILES = ICX_DEC_UNSTUFF_TILES;  // consecutive tiles per k_unstuff_count workgroup
+constexpr int DEC_SCATTER_TILES = ICX_DEC_SCATTER_TILES;  // ... per k_unstuff_scatter workgroup (4: +10 %, r4e)
 constexpr int DEC_PAD = 8;           // 0xFF bytes standing in for each RSTn marker
 constexpr int DEC_TAIL = 16;         // 0xFF bytes after the last interval
 constexpr uint32_t DEC_END = 0xFFFFFFFFu;
@@ -153,7 +160,10 @@ static_assert(offsetof(DecTab, qt) % 16 == 0 && sizeof(DecTab) % 16 == 0, "DecTa
 
 // k_dec_idct work items per image: tiles of 32 blocks (nblk_tiles),
 // DEC_IDCT_TILES consecutive tiles per workgroup.
-constexpr int DEC_IDCT_TILES = 4;
+#ifndef ICX_DEC_IDCT_TILES
+#define ICX_DEC_IDCT_TILES 1
+#endif
+constexpr int DEC_IDCT_TILES = ICX_DEC_IDCT_TILES;  // 4: +20 % (r4e) - one tile per workgroup at 8 per CU overlaps
 ICX_HD long long dec_idct_items(long long nblk_tiles)
 {
     return (nblk_tiles + DEC_IDCT_TILES - 1) / DEC_IDCT_TILES;
@@ -161,7 +171,10 @@ ICX_HD long long dec_idct_items(long long nblk_tiles)
 
 // k_dec_luma_color_420 work items per image: tiles of one MCU row x 8 MCUs,
 // DEC_LC_TILES consecutive tiles per workgroup.
-constexpr int DEC_LC_TILES = 4;
+#ifndef ICX_DEC_LC_TILES
+#define ICX_DEC_LC_TILES 4
+#endif
+constexpr int DEC_LC_TILES = ICX_DEC_LC_TILES;
 ICX_HD long long dec_lc_items(int mcux, int mcuy)
 {
     return ((long long)mcuy * ((mcux + 7) / 8) + DEC_LC_TILES - 1) / DEC_LC_TILES;

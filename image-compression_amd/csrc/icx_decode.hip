@@ -368,7 +368,7 @@ __global__ void __launch_bounds__(1024) k_unstuff_scan(const DecDesc* D, DecStat
     }
 }
 
-// Compact DEC_UNSTUFF_TILES consecutive tiles (all their loads issued
+// Compact DEC_SCATTER_TILES consecutive tiles (all their loads issued
 // first), one after the other: each thread applies the unstuffing rule to its
 // 16 bytes (fully unrolled, no dynamic register indexing) and places its
 // output bytes at its workgroup-local offset in a zeroed LDS copy of the
@@ -378,7 +378,7 @@ __global__ void __launch_bounds__(1024) k_unstuff_scan(const DecDesc* D, DecStat
 // unaligned head and tail bytes by single lanes.
 __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const DecState* S, Plan p)
 {
-    constexpr int U = DEC_UNSTUFF_TILES;
+    constexpr int U = DEC_SCATTER_TILES;
     __shared__ uint32_t sh[8];
     __shared__ uint32_t bufw[(DEC_TILE / 2 * DEC_PAD + 64) / 4];  // worst case: an RSTn marker every 2 bytes
     uint8_t* const buf = (uint8_t*)bufw;
@@ -1308,11 +1308,11 @@ void launch_stage(const StageJob* jobs, const Plan& tiles, int64_t nwg, hipStrea
     if (nwg > 0) hipLaunchKernelGGL(k_stage, grid_of(tiles, nwg), dim3(256), 0, st, jobs, tiles);
 }
 
-void launch_unstuff(const DecDesc* d, DecState* s, const Plan& tiles, int64_t ntiles, const int32_t* ids, int m,
-                    uint32_t sub_bits, hipStream_t st)
+void launch_unstuff(const DecDesc* d, DecState* s, const Plan& cnt, int64_t ncnt, const Plan& tiles, int64_t ntiles,
+                    const int32_t* ids, int m, uint32_t sub_bits, hipStream_t st)
 {
     if (ntiles <= 0 || m <= 0) return;
-    hipLaunchKernelGGL(k_unstuff_count, grid_of(tiles, ntiles), dim3(256), 0, st, d, s, tiles);
+    hipLaunchKernelGGL(k_unstuff_count, grid_of(cnt, ncnt), dim3(256), 0, st, d, s, cnt);
     hipLaunchKernelGGL(k_unstuff_scan, dim3((unsigned)m), dim3(1024), 0, st, d, s, ids, sub_bits);
     hipLaunchKernelGGL(k_unstuff_scatter, grid_of(tiles, ntiles), dim3(256), 0, st, d, s, tiles);
 }
