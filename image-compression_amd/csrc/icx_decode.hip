@@ -99,8 +99,9 @@ __device__ __forceinline__ Scan16 scan16(const uint8_t* scan, int64_t scan_len, 
     const uintptr_t p = (uintptr_t)(scan + base), a = p & ~(uintptr_t)15;
     const uint32_t sh = (uint32_t)(p & 15), q = sh >> 2, b = sh & 3;
     const bool more = a + 16 < (uintptr_t)(scan + scan_len);
-    const uint4 c0 = *(const uint4*)a;
-    uint4 c1 = *(const uint4*)(more ? a + 16 : a);  // unconditional: no branch and wait around the load
+    // global (not flat) loads: they wait on vmcnt alone, not on the LDS counter too
+    const uint4 c0 = *(const ICX_GLOBAL uint4*)a;
+    uint4 c1 = *(const ICX_GLOBAL uint4*)(more ? a + 16 : a);  // unconditional: no branch and wait around the load
     if (!more) c1 = make_uint4(0u, 0u, 0u, 0u);
     const uint32_t x[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
     uint32_t y[5];
@@ -248,7 +249,7 @@ __global__ void __launch_bounds__(256) k_unstuff_count(const DecDesc* D, DecStat
         const int64_t base = (tile0 + u) * DEC_TILE + threadIdx.x * 16;
         const int64_t bc = base < len ? base : len - 1;
         q[u] = scan16(d.scan, len, bc);
-        prev[u] = d.scan[bc > 0 ? bc - 1 : 0];
+        prev[u] = ((const ICX_GLOBAL uint8_t*)d.scan)[bc > 0 ? bc - 1 : 0];
     }
     uint32_t cnt[U];  // output bytes (bits 0..19) + RSTn markers << 20 of this thread's 16 bytes
 #pragma unroll
@@ -288,8 +289,8 @@ __global__ void __launch_bounds__(256) k_unstuff_count(const DecDesc* D, DecStat
         const int64_t tile = tile0 + u;
         if (tile < d.ntiles) {
             const uint32_t c = sh[u][0] + sh[u][1] + sh[u][2] + sh[u][3];
-            d.tile_cnt[tile] = c & 0xFFFFFu;
-            d.tile_rst[tile] = c >> 20;
+            ((ICX_GLOBAL uint32_t*)d.tile_cnt)[tile] = c & 0xFFFFFu;
+            ((ICX_GLOBAL uint32_t*)d.tile_rst)[tile] = c >> 20;
         }
     }
 }
@@ -397,7 +398,7 @@ __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const
         const int64_t base = (tile0 + u) * DEC_TILE + threadIdx.x * 16;
         const int64_t bc = base < len ? base : len - 1;
         q[u] = scan16(d.scan, len, bc);
-        prev[u] = d.scan[bc > 0 ? bc - 1 : 0];
+        prev[u] = ((const ICX_GLOBAL uint8_t*)d.scan)[bc > 0 ? bc - 1 : 0];
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -473,7 +474,7 @@ __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const
                 if ((rstm >> k) & 1) {
                     for (int q = 0; q < DEC_PAD; q++) buf[ob + q] = 0xFF;
                     ob += DEC_PAD;
-                    if (orr + 1 < (uint32_t)d.nseg_max) d.seg[orr + 1] = tile_off + ob;
+                    if (orr + 1 < (uint32_t)d.nseg_max) ((ICX_GLOBAL uint32_t*)d.seg)[orr + 1] = tile_off + ob;
                     orr++;
                 } else if ((keep >> k) & 1) {
                     buf[ob++] = (uint8_t)(vw[k >> 2] >> (8 * (k & 3)));
@@ -483,11 +484,12 @@ __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const
         __syncthreads();
         // tile output = global bytes [tile_off, tile_off + tb)
         const uint32_t head = min((4u - (tile_off & 3u)) & 3u, tb);
+        ICX_GLOBAL uint8_t* const ent = (ICX_GLOBAL uint8_t*)d.ent;
         if (threadIdx.x < head && (int64_t)(tile_off + threadIdx.x) < d.ent_cap)
-            d.ent[tile_off + threadIdx.x] = buf[threadIdx.x];
+            ent[tile_off + threadIdx.x] = buf[threadIdx.x];
         const uint32_t nw = (tb - head) >> 2;         // whole aligned dwords
         const uint32_t sh8 = head;                    // local byte of the first dword: head + 4k
-        uint32_t* const dstw = (uint32_t*)(d.ent + tile_off + head);  // 4-byte aligned
+        ICX_GLOBAL uint32_t* const dstw = (ICX_GLOBAL uint32_t*)(ent + tile_off + head);  // 4-byte aligned
         const int64_t cap_w = (d.ent_cap - (int64_t)(tile_off + head)) >> 2;
         for (uint32_t k = threadIdx.x; k < nw; k += 256) {
             const uint32_t lb = head + 4 * k;
@@ -496,7 +498,7 @@ __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const
         }
         const uint32_t t0 = head + 4 * nw;
         if (threadIdx.x < tb - t0 && (int64_t)(tile_off + t0 + threadIdx.x) < d.ent_cap)
-            d.ent[tile_off + t0 + threadIdx.x] = buf[t0 + threadIdx.x];
+            ent[tile_off + t0 + threadIdx.x] = buf[t0 + threadIdx.x];
     }
 }
 
