@@ -662,6 +662,9 @@ __global__ void __launch_bounds__(1024) k_dec_offsets(const DecDesc* D, DecState
 // without a pad dword, so 256 slots take 32 KiB and, with the 8 KiB of
 // first-level Huffman tables, a workgroup 40 KiB: four per CU.
 constexpr int SLOT_DW = 32;
+#ifndef ICX_DEC_FLUSH2
+#define ICX_DEC_FLUSH2 0
+#endif
 
 // A lane that finishes an owned block only records its index, and the wave
 // then copies every finished slot together (below), permuting to natural
@@ -735,7 +738,7 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
     PendSink sk{(uint8_t*)mys, (uint32_t)(lane & 62), -1};
     ICX_GLOBAL uint32_t* coefs32 = (ICX_GLOBAL uint32_t*)d.coefs;  // global_store: vmcnt only, not lgkmcnt
     ICX_GLOBAL int32_t* dcs = (ICX_GLOBAL int32_t*)d.dc;
-    const int zl = dec_zz((2 * lane) & 63), zh = dec_zz((2 * lane + 1) & 63);  // this lane's flush pair
+    const int zl = dec_zz((2 * lane) & 63), zh = dec_zz((2 * lane + 1) & 63);  // this lane's flush pair (lane % 32)
     while (__any(run)) {
         if (run) {
             w.step(sk);
@@ -743,6 +746,34 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
         }
         if (__any(run && w.R.low()) && run && w.R.wants()) w.R.top_up();
         uint64_t m = __ballot(sk.pend >= 0);
+#if ICX_DEC_FLUSH2
+        // two finished blocks per round: lanes 0..31 copy the first, 32..63 the second
+        while (m) {
+            const int l0 = __builtin_ctzll(m);
+            m &= m - 1;
+            const int l1 = m ? __builtin_ctzll(m) : l0;
+            const bool two = m != 0;
+            m &= m - 1;
+            const uint32_t lo0 = __builtin_amdgcn_readlane((uint32_t)sk.pend, l0);
+            const uint32_t hi0 = __builtin_amdgcn_readlane((uint32_t)((uint64_t)sk.pend >> 32), l0);
+            const uint32_t lo1 = __builtin_amdgcn_readlane((uint32_t)sk.pend, l1);
+            const uint32_t hi1 = __builtin_amdgcn_readlane((uint32_t)((uint64_t)sk.pend >> 32), l1);
+            const bool upper = lane >= 32;
+            const int l = upper ? l1 : l0;
+            const int64_t bi = (int64_t)(upper ? ((uint64_t)hi1 << 32) | lo1 : ((uint64_t)hi0 << 32) | lo0);
+            uint32_t* src = wave_slots + l * SLOT_DW;
+            if (!upper || two) {
+                const int q = lane & 31;
+                const uint16_t* s16 = (const uint16_t*)src;
+                const int lsw = l & 62;
+                const uint32_t v = s16[zl ^ lsw] | ((uint32_t)s16[zh ^ lsw] << 16);
+                __builtin_amdgcn_wave_barrier();  // every lane's reads before the zeroing
+                src[q] = 0;
+                coefs32[bi * 32 + q] = v;
+                if (q == 0) dcs[bi] = (int16_t)v;  // the DC difference, also for k_dec_dc's dense reads
+            }
+        }
+#else
         while (m) {
             const int l = __builtin_ctzll(m);
             m &= m - 1;
@@ -760,6 +791,7 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
                 if (lane == 0) dcs[bi] = (int16_t)v;  // the DC difference, also for k_dec_dc's dense reads
             }
         }
+#endif
         sk.pend = -1;
     }
     // The settled states are the true decode: an invalid code met on it
