@@ -602,9 +602,32 @@ ICX_HD uint32_t dec_lean_lookup(LeanPtr H, int ti, const ICX_GLOBAL DecSlow* slo
 {
     return dec_lean_symbol(&H[ti], &slow[ti], pk, ac);
 }
+#ifndef ICX_DEC_SCALAR2
+#define ICX_DEC_SCALAR2 0
+#endif
 ICX_HD uint32_t dec_lean_lookup(const SplitLean& H, int ti, const ICX_GLOBAL DecSlow* slow, uint32_t pk, bool ac)
 {
-    const uint32_t e = H.lut[ti][pk >> (16 - DEC_LUT_BITS)];
+    uint32_t e = H.lut[ti][pk >> (16 - DEC_LUT_BITS)];
+#if defined(__HIP_DEVICE_COMPILE__) && ICX_DEC_SCALAR2
+    // Second levels (codes longer than DEC_LUT_BITS, ~0.3 % of q95 symbols but
+    // a lane of the wave in ~15 % of steps) through the scalar cache, one lane
+    // at a time: a vector load here would be waited for with vmcnt, i.e.
+    // behind every coefficient store the wave still has in flight.
+    uint64_t m = __ballot(!(e & 31) && e && !(e & DEC_LEAN_SLOW));
+    if (m) {
+        const uint32_t off = (uint32_t)(ti * sizeof(DecLean) + offsetof(DecLean, lut2)) +
+                             ((((e >> 5) & (DEC_NSUB - 1)) << (16 - DEC_LUT_BITS)) | (pk & ((1u << (16 - DEC_LUT_BITS)) - 1))) * 2;
+        const uint64_t base = (uint64_t)(uintptr_t)H.full;
+        const int lane = (int)__lane_id();
+        do {
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t o = __builtin_amdgcn_readlane(off, l);
+            const uint32_t w = *(const __attribute__((address_space(4))) uint32_t*)(uintptr_t)(base + (o & ~3u));
+            if (lane == l) e = (w >> ((o & 2u) * 8)) & 0xFFFFu;
+        } while (m);
+    }
+#endif
     return (e & 31) || !e ? e : dec_lean_symbol(&H.full[ti], &slow[ti], pk, ac);
 }
 
