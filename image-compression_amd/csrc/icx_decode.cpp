@@ -146,9 +146,10 @@ uint32_t pick_sub_bits(uint64_t total_bits)
         if (v >= 64 && (v & (v - 1)) == 0) return (uint32_t)v;
     }
     // Long subsequences re-walk least (measured on 4K q95: 16384 beats 8192 for
-    // smooth and noise content); shorter ones only when the batch would not
-    // give the chip ~64k threads.
-    uint32_t S = 16384;
+    // smooth and noise content, 32768 beats 16384 by 3 % on configs[1]'s
+    // 1000-frame calls and ties at 200 frames, ab_r4g_dec.txt); shorter ones
+    // only when the batch would not give the chip ~64k threads.
+    uint32_t S = 32768;
     while (S > 2048 && total_bits / S < 65536) S /= 2;
     return S;
 }

@@ -1228,7 +1228,10 @@ __device__ __forceinline__ void lc_fetch(const LcImg& g, int item, int t, LcLoad
 __global__ void __launch_bounds__(256) k_dec_luma_color_420(const DecDesc* D, const DecState* S, Plan p)
 {
     __shared__ int32_t ws[32][8 * 9];
-    __shared__ __attribute__((aligned(16))) uint32_t ly[16][LC_W / 4];
+    // luma tile rows padded to 36 dwords: the IDCT's 8-byte row stores (lanes
+    // r = 0..7 of a block, one row each) spread over the banks instead of
+    // eight lanes on one bank pair at a 32-dword stride
+    __shared__ __attribute__((aligned(16))) uint32_t ly[16][LC_W / 4 + 4];
     __shared__ uint32_t lcb[2][LC_CE];  // per tile parity: [cb|cr][chroma row cy0-1+j][dword]; byte q <-> column cx0-4+q
     int slot;
     int64_t wg;
