@@ -145,11 +145,17 @@ uint32_t pick_sub_bits(uint64_t total_bits)
         const long v = atol(e);
         if (v >= 64 && (v & (v - 1)) == 0) return (uint32_t)v;
     }
-    // Long subsequences re-walk least (measured on 4K q95: 16384 beats 8192 for
-    // smooth and noise content, 32768 beats 16384 by 3 % on configs[1]'s
-    // 1000-frame calls and ties at 200 frames, ab_r4g_dec.txt); shorter ones
-    // only when the batch would not give the chip ~64k threads.
-    uint32_t S = 32768;
+    // Long subsequences re-walk least and need fewer warm-ups (k_dec_init walks
+    // `warm` bits per subsequence), short ones give the chip threads and keep
+    // the relaxation's re-walk launches short.  Measured on 4K q95 (half noise,
+    // e2e leg, ab_r4g_dec.txt / ab_r4h_dec_sub.txt / ab_r4i_dec_sub.txt):
+    // 1000 frames per call (62 Gbit) 16384 / 32768 / 65536 / 131072 bits:
+    // 96.6 / 93.5 / 90.3 / 96.0 ms; 200 frames (12.4 Gbit) 16384 / 32768 /
+    // 65536: 22.4 / 22.8 / 23.9 ms.  Longer subsequences while at least 2^19
+    // of them remain; below that 16384, and shorter only when the batch would
+    // not give the chip ~64k threads.
+    uint32_t S = 65536;
+    while (S > 16384 && total_bits / S < (1u << 19)) S /= 2;
     while (S > 2048 && total_bits / S < 65536) S /= 2;
     return S;
 }

@@ -907,10 +907,18 @@ ICX_HD DecLeanWriter<LeanPtr> dec_lean_writer(const DecDesc& d, LeanPtr H, const
 // count plus the difference at the checkpoint.  A re-walk from a corrected
 // entry state typically resynchronises within a few hundred bits, so relaunch
 // walks cost about one checkpoint interval instead of a whole subsequence.
-constexpr int DEC_CK_MAX = 7;
+#ifndef ICX_DEC_CK_DIV
+#define ICX_DEC_CK_DIV 8  // checkpoint intervals (= write-pass pieces) per subsequence
+#endif
+constexpr int DEC_CK_DIV = ICX_DEC_CK_DIV;
+constexpr int DEC_CK_MAX = DEC_CK_DIV - 1;
 constexpr uint64_t DEC_CK_NONE = ~0ull;
 constexpr uint64_t DEC_CK_STATE = (1ull << 48) - 1;
-ICX_HD uint32_t dec_ck_bits(uint32_t sub_bits) { return sub_bits / 8 > 2048 ? sub_bits / 8 : 2048; }
+ICX_HD uint32_t dec_ck_bits(uint32_t sub_bits)
+{
+    constexpr uint32_t floor_bits = 16384 / DEC_CK_DIV;
+    return sub_bits / DEC_CK_DIV > floor_bits ? sub_bits / DEC_CK_DIV : floor_bits;
+}
 ICX_HD int dec_ck_slots(uint32_t sub_bits)
 {
     const uint32_t c = dec_ck_bits(sub_bits);

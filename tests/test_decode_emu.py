@@ -22,11 +22,16 @@ BUILD = os.path.join(ROOT, "tests", "_build")
 @pytest.fixture(scope="module")
 def emu():
     os.makedirs(BUILD, exist_ok=True)
-    lib = os.path.join(BUILD, "dec_emu.so")
+    # ICX_EMU_FLAGS: extra compile flags (tuning macros of icx_decode.h, e.g.
+    # -DICX_DEC_CK_DIV=16) to check a variant's state machine before a GPU A/B
+    flags = os.environ.get("ICX_EMU_FLAGS", "").split()
+    lib = os.path.join(BUILD, "dec_emu%s.so" % ("_" + "_".join(f.strip("-").replace("=", "") for f in flags)
+                                                 if flags else ""))
     srcs = [os.path.join(ROOT, "tests", "dec_emu.cpp"), os.path.join(CSRC, "icx_jpeg_parse.cpp")]
     deps = srcs + [os.path.join(CSRC, "icx_decode.h"), os.path.join(CSRC, "icx_jpeg_parse.h")]
     if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(f) for f in deps):
-        subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", CSRC, "-o", lib] + srcs, check=True)
+        subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", CSRC] + flags + ["-o", lib] + srcs,
+                       check=True)
     L = ctypes.CDLL(lib)
     L.dec_emu_coefs.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                 ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
