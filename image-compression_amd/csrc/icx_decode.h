@@ -937,26 +937,32 @@ struct CkRecord {
     }
 };
 
-// Checkpoints of a re-walk: old = the previous walk's (a private copy), total =
-// its block count.  A match fixes up the later checkpoints' counts and sets
-// total to the new count.
-template <class P, class Q>
-struct CkCompare {
+// Checkpoints of a re-walk, compared in place: the previous walk's checkpoint
+// k is read into a register one mark ahead, before this walk overwrites it,
+// and on a match the later ones - not yet overwritten - are spliced with the
+// block-count difference.  No private copy of the previous walk's checkpoints
+// (k_dec_sync's relaunches kept one in LDS until round 4: 14 KiB a workgroup,
+// five workgroups per CU instead of eight).  o = ck[0] on entry.
+template <class P>
+struct CkInPlace {
     P ck;
-    Q old;
     int nck;
     uint32_t total;
+    uint64_t o;
     ICX_HD bool visit(int k, uint64_t s, uint32_t& nblk)
     {
-        const uint64_t o = old[k];
-        if (o != DEC_CK_NONE && ((o ^ s) & DEC_CK_STATE) == 0) {
-            const int32_t delta = (int32_t)(s >> 48) - (int32_t)(o >> 48);
-            for (int q = k + 1; q < nck; q++)
-                if (old[q] != DEC_CK_NONE) ck[q] = old[q] + ((uint64_t)(int64_t)delta << 48);
+        const uint64_t ok = o;
+        if (ok != DEC_CK_NONE && ((ok ^ s) & DEC_CK_STATE) == 0) {
+            const int32_t delta = (int32_t)(s >> 48) - (int32_t)(ok >> 48);
+            for (int q = k + 1; q < nck; q++) {
+                const uint64_t v = ck[q];
+                if (v != DEC_CK_NONE) ck[q] = v + ((uint64_t)(int64_t)delta << 48);
+            }
             ck[k] = s;
             nblk = total + (uint32_t)delta;
             return true;
         }
+        o = k + 1 < nck ? ck[k + 1] : DEC_CK_NONE;
         ck[k] = s;
         return false;
     }

@@ -561,7 +561,7 @@ __device__ __forceinline__ uint32_t selector(const DecTab* T)
 // differs from the stored next entry stores it and appends j + 1 to the next
 // worklist (only thread j writes E[j+1], so entries are unique per launch).
 // Launch 0 records each walk's checkpoints; a re-walk compares against them
-// (staged in LDS) and stops where it meets its previous walk (dec_sync_walk).
+// in place (CkInPlace) and stops where it meets its previous walk (dec_sync_walk).
 #ifndef ICX_DEC_AGG
 #define ICX_DEC_AGG 0  // k_dec_sync: wave-aggregated worklist / change-count atomics (+-0: few lanes change)
 #endif
@@ -570,7 +570,6 @@ __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecSta
                                                   int iter, int nimg, uint32_t* changed)
 {
     __shared__ __attribute__((aligned(16))) DecLean L[4];
-    __shared__ uint64_t ckl[FIRST ? 1 : 256][DEC_CK_MAX];
     int slot;
     int64_t wg;
     if (!plan_slot(p, slot, wg)) return;
@@ -596,9 +595,7 @@ __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecSta
         x = dec_sync_walk(d, (const DecLean*)L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
                           st.ent_len * 8, e, j * sub_bits, sub_bits, nb, early, ck);
     } else {
-        uint64_t* mine = ckl[FIRST ? 0 : threadIdx.x];
-        for (int q = 0; q < nck; q++) mine[q] = ckg[q];
-        CkCompare<ICX_GLOBAL uint64_t*, uint64_t*> ck{ckg, mine, nck, d.ncnt[j]};
+        CkInPlace<ICX_GLOBAL uint64_t*> ck{ckg, nck, d.ncnt[j], nck > 0 ? ckg[0] : DEC_CK_NONE};
         x = dec_sync_walk(d, (const DecLean*)L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
                           st.ent_len * 8, e, j * sub_bits, sub_bits, nb, early, ck);
     }

@@ -127,9 +127,7 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
                 x = dec_sync_walk(d, (const DecLean*)T.lean, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8,
                                   est[j], j * S, S, n, early, rec);
             } else {
-                uint64_t old[DEC_CK_MAX];
-                memcpy(old, mine, sizeof(old));
-                CkCompare<uint64_t*, uint64_t*> cmp{mine, old, nck, ncnt[j]};
+                CkInPlace<uint64_t*> cmp{mine, nck, ncnt[j], nck > 0 ? mine[0] : DEC_CK_NONE};
                 x = dec_sync_walk(d, (const DecLean*)T.lean, T.slow, sel, words.data(), seg.data(), (uint32_t)seg.size(), ent_len * 8,
                                   est[j], j * S, S, n, early, cmp);
                 if (early) dec_emu_early++;

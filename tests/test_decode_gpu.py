@@ -91,6 +91,23 @@ def test_decode_4k_q95_matches_oracle(codec, oracle, kind):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("sub_bits", [2048, 16384, 32768, 65536])
+def test_decode_subsequence_lengths(codec, oracle, monkeypatch, sub_bits):
+    """The subsequence length follows the batch size (pick_sub_bits: 65536
+    bits on configs[1]'s 1000-frame calls, 16384 at 200, 2048 for a lone
+    small file); every length, forced on one small mixed batch (ICX_DEC_SUB_BITS),
+    must decode what the oracle decodes - checkpoints, write-pass pieces and
+    relaxation at that length."""
+    datas = [_jpeg((smooth if i % 2 == 0 else noise)(h, w, 70 + i)[:, :, ::-1].copy(), quality=95, subsampling=2)
+             for i, (h, w) in enumerate([(2160, 3840), (2160, 3840), (1080, 1920), (333, 517)])]
+    monkeypatch.setenv("ICX_DEC_SUB_BITS", str(sub_bits))
+    res = codec.decode_jpg_batch(datas, subsampling=1)
+    for i, (data, (st, img)) in enumerate(zip(datas, res)):
+        rc, ref = oracle.jpeg_decode(data)
+        assert rc == 0 and st == N.OK, (i, st)
+        assert np.array_equal(img, ref), (sub_bits, i)
+
+
 def test_decode_batch_settling_at_different_launches(codec, oracle, dgolden):
     """One batch whose images settle their entry states at different sync
     launches (smooth frames early, uniform noise late, small files at once):
