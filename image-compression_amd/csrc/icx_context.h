@@ -47,8 +47,10 @@ struct DevArena {
         used = align_up(used, 256);
         void* p = base + used;
         used += n;
+        if (used > cap) overflow = true;  // a sizing bug: callers fail the call before any launch
         return p;
     }
+    bool overflow = false;
     ~DevArena() { if (base) hipFree(base); }
 };
 

@@ -464,6 +464,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             continue;
         }
         c->dev.used = 0;
+        c->dev.overflow = false;
         size_t host_need = (64 << 20) + up;
         for (DecItem* it : sub)
             if (!it->dev_in && !is_pinned_ptr(it->job->data)) host_need += align_up(it->job->len, 64);
@@ -557,6 +558,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         uint32_t* d_changed = (uint32_t*)c->dev.take((size_t)max_it * 4);
         uint32_t* d_wlcnt = (uint32_t*)c->dev.take((size_t)m * max_it * 4);
         for (int k = 0; k < m; k++) desc[k].wl_cnt = d_wlcnt;
+        if (c->dev.overflow) return fail(c, ICX_E_NOMEM, "device workspace overrun (workspace sizing)");
         uint32_t* h_changed = (uint32_t*)c->host.take(4);
         std::vector<int32_t> ids(m);
         for (int k = 0; k < m; k++) ids[k] = k;
