@@ -39,9 +39,6 @@ namespace icx {
 // workgroup sharing the coding tables, no workgroup barrier after the table
 // load: k_huff +2...5 %, step +7 % with the 4x chunk count in k_scan/k_stuff;
 // DESIGN.md §9.)
-#ifndef ICX_HUFF_SORT
-#define ICX_HUFF_SORT 0  // k_huff codes a chunk's blocks by descending list length (k_chunk_order)
-#endif
 constexpr int CHUNK_BLOCKS = 256;  // scan blocks per Huffman chunk
 constexpr int HUFF_THREADS = CHUNK_BLOCKS;
 constexpr int MAX_BLOCK_BITS = 1664;     // >= 22 (DC) + 63 * 26 (AC) bits, multiple of 32
@@ -95,10 +92,6 @@ struct ImgDesc {
     int32_t* coefs;        // candidate lists, COEF_SLOTS entries reserved per block (see above)
     uint32_t* coff;        // start of each block's list, in 4-entry (16-B) units
     uint8_t* ncoef;        // list length per block (1..64)
-    // per chunk position, the block k_huff's thread codes there (chunk
-    // blocks by descending list length, k_chunk_order) as 3 words: its list
-    // offset, its DC predecessor's list offset (~0: none), block | length << 8
-    uint32_t* order;
     uint32_t* scratch[2];
     uint32_t* chunk_bits[2];
     uint64_t* chunk_off[2];   // nchunks + 1 entries

@@ -15,7 +15,6 @@ hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat
 void launch_list_count(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st);
 void launch_fdct(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, int64_t tiles, int kind,
                  hipStream_t st);
-void launch_chunk_order(const ImgDesc* d, const Plan& p, int64_t chunks, hipStream_t st);
 void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t chunks, bool rev,
                  hipStream_t st);
 // k_scan: the trial's offsets, exact file size and one binary-search step (decide)

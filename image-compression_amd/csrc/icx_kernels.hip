@@ -890,63 +890,6 @@ __global__ __launch_bounds__(1024) void k_list_count(const ImgDesc* __restrict__
     }
 }
 
-// k_huff's block order inside each chunk (ICX_HUFF_SORT): a wave's 64 lanes
-// code 64 blocks in lockstep until its longest list ends, and neighbouring
-// blocks differ in length (an MCU's chroma lists are far shorter than its luma
-// lists, and luma lengths scatter), so the chunk's blocks are dealt to the
-// threads by descending list length (a counting sort over the 64 lengths):
-// each wave runs about as long as its own blocks need.  Per chunk position:
-// the block's list offset, its DC predecessor's list offset (~0 when the
-// image has none) and block | length << 8 - everything k_huff's first round
-// of loads fetched per block, so its prologue keeps two rounds of loads.  The
-// lists are fixed for all of an image's trials: one launch per FDCT.
-__global__ __launch_bounds__(CHUNK_BLOCKS) void k_chunk_order(const ImgDesc* __restrict__ descs,
-                                                              const int32_t* __restrict__ ids,
-                                                              const int64_t* __restrict__ prefix, int m)
-{
-    __shared__ uint32_t s_hist[64];
-    __shared__ uint32_t s_base[64];
-    const int slot = gridDim.y > 1 ? (int)blockIdx.y : find_slot(prefix, m, blockIdx.x);
-    const int img = ids ? ids[slot] : slot;
-    const ImgDesc& D = descs[img];
-    const int chunk = gridDim.y > 1 ? (int)blockIdx.x : (int)(blockIdx.x - prefix[slot]);
-    if (chunk >= D.nchunks) return;  // workgroup-uniform (2-D plans pad the image's row)
-    const int t = threadIdx.x;
-    const int64_t b0 = (int64_t)chunk * CHUNK_BLOCKS;
-    const int nb = (int)min((int64_t)CHUNK_BLOCKS, D.nblocks - b0);
-    const bool valid = t < nb;
-    const int64_t b = b0 + t;
-    int64_t pb;  // the previous block of the same component (k_huff's DC predictor)
-    if (D.ncomp == 3) {
-        const uint32_t k6 = (uint32_t)(b % 6);
-        if (k6 >= 1 && k6 <= 3) pb = b - 1;
-        else if (k6 == 0) pb = b >= 6 ? b - 3 : -1;
-        else pb = b >= 6 ? b - 6 : -1;
-    } else {
-        pb = b - 1;
-    }
-    const int cnt = valid ? (int)gp(D.ncoef)[b] : 0;
-    const uint32_t my_off = valid ? gp(D.coff)[b] : 0u;
-    const uint32_t prev_off = valid && pb >= 0 ? gp(D.coff)[pb] : ~0u;
-    if (t < 64) s_hist[t] = 0u;
-    __syncthreads();
-    const int key = 64 - cnt;  // descending length: bin 0 = 64 entries
-    const uint32_t rank = valid ? atomicAdd(&s_hist[key & 63], 1u) : 0u;
-    __syncthreads();
-    if (t < 64) {  // exclusive scan of the 64 bins by one wave
-        const uint32_t v = s_hist[t];
-        const uint32_t incl = (uint32_t)wave_incl_scan((int)v);
-        s_base[t] = incl - v;
-    }
-    __syncthreads();
-    if (valid) {
-        GAS uint32_t* o = gp(D.order) + 3 * (b0 + s_base[key & 63] + rank);
-        o[0] = my_off;
-        o[1] = prev_off;
-        o[2] = (uint32_t)t | ((uint32_t)cnt << 8);
-    }
-}
-
 // =================================================================== Huffman
 // jcdctmgr.c: sign(c) * ((|c| + d/2) / d) for d = q<<3, via the exact float
 // form of QNode (|c| <= 2^15, so y*d < 2^16 and the error stays < 2^-6/d).
@@ -1200,28 +1143,6 @@ __global__ __launch_bounds__(HUFF_THREADS, ICX_HUFF_WGS) void k_huff(const ImgDe
 
     const int64_t b0 = (int64_t)chunk * CHUNK_BLOCKS;
     const int nb = (int)min((int64_t)CHUNK_BLOCKS, D.nblocks - b0);
-#if ICX_HUFF_SORT
-    // this thread's block: the chunk's blocks by descending list length, with
-    // their list offsets (k_chunk_order) - one 12-byte load instead of the
-    // length and the two offsets
-    const bool valid = t < nb;
-    uint32_t orec[3] = {0u, ~0u, (uint32_t)t};
-    if (valid) {
-        const GAS uint32_t* o = gp(D.order) + 3 * (b0 + t);
-        orec[0] = o[0];
-        orec[1] = o[1];
-        orec[2] = o[2];
-    }
-    const int p = (int)(orec[2] & 255u);  // chunk-local block index
-    const int64_t b = b0 + p;
-    int tb = 0;
-    if (D.ncomp == 3) tb = ((uint32_t)(chunk % 3) * 4u + (uint32_t)p) % 6u >= 4u;
-    const int cnt = valid ? (int)(orec[2] >> 8) : 0;
-    const uint32_t my_off = orec[0];
-    const bool ext_prev = valid && orec[1] != ~0u;  // every predecessor's DC is fetched and quantised here
-    const uint32_t prev_off = ext_prev ? orec[1] : my_off;
-    if (!S.active) return;
-#else
     const bool valid = t < nb;
     const int64_t b = b0 + t;
     int tb = 0;
@@ -1256,7 +1177,6 @@ __global__ __launch_bounds__(HUFF_THREADS, ICX_HUFF_WGS) void k_huff(const ImgDe
     const uint32_t my_off = coff[valid ? b : b0];
     const uint32_t prev_off = coff[ext_prev ? pb : b0];
     if (!S.active) return;
-#endif
     const QNode& N = nodes[S.node];
     const int cur = S.cur;
     const float4 qv = N.qf[(t >> 6) & 1][t & 63];  // used by t < 128
@@ -1279,24 +1199,15 @@ __global__ __launch_bounds__(HUFF_THREADS, ICX_HUFF_WGS) void k_huff(const ImgDe
 
     const float2 q0t = s_qf[tb][0];
     const int dq = quant((int)__uint_as_float(ev[0] & ~0x3FFu), q0t.x, q0t.y);
-#if ICX_HUFF_SORT
-    const int qprev = ext_prev ? quant((int)__uint_as_float((uint32_t)prev_dc_raw & ~0x3FFu), q0t.x, q0t.y) : 0;
-#else
     const int from = __builtin_amdgcn_ds_bpermute((in_wave ? (int)(pb - b0) & 63 : lane) << 2, dq);
     int qprev = 0;
     if (in_wave) qprev = from;
     else if (ext_prev) qprev = quant((int)__uint_as_float((uint32_t)prev_dc_raw & ~0x3FFu), q0t.x, q0t.y);
-#endif
 
     // ---- 1. encode_one_block into the slot (rarely: into the block's HBM spill)
     int bits = 0;
-#if ICX_HUFF_SORT
-    const int me = p;  // slot and spill of the block coded here
-#else
-    const int me = t;
-#endif
     if (valid) {
-        const uint32_t sb = (uint32_t)(me * SLOT_WORDS * 4);
+        const uint32_t sb = (uint32_t)(t * SLOT_WORDS * 4);
         LdsSink sink{0, 0, sb, sb + (SLOT_WORDS - 1) * 4, slots};
         encode_block(sink, ev, lst, cnt, dq - qprev, &s_qf[0][0], s_ac[tb], s_dc[tb]);
         bits = (int)(sink.wb - sb) * 8 + sink.n;
@@ -1310,15 +1221,7 @@ __global__ __launch_bounds__(HUFF_THREADS, ICX_HUFF_WGS) void k_huff(const ImgDe
         }
     }
 
-#if ICX_HUFF_SORT
-    // ---- 2. back to block order (thread t = block t from here on), then the
-    // exclusive scan of block bits
-    s_bits[p] = (uint32_t)bits;
-    __syncthreads();
-    bits = valid ? (int)s_bits[t] : 0;
-#else
     // ---- 2. exclusive scan of block bits
-#endif
     const int incl = wave_incl_scan(bits);
     if (lane == 63) s_wsum[wv] = incl;
     __syncthreads();
@@ -2077,13 +1980,6 @@ void launch_fdct(const ImgDesc* d, ImgState* s, const QNode* n, const Plan& p, i
 void launch_list_count(const ImgDesc* d, ImgState* s, const Plan& p, hipStream_t st)
 {
     ICX_LAUNCH(k_list_count, dim3(p.m), dim3(1024), 0, st, d, s, plan_ids(p), p.m);
-}
-
-void launch_chunk_order(const ImgDesc* d, const Plan& p, int64_t chunks, hipStream_t st)
-{
-    if (chunks <= 0) return;
-    const dim3 grid = p.uniform > 0 && p.m > 1 ? dim3((unsigned)p.uniform, (unsigned)p.m) : dim3((unsigned)chunks);
-    ICX_LAUNCH(k_chunk_order, grid, dim3(CHUNK_BLOCKS), 0, st, d, plan_ids(p), p.prefix, p.m);
 }
 
 void launch_huff(const ImgDesc* d, const ImgState* s, const QNode* n, const Plan& p, int64_t wgs, bool rev,

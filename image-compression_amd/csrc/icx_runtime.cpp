@@ -439,7 +439,6 @@ void stage_pixels(Batch& B, int i, double scale)
     d.coefs = keep.coefs;
     d.coff = keep.coff;
     d.ncoef = keep.ncoef;
-    d.order = keep.order;
     d.cand_node = keep.cand_node;
     for (int k = 0; k < 2; k++) {
         d.scratch[k] = keep.scratch[k];
@@ -480,15 +479,6 @@ icx_status run_fdct(Batch& B, const std::vector<int>& ids)
             Timed tm(B.c, "count", (int64_t)sel.size(), true);
             launch_list_count(B.d_desc, B.d_state, P.p, B.c->stream);
         }
-    }
-    if (ICX_HUFF_SORT) {  // k_huff's block order per chunk, once per FDCT (the lists stay for every trial)
-        std::vector<int64_t> cnt;
-        for (int i : ids) cnt.push_back(B.desc[i].nchunks);
-        DPlan P;
-        icx_status s = make_plan(B, ids, cnt, P);
-        if (s || (s = B.up->flush())) return s;
-        Timed tm(B.c, "order", P.total, true);
-        launch_chunk_order(B.d_desc, P.p, P.total, B.c->stream);
     }
     return ICX_OK;
 }
@@ -618,8 +608,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
         ImgDesc g{};
         geometry(g, j.img.width, j.img.height, j.img.fmt);
         const size_t px = (size_t)j.img.width * j.img.height * channels(j.img.fmt);
-        size_t per = coef_bytes(g) + (size_t)g.nchunks * CHUNK_BLOCKS * (5 + (ICX_HUFF_SORT ? 12 : 0)) + 256 +
-                     (size_t)g.nblocks * BLOCK_WORDS * 4 + 1024 +
+        size_t per = coef_bytes(g) + (size_t)g.nchunks * CHUNK_BLOCKS * 5 + (size_t)g.nblocks * BLOCK_WORDS * 4 + 1024 +
                      2 * ((size_t)g.nchunks * CHUNK_WORDS + 1) * 4 +
                      (size_t)g.nchunks * (2 * 4 + 2 * 8 + 2 * 4 + 2 * 32 + 8) + 64 + 8 * 256 + 4096;
         if (mode == Mode::Fit) per += px;  // resize buffer
@@ -796,7 +785,6 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             d.coefs = (int32_t*)c->dev.take(coef_bytes(d));
             d.coff = (uint32_t*)c->dev.take((size_t)d.nchunks * CHUNK_BLOCKS * 4);
             d.ncoef = (uint8_t*)c->dev.take((size_t)d.nchunks * CHUNK_BLOCKS);
-            d.order = ICX_HUFF_SORT ? (uint32_t*)c->dev.take((size_t)d.nchunks * CHUNK_BLOCKS * 12) : nullptr;
             d.ovf = (uint32_t*)c->dev.take((size_t)d.nblocks * BLOCK_WORDS * 4 + 1024);
             for (int b = 0; b < 2; b++) {
                 d.scratch[b] = (uint32_t*)c->dev.take(((size_t)d.nchunks * CHUNK_WORDS + 1) * 4);
