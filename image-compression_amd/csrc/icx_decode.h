@@ -605,6 +605,9 @@ ICX_HD uint32_t dec_lean_lookup(LeanPtr H, int ti, const ICX_GLOBAL DecSlow* slo
 #ifndef ICX_DEC_SCALAR2
 #define ICX_DEC_SCALAR2 0
 #endif
+#ifndef ICX_DEC_LOCAL_WAIT
+#define ICX_DEC_LOCAL_WAIT 0
+#endif
 ICX_HD uint32_t dec_lean_lookup(const SplitLean& H, int ti, const ICX_GLOBAL DecSlow* slow, uint32_t pk, bool ac)
 {
     uint32_t e = H.lut[ti][pk >> (16 - DEC_LUT_BITS)];
@@ -628,7 +631,19 @@ ICX_HD uint32_t dec_lean_lookup(const SplitLean& H, int ti, const ICX_GLOBAL Dec
         } while (m);
     }
 #endif
+#if defined(__HIP_DEVICE_COMPILE__) && ICX_DEC_LOCAL_WAIT
+    // A long code's second level is a vector load.  Consumed inside the rare
+    // branch (the v_mov), it is also waited for there; consumed after the
+    // join, the compiler waited vmcnt(0) at the join on every step - behind
+    // every coefficient store the wave still had in flight.
+    if (!((e & 31) || !e)) {
+        const uint32_t e2 = dec_lean_symbol(&H.full[ti], &slow[ti], pk, ac);
+        asm volatile("v_mov_b32 %0, %1" : "=v"(e) : "v"(e2));
+    }
+    return e;
+#else
     return (e & 31) || !e ? e : dec_lean_symbol(&H.full[ti], &slow[ti], pk, ac);
+#endif
 }
 
 template <class P>
