@@ -602,11 +602,16 @@ ICX_HD uint32_t dec_lean_lookup(LeanPtr H, int ti, const ICX_GLOBAL DecSlow* slo
 {
     return dec_lean_symbol(&H[ti], &slow[ti], pk, ac);
 }
+// Write-pass second levels: through the scalar cache (SCALAR2) and the rare
+// vector fallback waited for inside its branch (LOCAL_WAIT).  Before, the
+// compiler waited vmcnt(0) after the look-up on every symbol step, i.e. for
+// every coefficient store the wave had in flight: decode 90.4 -> 88.5 ms per
+// 1000-frame call (profiles/r4/ab_r4n_dec_wait.txt).
 #ifndef ICX_DEC_SCALAR2
-#define ICX_DEC_SCALAR2 0
+#define ICX_DEC_SCALAR2 1
 #endif
 #ifndef ICX_DEC_LOCAL_WAIT
-#define ICX_DEC_LOCAL_WAIT 0
+#define ICX_DEC_LOCAL_WAIT 1
 #endif
 ICX_HD uint32_t dec_lean_lookup(const SplitLean& H, int ti, const ICX_GLOBAL DecSlow* slow, uint32_t pk, bool ac)
 {
