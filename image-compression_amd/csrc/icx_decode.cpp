@@ -432,7 +432,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             const int64_t scan_len = (int64_t)(it.job->len - it.J.scan_off);
             const int64_t nmcu = (int64_t)d.mcux * d.mcuy;
             d.nseg_max = it.J.ri ? (int32_t)((nmcu + it.J.ri - 1) / it.J.ri) + 1 : 1;
-            it.ent_cap = (size_t)scan_len + (size_t)(DEC_PAD - 2) * d.nseg_max + DEC_TAIL + 64 + 4 * DEC_WIN;
+            it.ent_cap = (size_t)scan_len + (size_t)(DEC_PAD - 2) * d.nseg_max + DEC_TAIL + 64 + 4 * DEC_WIN_MAX;
             it.ntiles = (scan_len + DEC_TILE - 1) / DEC_TILE;
             it.nblocks = d.nblocks;
             size_t per = (it.dev_in ? 0 : align_up(scan_len, 256)) + align_up(it.ent_cap, 256) + it.ntiles * 8 + 512 +

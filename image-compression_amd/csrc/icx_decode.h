@@ -233,13 +233,23 @@ ICX_HD uint32_t dec_be32(uint32_t v)
 #define ICX_DEC_WIN 8
 #endif
 constexpr int DEC_WIN = ICX_DEC_WIN;
-struct DecReader {
+// The write pass's window (DecLeanWriter): each top-up waits for the
+// coefficient stores the wave issued before it, so a longer window there
+// means fewer such waits (the state-only walks issue no stores).
+#ifndef ICX_DEC_WIN_WRITE
+#define ICX_DEC_WIN_WRITE ICX_DEC_WIN
+#endif
+constexpr int DEC_WIN_WRITE = ICX_DEC_WIN_WRITE;
+constexpr int DEC_WIN_MAX = DEC_WIN > DEC_WIN_WRITE ? DEC_WIN : DEC_WIN_WRITE;
+template <int WIN>
+struct DecReaderT {
+    static constexpr int DEC_WIN = WIN;  // (shadows the global inside the reader)
     const ICX_GLOBAL uint32_t* w;
     uint64_t buf;
     int avail;
     uint32_t wi;    // stream word index of q[0]
     int nq;         // valid words in q
-    uint32_t q[DEC_WIN];
+    uint32_t q[WIN];
 
     ICX_HD void fetch(uint32_t at)
     {
@@ -302,6 +312,7 @@ struct DecReader {
         return v;
     }
 };
+using DecReader = DecReaderT<DEC_WIN>;
 
 // HUFF_EXTEND (jdhuff.c)
 ICX_HD int dec_extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
@@ -824,7 +835,7 @@ struct DecLeanWriter {
     bool own;
     bool bad;
     int64_t blk_base;
-    DecReader R;
+    DecReaderT<DEC_WIN_WRITE> R;
     const uint32_t* words;
 
     ICX_HD int table(int bb, int zz) const { return dec_sel(selp, bb < nby ? 0 : bb - nby + 1, zz != 0 ? 1 : 0); }

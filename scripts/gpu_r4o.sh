@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 4 (n): write pass with the long-code load waited inside its branch
+# (ICX_DEC_LOCAL_WAIT), alone and with scalar-cache second levels: decode
+# parity with the variant, then the e2e A/B.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+ICX_LIB=$(pwd)/image-compression_amd/lib/libicx_w16.so timeout -k 10 600 python -u -m pytest tests/test_decode_gpu.py -x -q \
+    -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_r4o.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_r4o.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu_r4o.log
+ROUNDS=2 bash scripts/ab_e2e.sh base lib/libicx_w12.so lib/libicx_w16.so 2>&1 | tee gpurun_out/ab_r4o_dec_win.txt

@@ -80,7 +80,7 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
         }
     }
     const uint32_t ent_len = (uint32_t)ent.size();
-    for (int p = 0; p < DEC_TAIL + 64 + 4 * DEC_WIN; p++) ent.push_back(0xFF);
+    for (int p = 0; p < DEC_TAIL + 64 + 4 * DEC_WIN_MAX; p++) ent.push_back(0xFF);
     while (ent.size() % 4) ent.push_back(0xFF);
     std::vector<uint32_t> words(ent.size() / 4 + 2, 0xFFFFFFFFu);
     memcpy(words.data(), ent.data(), ent.size());
@@ -238,7 +238,7 @@ extern "C" long dec_emu_lean_check(const uint8_t* jpg, size_t len, int nstarts, 
     }
     const uint32_t ent_len = (uint32_t)ent.size();
     if (!ent_len) return 0;
-    for (int p = 0; p < DEC_TAIL + 64 + 4 * DEC_WIN; p++) ent.push_back(0xFF);
+    for (int p = 0; p < DEC_TAIL + 64 + 4 * DEC_WIN_MAX; p++) ent.push_back(0xFF);
     while (ent.size() % 4) ent.push_back(0xFF);
     std::vector<uint32_t> words(ent.size() / 4 + 2, 0xFFFFFFFFu);
     memcpy(words.data(), ent.data(), ent.size());
