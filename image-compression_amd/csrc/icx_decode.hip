@@ -662,6 +662,9 @@ constexpr int SLOT_DW = 32;
 #ifndef ICX_DEC_FLUSH2
 #define ICX_DEC_FLUSH2 0
 #endif
+#ifndef ICX_DEC_DC_LANE
+#define ICX_DEC_DC_LANE 0
+#endif
 
 // A lane that finishes an owned block only records its index, and the wave
 // then copies every finished slot together (below), permuting to natural
@@ -778,6 +781,20 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
             const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)sk.pend >> 32), l);
             const int64_t bi = (int64_t)(((uint64_t)hi << 32) | lo);
             uint32_t* src = wave_slots + l * SLOT_DW;
+#if ICX_DEC_DC_LANE
+            // lanes 0..31 store the block's 32 coefficient pairs, lane 32 (whose
+            // pair also starts at zig-zag 0) its DC difference into d.dc for
+            // k_dec_dc's dense reads - one store instruction per block
+            if (lane <= 32) {
+                const uint16_t* s16 = (const uint16_t*)src;
+                const int lsw = l & 62;
+                const uint32_t v = s16[zl ^ lsw] | ((uint32_t)s16[zh ^ lsw] << 16);
+                __builtin_amdgcn_wave_barrier();  // every lane's reads before the zeroing
+                src[lane & 31] = 0;               // (lane 32 zeroes word 0 with lane 0)
+                ICX_GLOBAL int32_t* dst = lane < 32 ? (ICX_GLOBAL int32_t*)coefs32 + bi * 32 + lane : dcs + bi;
+                *dst = lane < 32 ? (int32_t)v : (int32_t)(int16_t)v;
+            }
+#else
             if (lane < 32) {
                 const uint16_t* s16 = (const uint16_t*)src;
                 const int lsw = l & 62;
@@ -787,6 +804,7 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
                 coefs32[bi * 32 + lane] = v;
                 if (lane == 0) dcs[bi] = (int16_t)v;  // the DC difference, also for k_dec_dc's dense reads
             }
+#endif
         }
 #endif
         sk.pend = -1;
