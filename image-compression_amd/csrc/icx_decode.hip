@@ -663,7 +663,7 @@ constexpr int SLOT_DW = 32;
 #define ICX_DEC_FLUSH2 0
 #endif
 #ifndef ICX_DEC_DC_LANE
-#define ICX_DEC_DC_LANE 0
+#define ICX_DEC_DC_LANE 1  // 87.8 vs 88.3 ms per 1000-frame decode (profiles/r4/ab_r4o_dec_win.txt)
 #endif
 
 // A lane that finishes an owned block only records its index, and the wave

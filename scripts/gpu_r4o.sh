@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 4 (n): write pass with the long-code load waited inside its branch
-# (ICX_DEC_LOCAL_WAIT), alone and with scalar-cache second levels: decode
-# parity with the variant, then the e2e A/B.
+# Round 4 (o): the write pass's bit window (12 / 16 words) and one store
+# instruction per flushed block (ICX_DEC_DC_LANE): decode parity with two
+# variants, then the e2e A/B.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
