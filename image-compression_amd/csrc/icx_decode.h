@@ -160,11 +160,8 @@ static_assert(offsetof(DecTab, qt) % 16 == 0 && sizeof(DecTab) % 16 == 0, "DecTa
 
 // k_dec_idct work items per image: tiles of 32 blocks (nblk_tiles),
 // DEC_IDCT_TILES consecutive tiles per workgroup.
-#ifndef ICX_DEC_IDCT_REG
-#define ICX_DEC_IDCT_REG 0  // k_dec_idct: one thread per block, the whole 8x8 transform in registers
-#endif
 #ifndef ICX_DEC_IDCT_TILES
-#define ICX_DEC_IDCT_TILES (ICX_DEC_IDCT_REG ? 8 : 1)
+#define ICX_DEC_IDCT_TILES 1
 #endif
 constexpr int DEC_IDCT_TILES = ICX_DEC_IDCT_TILES;  // 4: +20 % (r4e) - one tile per workgroup at 8 per CU overlaps
 ICX_HD long long dec_idct_items(long long nblk_tiles)

@@ -1056,71 +1056,6 @@ __device__ __forceinline__ IdctBlk idct_blk(const DecDesc& d, int i)
     return r;
 }
 
-#if ICX_DEC_IDCT_REG
-// One thread per block (256 blocks per workgroup = DEC_IDCT_TILES tiles of
-// 32): dequantisation, both passes of jpeg_idct_islow and the range limit in
-// registers, no LDS and no barrier; rows go out as 8-byte stores (the lanes of
-// a wave hold neighbouring blocks of one block row, so a row's stores are
-// contiguous).
-__global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecState* S, Plan p)
-{
-    int slot;
-    int64_t wg;
-    if (!plan_slot(p, slot, wg)) return;
-    const int img = p.ids[slot];
-    const DecDesc& d = D[img];
-    if (S[img].status) return;
-    const int64_t nitem = d.fuse420 ? 2 * (int64_t)d.mcux * d.mcuy : d.nblocks;
-    const int64_t i = wg * 256 + threadIdx.x;
-    if (i >= nitem) return;
-    const IdctBlk cb = idct_blk(d, (int)i);
-    if (!cb.real) return;
-    const ICX_GLOBAL uint4* cq = (const ICX_GLOBAL uint4*)((const ICX_GLOBAL int16_t*)d.coefs + cb.b * 64);
-    const ICX_GLOBAL uint4* qq = (const ICX_GLOBAL uint4*)((const ICX_GLOBAL uint16_t*)d.tab->qt[cb.comp]);
-    uint4 q[8], t[8];
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-        q[r] = cq[r];
-        t[r] = qq[r];
-    }
-    const int32_t dcv = ((const ICX_GLOBAL int32_t*)d.dc)[cb.b];
-    int32_t w[64];
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-        const uint32_t a[4] = {q[r].x, q[r].y, q[r].z, q[r].w};
-        const uint32_t b[4] = {t[r].x, t[r].y, t[r].z, t[r].w};
-#pragma unroll
-        for (int c = 0; c < 8; c++)
-            w[r * 8 + c] = (int32_t)(int16_t)(a[c >> 1] >> (16 * (c & 1))) * (int32_t)((b[c >> 1] >> (16 * (c & 1))) & 0xFFFFu);
-    }
-    w[0] = dcv * (int32_t)(t[0].x & 0xFFFFu);
-#pragma unroll
-    for (int c = 0; c < 8; c++) {  // pass 1: columns
-        int32_t v[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = w[k * 8 + c];
-        idct8<CONST_BITS - PASS1_BITS>(v);
-#pragma unroll
-        for (int k = 0; k < 8; k++) w[k * 8 + c] = v[k];
-    }
-    ICX_GLOBAL uint8_t* const dst = (ICX_GLOBAL uint8_t*)d.plane[cb.comp] + (int64_t)cb.by * 8 * d.pw[cb.comp] + cb.bx * 8;
-    const int pitch = d.pw[cb.comp];
-#pragma unroll
-    for (int r = 0; r < 8; r++) {  // pass 2: rows
-        int32_t v[8];
-#pragma unroll
-        for (int c = 0; c < 8; c++) v[c] = w[r * 8 + c];
-        idct8<CONST_BITS + PASS1_BITS + 3>(v);
-        uint32_t lo = 0, hi = 0;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            lo |= idct_limit(v[c]) << (8 * c);
-            hi |= idct_limit(v[c + 4]) << (8 * c);
-        }
-        *(ICX_GLOBAL uint2*)(dst + (int64_t)r * pitch) = make_uint2(lo, hi);
-    }
-}
-#else
 __global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecState* S, Plan p)
 {
     __shared__ int32_t ws[32][8 * 9];
@@ -1169,7 +1104,6 @@ __global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecSta
         dc = ndc;
     }
 }
-#endif
 
 // ----------------------------------------------------------- colour output
 // Upsampled chroma sample of component plane P at full-resolution (X, Y)
