@@ -920,12 +920,6 @@ constexpr int TABLE_LDS_WORDS = TAB_WORDS > OUT_WORDS + 8 + 8 * FF_COPIES ? TAB_
 constexpr int AC_SIZES = 11;                // AC magnitude categories 0..10 (8-bit JPEG)
 constexpr int AC_ENTRIES = 16 * AC_SIZES;   // (run, size) slots per table
 
-#ifndef ICX_HUFF_PUT_NB
-#define ICX_HUFF_PUT_NB 0
-#endif
-#ifndef ICX_HUFF_ZRL_ANY
-#define ICX_HUFF_ZRL_ANY 0
-#endif
 // Per-thread bit sinks: a 64-bit accumulator flushing whole 32-bit words.
 // LdsSink writes the thread's LDS slot, clamped to its last word; a block that
 // outgrows the slot (bits > SLOT_BITS) is coded again into a GlobalSink.
@@ -938,22 +932,11 @@ struct LdsSink {
     {
         acc = (acc << len) | v;
         n += len;
-#if ICX_HUFF_PUT_NB
-        // branch-free: the slot word at wb is written on every put (a partial
-        // word is rewritten by a later put or by finish(); one past the
-        // block's last word lies outside its bit count), wb advances once 32
-        // bits are complete - no exec-mask save / restore per coded entry
-        const bool full = n >= 32;
-        n -= full ? 32 : 0;
-        *(uint32_t*)((char*)slots + min(wb, wlast)) = (uint32_t)(acc >> n);
-        wb += full ? 4u : 0u;
-#else
         if (n >= 32) {
             n -= 32;
             *(uint32_t*)((char*)slots + min(wb, wlast)) = (uint32_t)(acc >> n);
             wb += 4;
         }
-#endif
     }
     __device__ __forceinline__ void finish()
     {
@@ -1095,13 +1078,10 @@ __device__ __forceinline__ void encode_block(Sink& sink, const uint32_t (&ev)[PR
         if (i < cnt && y >= 1.0f) {
             const uint32_t k = (e >> 3) & 63;
             uint32_t run = k - last - 1;
-#if ICX_HUFF_ZRL_ANY
-            if (__any(run >= 16))  // a wave-uniform test: no exec-mask save / restore on the common path
-#endif
-                while (run >= 16) {
-                    sink.put(zrl.x, (int)zrl.y);
-                    run -= 16;
-                }
+            while (run >= 16) {
+                sink.put(zrl.x, (int)zrl.y);
+                run -= 16;
+            }
             const uint32_t u = (uint32_t)y;                    // |q| >= 1
             const int sz = __builtin_amdgcn_frexp_expf(y);     // bit length of |q|
             const uint2 c2 = ac_entry(ac, run, sz, stride);
