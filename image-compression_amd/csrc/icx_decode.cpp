@@ -435,7 +435,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             it.ent_cap = (size_t)scan_len + (size_t)(DEC_PAD - 2) * d.nseg_max + DEC_TAIL + 64 + 4 * DEC_WIN_MAX;
             it.ntiles = (scan_len + DEC_TILE - 1) / DEC_TILE;
             it.nblocks = d.nblocks;
-            size_t per = (it.dev_in ? 0 : align_up(scan_len, 256)) + align_up(it.ent_cap, 256) + it.ntiles * 8 + 512 +
+            size_t per = (it.dev_in ? 0 : align_up(scan_len, 256)) + align_up(it.ent_cap, 256) + it.ntiles * 24 + 512 +
                          (size_t)d.nseg_max * 4 + (size_t)d.nblocks * (128 + 4) + sizeof(DecTab) + 4096;
             for (int k = 0; k < 3; k++) per += align_up((size_t)d.pw[k] * d.ph[k], 256);
             per += (size_t)(it.ent_cap * 8 / 2048 + 2) * (8 + 2 + 4 + 4);  // subsequence arrays at S >= 2048
@@ -558,6 +558,21 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         uint32_t* d_changed = (uint32_t*)c->dev.take((size_t)max_it * 4);
         uint32_t* d_wlcnt = (uint32_t*)c->dev.take((size_t)m * max_it * 4);
         for (int k = 0; k < m; k++) desc[k].wl_cnt = d_wlcnt;
+        int64_t max_tiles = 0;
+        if (ICX_DEC_ONEPASS) {  // look-back tile states of the whole sub-batch: one block, one clear
+            int64_t all = 0;
+            for (int k = 0; k < m; k++) {
+                all += sub[k]->ntiles;
+                max_tiles = std::max<int64_t>(max_tiles, sub[k]->ntiles);
+            }
+            UnstuffTile* ts = (UnstuffTile*)c->dev.take((size_t)all * sizeof(UnstuffTile) + 64);
+            e = hipMemsetAsync(ts, 0, (size_t)all * sizeof(UnstuffTile), c->stream);
+            if (e != hipSuccess) return hip_fail(c, e, "tile state clear");
+            for (int k = 0; k < m; k++) {
+                desc[k].tstate = ts;
+                ts += sub[k]->ntiles;
+            }
+        }
         if (c->dev.overflow) return fail(c, ICX_E_NOMEM, "device workspace overrun (workspace sizing)");
         uint32_t* h_changed = (uint32_t*)c->host.take(4);
         std::vector<int32_t> ids(m);
@@ -592,7 +607,10 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         if (e != hipSuccess) return hip_fail(c, e, "counter clear");
         {
             Timed tm(c, "dec_unstuff", stuffed);
-            launch_unstuff(d_desc, d_state, Pc.p, Pc.total, Pt.p, Pt.total, d_ids, m, S, c->stream);
+            if (ICX_DEC_ONEPASS)
+                launch_unstuff_onepass(d_desc, d_state, d_ids, m, max_tiles, S, c->stream);
+            else
+                launch_unstuff(d_desc, d_state, Pc.p, Pc.total, Pt.p, Pt.total, d_ids, m, S, c->stream);
         }
         {
             Timed tm(c, "dec_init", stuffed);

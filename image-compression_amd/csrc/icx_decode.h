@@ -110,6 +110,8 @@ struct DecTab {
     uint8_t pad[9];
 };
 
+struct UnstuffTile;
+
 // Per-image descriptor (host-built, read-only on the device).
 struct DecDesc {
     const uint8_t* scan;   // entropy-coded segment (stuffed), device
@@ -118,6 +120,7 @@ struct DecDesc {
     int64_t ent_cap;       // bytes allocated for ent
     uint32_t* tile_cnt;    // per unstuff tile: output bytes, then exclusive offsets
     uint32_t* tile_rst;    // per unstuff tile: RSTn markers, then exclusive offsets
+    UnstuffTile* tstate;   // k_unstuff_onepass: per tile (ntiles)
     uint32_t* seg;         // interval start byte offsets in ent (nseg_max entries)
     uint64_t* est;         // entry state per subsequence (nsub_max + 1)
     uint64_t* ck;          // sync-walk checkpoints, DEC_CK_MAX per subsequence (dec_sync_walk)
@@ -198,8 +201,22 @@ struct DecState {
     uint32_t nsub;         // subsequences in use
     uint32_t total_blocks; // blocks the entropy decode produced
     int32_t status;        // 0 ok, 6 corrupt
-    int32_t pad;
+    uint32_t ticket;       // k_unstuff_onepass: next tile to hand out (0 before the launch)
 };
+
+// k_unstuff_onepass's per-tile state for the decoupled look-back (zeroed before
+// the launch): status = 0 not ready, 1 aggregate (this tile alone), 2
+// inclusive prefix (every tile up to this one); | UT_TERM when a terminating
+// marker lies in (aggregate) / up to (prefix) the tile.
+struct UnstuffTile {
+    uint32_t status;
+    uint32_t rst;      // RSTn markers
+    uint64_t bytes;    // unstuffed bytes (RSTn -> DEC_PAD)
+};
+constexpr uint32_t UT_AGG = 1, UT_PREFIX = 2, UT_TERM = 4;
+#ifndef ICX_DEC_ONEPASS
+#define ICX_DEC_ONEPASS 0  // unstuffing in one pass over the scan (decoupled look-back) instead of count / scan / scatter
+#endif
 
 ICX_HD uint64_t dec_pack(uint32_t pos, int b, int z) { return ((uint64_t)pos << 16) | ((uint64_t)b << 8) | (uint64_t)z; }
 ICX_HD uint32_t dec_pos(uint64_t st) { return (uint32_t)(st >> 16); }

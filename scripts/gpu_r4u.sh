@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 4 (u): one-pass unstuffing with a decoupled look-back (ICX_DEC_ONEPASS):
+# decode and pipeline parity with that build, then the e2e A/B.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+ICX_LIB=$(pwd)/image-compression_amd/lib/libicx_op.so timeout -k 10 600 python -u -m pytest tests/test_decode_gpu.py \
+    tests/test_pipeline_gpu.py -x -q -m gpu --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu_r4u.log 2>&1 \
+    || { tail -40 gpurun_out/pytest_gpu_r4u.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu_r4u.log
+ROUNDS=2 bash scripts/ab_e2e.sh base lib/libicx_op.so 2>&1 | tee gpurun_out/ab_r4u_dec_onepass.txt
