@@ -435,7 +435,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             it.ent_cap = (size_t)scan_len + (size_t)(DEC_PAD - 2) * d.nseg_max + DEC_TAIL + 64 + 4 * DEC_WIN_MAX;
             it.ntiles = (scan_len + DEC_TILE - 1) / DEC_TILE;
             it.nblocks = d.nblocks;
-            size_t per = (it.dev_in ? 0 : align_up(scan_len, 256)) + align_up(it.ent_cap, 256) + it.ntiles * 24 + 512 +
+            size_t per = (it.dev_in ? 0 : align_up(scan_len, 256)) + align_up(it.ent_cap, 256) + it.ntiles * 40 + 512 +
                          (size_t)d.nseg_max * 4 + (size_t)d.nblocks * (128 + 4) + sizeof(DecTab) + 4096;
             for (int k = 0; k < 3; k++) per += align_up((size_t)d.pw[k] * d.ph[k], 256);
             per += (size_t)(it.ent_cap * 8 / 2048 + 2) * (8 + 2 + 4 + 4);  // subsequence arrays at S >= 2048
@@ -611,6 +611,48 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
                 launch_unstuff_onepass(d_desc, d_state, d_ids, m, max_tiles, S, c->stream);
             else
                 launch_unstuff(d_desc, d_state, Pc.p, Pc.total, Pt.p, Pt.total, d_ids, m, S, c->stream);
+        }
+        if (getenv("ICX_DEC_DEBUG_UNSTUFF")) {  // development check: the device stream against the host rule
+            (void)hipStreamSynchronize(c->stream);
+            std::vector<DecState> hs(m);
+            (void)hipMemcpy(hs.data(), d_state, sizeof(DecState) * m, hipMemcpyDeviceToHost);
+            for (int k = 0; k < std::min(m, 3); k++) {
+                const DecDesc& dd = desc[k];
+                std::vector<uint8_t> sc(dd.scan_len), en(hs[k].ent_len);
+                (void)hipMemcpy(sc.data(), dd.scan, dd.scan_len, hipMemcpyDefault);
+                (void)hipMemcpy(en.data(), dd.ent, en.size(), hipMemcpyDeviceToHost);
+                std::vector<uint8_t> ref;
+                int64_t end = dd.scan_len;
+                for (int64_t i = 0; i + 1 < dd.scan_len; i++)
+                    if (sc[i] == 0xFF && sc[i + 1] != 0x00 && sc[i + 1] != 0xFF && !(sc[i + 1] >= 0xD0 && sc[i + 1] <= 0xD7)) {
+                        end = i;
+                        break;
+                    }
+                int nr = 0;
+                for (int64_t i = 0; i < end; i++) {
+                    int rst;
+                    const int kk = dec_unstuff_rule(i ? sc[i - 1] : 0, sc[i], i + 1 < dd.scan_len ? sc[i + 1] : 0, &rst);
+                    if (rst) {
+                        for (int p = 0; p < DEC_PAD; p++) ref.push_back(0xFF);
+                        nr++;
+                    } else if (kk) {
+                        ref.push_back(sc[i]);
+                    }
+                }
+                size_t mis = 0;
+                while (mis < std::min(ref.size(), en.size()) && ref[mis] == en[mis]) mis++;
+                fprintf(stderr, "[unstuff %d] scan %lld ntiles %d ent_len %u ref %zu nseg %u ref_rst %d nsub %u status %d ticket %u first_mismatch %zu\n",
+                        k, (long long)dd.scan_len, dd.ntiles, hs[k].ent_len, ref.size(), hs[k].nseg, nr, hs[k].nsub,
+                        hs[k].status, hs[k].ticket, mis);
+                if (ICX_DEC_ONEPASS) {
+                    std::vector<UnstuffTile> ts(dd.ntiles);
+                    (void)hipMemcpy(ts.data(), dd.tstate, sizeof(UnstuffTile) * dd.ntiles, hipMemcpyDeviceToHost);
+                    for (int t = 0; t < std::min(dd.ntiles, 12); t++)
+                        fprintf(stderr, "   tile %d status %u bytes %llu / %llu rst %u / %u\n", t, ts[t].status,
+                                (unsigned long long)ts[t].bytes[0], (unsigned long long)ts[t].bytes[1], ts[t].rst[0],
+                                ts[t].rst[1]);
+                }
+            }
         }
         {
             Timed tm(c, "dec_init", stuffed);

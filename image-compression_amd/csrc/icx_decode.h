@@ -210,8 +210,11 @@ struct DecState {
 // marker lies in (aggregate) / up to (prefix) the tile.
 struct UnstuffTile {
     uint32_t status;
-    uint32_t rst;      // RSTn markers
-    uint64_t bytes;    // unstuffed bytes (RSTn -> DEC_PAD)
+    uint32_t rst[2];   // RSTn markers: [0] this tile alone, [1] up to it
+    uint32_t pad;
+    uint64_t bytes[2]; // unstuffed bytes (RSTn -> DEC_PAD), as rst: each written once, before
+                       // the status that announces it (a prefix published later cannot
+                       // change an aggregate a reader of the older status fetches)
 };
 constexpr uint32_t UT_AGG = 1, UT_PREFIX = 2, UT_TERM = 4;
 #ifndef ICX_DEC_ONEPASS

@@ -526,8 +526,9 @@ struct UtVal {
 __device__ __forceinline__ void ut_publish(UnstuffTile* t, uint32_t state, const UtVal& v)
 {
     ICX_GLOBAL UnstuffTile* g = (ICX_GLOBAL UnstuffTile*)t;
-    g->bytes = v.bytes;
-    g->rst = v.rst;
+    const int k = state == UT_PREFIX ? 1 : 0;
+    g->bytes[k] = v.bytes;
+    g->rst[k] = v.rst;
     __hip_atomic_store(&t->status, state | (v.term ? UT_TERM : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -548,9 +549,10 @@ __device__ __forceinline__ UtVal ut_lookback(UnstuffTile* T, int tile, bool& stu
         uint32_t r = 0;
         if (i >= 0) {
             st = __hip_atomic_load(&T[i].status, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            if (st & 3) {
-                b = ((const ICX_GLOBAL UnstuffTile*)T)[i].bytes;
-                r = ((const ICX_GLOBAL UnstuffTile*)T)[i].rst;
+            if (st & 3) {  // the aggregate or the prefix, whichever the status announces
+                const int k = (st & 3) == UT_PREFIX ? 1 : 0;
+                b = ((const ICX_GLOBAL UnstuffTile*)T)[i].bytes[k];
+                r = ((const ICX_GLOBAL UnstuffTile*)T)[i].rst[k];
             }
         }
         const uint64_t isp = __ballot((st & 3) == UT_PREFIX);
