@@ -205,18 +205,23 @@ struct DecState {
 };
 
 // k_unstuff_onepass's per-tile state for the decoupled look-back (zeroed before
-// the launch): status = 0 not ready, 1 aggregate (this tile alone), 2
-// inclusive prefix (every tile up to this one); | UT_TERM when a terminating
-// marker lies in (aggregate) / up to (prefix) the tile.
+// the launch): two self-contained 64-bit words, this tile's aggregate and the
+// inclusive prefix up to it, each = 1 (valid) | term << 1 (a terminating
+// marker in / up to the tile) | RSTn count << 2 (22 bits) | bytes << 24
+// (40 bits).  One relaxed device-scope atomic per word: a reader never pairs
+// a status with data from another publication, and no acquire (an L2
+// invalidation per poll) is needed.
 struct UnstuffTile {
-    uint32_t status;
-    uint32_t rst[2];   // RSTn markers: [0] this tile alone, [1] up to it
-    uint32_t pad;
-    uint64_t bytes[2]; // unstuffed bytes (RSTn -> DEC_PAD), as rst: each written once, before
-                       // the status that announces it (a prefix published later cannot
-                       // change an aggregate a reader of the older status fetches)
+    uint64_t agg;
+    uint64_t pre;
 };
-constexpr uint32_t UT_AGG = 1, UT_PREFIX = 2, UT_TERM = 4;
+constexpr uint32_t UT_RST_MAX = (1u << 22) - 1;
+ICX_HD uint64_t ut_word(bool term, uint32_t rst, uint64_t bytes)
+{
+    // (more markers than fit: the file has more than its intervals and is
+    // reported corrupt by the interval check either way)
+    return 1ull | (term ? 2ull : 0ull) | ((uint64_t)(rst < UT_RST_MAX ? rst : UT_RST_MAX) << 2) | (bytes << 24);
+}
 #ifndef ICX_DEC_ONEPASS
 #define ICX_DEC_ONEPASS 0  // unstuffing in one pass over the scan (decoupled look-back) instead of count / scan / scatter
 #endif

@@ -523,13 +523,9 @@ struct UtVal {
     bool term;
 };
 
-__device__ __forceinline__ void ut_publish(UnstuffTile* t, uint32_t state, const UtVal& v)
+__device__ __forceinline__ void ut_publish(uint64_t* w, const UtVal& v)
 {
-    ICX_GLOBAL UnstuffTile* g = (ICX_GLOBAL UnstuffTile*)t;
-    const int k = state == UT_PREFIX ? 1 : 0;
-    g->bytes[k] = v.bytes;
-    g->rst[k] = v.rst;
-    __hip_atomic_store(&t->status, state | (v.term ? UT_TERM : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(w, ut_word(v.term, v.rst, v.bytes), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Exclusive prefix of tile `tile` (> 0) by wave 0; every lane returns it.
@@ -544,21 +540,23 @@ __device__ __forceinline__ UtVal ut_lookback(UnstuffTile* T, int tile, bool& stu
     stuck = false;
     for (;;) {
         const int i = top - lane;
-        uint32_t st = UT_PREFIX;  // tile -1: an empty prefix
-        uint64_t b = 0;
-        uint32_t r = 0;
+        uint32_t st = 2;  // 0 not ready, 1 aggregate, 2 prefix (tile -1: an empty prefix)
+        uint64_t w = 1;   // valid, empty
         if (i >= 0) {
-            st = __hip_atomic_load(&T[i].status, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            if (st & 3) {  // the aggregate or the prefix, whichever the status announces
-                const int k = (st & 3) == UT_PREFIX ? 1 : 0;
-                b = ((const ICX_GLOBAL UnstuffTile*)T)[i].bytes[k];
-                r = ((const ICX_GLOBAL UnstuffTile*)T)[i].rst[k];
+            w = __hip_atomic_load(&T[i].pre, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            st = 2;
+            if (!(w & 1)) {
+                w = __hip_atomic_load(&T[i].agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                st = (w & 1) ? 1 : 0;
             }
         }
-        const uint64_t isp = __ballot((st & 3) == UT_PREFIX);
+        const bool term = (w & 2) != 0;
+        const uint32_t r = (uint32_t)(w >> 2) & UT_RST_MAX;
+        const uint64_t b = w >> 24;
+        const uint64_t isp = __ballot(st == 2);
         const int firstp = isp ? __builtin_ctzll(isp) : 64;  // nearest prefix (lane = distance - 1)
         const uint64_t below = firstp >= 64 ? ~0ull : ((1ull << firstp) - 1);  // lanes before it
-        if (__ballot((st & 3) == 0) & below) {  // a tile between us and the prefix is not ready
+        if (__ballot(st == 0) & below) {  // a tile between us and the prefix is not ready
             if (++polls > (1u << 22)) {
                 stuck = true;
                 return carry;
@@ -568,7 +566,7 @@ __device__ __forceinline__ UtVal ut_lookback(UnstuffTile* T, int tile, bool& stu
         }
         // aggregates of lanes below firstp (tiles top .. top - firstp + 1); the
         // lowest-tile terminated one (highest lane) absorbs everything above it
-        const uint64_t tm = __ballot((st & UT_TERM) != 0 && (st & 3) == UT_AGG) & below;
+        const uint64_t tm = __ballot(term && st == 1) & below;
         const int kt = tm ? 63 - __builtin_clzll(tm) : -1;  // highest lane with a terminated aggregate
         const bool use = lane < firstp && lane >= (kt >= 0 ? kt : 0);
         uint64_t sb = use ? b : 0;
@@ -581,11 +579,10 @@ __device__ __forceinline__ UtVal ut_lookback(UnstuffTile* T, int tile, bool& stu
         if (kt >= 0) carry = UtVal{sb, sr, true};
         else carry = UtVal{carry.bytes + sb, carry.rst + sr, carry.term};
         if (firstp < 64) {  // the nearest prefix: it comes first in order
-            const uint32_t ps = (uint32_t)__shfl((int)st, firstp, 64);
-            const uint64_t pb = __shfl(b, firstp, 64);
-            const uint32_t pr = (uint32_t)__shfl((int)r, firstp, 64);
-            if (ps & UT_TERM) return UtVal{pb, pr, true};
-            return UtVal{pb + carry.bytes, pr + carry.rst, carry.term};
+            const uint64_t pw = __shfl(w, firstp, 64);
+            const UtVal p{pw >> 24, (uint32_t)(pw >> 2) & UT_RST_MAX, (pw & 2) != 0};
+            if (p.term) return p;
+            return UtVal{p.bytes + carry.bytes, p.rst + carry.rst, carry.term};
         }
         top -= 64;
     }
@@ -659,13 +656,13 @@ __global__ void __launch_bounds__(256) k_unstuff_onepass(const DecDesc* D, DecSt
         UtVal exv{0, 0, false};
         bool stuck = false;
         if (tile == 0) {
-            if (threadIdx.x == 0) ut_publish(&d.tstate[0], UT_PREFIX, local);
+            if (threadIdx.x == 0) ut_publish(&d.tstate[0].pre, local);
         } else {
-            if (threadIdx.x == 0) ut_publish(&d.tstate[tile], UT_AGG, local);
+            if (threadIdx.x == 0) ut_publish(&d.tstate[tile].agg, local);
             exv = ut_lookback(d.tstate, tile, stuck);
             if (threadIdx.x == 0) {
                 const UtVal inc = exv.term ? exv : UtVal{exv.bytes + tb, exv.rst + tr, term_local};
-                ut_publish(&d.tstate[tile], UT_PREFIX, inc);
+                ut_publish(&d.tstate[tile].pre, inc);
                 if (stuck) atomicOr(&st.status, 6);
             }
         }
