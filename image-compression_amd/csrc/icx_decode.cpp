@@ -435,7 +435,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             it.ent_cap = (size_t)scan_len + (size_t)(DEC_PAD - 2) * d.nseg_max + DEC_TAIL + 64 + 4 * DEC_WIN_MAX;
             it.ntiles = (scan_len + DEC_TILE - 1) / DEC_TILE;
             it.nblocks = d.nblocks;
-            size_t per = (it.dev_in ? 0 : align_up(scan_len, 256)) + align_up(it.ent_cap, 256) + it.ntiles * 24 + 512 +
+            size_t per = (it.dev_in ? 0 : align_up(scan_len, 256)) + align_up(it.ent_cap, 256) + it.ntiles * 8 + 512 +
                          (size_t)d.nseg_max * 4 + (size_t)d.nblocks * (128 + 4) + sizeof(DecTab) + 4096;
             for (int k = 0; k < 3; k++) per += align_up((size_t)d.pw[k] * d.ph[k], 256);
             per += (size_t)(it.ent_cap * 8 / 2048 + 2) * (8 + 2 + 4 + 4);  // subsequence arrays at S >= 2048
@@ -558,24 +558,6 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         uint32_t* d_changed = (uint32_t*)c->dev.take((size_t)max_it * 4);
         uint32_t* d_wlcnt = (uint32_t*)c->dev.take((size_t)m * max_it * 4);
         for (int k = 0; k < m; k++) desc[k].wl_cnt = d_wlcnt;
-        int64_t max_tiles = 0;
-        bool onepass = ICX_DEC_ONEPASS;
-        for (int k = 0; k < m && onepass; k++)  // the look-back words hold 22-bit RSTn counts
-            if (desc[k].nseg_max > (int32_t)UT_RST_MAX) onepass = false;
-        if (onepass) {  // look-back tile states of the whole sub-batch: one block, one clear
-            int64_t all = 0;
-            for (int k = 0; k < m; k++) {
-                all += sub[k]->ntiles;
-                max_tiles = std::max<int64_t>(max_tiles, sub[k]->ntiles);
-            }
-            UnstuffTile* ts = (UnstuffTile*)c->dev.take((size_t)all * sizeof(UnstuffTile) + 64);
-            e = hipMemsetAsync(ts, 0, (size_t)all * sizeof(UnstuffTile), c->stream);
-            if (e != hipSuccess) return hip_fail(c, e, "tile state clear");
-            for (int k = 0; k < m; k++) {
-                desc[k].tstate = ts;
-                ts += sub[k]->ntiles;
-            }
-        }
         if (c->dev.overflow) return fail(c, ICX_E_NOMEM, "device workspace overrun (workspace sizing)");
         uint32_t* h_changed = (uint32_t*)c->host.take(4);
         std::vector<int32_t> ids(m);
@@ -610,10 +592,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         if (e != hipSuccess) return hip_fail(c, e, "counter clear");
         {
             Timed tm(c, "dec_unstuff", stuffed);
-            if (onepass)
-                launch_unstuff_onepass(d_desc, d_state, d_ids, m, max_tiles, S, c->stream);
-            else
-                launch_unstuff(d_desc, d_state, Pc.p, Pc.total, Pt.p, Pt.total, d_ids, m, S, c->stream);
+            launch_unstuff(d_desc, d_state, Pc.p, Pc.total, Pt.p, Pt.total, d_ids, m, S, c->stream);
         }
         if (getenv("ICX_DEC_DEBUG_UNSTUFF")) {  // development check: the device stream against the host rule
             (void)hipStreamSynchronize(c->stream);
@@ -644,16 +623,9 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
                 }
                 size_t mis = 0;
                 while (mis < std::min(ref.size(), en.size()) && ref[mis] == en[mis]) mis++;
-                fprintf(stderr, "[unstuff %d] scan %lld ntiles %d ent_len %u ref %zu nseg %u ref_rst %d nsub %u status %d ticket %u first_mismatch %zu\n",
+                fprintf(stderr, "[unstuff %d] scan %lld ntiles %d ent_len %u ref %zu nseg %u ref_rst %d nsub %u status %d first_mismatch %zu\n",
                         k, (long long)dd.scan_len, dd.ntiles, hs[k].ent_len, ref.size(), hs[k].nseg, nr, hs[k].nsub,
-                        hs[k].status, hs[k].ticket, mis);
-                if (onepass) {
-                    std::vector<UnstuffTile> ts(dd.ntiles);
-                    (void)hipMemcpy(ts.data(), dd.tstate, sizeof(UnstuffTile) * dd.ntiles, hipMemcpyDeviceToHost);
-                    for (int t = 0; t < std::min(dd.ntiles, 12); t++)
-                        fprintf(stderr, "   tile %d agg %016llx pre %016llx\n", t, (unsigned long long)ts[t].agg,
-                                (unsigned long long)ts[t].pre);
-                }
+                        hs[k].status, mis);
             }
         }
         {

@@ -110,8 +110,6 @@ struct DecTab {
     uint8_t pad[9];
 };
 
-struct UnstuffTile;
-
 // Per-image descriptor (host-built, read-only on the device).
 struct DecDesc {
     const uint8_t* scan;   // entropy-coded segment (stuffed), device
@@ -120,7 +118,6 @@ struct DecDesc {
     int64_t ent_cap;       // bytes allocated for ent
     uint32_t* tile_cnt;    // per unstuff tile: output bytes, then exclusive offsets
     uint32_t* tile_rst;    // per unstuff tile: RSTn markers, then exclusive offsets
-    UnstuffTile* tstate;   // k_unstuff_onepass: per tile (ntiles)
     uint32_t* seg;         // interval start byte offsets in ent (nseg_max entries)
     uint64_t* est;         // entry state per subsequence (nsub_max + 1)
     uint64_t* ck;          // sync-walk checkpoints, DEC_CK_MAX per subsequence (dec_sync_walk)
@@ -201,30 +198,9 @@ struct DecState {
     uint32_t nsub;         // subsequences in use
     uint32_t total_blocks; // blocks the entropy decode produced
     int32_t status;        // 0 ok, 6 corrupt
-    uint32_t ticket;       // k_unstuff_onepass: next tile to hand out (0 before the launch)
+    int32_t pad;
 };
 
-// k_unstuff_onepass's per-tile state for the decoupled look-back (zeroed before
-// the launch): two self-contained 64-bit words, this tile's aggregate and the
-// inclusive prefix up to it, each = 1 (valid) | term << 1 (a terminating
-// marker in / up to the tile) | RSTn count << 2 (22 bits) | bytes << 24
-// (40 bits).  One relaxed device-scope atomic per word: a reader never pairs
-// a status with data from another publication, and no acquire (an L2
-// invalidation per poll) is needed.
-struct UnstuffTile {
-    uint64_t agg;
-    uint64_t pre;
-};
-constexpr uint32_t UT_RST_MAX = (1u << 22) - 1;
-ICX_HD uint64_t ut_word(bool term, uint32_t rst, uint64_t bytes)
-{
-    // (more markers than fit: the file has more than its intervals and is
-    // reported corrupt by the interval check either way)
-    return 1ull | (term ? 2ull : 0ull) | ((uint64_t)(rst < UT_RST_MAX ? rst : UT_RST_MAX) << 2) | (bytes << 24);
-}
-#ifndef ICX_DEC_ONEPASS
-#define ICX_DEC_ONEPASS 0  // unstuffing in one pass over the scan (decoupled look-back) instead of count / scan / scatter
-#endif
 
 ICX_HD uint64_t dec_pack(uint32_t pos, int b, int z) { return ((uint64_t)pos << 16) | ((uint64_t)b << 8) | (uint64_t)z; }
 ICX_HD uint32_t dec_pos(uint64_t st) { return (uint32_t)(st >> 16); }

@@ -502,269 +502,6 @@ __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const
     }
 }
 
-// ------------------------------------------------------- one-pass unstuffing
-// k_unstuff_count + k_unstuff_scan + k_unstuff_scatter in one pass over the
-// stuffed scan (ICX_DEC_ONEPASS): a workgroup takes the next tile of its image
-// from the image's ticket (so every tile it waits on belongs to a workgroup
-// that started earlier), counts the tile's output bytes and RSTn markers up to
-// its first terminating marker, publishes that aggregate, and finds its
-// exclusive prefix by a decoupled look-back - one wave reads the states of the
-// 64 preceding tiles at a time, sums aggregates back to the nearest inclusive
-// prefix, waits while a tile before it is not ready - then publishes its
-// inclusive prefix and compacts its bytes at that offset exactly as
-// k_unstuff_scatter does.  Tiles after the image's first terminating marker
-// output nothing; the tile holding it (or the image's last tile) finishes the
-// image's stream (length, tail pad, interval and subsequence counts) as
-// k_unstuff_scan did.  Combining prefixes: a terminated prefix absorbs
-// everything after it.
-struct UtVal {
-    uint64_t bytes;
-    uint32_t rst;
-    bool term;
-};
-
-__device__ __forceinline__ void ut_publish(uint64_t* w, const UtVal& v)
-{
-    __hip_atomic_store(w, ut_word(v.term, v.rst, v.bytes), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Exclusive prefix of tile `tile` (> 0) by wave 0; every lane returns it.
-// A bounded spin: a tile not ready after ~2^22 polls marks the image corrupt
-// (cannot happen when every earlier tile's workgroup is running).
-__device__ __forceinline__ UtVal ut_lookback(UnstuffTile* T, int tile, bool& stuck)
-{
-    const int lane = threadIdx.x & 63;
-    UtVal carry{0, 0, false};  // tiles above the current window, up to tile - 1
-    int top = tile - 1;        // the window's highest tile
-    uint32_t polls = 0;
-    stuck = false;
-    for (;;) {
-        const int i = top - lane;
-        uint32_t st = 2;  // 0 not ready, 1 aggregate, 2 prefix (tile -1: an empty prefix)
-        uint64_t w = 1;   // valid, empty
-        if (i >= 0) {
-            w = __hip_atomic_load(&T[i].pre, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            st = 2;
-            if (!(w & 1)) {
-                w = __hip_atomic_load(&T[i].agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                st = (w & 1) ? 1 : 0;
-            }
-        }
-        const bool term = (w & 2) != 0;
-        const uint32_t r = (uint32_t)(w >> 2) & UT_RST_MAX;
-        const uint64_t b = w >> 24;
-        const uint64_t isp = __ballot(st == 2);
-        const int firstp = isp ? __builtin_ctzll(isp) : 64;  // nearest prefix (lane = distance - 1)
-        const uint64_t below = firstp >= 64 ? ~0ull : ((1ull << firstp) - 1);  // lanes before it
-        if (__ballot(st == 0) & below) {  // a tile between us and the prefix is not ready
-            if (++polls > (1u << 22)) {
-                stuck = true;
-                return carry;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        // aggregates of lanes below firstp (tiles top .. top - firstp + 1); the
-        // lowest-tile terminated one (highest lane) absorbs everything above it
-        const uint64_t tm = __ballot(term && st == 1) & below;
-        const int kt = tm ? 63 - __builtin_clzll(tm) : -1;  // highest lane with a terminated aggregate
-        const bool use = lane < firstp && lane >= (kt >= 0 ? kt : 0);
-        uint64_t sb = use ? b : 0;
-        uint32_t sr = use ? r : 0u;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            sb += __shfl_xor(sb, o, 64);
-            sr += __shfl_xor(sr, o, 64);
-        }
-        if (kt >= 0) carry = UtVal{sb, sr, true};
-        else carry = UtVal{carry.bytes + sb, carry.rst + sr, carry.term};
-        if (firstp < 64) {  // the nearest prefix: it comes first in order
-            const uint64_t pw = __shfl(w, firstp, 64);
-            const UtVal p{pw >> 24, (uint32_t)(pw >> 2) & UT_RST_MAX, (pw & 2) != 0};
-            if (p.term) return p;
-            return UtVal{p.bytes + carry.bytes, p.rst + carry.rst, carry.term};
-        }
-        top -= 64;
-    }
-}
-
-__global__ void __launch_bounds__(256) k_unstuff_onepass(const DecDesc* D, DecState* S, const int32_t* ids, int m,
-                                                         uint32_t sub_bits)
-{
-    __shared__ uint32_t sh[8];
-    __shared__ uint32_t bufw[(DEC_TILE / 2 * DEC_PAD + 64) / 4];  // worst case: an RSTn marker every 2 bytes
-    __shared__ int s_tile;
-    __shared__ uint32_t s_mark;
-    __shared__ uint64_t s_exb;
-    __shared__ uint32_t s_exr, s_exterm;
-    uint8_t* const buf = (uint8_t*)bufw;
-    // images interleaved (workgroup w: image w % m, slot w / m), so an image's
-    // tiles start about as fast as they finish
-    const int img = ids[blockIdx.x % (unsigned)m];
-    const int slot = (int)(blockIdx.x / (unsigned)m);
-    const DecDesc& d = D[img];
-    DecState& st = S[img];
-    if (slot >= d.ntiles) return;  // workgroup-uniform
-    if (threadIdx.x == 0) {
-        s_tile = (int)atomicAdd(&st.ticket, 1u);
-        s_mark = ~0u;
-    }
-    __syncthreads();
-    const int tile = s_tile;  // < ntiles: exactly ntiles workgroups of this image get a ticket
-    const int64_t len = d.scan_len;
-    const int64_t base = (int64_t)tile * DEC_TILE + threadIdx.x * 16;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    bool plain = false;  // 16 data bytes, no 0xFF among them or before them
-    uint32_t keep = 0, rstm = 0;
-    if (base < len) {
-        const Scan16 q = scan16(d.scan, len, base);
-        v = q.v;
-        const int prev = base > 0 ? ((const ICX_GLOBAL uint8_t*)d.scan)[base - 1] : 0;
-        plain = base + 16 <= len && !any_ff(v, prev);
-        if (!plain) {
-            const Unstuff16 x = unstuff16(classify16(v), prev, q.next);
-            const int64_t rem = len - base;
-            const uint32_t valid = rem >= 16 ? 0xFFFFu : (1u << rem) - 1;
-            keep = x.keep & valid;
-            rstm = x.rst & valid;
-            const uint32_t mk = x.mark & (rem - 1 >= 16 ? 0xFFFFu : (1u << (rem - 1)) - 1);  // needs its next byte
-            if (mk) atomicMin(&s_mark, threadIdx.x * 16u + (uint32_t)__builtin_ctz(mk));
-        }
-    }
-    __syncthreads();
-    const uint32_t mark = s_mark;  // the tile's first terminating marker (tile byte), ~0: none
-    const bool term_local = mark != ~0u;
-    if (term_local) {  // bytes from the marker on drop out
-        const int lo = (int)mark - (int)threadIdx.x * 16;
-        if (lo <= 0) {
-            plain = false;
-            keep = rstm = 0;
-        } else if (lo < 16) {
-            const uint32_t mm = (1u << lo) - 1;
-            keep = plain ? mm : keep & mm;
-            rstm &= mm;
-            plain = false;
-        }
-    }
-    const uint32_t nr = (uint32_t)__popc(rstm);
-    const uint32_t nb = plain ? 16u : (uint32_t)__popc(keep) + DEC_PAD * nr;
-    uint32_t tot;  // one scan of bytes (bits 0..19) and RSTn markers (<< 20)
-    const uint32_t ex = block_exscan<256>(nb | (nr << 20), sh, tot);
-    const uint32_t tb = tot & 0xFFFFFu, tr = tot >> 20;
-    const UtVal local{tb, tr, term_local};
-    if (threadIdx.x < 64) {
-        UtVal exv{0, 0, false};
-        bool stuck = false;
-        if (tile == 0) {
-            if (threadIdx.x == 0) ut_publish(&d.tstate[0].pre, local);
-        } else {
-            if (threadIdx.x == 0) ut_publish(&d.tstate[tile].agg, local);
-            exv = ut_lookback(d.tstate, tile, stuck);
-            if (threadIdx.x == 0) {
-                const UtVal inc = exv.term ? exv : UtVal{exv.bytes + tb, exv.rst + tr, term_local};
-                ut_publish(&d.tstate[tile].pre, inc);
-                if (stuck) atomicOr(&st.status, 6);
-            }
-        }
-        if (threadIdx.x == 0) {
-            s_exb = exv.bytes;
-            s_exr = exv.rst;
-            s_exterm = exv.term || stuck ? 1u : 0u;
-        }
-    }
-    __syncthreads();
-    if (s_exterm) return;  // after the image's terminating marker: no output (workgroup-uniform)
-    const uint64_t tile_off64 = s_exb;
-    const uint32_t tile_off = (uint32_t)tile_off64;
-    uint32_t ob = ex & 0xFFFFFu;
-    uint32_t orr = (ex >> 20) + s_exr;
-    for (uint32_t k = threadIdx.x; k < (tb + 7) / 4; k += 256) bufw[k] = 0;
-    __syncthreads();
-    if (plain) {
-        const uint32_t s8 = (ob & 3) * 8;
-        uint32_t* wp = bufw + (ob >> 2);
-        if (s8 == 0) {
-            wp[0] = v.x; wp[1] = v.y; wp[2] = v.z; wp[3] = v.w;
-        } else {
-            atomicOr(wp, v.x << s8);
-            wp[1] = (v.x >> (32 - s8)) | (v.y << s8);
-            wp[2] = (v.y >> (32 - s8)) | (v.z << s8);
-            wp[3] = (v.z >> (32 - s8)) | (v.w << s8);
-            atomicOr(wp + 4, v.w >> (32 - s8));
-        }
-    } else if (nr == 0 && nb > 0) {
-        uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        uint32_t drop = ~keep & 0xFFFFu;
-        while (drop) {
-            const int k = 31 - __builtin_clz(drop);
-            drop &= ~(1u << k);
-            const int q = k >> 2;
-            const uint32_t low = (1u << (8 * (k & 3))) - 1u;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t up = j < 3 ? w[j + 1] << 24 : 0u;
-                if (j > q) w[j] = (w[j] >> 8) | up;
-                else if (j == q) w[j] = (w[j] & low) | ((w[j] >> 8) & ~low) | up;
-            }
-        }
-        const uint32_t s8 = (ob & 3) * 8;
-        uint32_t* wp = bufw + (ob >> 2);
-        atomicOr(wp, w[0] << s8);
-#pragma unroll
-        for (int j = 1; j < 4; j++) atomicOr(wp + j, (w[j] << s8) | (s8 ? w[j - 1] >> (32 - s8) : 0u));
-        if (s8) atomicOr(wp + 4, w[3] >> (32 - s8));
-    } else if (nr > 0) {  // RSTn codes (restart intervals): byte by byte
-        const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            if ((rstm >> k) & 1) {
-                for (int q = 0; q < DEC_PAD; q++) buf[ob + q] = 0xFF;
-                ob += DEC_PAD;
-                if (orr + 1 < (uint32_t)d.nseg_max) ((ICX_GLOBAL uint32_t*)d.seg)[orr + 1] = tile_off + ob;
-                orr++;
-            } else if ((keep >> k) & 1) {
-                buf[ob++] = (uint8_t)(vw[k >> 2] >> (8 * (k & 3)));
-            }
-        }
-    }
-    __syncthreads();
-    ICX_GLOBAL uint8_t* const ent = (ICX_GLOBAL uint8_t*)d.ent;
-    const uint32_t head = min((4u - (tile_off & 3u)) & 3u, tb);
-    if (threadIdx.x < head && (int64_t)(tile_off + threadIdx.x) < d.ent_cap) ent[tile_off + threadIdx.x] = buf[threadIdx.x];
-    const uint32_t nw = (tb - head) >> 2;
-    ICX_GLOBAL uint32_t* const dstw = (ICX_GLOBAL uint32_t*)(ent + tile_off + head);
-    const int64_t cap_w = (d.ent_cap - (int64_t)(tile_off + head)) >> 2;
-    for (uint32_t k = threadIdx.x; k < nw; k += 256) {
-        const uint32_t lb = head + 4 * k;
-        const uint32_t val = __builtin_amdgcn_alignbyte(bufw[(lb >> 2) + 1], bufw[lb >> 2], head);
-        if ((int64_t)k < cap_w) dstw[k] = val;
-    }
-    const uint32_t t0 = head + 4 * nw;
-    if (threadIdx.x < tb - t0 && (int64_t)(tile_off + t0 + threadIdx.x) < d.ent_cap)
-        ent[tile_off + t0 + threadIdx.x] = buf[t0 + threadIdx.x];
-    // the image's stream ends in this tile: length, tail pad, counts (k_unstuff_scan's epilogue)
-    if (term_local || tile == d.ntiles - 1) {
-        const uint64_t len_b = tile_off64 + tb;
-        const uint32_t nrst = s_exr + tr;
-        const bool fits = (int64_t)len_b + DEC_TAIL + 8 <= d.ent_cap;  // more RSTn markers than intervals: corrupt
-        if (fits)
-            for (int k = threadIdx.x; k < DEC_TAIL + 8; k += blockDim.x) ent[len_b + k] = 0xFF;
-        if (threadIdx.x == 0) {
-            if (!fits) atomicOr(&st.status, 6);
-            st.ent_len = (uint32_t)len_b;
-            st.nseg = nrst + 1 <= (uint32_t)d.nseg_max ? nrst + 1 : (uint32_t)d.nseg_max;
-            if (nrst + 1 > (uint32_t)d.nseg_max) atomicOr(&st.status, 6);
-            uint32_t nsub = (uint32_t)((len_b * 8 + sub_bits - 1) / sub_bits);
-            if (nsub > (uint32_t)d.nsub_max) {
-                nsub = d.nsub_max;
-                atomicOr(&st.status, 6);
-            }
-            st.nsub = nsub;
-            ((ICX_GLOBAL uint32_t*)d.seg)[0] = 0;
-        }
-    }
-}
-
 // ------------------------------------------------------------ entropy decode
 // Initial entry-state estimates: subsequence j starts decoding `warm` bits
 // before its first bit from a guessed state (block 0, DC next) and takes the
@@ -1621,13 +1358,6 @@ static dim3 grid_of(const Plan& p, int64_t nwg)
 void launch_stage(const StageJob* jobs, const Plan& tiles, int64_t nwg, hipStream_t st)
 {
     if (nwg > 0) hipLaunchKernelGGL(k_stage, grid_of(tiles, nwg), dim3(256), 0, st, jobs, tiles);
-}
-
-void launch_unstuff_onepass(const DecDesc* d, DecState* s, const int32_t* ids, int m, int64_t max_tiles,
-                            uint32_t sub_bits, hipStream_t st)
-{
-    if (max_tiles <= 0 || m <= 0) return;
-    hipLaunchKernelGGL(k_unstuff_onepass, dim3((unsigned)(max_tiles * m)), dim3(256), 0, st, d, s, ids, m, sub_bits);
 }
 
 void launch_unstuff(const DecDesc* d, DecState* s, const Plan& cnt, int64_t ncnt, const Plan& tiles, int64_t ntiles,

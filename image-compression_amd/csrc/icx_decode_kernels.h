@@ -10,9 +10,6 @@ namespace icx {
 // tiles: per job ceil(dst_len / STAGE_TILE) workgroups (Plan.ids unused)
 void launch_stage(const StageJob* jobs, const Plan& tiles, int64_t nwg, hipStream_t st);
 // cnt / tiles: per image ceil(ntiles / DEC_UNSTUFF_TILES) / ceil(ntiles / DEC_SCATTER_TILES) work items (4 KiB stuffed tiles)
-// one workgroup per (image, tile slot), images interleaved: m * max_tiles workgroups
-void launch_unstuff_onepass(const DecDesc* d, DecState* s, const int32_t* ids, int m, int64_t max_tiles,
-                            uint32_t sub_bits, hipStream_t st);
 void launch_unstuff(const DecDesc* d, DecState* s, const Plan& cnt, int64_t ncnt, const Plan& tiles, int64_t ntiles,
                     const int32_t* ids, int m, uint32_t sub_bits, hipStream_t st);
 // subs: per image ceil((nsub_max + 1) / 256) workgroups
