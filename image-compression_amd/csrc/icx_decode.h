@@ -201,7 +201,6 @@ struct DecState {
     int32_t pad;
 };
 
-
 ICX_HD uint64_t dec_pack(uint32_t pos, int b, int z) { return ((uint64_t)pos << 16) | ((uint64_t)b << 8) | (uint64_t)z; }
 ICX_HD uint32_t dec_pos(uint64_t st) { return (uint32_t)(st >> 16); }
 
