@@ -407,6 +407,33 @@ ICX_HD int dec_zz(int n)
 // 63, as jpeg_natural_order's tail), the finished block to sink.flush_if.
 // Table index of (component, DC or AC) from the packed selector (dec_selector).
 ICX_HD int dec_sel(uint32_t selp, int comp, int ac) { return (int)((selp >> (4 * (2 * comp + ac))) & 3); }
+#ifndef ICX_DEC_BSEL
+#define ICX_DEC_BSEL 1
+#endif
+// The same per block of the walk's MCU: 4 bits per block-in-MCU bb (DC table
+// index, then AC table index), so the lean walks pick the next table with one
+// shift instead of the component arithmetic (nbmcu <= 10: 40 bits).
+ICX_HD uint64_t dec_block_sel(uint32_t selp, int nby, int nbmcu)
+{
+    uint64_t r = 0;
+    for (int bb = 0; bb < nbmcu && bb < 16; bb++) {
+        const int comp = bb < nby ? 0 : bb - nby + 1;
+        r |= (uint64_t)dec_sel(selp, comp, 0) << (4 * bb) | (uint64_t)dec_sel(selp, comp, 1) << (4 * bb + 2);
+    }
+    return r;
+}
+ICX_HD int dec_block_table(uint64_t bsel, int bb, int zz) { return (int)((bsel >> (4 * bb + (zz != 0 ? 2 : 0))) & 3); }
+// The map is the same for every lane of a workgroup (one image): kept in
+// scalar registers on the device.
+ICX_HD uint64_t dec_uniform(uint64_t v)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+#else
+    return v;
+#endif
+}
 
 // Sink of an owned walk: put(zig-zag index, value) per symbol (index 0 = the
 // DC difference), flush_if(block complete and owned, index).  Every symbol
@@ -688,12 +715,17 @@ struct DecLeanWalker {
     const ICX_GLOBAL uint32_t* seg;
     uint32_t nseg, ent_bits;
     int nby, nbmcu;
+    uint64_t bsel;  // dec_block_sel
     uint32_t pos, n;
     int b, z, ti;  // ti: table of the next symbol (component of block b, DC at z == 0)
     DecReader R;
     const uint32_t* words;
 
+#if ICX_DEC_BSEL
+    ICX_HD int table(int bb, int zz) const { return dec_block_table(bsel, bb, zz); }
+#else
     ICX_HD int table(int bb, int zz) const { return dec_sel(selp, bb < nby ? 0 : bb - nby + 1, zz != 0 ? 1 : 0); }
+#endif
     ICX_HD void start(uint64_t st)
     {
         pos = dec_pos(st);
@@ -778,6 +810,7 @@ ICX_HD DecLeanWalker<LeanPtr> dec_lean_walker(const DecDesc& d, LeanPtr H, const
     w.ent_bits = ent_bits;
     w.nby = d.nby;
     w.nbmcu = d.wmcu;
+    w.bsel = dec_uniform(dec_block_sel(selp, d.nby, d.wmcu));
     return w;
 }
 
@@ -830,6 +863,7 @@ struct DecLeanWriter {
     int nby, nbmcu;
     int ri, nbm;
     int64_t nblocks;
+    uint64_t bsel;  // dec_block_sel
     uint32_t pos, n;
     int b, z, ti;
     bool own;
@@ -838,7 +872,11 @@ struct DecLeanWriter {
     DecReaderT<DEC_WIN_WRITE> R;
     const uint32_t* words;
 
+#if ICX_DEC_BSEL
+    ICX_HD int table(int bb, int zz) const { return dec_block_table(bsel, bb, zz); }
+#else
     ICX_HD int table(int bb, int zz) const { return dec_sel(selp, bb < nby ? 0 : bb - nby + 1, zz != 0 ? 1 : 0); }
+#endif
     ICX_HD void start(uint64_t st)
     {
         pos = dec_pos(st);
@@ -925,6 +963,7 @@ ICX_HD DecLeanWriter<LeanPtr> dec_lean_writer(const DecDesc& d, LeanPtr H, const
     w.nbm = d.nbmcu;
     w.nblocks = d.nblocks;
     w.blk_base = blk_base;
+    w.bsel = dec_uniform(dec_block_sel(selp, d.nby, d.wmcu));
     return w;
 }
 
