@@ -408,7 +408,7 @@ ICX_HD int dec_zz(int n)
 // Table index of (component, DC or AC) from the packed selector (dec_selector).
 ICX_HD int dec_sel(uint32_t selp, int comp, int ac) { return (int)((selp >> (4 * (2 * comp + ac))) & 3); }
 #ifndef ICX_DEC_BSEL
-#define ICX_DEC_BSEL 0
+#define ICX_DEC_BSEL 1  // decode -0.4 % (profiles/r4/ab_r4x_dec_bsel.txt)
 #endif
 // The same per block of the walk's MCU: 4 bits per block-in-MCU bb (DC table
 // index, then AC table index), so the lean walks pick the next table with one
