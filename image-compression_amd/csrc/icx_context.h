@@ -203,10 +203,13 @@ struct icx_ctx {
     // arenas while the previous sub-batch computes, outputs leave (io_down)
     // while the next one computes; created on first use.
     hipStream_t io_up = nullptr, io_down = nullptr;
-    // decoder: images whose entry states settled early finish on dec_aux while
-    // the others keep relaxing on `stream` (created at the first decode)
-    hipStream_t dec_aux = nullptr;
-    hipEvent_t ev_dec_split = nullptr, ev_dec_aux = nullptr;
+    // decoder: images whose entry states settled early finish on the dec_aux
+    // streams (one per settling check, round robin) while the others keep
+    // relaxing on `stream` (created at the first decode)
+    static constexpr int DEC_AUX_MAX = 4;
+    int n_dec_aux = 0;
+    hipStream_t dec_aux[DEC_AUX_MAX] = {};
+    hipEvent_t ev_dec_split = nullptr, ev_dec_aux[DEC_AUX_MAX] = {};
     icx::DevArena stage[2];
     hipEvent_t ev_up[2] = {nullptr, nullptr}, ev_down[2] = {nullptr, nullptr}, ev_done = nullptr;
 };

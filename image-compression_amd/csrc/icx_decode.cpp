@@ -684,16 +684,24 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             }
             return ICX_OK;
         };
-        if (!c->dec_aux) {
-            hipError_t he2 = hipStreamCreateWithFlags(&c->dec_aux, hipStreamNonBlocking);
-            if (he2 == hipSuccess) he2 = hipEventCreateWithFlags(&c->ev_dec_split, hipEventDisableTiming);
-            if (he2 == hipSuccess) he2 = hipEventCreateWithFlags(&c->ev_dec_aux, hipEventDisableTiming);
+        // tails of different checks go to different aux streams, so a check's
+        // images need not wait behind the previous check's tail
+        static const int NAUX = std::min(icx_ctx::DEC_AUX_MAX,
+                                         std::max(1, getenv("ICX_DEC_AUX") ? atoi(getenv("ICX_DEC_AUX")) : 1));
+        if (!c->ev_dec_split) {
+            hipError_t he2 = hipEventCreateWithFlags(&c->ev_dec_split, hipEventDisableTiming);
             if (he2 != hipSuccess) return hip_fail(c, he2, "decode aux stream");
+        }
+        while (c->n_dec_aux < NAUX) {
+            hipError_t he2 = hipStreamCreateWithFlags(&c->dec_aux[c->n_dec_aux], hipStreamNonBlocking);
+            if (he2 == hipSuccess) he2 = hipEventCreateWithFlags(&c->ev_dec_aux[c->n_dec_aux], hipEventDisableTiming);
+            if (he2 != hipSuccess) return hip_fail(c, he2, "decode aux stream");
+            c->n_dec_aux++;
         }
         uint32_t* h_wl = (uint32_t*)c->host.take((size_t)m * 4);
         if (!h_wl) return fail(c, ICX_E_NOMEM, "pinned staging exhausted");
         std::vector<char> tailed(m, 0);
-        bool aux_used = false;
+        int aux_used = 0, aux_next = 0;  // aux streams used by this call (the first aux_used)
         int it = 0;
         static const char* const sync_names[] = {"dec_sync", "dec_sync_r1", "dec_sync_r2", "dec_sync_r3",
                                                  "dec_sync_r4", "dec_sync_r5", "dec_sync_r6", "dec_sync_r7+"};
@@ -716,8 +724,9 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
                 if (!tailed[k] && h_wl[k] == 0) early.push_back(k);
             if (!early.empty()) {
                 for (int k : early) tailed[k] = 1;
-                if (icx_status st = tail(early, c->dec_aux)) return st;
-                aux_used = true;
+                if (icx_status st = tail(early, c->dec_aux[aux_next % NAUX])) return st;
+                aux_next++;
+                aux_used = std::min(aux_next, NAUX);
             }
         }
         c->stats["dec_sync_iters"].launches += it;
@@ -735,9 +744,9 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             if (!tailed[k]) rest.push_back(k);
         if (!rest.empty())
             if (icx_status st = tail(rest, c->stream)) return st;
-        if (aux_used) {  // the final download waits for the aux stream's images too
-            e = hipEventRecord(c->ev_dec_aux, c->dec_aux);
-            if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_dec_aux, 0);
+        for (int k = 0; k < aux_used; k++) {  // the final download waits for the aux streams' images too
+            e = hipEventRecord(c->ev_dec_aux[k], c->dec_aux[k]);
+            if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_dec_aux[k], 0);
             if (e != hipSuccess) return hip_fail(c, e, "decode stream join");
         }
         DecState* h_state = (DecState*)c->host.take(sizeof(DecState) * m);

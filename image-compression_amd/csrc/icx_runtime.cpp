@@ -1211,12 +1211,12 @@ void icx_destroy(icx_ctx* ctx)
     for (auto p : ctx->d_inv)
         if (p) hipFree(p);
     hipStreamDestroy(ctx->stream);
-    if (ctx->dec_aux) {
-        hipStreamSynchronize(ctx->dec_aux);
-        hipStreamDestroy(ctx->dec_aux);
-        hipEventDestroy(ctx->ev_dec_split);
-        hipEventDestroy(ctx->ev_dec_aux);
+    for (int k = 0; k < ctx->n_dec_aux; k++) {
+        hipStreamSynchronize(ctx->dec_aux[k]);
+        hipStreamDestroy(ctx->dec_aux[k]);
+        hipEventDestroy(ctx->ev_dec_aux[k]);
     }
+    if (ctx->ev_dec_split) hipEventDestroy(ctx->ev_dec_split);
     if (ctx->io_up) {
         hipStreamSynchronize(ctx->io_up);
         hipStreamSynchronize(ctx->io_down);

@@ -3,7 +3,8 @@
 // subsequence, how long the runs of consecutive wrong estimates are (= the
 // re-walk launches a file needs), and whether K candidate warm-ups per
 // subsequence (mode 0: lengths warm, 2 warm, ...; mode m > 0: start offsets
-// warm + i * m bits) would contain the true state.  Uses the product's state
+// warm + i * m bits; mode -1: warm-ups starting in each block of the MCU)
+// would contain the true state.  Uses the product's state
 // machine (icx_decode.h) on one JPEG file:
 //   g++ -O2 -std=c++17 -I image-compression_amd/csrc -I include scripts/dec_warmup_stats.cpp \
 //       image-compression_amd/csrc/icx_jpeg_parse.cpp -o /tmp/dws
@@ -75,8 +76,10 @@ int main(int argc, char** argv)
     for (uint32_t j = 1; j < nsub; j++) {
         std::set<uint64_t> cs;
         for (int m = 0; m < K; m++) {
-            uint32_t w = mode == 0 ? warm * (m + 1) : warm + m * (mode);
-            uint64_t e = walk(dec_pack(j * S > w ? j * S - w : 0, 0, 0), j * S);
+            // mode -1: one warm-up per starting block of the MCU (block phase m)
+            uint32_t w = mode == 0 ? warm * (m + 1) : mode < 0 ? warm : warm + m * (mode);
+            const int b0 = mode < 0 ? m % d.nbmcu : 0;
+            uint64_t e = walk(dec_pack(j * S > w ? j * S - w : 0, b0, 0), j * S);
             if (m == 0) { ok1[j] = e == tru[j]; hit1 += ok1[j]; posok += dec_pos(e) == dec_pos(tru[j]); }
             cs.insert(e);
         }
