@@ -255,8 +255,9 @@ struct DecReaderT {
     {
         wi = at;
         nq = DEC_WIN;
+        const ICX_GLOBAL uint32_t* const wa = w + at;  // one address, the words at immediate offsets
 #pragma unroll
-        for (int j = 0; j < DEC_WIN; j++) q[j] = w[at + j];
+        for (int j = 0; j < DEC_WIN; j++) q[j] = wa[j];
 #if defined(__HIP_DEVICE_COMPILE__)
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing later waits on q
 #endif
