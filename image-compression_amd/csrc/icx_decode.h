@@ -44,6 +44,14 @@ namespace icx {
 
 constexpr int DEC_SUB_BITS = 1024;   // bits per subsequence (one thread)
 constexpr int DEC_LUT_BITS = 10;     // Huffman fast-lookup width
+// k_dec_write workgroup size.  The pass is LDS-limited (a 128-B block slot
+// per lane + the first-level tables): 256 lanes = 40 KiB, four workgroups =
+// 16 waves per CU.  576 lanes (80 KiB, meant as two workgroups = 18 waves)
+// measured +28 % decode: one workgroup per CU (profiles/r4/ab_r4zb_dec_write.txt).
+#ifndef ICX_DEC_WRITE_NT
+#define ICX_DEC_WRITE_NT 256
+#endif
+constexpr int DEC_WRITE_NT = ICX_DEC_WRITE_NT;
 constexpr int DEC_TILE = 4096;       // stuffed bytes per unstuff tile (256 threads x 16)
 #ifndef ICX_DEC_UNSTUFF_TILES
 #define ICX_DEC_UNSTUFF_TILES 4
@@ -315,6 +323,9 @@ struct DecReaderT {
 };
 using DecReader = DecReaderT<DEC_WIN>;
 
+#ifndef ICX_DEC_EXT_BF
+#define ICX_DEC_EXT_BF 1  // write walk: branch-free value extension (-0.9 %, profiles/r4/ab_r4zb_dec_write.txt)
+#endif
 // HUFF_EXTEND (jdhuff.c)
 ICX_HD int dec_extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
@@ -905,7 +916,13 @@ struct DecLeanWriter {
         const uint32_t v = (uint32_t)(R.buf >> (64 - c)) & ((1u << sz) - 1u);
         R.skip(c);
         pos += (uint32_t)c;
+#if ICX_DEC_EXT_BF
+        // HUFF_EXTEND without the sz == 0 branch: v = 0 and half = 0 then
+        const int half = (1 << sz) >> 1;
+        const int x = (int)v - ((int)v < half ? (1 << sz) - 1 : 0);
+#else
         const int x = sz ? dec_extend((int)v, sz) : 0;
+#endif
         const int zc = z + zadd - 1;  // zig-zag index of a coefficient (DC: 0)
         sink.put(!own ? 0 : sz ? (zc > 63 ? 63 : zc) : z, x);
         z += zadd;

@@ -689,10 +689,10 @@ struct PendSink {
 // which on q95 content is most iterations.  Only the first levels of the
 // Huffman tables are in LDS (SplitHuff): the second levels of the few codes
 // longer than 10 bits are read from the image's tables in global memory.
-__global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S, Plan p, uint32_t sub_bits)
+__global__ void __launch_bounds__(DEC_WRITE_NT) k_dec_write(const DecDesc* D, DecState* S, Plan p, uint32_t sub_bits)
 {
     __shared__ __attribute__((aligned(16))) uint16_t L1[4][1 << DEC_LUT_BITS];
-    __shared__ __attribute__((aligned(16))) uint32_t slots[256 * SLOT_DW];
+    __shared__ __attribute__((aligned(16))) uint32_t slots[DEC_WRITE_NT * SLOT_DW];
     int slot;
     int64_t wg;
     if (!plan_slot(p, slot, wg)) return;
@@ -704,8 +704,8 @@ __global__ void __launch_bounds__(256) k_dec_write(const DecDesc* D, DecState* S
     // subsequence sit in neighbouring lanes, so a wave reads a contiguous
     // stretch of the stream
     const int np = dec_pieces(sub_bits);
-    const int64_t t = wg * 256 + threadIdx.x;
-    if (wg * 256 >= (int64_t)st.nsub * np) return;
+    const int64_t t = wg * DEC_WRITE_NT + threadIdx.x;
+    if (wg * DEC_WRITE_NT >= (int64_t)st.nsub * np) return;
     const int64_t j = t / np;
     const int lane = threadIdx.x & 63;
     uint32_t* wave_slots = slots + (threadIdx.x - lane) * SLOT_DW;
@@ -1391,7 +1391,7 @@ void launch_dec_offsets(const DecDesc* d, DecState* s, const int32_t* ids, int m
 void launch_dec_write(const DecDesc* d, DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
                       hipStream_t st)
 {
-    if (nwg > 0) hipLaunchKernelGGL(k_dec_write, grid_of(subs, nwg), dim3(256), 0, st, d, s, subs, sub_bits);
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_write, grid_of(subs, nwg), dim3(DEC_WRITE_NT), 0, st, d, s, subs, sub_bits);
 }
 
 void launch_dec_dc(const DecDesc* d, const DecState* s, const int32_t* ids, int m, hipStream_t st)
