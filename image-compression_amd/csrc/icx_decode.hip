@@ -659,6 +659,9 @@ __global__ void __launch_bounds__(1024) k_dec_offsets(const DecDesc* D, DecState
 // without a pad dword, so 256 slots take 32 KiB and, with the 8 KiB of
 // first-level Huffman tables, a workgroup 40 KiB: four per CU.
 constexpr int SLOT_DW = 32;
+#ifndef ICX_DEC_WRITE_UNROLL2
+#define ICX_DEC_WRITE_UNROLL2 1  // with a 9-word write window: -2.1 % (profiles/r4/ab_r4zd_dec_unroll.txt)
+#endif
 #ifndef ICX_DEC_FLUSH2
 #define ICX_DEC_FLUSH2 0
 #endif
@@ -672,9 +675,27 @@ constexpr int SLOT_DW = 32;
 struct PendSink {
     uint8_t* slot;  // this lane's slot
     uint32_t sw;    // lane & 62
+#if ICX_DEC_PEND32
+    int64_t base;   // the piece's first block
+    int32_t pend;   // block waiting for the wave flush, from base; -1 = none
+    __device__ __forceinline__ void flush_if(bool c, int64_t bi) { pend = c ? (int32_t)(bi - base) : pend; }
+    __device__ __forceinline__ int64_t block_of(int l) const
+    {
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)base, l);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)base >> 32), l);
+        return (int64_t)(((uint64_t)hi << 32) | lo) + (int64_t)__builtin_amdgcn_readlane((uint32_t)pend, l);
+    }
+#else
     int64_t pend;   // block waiting for the wave flush, -1 = none
-    __device__ __forceinline__ void put(int z, int v) { *(int16_t*)(slot + ((z ^ sw) << 1)) = (int16_t)v; }
     __device__ __forceinline__ void flush_if(bool c, int64_t bi) { pend = c ? bi : pend; }
+    __device__ __forceinline__ int64_t block_of(int l) const
+    {
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)pend, l);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)pend >> 32), l);
+        return (int64_t)(((uint64_t)hi << 32) | lo);
+    }
+#endif
+    __device__ __forceinline__ void put(int z, int v) { *(int16_t*)(slot + ((z ^ sw) << 1)) = (int16_t)v; }
 };
 
 // Write pass.  The walk runs in a wave-uniform loop, one symbol per lane per
@@ -735,80 +756,102 @@ __global__ void __launch_bounds__(DEC_WRITE_NT) k_dec_write(const DecDesc* D, De
             run = w.running(stop);
         }
     }
+#if ICX_DEC_PEND32
+    PendSink sk{(uint8_t*)mys, (uint32_t)(lane & 62), pc.blk, -1};
+#else
     PendSink sk{(uint8_t*)mys, (uint32_t)(lane & 62), -1};
+#endif
     ICX_GLOBAL uint32_t* coefs32 = (ICX_GLOBAL uint32_t*)d.coefs;  // global_store: vmcnt only, not lgkmcnt
     ICX_GLOBAL int32_t* dcs = (ICX_GLOBAL int32_t*)d.dc;
     const int zl = dec_zz((2 * lane) & 63), zh = dec_zz((2 * lane + 1) & 63);  // this lane's flush pair (lane % 32)
+    // copy the wave's finished blocks out of their slots (after every step: a
+    // lane's next block reuses its slot)
+    auto flush = [&]() {
+    uint64_t m = __ballot(sk.pend >= 0);
+#if ICX_DEC_FLUSH2
+    // two finished blocks per round: lanes 0..31 copy the first, 32..63 the second
+    while (m) {
+        const int l0 = __builtin_ctzll(m);
+        m &= m - 1;
+        const int l1 = m ? __builtin_ctzll(m) : l0;
+        const bool two = m != 0;
+        m &= m - 1;
+        const int64_t b0 = sk.block_of(l0), b1 = sk.block_of(l1);
+        const bool upper = lane >= 32;
+        const int l = upper ? l1 : l0;
+        const int64_t bi = upper ? b1 : b0;
+        uint32_t* src = wave_slots + l * SLOT_DW;
+        if (!upper || two) {
+            const int q = lane & 31;
+            const uint16_t* s16 = (const uint16_t*)src;
+            const int lsw = l & 62;
+            const uint32_t v = s16[zl ^ lsw] | ((uint32_t)s16[zh ^ lsw] << 16);
+            __builtin_amdgcn_wave_barrier();  // every lane's reads before the zeroing
+            src[q] = 0;
+            coefs32[bi * 32 + q] = v;
+            if (q == 0) dcs[bi] = (int16_t)v;  // the DC difference, also for k_dec_dc's dense reads
+        }
+    }
+#else
+    while (m) {
+        const int l = __builtin_ctzll(m);
+        m &= m - 1;
+        const int64_t bi = sk.block_of(l);
+        uint32_t* src = wave_slots + l * SLOT_DW;
+#if ICX_DEC_DC_LANE
+        // lanes 0..31 store the block's 32 coefficient pairs, lane 32 (whose
+        // pair also starts at zig-zag 0) its DC difference into d.dc for
+        // k_dec_dc's dense reads - one store instruction per block
+        if (lane <= 32) {
+            const uint16_t* s16 = (const uint16_t*)src;
+            const int lsw = l & 62;
+            const uint32_t v = s16[zl ^ lsw] | ((uint32_t)s16[zh ^ lsw] << 16);
+            __builtin_amdgcn_wave_barrier();  // every lane's reads before the zeroing
+            src[lane & 31] = 0;               // (lane 32 zeroes word 0 with lane 0)
+            ICX_GLOBAL int32_t* dst = lane < 32 ? (ICX_GLOBAL int32_t*)coefs32 + bi * 32 + lane : dcs + bi;
+            *dst = lane < 32 ? (int32_t)v : (int32_t)(int16_t)v;
+        }
+#else
+        if (lane < 32) {
+            const uint16_t* s16 = (const uint16_t*)src;
+            const int lsw = l & 62;
+            const uint32_t v = s16[zl ^ lsw] | ((uint32_t)s16[zh ^ lsw] << 16);
+            __builtin_amdgcn_wave_barrier();  // every lane's reads before the zeroing
+            src[lane] = 0;
+            coefs32[bi * 32 + lane] = v;
+            if (lane == 0) dcs[bi] = (int16_t)v;  // the DC difference, also for k_dec_dc's dense reads
+        }
+#endif
+    }
+#endif
+    sk.pend = -1;
+    };
+#if ICX_DEC_WRITE_UNROLL2
+    // two steps per top-up check: a step consumes at most one window word, so
+    // a lane holding >= 1 word at every refill needs the top-up once any holds <= 2
+    while (__any(run)) {
+        if (run) {
+            w.step(sk);
+            run = w.running(stop);
+        }
+        flush();
+        if (run) {
+            w.step(sk);
+            run = w.running(stop);
+        }
+        if (__any(run && w.R.nq <= 2) && run) w.R.top_up();
+        flush();
+    }
+#else
     while (__any(run)) {
         if (run) {
             w.step(sk);
             run = w.running(stop);
         }
         if (__any(run && w.R.low()) && run && w.R.wants()) w.R.top_up();
-        uint64_t m = __ballot(sk.pend >= 0);
-#if ICX_DEC_FLUSH2
-        // two finished blocks per round: lanes 0..31 copy the first, 32..63 the second
-        while (m) {
-            const int l0 = __builtin_ctzll(m);
-            m &= m - 1;
-            const int l1 = m ? __builtin_ctzll(m) : l0;
-            const bool two = m != 0;
-            m &= m - 1;
-            const uint32_t lo0 = __builtin_amdgcn_readlane((uint32_t)sk.pend, l0);
-            const uint32_t hi0 = __builtin_amdgcn_readlane((uint32_t)((uint64_t)sk.pend >> 32), l0);
-            const uint32_t lo1 = __builtin_amdgcn_readlane((uint32_t)sk.pend, l1);
-            const uint32_t hi1 = __builtin_amdgcn_readlane((uint32_t)((uint64_t)sk.pend >> 32), l1);
-            const bool upper = lane >= 32;
-            const int l = upper ? l1 : l0;
-            const int64_t bi = (int64_t)(upper ? ((uint64_t)hi1 << 32) | lo1 : ((uint64_t)hi0 << 32) | lo0);
-            uint32_t* src = wave_slots + l * SLOT_DW;
-            if (!upper || two) {
-                const int q = lane & 31;
-                const uint16_t* s16 = (const uint16_t*)src;
-                const int lsw = l & 62;
-                const uint32_t v = s16[zl ^ lsw] | ((uint32_t)s16[zh ^ lsw] << 16);
-                __builtin_amdgcn_wave_barrier();  // every lane's reads before the zeroing
-                src[q] = 0;
-                coefs32[bi * 32 + q] = v;
-                if (q == 0) dcs[bi] = (int16_t)v;  // the DC difference, also for k_dec_dc's dense reads
-            }
-        }
-#else
-        while (m) {
-            const int l = __builtin_ctzll(m);
-            m &= m - 1;
-            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)sk.pend, l);
-            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)sk.pend >> 32), l);
-            const int64_t bi = (int64_t)(((uint64_t)hi << 32) | lo);
-            uint32_t* src = wave_slots + l * SLOT_DW;
-#if ICX_DEC_DC_LANE
-            // lanes 0..31 store the block's 32 coefficient pairs, lane 32 (whose
-            // pair also starts at zig-zag 0) its DC difference into d.dc for
-            // k_dec_dc's dense reads - one store instruction per block
-            if (lane <= 32) {
-                const uint16_t* s16 = (const uint16_t*)src;
-                const int lsw = l & 62;
-                const uint32_t v = s16[zl ^ lsw] | ((uint32_t)s16[zh ^ lsw] << 16);
-                __builtin_amdgcn_wave_barrier();  // every lane's reads before the zeroing
-                src[lane & 31] = 0;               // (lane 32 zeroes word 0 with lane 0)
-                ICX_GLOBAL int32_t* dst = lane < 32 ? (ICX_GLOBAL int32_t*)coefs32 + bi * 32 + lane : dcs + bi;
-                *dst = lane < 32 ? (int32_t)v : (int32_t)(int16_t)v;
-            }
-#else
-            if (lane < 32) {
-                const uint16_t* s16 = (const uint16_t*)src;
-                const int lsw = l & 62;
-                const uint32_t v = s16[zl ^ lsw] | ((uint32_t)s16[zh ^ lsw] << 16);
-                __builtin_amdgcn_wave_barrier();  // every lane's reads before the zeroing
-                src[lane] = 0;
-                coefs32[bi * 32 + lane] = v;
-                if (lane == 0) dcs[bi] = (int16_t)v;  // the DC difference, also for k_dec_dc's dense reads
-            }
-#endif
-        }
-#endif
-        sk.pend = -1;
+        flush();
     }
+#endif
     // The settled states are the true decode: an invalid code met on it
     // (outside an interval's padding) means corrupt data (jdhuff.c warns and
     // zero-fills there; the caller decides what to do with the file).
