@@ -151,11 +151,13 @@ uint32_t pick_sub_bits(uint64_t total_bits)
     // e2e leg, ab_r4g_dec.txt / ab_r4h_dec_sub.txt / ab_r4i_dec_sub.txt):
     // 1000 frames per call (62 Gbit) 16384 / 32768 / 65536 / 131072 bits:
     // 96.6 / 93.5 / 90.3 / 96.0 ms; 200 frames (12.4 Gbit) 16384 / 32768 /
-    // 65536: 22.4 / 22.8 / 23.9 ms.  Longer subsequences while at least 2^19
-    // of them remain; below that 16384, and shorter only when the batch would
-    // not give the chip ~64k threads.
+    // 65536: 22.4 / 22.8 / 23.9 ms.  With the two-step walks (round 4 end,
+    // ab_r4zf_dec_win_sub.txt / ab_r4zg_dec_sub.txt) 200 frames: 16384 /
+    // 32768 / 65536 = 20.7 / 20.2 / 21.9 ms.  65536 while at least 2^19 of
+    // them remain, 32768 while 2^18 do; below that 16384, and shorter only
+    // when the batch would not give the chip ~64k threads.
     uint32_t S = 65536;
-    while (S > 16384 && total_bits / S < (1u << 19)) S /= 2;
+    if (total_bits / S < (1u << 19)) S = total_bits / 32768 >= (1u << 18) ? 32768 : 16384;
     while (S > 2048 && total_bits / S < 65536) S /= 2;
     return S;
 }

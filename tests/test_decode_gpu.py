@@ -94,7 +94,7 @@ def test_decode_4k_q95_matches_oracle(codec, oracle, kind):
 @pytest.mark.parametrize("sub_bits", [2048, 16384, 32768, 65536])
 def test_decode_subsequence_lengths(codec, oracle, monkeypatch, sub_bits):
     """The subsequence length follows the batch size (pick_sub_bits: 65536
-    bits on configs[1]'s 1000-frame calls, 16384 at 200, 2048 for a lone
+    bits on configs[1]'s 1000-frame calls, 32768 at 200, 2048 for a lone
     small file); every length, forced on one small mixed batch (ICX_DEC_SUB_BITS),
     must decode what the oracle decodes - checkpoints, write-pass pieces and
     relaxation at that length."""
