@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <set>
 #include <string>
@@ -212,6 +213,12 @@ struct icx_ctx {
     hipEvent_t ev_dec_split = nullptr, ev_dec_aux[DEC_AUX_MAX] = {};
     icx::DevArena stage[2];
     hipEvent_t ev_up[2] = {nullptr, nullptr}, ev_down[2] = {nullptr, nullptr}, ev_done = nullptr;
+    // icx_upload: host threads push file bytes to HBM on their own copy
+    // streams, without `mu`, while a batch call runs its kernels on `stream`
+    static constexpr int UP_STREAMS = 4;
+    std::mutex up_mu[UP_STREAMS];
+    hipStream_t up_stream[UP_STREAMS] = {};
+    std::atomic<unsigned> up_next{0};
 };
 
 namespace icx {

@@ -251,8 +251,9 @@ icx_status run_progressive(icx_ctx* c, std::vector<DecItem>& items, int16_t* coe
             pos++;
         }
         const int m = (int)sub.size();
+        // (three plans below: Wb, Wr, Wp)
         const size_t up = Uploader::need<DecTab>(m) + Uploader::need<DecDesc>(m) + Uploader::need<DecState>(m) +
-                          Uploader::need<int32_t>(m) + 2 * Uploader::need<int64_t>(m + 1) + 4096;
+                          Uploader::need<int32_t>(m) + 3 * Uploader::need<int64_t>(m + 1) + 4096;
         hipError_t e = c->dev.reserve(need + up);
         if (e == hipSuccess) e = c->host.reserve(hneed + up);
         if (e != hipSuccess) return hip_fail(c, e, "progressive decode workspace");
@@ -453,8 +454,9 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         const int m = (int)sub.size();
         const uint32_t S = pick_sub_bits(bits);
         // every small argument array of the sub-batch travels in one packed upload
+        // (three whole-sub-batch plans below: Pt, Pc, Ps)
         const size_t up = Uploader::need<DecTab>(m) + Uploader::need<DecDesc>(m) + Uploader::need<DecState>(m) +
-                          Uploader::need<int32_t>(m) + 2 * Uploader::need<int64_t>(m + 1) +
+                          Uploader::need<int32_t>(m) + 3 * Uploader::need<int64_t>(m + 1) +
                           // the decode tails (subsets settled at one check): ids and 4 plans each; each
                           // image is in one tail, so at most m + 1 tails of 36 B per image + alignment
                           36 * (size_t)m + (size_t)(m + 1) * (64 + 4 * 72);
@@ -920,6 +922,24 @@ icx_status icx_memcpy(icx_ctx* ctx, void* dst, const void* src, size_t bytes)
     if (e == hipSuccess) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     return e == hipSuccess ? ICX_OK : hip_fail(ctx, e, "hipMemcpy");
+}
+
+icx_status icx_upload(icx_ctx* ctx, void* dst, const void* src, size_t bytes)
+{
+    if (!ctx || ((!dst || !src) && bytes)) return ICX_E_NULL;
+    if (!bytes) return ICX_OK;
+    const int k = (int)(ctx->up_next.fetch_add(1, std::memory_order_relaxed) % icx_ctx::UP_STREAMS);
+    hipError_t e;
+    {
+        std::lock_guard<std::mutex> lk(ctx->up_mu[k]);
+        e = hipSetDevice(ctx->device);
+        if (e == hipSuccess && !ctx->up_stream[k]) e = hipStreamCreateWithFlags(&ctx->up_stream[k], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->up_stream[k]);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->up_stream[k]);
+    }
+    if (e == hipSuccess) return ICX_OK;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    return hip_fail(ctx, e, "icx_upload");
 }
 
 icx_status icx_debug_decode_coefs(icx_ctx* ctx, const uint8_t* data, size_t len, int16_t* coefs, size_t ncoefs)

@@ -210,12 +210,20 @@ constexpr size_t kMaxRaw = (size_t)1 << 30;
 constexpr size_t kIdat = 32768;  // IDATOutputStream chunk length
 constexpr int kDefaultLevel = 4; // PNGImageWriter.DEFAULT_COMPRESSION_LEVEL
 
+// A palette raster's colour map as validate() (icx_runtime.cpp) takes it:
+// 1..256 entries for INDEXED8, 1..16 for BINARY1 (IndexColorModel of a
+// TYPE_BYTE_BINARY raster: at most 4 bits per pixel).
+static bool palette_ok(const icx_image* img)
+{
+    if (img->fmt != ICX_INDEXED8 && img->fmt != ICX_BINARY1) return true;
+    const int maxn = img->fmt == ICX_BINARY1 ? 16 : 256;
+    return img->palette && img->palette_len >= 1 && img->palette_len <= maxn;
+}
+
 size_t icx_png_bound(const icx_image* img)
 {
     if (!img || img->width <= 0 || img->height <= 0) return 0;
-    if ((img->fmt == ICX_INDEXED8 || img->fmt == ICX_BINARY1) && (!img->palette || img->palette_len < 1 ||
-                                                                  img->palette_len > 256))
-        return 0;
+    if (!palette_ok(img)) return 0;
     const size_t raw = (size_t)img->height * (png_row_bytes(img) + 1);
     if (raw > kMaxRaw) return 0;
     const size_t z = (size_t)compressBound((uLong)raw);
@@ -229,6 +237,7 @@ icx_status icx_png_encode(const icx_image* img, int32_t level, uint8_t* out, siz
         img->stride < img->width * src_bpp(img->fmt) || level < -1 || level > 9)
         return ICX_E_INVALID;
     if (icx::is_device_ptr(img->px)) return ICX_E_INVALID;  // host rows only
+    if (!palette_ok(img)) return ICX_E_INVALID;             // no map, or more entries than the depth holds
     const size_t need = icx_png_bound(img);
     if (need == 0) return ICX_E_UNSUPPORTED;  // over kMaxRaw
     *out_len = need;

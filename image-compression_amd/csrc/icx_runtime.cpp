@@ -1050,58 +1050,78 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
 }  // namespace
 
 // ============================================================ C ABI
-extern "C" {
+namespace {
+// Constant tables of the encoder (zig-zag, Huffman codes, marker templates,
+// dither errors): built once per process, uploaded once per DEVICE
+// (__constant__ symbols live on every device: a pool over several GPUs
+// needs them on each).
+struct Consts {
+    uint8_t nat2zz[64], zz2nat[64];
+    uint32_t dc[2][16] = {}, ac[2][256] = {};
+    uint8_t hdr[4][HDR_COLOR] = {};
+    int8_t dith[3][64];
+};
+const Consts& consts();
 
-int icx_abi_version(void) { return ICX_ABI_VERSION; }
-
-const char* icx_status_string(icx_status s)
+// The self-check's known-answer images: a 16x16 BGR24 frame and a 16x16
+// GRAY8 frame of busy content (every AC table is reached), encoded at
+// quality 0.75 with the default table layout.  Their files' length and
+// 64-bit FNV-1a digest are pinned against the CPU oracle by
+// tests/test_capi.py (test_self_check_vectors_match_oracle).
+constexpr float kSelfCheckQ = 0.75f;
+void self_check_image(int grey, uint8_t* px)
 {
-    switch (s) {
-    case ICX_OK: return "ok";
-    case ICX_E_INVALID: return "invalid argument";
-    case ICX_E_NOMEM: return "out of memory";
-    case ICX_E_DEVICE: return "device error";
-    case ICX_E_BUFFER: return "output buffer too small";
-    case ICX_E_UNSUPPORTED: return "unsupported input";
-    case ICX_E_CORRUPT: return "corrupt input";
-    case ICX_E_NULL: return "null argument";
-    }
-    return "unknown";
+    const int nch = grey ? 1 : 3;
+    for (int y = 0; y < 16; y++)
+        for (int x = 0; x < 16; x++)
+            for (int c = 0; c < nch; c++)
+                px[(y * 16 + x) * nch + c] = (uint8_t)((x * 37 + y * 91 + c * 53 + x * y * 13 + ((x ^ y) & 5) * 29) & 255);
+}
+constexpr uint64_t kSelfCheckDigest[2] = {0x937d6de3e49b4eb4ull, 0xae63ed12585b37ccull};  // [colour, grey]
+constexpr int64_t kSelfCheckLen[2] = {776, 470};
+uint64_t fnv1a64(const uint8_t* p, size_t n)
+{
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < n; i++) h = (h ^ p[i]) * 0x100000001b3ull;
+    return h;
 }
 
-const char* icx_last_error(const icx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
-
-icx_status icx_create(int device, icx_ctx** out)
+// One colour and one grey 16x16 encode on the context's own device, compared
+// with the known answers: a constant table missing or wrong on this device
+// (an upload to the wrong device, a stale symbol) fails icx_create instead of
+// corrupting this GPU's output.
+icx_status self_check(icx_ctx* c)
 {
-    if (!out) return ICX_E_NULL;
-    *out = nullptr;
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
-        (void)hipGetLastError();
-        return ICX_E_DEVICE;
+    if (const char* e = getenv("ICX_SELF_CHECK"))
+        if (atoi(e) == 0) return ICX_OK;
+    uint8_t px[2][16 * 16 * 3];
+    uint8_t out[2][2048];
+    icx_fit_job j[2] = {};
+    for (int g = 0; g < 2; g++) {
+        self_check_image(g, px[g]);
+        j[g].img = icx_image{px[g], 16, 16, g ? 16 : 48, g ? ICX_GRAY8 : ICX_BGR24, nullptr, 0};
+        j[g].quality = kSelfCheckQ;
+        j[g].out = out[g];
+        j[g].cap = sizeof(out[g]);
+        j[g].target_max_size = INT64_MAX;
     }
-    if (device < 0 || device >= n) return ICX_E_INVALID;
-    if (hipSetDevice(device) != hipSuccess) return ICX_E_DEVICE;
-    icx_ctx* c = new icx_ctx();
-    c->device = device;
-    c->hpool.host = true;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete c;
-        return ICX_E_DEVICE;
+    const icx_status s = run_batch(c, j, 2, Mode::Encode);
+    if (s != ICX_OK) return s;
+    for (int g = 0; g < 2; g++) {
+        if (j[g].status != ICX_OK) return fail(c, ICX_E_DEVICE, "device self-check: encode failed");
+        if ((int64_t)j[g].out_len != kSelfCheckLen[g] || fnv1a64(out[g], j[g].out_len) != kSelfCheckDigest[g])
+            return fail(c, ICX_E_DEVICE, g ? "device self-check: grey known answer differs"
+                                           : "device self-check: colour known answer differs");
     }
-    // constant tables: zig-zag, Huffman codes, marker templates, dither
-    // errors - built once, uploaded once per DEVICE (__constant__ symbols
-    // live on every device: a pool over several GPUs needs them on each)
-    struct Consts {
-        uint8_t nat2zz[64], zz2nat[64];
-        uint32_t dc[2][16] = {}, ac[2][256] = {};
-        uint8_t hdr[4][HDR_COLOR] = {};
-        int8_t dith[3][64];
-    };
+    return ICX_OK;
+}
+}  // namespace
+
+namespace {
+const Consts& consts()
+{
     static std::once_flag once;
     static Consts K;
-    static std::mutex up_mu;
-    static std::vector<int> up_done;
     std::call_once(once, [] {
         uint8_t* nat2zz = K.nat2zz;
         uint8_t* zz2nat = K.zz2nat;
@@ -1173,6 +1193,83 @@ icx_status icx_create(int device, icx_ctx** out)
         }
         dither_tables(K.dith);
     });
+    return K;
+}
+}  // namespace
+
+extern "C" {
+
+int icx_abi_version(void) { return ICX_ABI_VERSION; }
+
+const char* icx_status_string(icx_status s)
+{
+    switch (s) {
+    case ICX_OK: return "ok";
+    case ICX_E_INVALID: return "invalid argument";
+    case ICX_E_NOMEM: return "out of memory";
+    case ICX_E_DEVICE: return "device error";
+    case ICX_E_BUFFER: return "output buffer too small";
+    case ICX_E_UNSUPPORTED: return "unsupported input";
+    case ICX_E_CORRUPT: return "corrupt input";
+    case ICX_E_NULL: return "null argument";
+    }
+    return "unknown";
+}
+
+const char* icx_last_error(const icx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+
+int32_t icx_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+void icx_debug_self_check_image(int32_t grey, uint8_t* px, uint64_t* digest, int64_t* len)
+{
+    const int g = grey ? 1 : 0;
+    if (px) self_check_image(g, px);
+    if (digest) *digest = kSelfCheckDigest[g];
+    if (len) *len = kSelfCheckLen[g];
+}
+
+icx_status icx_debug_corrupt_constants(int32_t device, int32_t on)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return ICX_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return ICX_E_DEVICE;
+    const Consts& K = consts();
+    Consts bad = K;
+    if (on) bad.ac[0][0x01] ^= 0x100;  // the luma AC code of run 0 / size 1: wrong bits, same length
+    return upload_constants(bad.nat2zz, bad.zz2nat, bad.dc, bad.ac, bad.hdr, bad.dith) == hipSuccess ? ICX_OK
+                                                                                                      : ICX_E_DEVICE;
+}
+
+icx_status icx_create(int device, icx_ctx** out)
+{
+    if (!out) return ICX_E_NULL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        (void)hipGetLastError();
+        return ICX_E_DEVICE;
+    }
+    if (device < 0 || device >= n) return ICX_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return ICX_E_DEVICE;
+    icx_ctx* c = new icx_ctx();
+    c->device = device;
+    c->hpool.host = true;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return ICX_E_DEVICE;
+    }
+    static std::mutex up_mu;
+    static std::vector<int> up_done;
+    const Consts& K = consts();
     hipError_t up = hipSuccess;
     {
         std::lock_guard<std::mutex> lk(up_mu);
@@ -1197,9 +1294,14 @@ icx_status icx_create(int device, icx_ctx** out)
         budget_mb = std::max<size_t>(2048, (free_b / 5 * 2) >> 20);
     if (const char* env = getenv("ICX_WORKSPACE_MB")) budget_mb = (size_t)atoll(env);
     c->budget = budget_mb << 20;
+    if (self_check(c) != ICX_OK) {
+        icx_destroy(c);
+        return ICX_E_DEVICE;
+    }
     *out = c;
     return ICX_OK;
 }
+
 
 void icx_destroy(icx_ctx* ctx)
 {
@@ -1217,6 +1319,11 @@ void icx_destroy(icx_ctx* ctx)
         hipEventDestroy(ctx->ev_dec_aux[k]);
     }
     if (ctx->ev_dec_split) hipEventDestroy(ctx->ev_dec_split);
+    for (int k = 0; k < icx_ctx::UP_STREAMS; k++)
+        if (ctx->up_stream[k]) {
+            hipStreamSynchronize(ctx->up_stream[k]);
+            hipStreamDestroy(ctx->up_stream[k]);
+        }
     if (ctx->io_up) {
         hipStreamSynchronize(ctx->io_up);
         hipStreamSynchronize(ctx->io_down);

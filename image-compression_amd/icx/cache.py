@@ -50,6 +50,50 @@ class LockedDict(dict):
         self.lock = threading.Lock()
 
 
+class SharedCache(LockedDict):
+    """The L1 map shared by every rank of a multi-process run: the
+    reference's one ConcurrentHashMap (CompressionBatch.java:71) when the
+    file list is sharded over one process per GPU.
+
+    Each rank keeps a local map (loaded from the same L2 file); an entry a
+    rank learns is also appended to one log key in the process group's
+    key-value store (the torchrun rendezvous TCPStore: 16 bytes per entry,
+    no collective, ranks never wait on each other), and refresh() - called
+    by the pipeline before it probes a group's keys - applies the entries
+    other ranks appended since the last refresh.  Every rank applies the log
+    in its order, so all converge on the same last-writer-wins map."""
+
+    LOG = "icx/learned_cache/log"
+    _REC = np.dtype([("w", "<i4"), ("h", "<i4"), ("s", "<i8"), ("q", "<f4"), ("scale", "<f8")])
+
+    def __init__(self, store, *a, **k):
+        super().__init__(*a, **k)
+        self.store = store
+        self._seen = 0  # bytes of the log applied so far
+
+    def __setitem__(self, key, value):
+        super().__setitem__(key, value)
+        rec = np.zeros(1, self._REC)
+        rec[0] = (key.width_bucket, key.height_bucket, key.size_bucket, np.float32(value.quality), value.scale)
+        self.store.append(self.LOG, rec.tobytes())
+
+    def refresh(self) -> int:
+        """Apply the log's new entries (other ranks' and this rank's own, in
+        log order); returns how many were read."""
+        if not self.store.check([self.LOG]):
+            return 0
+        data = self.store.get(self.LOG)
+        n = (len(data) - self._seen) // self._REC.itemsize
+        if n <= 0:
+            return 0
+        recs = np.frombuffer(data, self._REC, n, self._seen)
+        self._seen += n * self._REC.itemsize
+        for r in recs:
+            dict.__setitem__(self, SimilarityKey(int(r["w"]), int(r["h"]), int(r["s"])),
+                             LearnedParams(float(r["q"]), float(r["scale"])))
+        return n
+
+
 class CacheManager:
     def __init__(self, path):
         self.path = db_file(path)

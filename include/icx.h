@@ -144,6 +144,20 @@ icx_status icx_pool_create(const int32_t* devices, int32_t ndev, icx_pool** out)
 void icx_pool_destroy(icx_pool* pool);
 int32_t icx_pool_size(const icx_pool* pool);
 icx_ctx* icx_pool_context(icx_pool* pool, int32_t i);
+/* GPUs visible to this process (0 when there are none): the CLI's default
+ * device list when one process drives the node. */
+int32_t icx_device_count(void);
+/* icx_create's device self-check: every new context
+ * encodes a fixed 16x16 BGR24 and a fixed 16x16 GRAY8 frame at quality 0.75
+ * on its own device and compares the files with known answers (length and
+ * 64-bit FNV-1a digest, pinned against the CPU oracle by the tests); a
+ * mismatch fails icx_create with ICX_E_DEVICE, so a constant table missing
+ * or wrong on one GPU cannot silently corrupt that GPU's output.  Debug
+ * helpers: the known-answer image (px: 16*16*3 or 16*16 bytes) and its
+ * expected file; and a hook that overwrites (on = 1) or restores (on = 0)
+ * the encoder's constant Huffman tables on `device`. */
+void icx_debug_self_check_image(int32_t grey, uint8_t* px, uint64_t* digest, int64_t* len);
+icx_status icx_debug_corrupt_constants(int32_t device, int32_t on);
 /* Last error text recorded on this context (never NULL). */
 const char* icx_last_error(const icx_ctx* ctx);
 int icx_abi_version(void);
@@ -327,6 +341,12 @@ icx_status icx_host_alloc(icx_ctx* ctx, size_t bytes, void** ptr);
 icx_status icx_host_free(icx_ctx* ctx, void* ptr);
 /* Synchronous copy between any two of host / this context's device memory. */
 icx_status icx_memcpy(icx_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* Host -> this context's device memory, synchronous (the bytes are in HBM
+ * when it returns), on a copy stream of its own and without waiting for a
+ * batch call running on the context: reader threads push file bytes to the
+ * GPU while the decode / encode kernels of other files run (the files ->
+ * files path; the decode then reads device-resident files). */
+icx_status icx_upload(icx_ctx* ctx, void* dst, const void* src, size_t bytes);
 
 /* ------------------------------------------------------- parity / metrics */
 /* Quantised coefficients after DC prediction (natural order, 64 per block,

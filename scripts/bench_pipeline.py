@@ -114,7 +114,10 @@ def main():
                      "images_per_s": round(rep.total / dt, 1), "mp_per_s": round(rep.megapixels / dt, 1),
                      "success": rep.success, "failed": rep.failed, "skipped": rep.skipped,
                      "in_bytes": rep.original_size, "out_bytes": rep.compressed_size,
-                     "device_ms": dev, "device_ms_total": round(sum(dev.values()), 1), "library_host_spans": host,
+                     "device_ms": dev, "device_ms_total": round(sum(dev.values()), 1),
+                     # kernel time / wall (an upper bound on the busy fraction where
+                     # launches of two streams or contexts overlap)
+                     "device_busy_frac": round(sum(dev.values()) / (dt * 1e3), 3), "library_host_spans": host,
                      "host_threads": a.decode_threads or pipeline.host_cores()[0], "stages": rep.stages,
                      "file_read_GBps": round(rep.original_size / dt / 1e9, 2)})
     for c in codecs:

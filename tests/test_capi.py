@@ -92,3 +92,24 @@ def test_missing_library_fails_loudly(monkeypatch):
     monkeypatch.setattr(N, "LIB_PATH", "/nonexistent/libicx.so")
     with pytest.raises(N.NativeLibraryError):
         N.load()
+
+
+def test_self_check_vectors_match_oracle(oracle):
+    """icx_create's device self-check compares two known-answer files with
+    what the context's GPU encodes; the known answers (length, FNV-1a 64)
+    are the CPU oracle's files for the same images at q = 0.75."""
+    L = N.load()
+
+    def fnv(b):
+        h = 0xcbf29ce484222325
+        for x in b:
+            h = ((h ^ x) * 0x100000001b3) & 0xffffffffffffffff
+        return h
+
+    for grey in (0, 1):
+        px = np.zeros((16, 16) if grey else (16, 16, 3), np.uint8)
+        dig, n = ctypes.c_uint64(), ctypes.c_int64()
+        L.icx_debug_self_check_image(grey, px.ctypes.data, ctypes.byref(dig), ctypes.byref(n))
+        assert len(np.unique(px)) > 64  # busy content: many AC codes
+        data = oracle.encode(px, 0.75)
+        assert (len(data), fnv(data)) == (n.value, dig.value), grey

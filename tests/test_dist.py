@@ -136,3 +136,71 @@ def test_two_rank_leg_timing_is_max_over_ranks():
     for rank, wall, mx in got:
         assert wall >= 0.29, (rank, wall)  # the barrier waits for rank 1's 0.3 s
         assert abs(mx - 0.2) < 1e-9
+
+
+def _shared_cache_worker(rank, world, port, a, b, out, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "image-compression_amd"))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    from torch.distributed.distributed_c10d import _get_default_store
+    from icx import pipeline
+    from icx.cache import SharedCache
+    from icx.core import CompressionParams
+    from tests.stub_codec import OracleCodec
+
+    class RecCodec(OracleCodec):
+        seen = []
+
+        def fit(self, images, target, quality, cached=None, outputs=None):
+            res = super().fit(images, target, quality, cached, outputs)
+            RecCodec.seen += [(c is not None, r["cache_hit"]) for c, r in zip(cached or [None] * len(res), res)]
+            return res
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cache = SharedCache(_get_default_store())
+    P = CompressionParams(0.25, 1000, 100, 60, 40000)
+    lst = os.path.join(out, f"list{rank}.txt")
+    with open(lst, "w") as f:
+        f.write(a if rank == 0 else b)
+    batch = pipeline.CompressionBatch(lst, os.path.join(out, f"o{rank}"), P, 1, os.path.join(out, "c"),
+                                      codecs=[RecCodec()], group_size=1)
+    if rank == 1:
+        dist.barrier()  # rank 0 has learned file a's parameters
+    rep = batch.execute(cache=cache, save_cache=False)
+    if rank == 0:
+        dist.barrier()
+    q.put((rank, rep.success, RecCodec.seen, len(cache)))
+    dist.destroy_process_group()
+
+
+def test_ranks_share_one_learned_cache(tmp_path):
+    """under torchrun every rank had its own L1 map, so a
+    key learned on rank 0 was no hit on rank 1 during the run.  With
+    SharedCache (the process group's store carries new entries) rank 1's
+    file, whose similarity key equals the one rank 0 learned earlier in the
+    same run, is probed with the learned parameters and hits (one encode),
+    as under the reference's single ConcurrentHashMap."""
+    img = noise(150, 220, 5)
+    a = tmp_path / "a.jpg"
+    Image.fromarray(img).save(a, "JPEG", quality=95)
+    b = tmp_path / "b.jpg"
+    b.write_bytes(a.read_bytes())  # same dims and size bucket: the same SimilarityKey
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_shared_cache_worker, args=(r, 2, port, str(a), str(b), str(tmp_path), q))
+          for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in ps)
+    (r0, ok0, seen0, n0), (r1, ok1, seen1, n1) = res
+    assert ok0 == ok1 == 1
+    assert seen0 == [(False, False)]  # rank 0: cold, full search, learns the key
+    assert seen1 == [(True, True)]    # rank 1: probed with rank 0's entry, and it fits
+    assert n1 == 1

@@ -206,3 +206,59 @@ def test_png_reader_rasters(tmp_path):
     if r is not None and isinstance(r, IndexedImage):  # Pillow wrote a 2-bit grey file
         assert r.fmt == N.BINARY1 and list(r.palette) == [0xff000000, 0xff555555, 0xffaaaaaa, 0xffffffff]
         assert np.array_equal(r.indices, g // 85)
+
+
+def _bayer8():
+    """AWT make_uns_ordered_dither_array: the recursive 8x8 ordered-dither order."""
+    oda = np.zeros((8, 8), np.int64)
+    k = 1
+    while k < 8:
+        for i in range(k):
+            for j in range(k):
+                v = oda[i, j]
+                oda[i, j] = v * 4
+                oda[i + k, j + k] = v * 4 + 1
+                oda[i, j + k] = v * 4 + 2
+                oda[i + k, j] = v * 4 + 3
+        k *= 2
+    return oda
+
+
+def test_palette_invariants_pinned_without_java2d():
+    """Invariants of the (parity-unpinned) palette restatement that hold
+    whatever Java2D's exact claim order is, so a refactor cannot drift
+    silently: the dither matrix is a permutation of 0..63 scaled to [-20, 20)
+    (make_dither_arrays), and every map entry's own 5-bit colour cell maps to
+    an entry of that same cell (initCubemap seeds each entry's cell with it)."""
+    bay = _bayer8()
+    assert sorted(bay.ravel().tolist()) == list(range(64))
+    d = np.zeros((3, 64), np.int8)
+    N.load().icx_dither_tables(d.ctypes.data)
+    assert np.array_equal(d[0].reshape(8, 8), bay * 40 // 64 - 20)
+    rng = np.random.default_rng(17)
+    maps = [default_palette(False), default_palette(True)]
+    maps += [(0xff000000 | rng.integers(0, 1 << 24, n)).astype(np.uint32) for n in (2, 7, 64, 256)]
+    for pal in maps:
+        cube = _icx_cube(pal)
+        cells = ((pal >> 9) & 0x7c00) | ((pal >> 6) & 0x3e0) | ((pal >> 3) & 0x1f)
+        got = pal[cube[cells.astype(np.int64)]]
+        got_cells = ((got >> 9) & 0x7c00) | ((got >> 6) & 0x3e0) | ((got >> 3) & 0x1f)
+        assert np.array_equal(got_cells, cells), len(pal)
+
+
+def test_png_encode_rejects_bad_colour_maps():
+    """icx_png_encode validates a palette raster's map as validate() does:
+    null map, no entries, more than 16 for BINARY1 or 256 for INDEXED8."""
+    L = N.load()
+    idx = np.zeros((4, 4), np.uint8)
+    pal = np.full(300, 0xff000000, np.uint32)
+    out = np.zeros(1 << 16, np.uint8)
+    n = ctypes.c_size_t()
+    for fmt, ptr, count in ((N.INDEXED8, None, 4), (N.INDEXED8, pal.ctypes.data, 0), (N.INDEXED8, pal.ctypes.data, 257),
+                            (N.BINARY1, pal.ctypes.data, 17), (N.BINARY1, None, 2)):
+        img = N.Image(idx.ctypes.data, 4, 4, 4, fmt, ptr, count)
+        st = L.icx_png_encode(ctypes.byref(img), -1, out.ctypes.data, out.nbytes, ctypes.byref(n))
+        assert st == N.E_INVALID, (fmt, count, st)
+    for fmt, count in ((N.INDEXED8, 256), (N.BINARY1, 16), (N.BINARY1, 2)):
+        img = N.Image(idx.ctypes.data, 4, 4, 4, fmt, pal.ctypes.data, count)
+        assert L.icx_png_encode(ctypes.byref(img), -1, out.ctypes.data, out.nbytes, ctypes.byref(n)) == N.OK

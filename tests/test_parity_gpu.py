@@ -581,3 +581,67 @@ def test_palette_resize_matches_restatement(codec, oracle):
             assert np.array_equal(r.indices, want), (im.shape, im.fmt)
         else:
             assert np.array_equal(r, oracle.resize(im, r.shape[1], r.shape[0]))
+
+
+def test_create_self_check_catches_a_bad_device_constant(codec, oracle):
+    """icx_create encodes two known-answer frames on its
+    own device; with the encoder's Huffman constants overwritten on that
+    device (debug hook) icx_create fails with ICX_E_DEVICE, and once they
+    are restored it succeeds again.  The check costs < 1 ms per context."""
+    import ctypes
+    import time
+    L = N.load()
+    ctx = ctypes.c_void_p()
+    assert L.icx_debug_corrupt_constants(0, 1) == N.OK
+    try:
+        assert L.icx_create(0, ctypes.byref(ctx)) == N.E_DEVICE
+        # an encode on the corrupted device differs from the oracle (what the check guards against)
+        img = noise(16, 16, 3)
+        assert codec.compress_jpg_to_stream(img, 0.75) != oracle.encode(img, 0.75)
+    finally:
+        assert L.icx_debug_corrupt_constants(0, 0) == N.OK
+    assert codec.compress_jpg_to_stream(img, 0.75) == oracle.encode(img, 0.75)
+    times = {}
+    import os
+    for mode in ("0", "1", "0", "1"):
+        os.environ["ICX_SELF_CHECK"] = mode
+        try:
+            t0 = time.perf_counter()
+            for _ in range(5):
+                c = ctypes.c_void_p()
+                assert L.icx_create(0, ctypes.byref(c)) == N.OK
+                L.icx_destroy(c)
+            times[mode] = (time.perf_counter() - t0) / 5
+        finally:
+            del os.environ["ICX_SELF_CHECK"]
+    print("icx_create ms without / with the self-check:", times["0"] * 1e3, times["1"] * 1e3)
+    assert times["1"] - times["0"] < 1e-3, times
+
+
+def test_upload_from_a_reader_thread_during_a_call(codec):
+    """icx_upload copies host bytes to the context's device on a copy stream
+    of its own, concurrently with a batch call on the same context."""
+    import threading
+    from icx.core import DeviceImage, PinnedBuffer
+    rng = np.random.default_rng(4)
+    src = [PinnedBuffer(codec, 3 << 20) for _ in range(8)]
+    dst = [DeviceImage(codec, (3 << 20,)) for _ in range(8)]
+    for s in src:
+        s.array[:] = rng.integers(0, 256, s.size, dtype=np.uint8)
+    errs = []
+
+    def reader():
+        try:
+            for s, d in zip(src, dst):
+                codec._check(codec._lib.icx_upload(codec._ctx, d.ptr, s.ptr, s.size), "icx_upload")
+        except Exception as e:
+            errs.append(e)
+
+    t = threading.Thread(target=reader)
+    img = noise(1080, 1920, 9)
+    t.start()
+    codec.fit([img] * 4, 1 << 18, 0.25)
+    t.join()
+    assert not errs
+    for s, d in zip(src, dst):
+        assert np.array_equal(d.numpy(), s.array)

@@ -159,6 +159,19 @@ def test_cli_defaults():
     assert a.timeOut == 24 and a.cache_db == "image-compression-cache"
 
 
+def test_cli_default_devices():
+    """without --devices one process drives every
+    visible GPU (one shared L1 cache); under torchrun a rank takes its
+    LOCAL_RANK's GPU; --devices wins; no GPU visible -> device 0."""
+    from icx.cli import default_devices
+    assert default_devices(None, 1, 0, 8) == list(range(8))
+    assert default_devices(None, 1, 0, 1) == [0]
+    assert default_devices(None, 1, 0, 0) == [0]
+    assert default_devices(None, 8, 5, 8) == [5]
+    assert default_devices("0,0,3", 1, 0, 8) == [0, 0, 3]
+    assert default_devices("2", 4, 1, 8) == [2]
+
+
 def test_shard_partition():
     lines = [f"f{i}" for i in range(11)]
     parts = [pipeline.shard(lines, r, 3) for r in range(3)]
@@ -527,3 +540,80 @@ def test_cache_errors_do_not_abort(tmp_path, caplog):
     lst.write_text("missing.jpg\n")
     rep = pipeline.CompressionBatch(lst, tmp_path / "out", P, 1, bad, codecs=[OracleCodec()]).execute()
     assert rep.total == 0
+
+
+def test_worker_failure_fails_its_group_not_the_run(tmp_path):
+    """an error escaping a group (here a BaseException out of the
+    fit, which compress_jpeg_group does not catch) fails that group's files
+    (FAILED_UNKNOWN) instead of killing the GPU worker thread, so the next
+    groups still compress; and a pinned-buffer allocation failure falls back
+    to host output buffers."""
+    files = []
+    for i in range(4):
+        f = tmp_path / f"w{i}.jpg"
+        write_jpeg(f, noise(60 + i, 100, 80 + i))
+        files.append(str(f))
+
+    class Boom(BaseException):
+        pass
+
+    class FlakyCodec(OracleCodec):
+        def fit(self, images, *a, **k):
+            if self.calls == 0:
+                self.calls += 1
+                raise Boom()
+            return super().fit(images, *a, **k)
+
+    lst = tmp_path / "list.txt"
+    lst.write_text("\n".join(files) + "\n")
+    P = CompressionParams(0.25, 1000, 50, 50, 20000)
+    rep = pipeline.CompressionBatch(lst, tmp_path / "out", P, 1, tmp_path / "cache", codecs=[FlakyCodec()],
+                                    group_size=2, decode_threads=1).execute(cache=LockedDict())
+    assert rep.total == 4 and rep.success == 2, rep.counts
+    assert rep.counts[CompressionResult.FAILED_UNKNOWN] == 2
+
+    class NoPinned(OracleCodec):
+        _ctx = object()  # looks like a libicx codec: the pipeline asks for pinned buffers
+
+    def no_pinned(codec, size):
+        raise icx.core.N.IcxError(icx.core.N.E_NOMEM, "hipHostMalloc")
+
+    import icx.core
+    orig = icx.core.PinnedBuffer.__init__
+    icx.core.PinnedBuffer.__init__ = no_pinned
+    try:
+        it = pipeline._Item(0, files[0])
+        it.decoded = pipeline.DecodedImage(np.zeros((8, 8, 3), np.uint8), "jpeg", 8, 8, 1)
+        assert pipeline._pinned_outputs(NoPinned(), [it], P) is None
+    finally:
+        icx.core.PinnedBuffer.__init__ = orig
+
+
+def test_stage_times_are_per_batch(tmp_path):
+    """Two batches in one process keep their own StageTimes (a
+    module-global timer let one run's end cut off the other's timing)."""
+    files = []
+    for i in range(3):
+        f = tmp_path / f"s{i}.jpg"
+        write_jpeg(f, noise(60 + i, 100, 90 + i))
+        files.append(str(f))
+    lst = tmp_path / "list.txt"
+    lst.write_text("\n".join(files) + "\n")
+    P = CompressionParams(0.25, 1000, 50, 50, 20000)
+    import threading
+    reps = {}
+
+    def run(k):
+        b = pipeline.CompressionBatch(lst, tmp_path / f"out{k}", P, 1, tmp_path / f"cache{k}",
+                                      codecs=[OracleCodec()], group_size=3, stage_times=True)
+        reps[k] = b.execute(cache=LockedDict())
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for k in range(2):
+        assert reps[k].success == 3
+        assert reps[k].stages["write"]["calls"] == 3, reps[k].stages
+        assert reps[k].stages["gpu_fit"]["calls"] == 1
