@@ -93,10 +93,25 @@ struct DecSlow {
 // prefix of longer codes consumes 0 bits: DEC_LEAN_LONG | k << 5 (second
 // level lut2[k]) or DEC_LEAN_LONG | DEC_LEAN_SLOW (canonical maxcode loop).
 // One step is then a look-up, a skip and an add; no symbol decoding.
+//
+// Symbol pairs (round 5).  A first-level entry of an AC table also says, in
+// its high half, what the NEXT symbol does when that symbol's whole code lies
+// inside the same 10-bit look-ahead (first symbol's code + extra bits + the
+// second's code <= 10 bits): bits 16..19 its code length (0 = no pair), 20..23
+// its extra bits, 24..30 its zig-zag advance.  A walk applies both symbols in
+// one step unless the first ends the block (z + advance >= 64: the next
+// symbol is then the next block's DC).  Over 4K q95 content a 10-bit window
+// pairs 40 % (smooth) / 32 % (noise) of the symbol steps away
+// (scripts/dec_pair_stats.cpp).  Every walker (warm-up, sync, write pass, the
+// CPU emulator) steps the same way, so the states they visit - subsequence
+// exits, checkpoints, piece starts - are the same pair-step boundaries; two
+// walks that resynchronise on different phases of a pair meet again at the
+// next block end, where no pair reaches across.
 constexpr uint32_t DEC_LEAN_LONG = 0x400u, DEC_LEAN_SLOW = 0x200u;
+constexpr int DEC_PAIR_SHIFT = 16;
 struct DecLean {
-    uint16_t lut[1 << DEC_LUT_BITS];
-    uint16_t lut2[DEC_NSUB][1 << (16 - DEC_LUT_BITS)];
+    uint32_t lut[1 << DEC_LUT_BITS];                     // (pair << 16) | entry
+    uint16_t lut2[DEC_NSUB][1 << (16 - DEC_LUT_BITS)];  // entries of codes longer than 10 bits (no pairs)
 };
 ICX_HD uint16_t dec_lean_entry(int len, int sym, bool ac)
 {
@@ -650,7 +665,7 @@ ICX_HD uint32_t dec_lean_symbol(LeanPtr t, const ICX_GLOBAL DecSlow* slow, uint3
 // First levels in one place (LDS) and the whole tables in global memory
 // (k_dec_write keeps only the 10-bit first levels in LDS).
 struct SplitLean {
-    const uint16_t (*lut)[1 << DEC_LUT_BITS];
+    const uint32_t (*lut)[1 << DEC_LUT_BITS];
     const ICX_GLOBAL DecLean* full;
 };
 template <class LeanPtr>
@@ -736,6 +751,7 @@ struct DecLeanWalker {
     uint64_t bsel;  // dec_block_sel
     uint32_t pos, n;
     int b, z, ti;  // ti: table of the next symbol (component of block b, DC at z == 0)
+    bool two;      // the last step was a symbol pair (tests compare against DecWalker's single steps)
     DecReader R;
     const uint32_t* words;
 
@@ -775,12 +791,16 @@ struct DecLeanWalker {
     {
         R.refill();
         const uint32_t e = dec_lean_lookup(H, ti, slow, R.peek16(), z != 0);
-        const int c = act ? (int)(e & 31) : 0;
+        const int c1 = act ? (int)(e & 31) : 0;
         // straight-line transition (an invalid entry, 0, leaves the state as
         // it is), then the rare invalid-code path overrides it
+        const int z1 = z + (act ? (int)((e >> 5) & 127) : 0);
+        // the pair's second symbol, unless the first ended the block
+        two = act && ((e >> DEC_PAIR_SHIFT) & 15) != 0 && z1 < 64;
+        const int c = c1 + (two ? (int)(((e >> 16) & 15) + ((e >> 20) & 15)) : 0);
         R.skip(c);
         pos += (uint32_t)c;
-        z += act ? (int)((e >> 5) & 127) : 0;
+        z = z1 + (two ? (int)((e >> 24) & 127) : 0);
         const bool end = z >= 64;
         n += end ? 1u : 0u;
         const int bn = b + 1 == nbmcu ? 0 : b + 1;
@@ -894,6 +914,7 @@ struct DecLeanWriter {
     int b, z, ti;
     bool own;
     bool bad;
+    bool two;  // the last step was a symbol pair
     int64_t blk_base;
     uint32_t nlim;  // blocks from blk_base to the image's end (clamped to 32 bits)
     DecReaderT<DEC_WIN_WRITE> R;
@@ -923,11 +944,12 @@ struct DecLeanWriter {
         R.refill();
         const uint32_t e = dec_lean_lookup(H, ti, slow, R.peek16(), z != 0);
         const int c = (int)(e & 31);
+        two = false;
         if (c == 0) {  // no valid code here
             invalid();
             return;
         }
-        const int sz = (int)(e >> 12), zadd = (int)((e >> 5) & 127);
+        const int sz = (int)((e >> 12) & 15), zadd = (int)((e >> 5) & 127);
         const uint32_t v = (uint32_t)(R.buf >> (64 - c)) & ((1u << sz) - 1u);
         R.skip(c);
         pos += (uint32_t)c;
@@ -941,6 +963,22 @@ struct DecLeanWriter {
         const int zc = z + zadd - 1;  // zig-zag index of a coefficient (DC: 0)
         sink.put(!own ? 0 : sz ? (zc > 63 ? 63 : zc) : z, x);
         z += zadd;
+        // the pair's second symbol (an AC code inside the same look-ahead),
+        // unless the first ended the block: its value bits follow its code
+        const int len2 = (int)((e >> DEC_PAIR_SHIFT) & 15);
+        two = len2 != 0 && z < 64;
+        if (two) {
+            const int sz2 = (int)((e >> 20) & 15), zadd2 = (int)((e >> 24) & 127);
+            const int c2 = len2 + sz2;
+            const uint32_t v2 = (uint32_t)(R.buf >> (64 - c2)) & ((1u << sz2) - 1u);
+            R.skip(c2);
+            pos += (uint32_t)c2;
+            const int half2 = (1 << sz2) >> 1;
+            const int x2 = (int)v2 - ((int)v2 < half2 ? (1 << sz2) - 1 : 0);
+            const int zc2 = z + zadd2 - 1;
+            sink.put(!own ? 0 : sz2 ? (zc2 > 63 ? 63 : zc2) : z, x2);
+            z += zadd2;
+        }
         const bool end = z >= 64;
 #if ICX_DEC_PEND32
         sink.flush_if(end && own && n < nlim, blk_base + n);  // 32-bit bound: nlim = nblocks - blk_base

@@ -510,12 +510,32 @@ __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const
 // estimates are already the fixed point and the first sync launch confirms
 // them; the rest are repaired by the relaxation like any other guess.
 __device__ __forceinline__ void load_tables(const DecTab* T, DecLean* L);
+__device__ __forceinline__ void load_first_levels(const DecTab* T, uint32_t (*L1)[1 << DEC_LUT_BITS]);
 __device__ __forceinline__ uint32_t selector(const DecTab* T);
+
+// The state-only walks (k_dec_init, k_dec_sync) keep the first levels of the
+// image's tables in LDS (32-bit entries with the symbol pairs: 16 KiB) and
+// read the second levels of the rare long codes through the scalar cache, as
+// the write pass does (SplitLean); ICX_DEC_SYNC_SPLIT=0: both levels in LDS
+// (24 KiB).
+#ifndef ICX_DEC_SYNC_SPLIT
+#define ICX_DEC_SYNC_SPLIT 1
+#endif
+#if ICX_DEC_SYNC_SPLIT
+#define DEC_WALK_TABLES                                                                   \
+    __shared__ __attribute__((aligned(16))) uint32_t L1[4][1 << DEC_LUT_BITS];
+#define DEC_WALK_LOAD(T) load_first_levels(T, L1)
+#define DEC_WALK_H(T) SplitLean{(const uint32_t (*)[1 << DEC_LUT_BITS])L1, (const ICX_GLOBAL DecLean*)(T)->lean}
+#else
+#define DEC_WALK_TABLES __shared__ __attribute__((aligned(16))) DecLean L[4];
+#define DEC_WALK_LOAD(T) load_tables(T, L)
+#define DEC_WALK_H(T) ((const DecLean*)L)
+#endif
 
 __global__ void __launch_bounds__(256) k_dec_init(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
                                                   uint32_t warm)
 {
-    __shared__ __attribute__((aligned(16))) DecLean L[4];
+    DEC_WALK_TABLES
     int slot;
     int64_t wg;
     if (!plan_slot(p, slot, wg)) return;
@@ -524,14 +544,14 @@ __global__ void __launch_bounds__(256) k_dec_init(const DecDesc* D, const DecSta
     const DecState& st = S[img];
     const int64_t j = wg * 256 + threadIdx.x;
     const bool live = st.status == 0 && wg * 256 < (int64_t)st.nsub;
-    if (live) load_tables(d.tab, L);
+    if (live) DEC_WALK_LOAD(d.tab);
     if (j > d.nsub_max) return;
     const uint32_t start = (uint32_t)j * sub_bits;
     uint64_t e = dec_pack(start, 0, 0);
     if (live && j > 0 && j < st.nsub && warm > 0) {
         const uint32_t from = start > warm ? start - warm : 0;
         uint32_t n;
-        e = dec_lean_walk(d, (const DecLean*)L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg,
+        e = dec_lean_walk(d, DEC_WALK_H(d.tab), d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg,
                           st.nseg, st.ent_len * 8, dec_pack(from, 0, 0), start, n);
     }
     d.est[j] = e;
@@ -545,6 +565,18 @@ __device__ __forceinline__ void load_tables(const DecTab* T, DecLean* L)
     uint4* dst = (uint4*)L;
     const int n = (int)(sizeof(DecLean) * T->ntab / 16);
     for (int k = threadIdx.x; k < n; k += blockDim.x) dst[k] = src[k];
+    __syncthreads();
+}
+
+// The first levels (10-bit look-ups) of the image's distinct tables, in LDS.
+__device__ __forceinline__ void load_first_levels(const DecTab* T, uint32_t (*L1)[1 << DEC_LUT_BITS])
+{
+    constexpr int per = (int)(sizeof(L1[0]) / 16);
+    const int n = (int)T->ntab * per;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const int t = k / per, o = k % per;
+        ((uint4*)L1[t])[o] = ((const uint4*)T->lean[t].lut)[o];
+    }
     __syncthreads();
 }
 
@@ -569,7 +601,7 @@ template <bool FIRST>
 __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
                                                   int iter, int nimg, uint32_t* changed)
 {
-    __shared__ __attribute__((aligned(16))) DecLean L[4];
+    DEC_WALK_TABLES
     int slot;
     int64_t wg;
     if (!plan_slot(p, slot, wg)) return;
@@ -580,7 +612,7 @@ __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecSta
     const int64_t k = wg * 256 + threadIdx.x;
     const uint32_t n = FIRST ? st.nsub : d.wl_cnt[(int64_t)(iter - 1) * nimg + img];
     if (wg * 256 >= (int64_t)n) return;
-    load_tables(d.tab, L);
+    DEC_WALK_LOAD(d.tab);
     if (k >= n) return;
     const uint32_t j = FIRST ? (uint32_t)k : d.wl[iter & 1][k];
     if (j >= st.nsub) return;
@@ -592,11 +624,11 @@ __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecSta
     uint64_t x;
     if (FIRST) {
         CkRecord<ICX_GLOBAL uint64_t*> ck{ckg, nck};
-        x = dec_sync_walk(d, (const DecLean*)L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
+        x = dec_sync_walk(d, DEC_WALK_H(d.tab), d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
                           st.ent_len * 8, e, j * sub_bits, sub_bits, nb, early, ck);
     } else {
         CkInPlace<ICX_GLOBAL uint64_t*> ck{ckg, nck, d.ncnt[j], nck > 0 ? ckg[0] : DEC_CK_NONE};
-        x = dec_sync_walk(d, (const DecLean*)L, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
+        x = dec_sync_walk(d, DEC_WALK_H(d.tab), d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg, st.nseg,
                           st.ent_len * 8, e, j * sub_bits, sub_bits, nb, early, ck);
     }
     d.ncnt[j] = nb;
@@ -712,7 +744,7 @@ struct PendSink {
 // longer than 10 bits are read from the image's tables in global memory.
 __global__ void __launch_bounds__(DEC_WRITE_NT) k_dec_write(const DecDesc* D, DecState* S, Plan p, uint32_t sub_bits)
 {
-    __shared__ __attribute__((aligned(16))) uint16_t L1[4][1 << DEC_LUT_BITS];
+    __shared__ __attribute__((aligned(16))) uint32_t L1[4][1 << DEC_LUT_BITS];
     __shared__ __attribute__((aligned(16))) uint32_t slots[DEC_WRITE_NT * SLOT_DW];
     int slot;
     int64_t wg;
@@ -745,7 +777,7 @@ __global__ void __launch_bounds__(DEC_WRITE_NT) k_dec_write(const DecDesc* D, De
         pc = dec_piece((const ICX_GLOBAL uint64_t*)d.est, (const ICX_GLOBAL uint64_t*)d.ck,
                        (const ICX_GLOBAL uint32_t*)d.boff, (uint32_t)j, (int)(t - j * np), sub_bits);
     const uint32_t stop = pc.stop;
-    const SplitLean H{(const uint16_t (*)[1 << DEC_LUT_BITS])L1, (const ICX_GLOBAL DecLean*)d.tab->lean};
+    const SplitLean H{(const uint32_t (*)[1 << DEC_LUT_BITS])L1, (const ICX_GLOBAL DecLean*)d.tab->lean};
     DecLeanWriter<SplitLean> w = dec_lean_writer(d, H, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg,
                                                  st.nseg, st.ent_len * 8, pc.blk);
     bool run = false;

@@ -1,6 +1,7 @@
 // icx_jpeg_parse.cpp — see icx_jpeg_parse.h.
 #include "icx_jpeg_parse.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 namespace icx {
@@ -215,7 +216,11 @@ bool build_dec_huff(const uint8_t* bits, const uint8_t* vals, int n, DecHuff& t,
     return true;
 }
 
-// DecLean of a built table (DC or AC class): every code's state transition.
+// DecLean of a built table (DC or AC class): every code's state transition,
+// and for AC tables the symbol pairs (icx_decode.h): when the first code's
+// bits and extra bits leave room in the 10-bit look-ahead for the whole of
+// the next code, the entry also carries that code's length, extra bits and
+// advance.  ICX_DEC_PAIR=0 builds no pairs (A/B).
 void build_dec_lean(const DecHuff& h, bool ac, DecLean& lean)
 {
     auto conv = [ac](uint16_t e) -> uint16_t {
@@ -223,7 +228,27 @@ void build_dec_lean(const DecHuff& h, bool ac, DecLean& lean)
         if (e & DEC_SLOW) return (uint16_t)(DEC_LEAN_LONG | DEC_LEAN_SLOW);                // same second level
         return e ? dec_lean_entry(e >> 8, e & 255, ac) : (uint16_t)0;
     };
-    for (int i = 0; i < (1 << DEC_LUT_BITS); i++) lean.lut[i] = conv(h.lut[i]);
+    static const bool pairs = !getenv("ICX_DEC_PAIR") || atoi(getenv("ICX_DEC_PAIR")) != 0;
+    for (int i = 0; i < (1 << DEC_LUT_BITS); i++) {
+        const uint16_t e = h.lut[i];
+        uint32_t x = conv(e);
+        const bool simple = e && !(e & (DEC_SUB | DEC_SLOW));
+        if (pairs && ac && simple) {
+            const int len1 = e >> 8, sz1 = e & 15, run1 = (e & 255) >> 4;
+            const int c1 = len1 + sz1;
+            const bool ends = sz1 == 0 && run1 != 15;  // EOB and the other size-0 symbols end the block
+            if (!ends && c1 < DEC_LUT_BITS) {
+                const int room = DEC_LUT_BITS - c1;
+                const uint16_t e2 = h.lut[(i << c1) & ((1 << DEC_LUT_BITS) - 1)];  // the next code's first bits
+                if (e2 && !(e2 & (DEC_SUB | DEC_SLOW)) && (e2 >> 8) <= room) {
+                    const uint32_t l2 = conv(e2);                     // (length + extra) | advance | extra
+                    const uint32_t len2 = e2 >> 8, sz2 = (l2 >> 12) & 15, zadd2 = (l2 >> 5) & 127;
+                    x |= (len2 | sz2 << 4 | zadd2 << 8) << DEC_PAIR_SHIFT;
+                }
+            }
+        }
+        lean.lut[i] = x;
+    }
     for (int k = 0; k < DEC_NSUB; k++)
         for (int i = 0; i < (1 << (16 - DEC_LUT_BITS)); i++) lean.lut2[k][i] = conv(h.lut2[k][i]);
 }

@@ -11,6 +11,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -206,6 +207,7 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
 // invalid codes, overshooting runs and interval jumps - both walk `steps`
 // symbols and must agree on the state and block count after every one.
 // Returns the number of disagreeing steps (0), or a negative status.
+extern "C" long dec_emu_pairs = 0;  // symbol-pair steps the lean checks met (all calls)
 extern "C" long dec_emu_lean_check(const uint8_t* jpg, size_t len, int nstarts, int steps, int seed)
 {
     JpegHeader J;
@@ -243,7 +245,7 @@ extern "C" long dec_emu_lean_check(const uint8_t* jpg, size_t len, int nstarts, 
     std::vector<uint32_t> words(ent.size() / 4 + 2, 0xFFFFFFFFu);
     memcpy(words.data(), ent.data(), ent.size());
     std::mt19937 rng((uint32_t)seed);
-    long bad = 0;
+    long bad = 0, pairs = 0;
     for (int s = 0; s < nstarts; s++) {
         const uint64_t e0 = dec_pack(rng() % (ent_len * 8), (int)(rng() % (uint32_t)d.wmcu), (int)(rng() % 64));
         DecWalker<false, const DecHuff*> a = dec_walker<false>(d, (const DecHuff*)T.h, T.slow, sel, words.data(),
@@ -257,6 +259,14 @@ extern "C" long dec_emu_lean_check(const uint8_t* jpg, size_t len, int nstarts, 
             a.step(ns);
             if (rng() % 4 == 0) b.step(false);  // an idle lane's step (device loops) changes nothing
             b.step();
+            if (b.two) {  // a symbol pair: the spec's next symbol too (the same block's next AC code)
+                pairs++;
+                if (!a.running(DEC_END) || a.z == 0) {
+                    bad++;
+                    break;
+                }
+                a.step(ns);
+            }
             if (a.state() != b.state() || a.n != b.n) {
                 bad++;
                 break;
@@ -287,6 +297,14 @@ extern "C" long dec_emu_lean_check(const uint8_t* jpg, size_t len, int nstarts, 
         for (int k = 0; k < steps && a.running(DEC_END) && b.running(DEC_END); k++) {
             a.step(ra);
             b.step(rb);
+            if (b.two) {
+                pairs++;
+                if (!a.running(DEC_END) || a.z == 0) {
+                    bad++;
+                    break;
+                }
+                a.step(ra);
+            }
             if (a.state() != b.state() || a.n != b.n || a.bad != b.bad || a.own != b.own) {
                 bad++;
                 break;
@@ -294,6 +312,7 @@ extern "C" long dec_emu_lean_check(const uint8_t* jpg, size_t len, int nstarts, 
         }
         if (ra.ev != rb.ev) bad++;
     }
+    dec_emu_pairs += pairs;
     return bad;
 }
 

@@ -174,3 +174,6 @@ def test_lean_walk_equals_full_walk(emu, oracle):
         assert bad == 0, (k, bad)
         checked += 1
     assert checked > 100
+    # the lean walkers step symbol pairs (icx_decode.h): each pair step was
+    # checked against two of the spec's single steps
+    assert ctypes.c_long.in_dll(emu, "dec_emu_pairs").value > 1000
