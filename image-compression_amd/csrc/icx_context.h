@@ -211,6 +211,7 @@ struct icx_ctx {
     int n_dec_aux = 0;
     hipStream_t dec_aux[DEC_AUX_MAX] = {};
     hipEvent_t ev_dec_split = nullptr, ev_dec_aux[DEC_AUX_MAX] = {};
+    hipEvent_t ev_dec_wr[DEC_AUX_MAX] = {};  // an aux stream's last write pass (split tails)
     icx::DevArena stage[2];
     hipEvent_t ev_up[2] = {nullptr, nullptr}, ev_down[2] = {nullptr, nullptr}, ev_done = nullptr;
     // icx_upload: host threads push file bytes to HBM on their own copy

@@ -644,7 +644,8 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         // chains of unsynchronised subsequences one link per launch and leave
         // most of the chip idle, so the settled images' write, DC, IDCT and
         // colour passes fill it.
-        auto tail = [&](const std::vector<int>& ks, hipStream_t s) -> icx_status {
+        auto tail = [&](const std::vector<int>& ks, hipStream_t s, hipEvent_t wait_ev = nullptr,
+                        hipEvent_t write_done = nullptr) -> icx_status {
             std::vector<int32_t> sid(ks.begin(), ks.end());
             std::vector<int64_t> a, b, r, q;
             int64_t stf = 0, tpx = 0;
@@ -666,10 +667,18 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
                 if (he2 == hipSuccess) he2 = hipStreamWaitEvent(s, c->ev_dec_split, 0);
                 if (he2 != hipSuccess) return hip_fail(c, he2, "decode stream split");
             }
+            if (wait_ev) {  // the previous part's write pass (split tails, below)
+                hipError_t he2 = hipStreamWaitEvent(s, wait_ev, 0);
+                if (he2 != hipSuccess) return hip_fail(c, he2, "decode tail order");
+            }
             launch_dec_offsets(d_desc, d_state, d_sid, n, s);
             {
                 Timed tm(c, "dec_write", stf, false, s);
                 launch_dec_write(d_desc, d_state, Ws.p, Ws.total, S, s);
+            }
+            if (write_done) {
+                hipError_t he2 = hipEventRecord(write_done, s);
+                if (he2 != hipSuccess) return hip_fail(c, he2, "decode tail order");
             }
             {
                 Timed tm(c, "dec_dc", n, false, s);
@@ -690,8 +699,15 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         };
         // tails of different checks go to different aux streams, so a check's
         // images need not wait behind the previous check's tail
-        static const int NAUX = std::min(icx_ctx::DEC_AUX_MAX,
-                                         std::max(1, getenv("ICX_DEC_AUX") ? atoi(getenv("ICX_DEC_AUX")) : 1));
+        // A large tail (most of a big call's images settle at the first check)
+        // goes in TAIL_SPLIT parts on as many aux streams, part p's write pass
+        // after part p-1's: the latency-bound entropy write of one part runs
+        // beside the bandwidth-bound pixel passes (DC, IDCT, colour) of the
+        // part before it instead of after them.
+        static const int TAIL_SPLIT = std::min(icx_ctx::DEC_AUX_MAX,
+                                               std::max(1, getenv("ICX_DEC_TAIL_SPLIT") ? atoi(getenv("ICX_DEC_TAIL_SPLIT")) : 1));
+        static const int NAUX = std::max(TAIL_SPLIT, std::min(icx_ctx::DEC_AUX_MAX,
+                                         std::max(1, getenv("ICX_DEC_AUX") ? atoi(getenv("ICX_DEC_AUX")) : 1)));
         if (!c->ev_dec_split) {
             hipError_t he2 = hipEventCreateWithFlags(&c->ev_dec_split, hipEventDisableTiming);
             if (he2 != hipSuccess) return hip_fail(c, he2, "decode aux stream");
@@ -699,6 +715,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         while (c->n_dec_aux < NAUX) {
             hipError_t he2 = hipStreamCreateWithFlags(&c->dec_aux[c->n_dec_aux], hipStreamNonBlocking);
             if (he2 == hipSuccess) he2 = hipEventCreateWithFlags(&c->ev_dec_aux[c->n_dec_aux], hipEventDisableTiming);
+            if (he2 == hipSuccess) he2 = hipEventCreateWithFlags(&c->ev_dec_wr[c->n_dec_aux], hipEventDisableTiming);
             if (he2 != hipSuccess) return hip_fail(c, he2, "decode aux stream");
             c->n_dec_aux++;
         }
@@ -728,8 +745,16 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
                 if (!tailed[k] && h_wl[k] == 0) early.push_back(k);
             if (!early.empty()) {
                 for (int k : early) tailed[k] = 1;
-                if (icx_status st = tail(early, c->dec_aux[aux_next % NAUX])) return st;
-                aux_next++;
+                const int parts = (int)early.size() >= 32 * TAIL_SPLIT ? TAIL_SPLIT : 1;
+                for (int q = 0; q < parts; q++) {
+                    const size_t a = early.size() * q / parts, b = early.size() * (q + 1) / parts;
+                    const std::vector<int> part(early.begin() + a, early.begin() + b);
+                    const int sx = aux_next % NAUX, sp = (aux_next + NAUX - 1) % NAUX;
+                    if (icx_status st = tail(part, c->dec_aux[sx], q ? c->ev_dec_wr[sp] : nullptr,
+                                             parts > 1 ? c->ev_dec_wr[sx] : nullptr))
+                        return st;
+                    aux_next++;
+                }
                 aux_used = std::min(aux_next, NAUX);
             }
         }

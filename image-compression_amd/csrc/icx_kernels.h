@@ -6,6 +6,11 @@
 
 namespace icx {
 
+// Digest of the encoder's constant tables: on the device (from its symbols,
+// into *out) and on the host (from the tables upload_constants takes).
+void launch_const_digest(uint64_t* out, hipStream_t st);
+uint64_t const_digest_host(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat[64], const uint32_t dc[2][16],
+                           const uint32_t ac[2][256], const uint8_t hdr[4][HDR_COLOR], const int8_t dith[3][64]);
 hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat[64],
                             const uint32_t dc[2][16], const uint32_t ac[2][256],
                             const uint8_t hdr[4][HDR_COLOR], const int8_t dith[3][64]);

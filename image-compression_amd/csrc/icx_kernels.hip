@@ -1920,6 +1920,64 @@ __global__ __launch_bounds__(256) void k_resize(ResizeArgs one, const ResizeArgs
 }
 
 // =================================================================== host side
+// FNV-1a over the constant tables' bytes, in upload order (dith, nat_to_zz,
+// zz_to_nat, dc, ac, acx, hdr): the device computes it from its own symbols
+// (k_const_digest, one thread, ~6 KB), the host from the tables it uploads;
+// icx_create compares the two on every new context (icx_runtime.cpp).
+struct FnvAcc {
+    uint64_t h = 0xcbf29ce484222325ull;
+    __host__ __device__ void add(const void* p, int n)
+    {
+        const uint8_t* b = (const uint8_t*)p;
+        for (int i = 0; i < n; i++) h = (h ^ b[i]) * 0x100000001b3ull;
+    }
+};
+
+__global__ void k_const_digest(uint64_t* out)
+{
+    if (threadIdx.x != 0) return;
+    FnvAcc f;
+    f.add(c_dith, sizeof(c_dith));
+    f.add(c_nat_to_zz, sizeof(c_nat_to_zz));
+    f.add(c_zz_to_nat, sizeof(c_zz_to_nat));
+    f.add(c_dc, sizeof(c_dc));
+    f.add(c_ac, sizeof(c_ac));
+    f.add(c_acx, sizeof(c_acx));
+    f.add(c_hdr, sizeof(c_hdr));
+    *out = f.h;
+}
+
+void launch_const_digest(uint64_t* out, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_const_digest, dim3(1), dim3(64), 0, st, out);
+}
+
+static void derive_acx(const uint32_t ac[2][256], uint2 (&acx)[2][16 * 11])
+{
+    for (int c = 0; c < 2; c++)
+        for (int run = 0; run < 16; run++)
+            for (int sz = 0; sz < 11; sz++) {
+                const uint32_t h = ac[c][(run << 4) | sz];
+                acx[c][run * 11 + sz] = make_uint2((h >> 8) << sz, (h & 255) + sz);
+            }
+}
+
+uint64_t const_digest_host(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat[64], const uint32_t dc[2][16],
+                           const uint32_t ac[2][256], const uint8_t hdr[4][HDR_COLOR], const int8_t dith[3][64])
+{
+    uint2 acx[2][16 * 11];
+    derive_acx(ac, acx);
+    FnvAcc f;
+    f.add(dith, 3 * 64);
+    f.add(nat_to_zz, 64);
+    f.add(zz_to_nat, 64);
+    f.add(dc, sizeof(uint32_t) * 2 * 16);
+    f.add(ac, sizeof(uint32_t) * 2 * 256);
+    f.add(acx, sizeof(acx));
+    f.add(hdr, 4 * HDR_COLOR);
+    return f.h;
+}
+
 hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat[64],
                             const uint32_t dc[2][16], const uint32_t ac[2][256],
                             const uint8_t hdr[4][HDR_COLOR], const int8_t dith[3][64])
@@ -1931,12 +1989,7 @@ hipError_t upload_constants(const uint8_t nat_to_zz[64], const uint8_t zz_to_nat
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_dc), dc, sizeof(uint32_t) * 2 * 16))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_ac), ac, sizeof(uint32_t) * 2 * 256))) return e;
     uint2 acx[2][16 * 11];
-    for (int c = 0; c < 2; c++)
-        for (int run = 0; run < 16; run++)
-            for (int sz = 0; sz < 11; sz++) {
-                const uint32_t h = ac[c][(run << 4) | sz];
-                acx[c][run * 11 + sz] = make_uint2((h >> 8) << sz, (h & 255) + sz);
-            }
+    derive_acx(ac, acx);
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_acx), acx, sizeof(acx)))) return e;
     return hipMemcpyToSymbol(HIP_SYMBOL(c_hdr), hdr, 4 * HDR_COLOR);
 }

@@ -1086,14 +1086,21 @@ uint64_t fnv1a64(const uint8_t* p, size_t n)
     return h;
 }
 
-// One colour and one grey 16x16 encode on the context's own device, compared
-// with the known answers: a constant table missing or wrong on this device
-// (an upload to the wrong device, a stale symbol) fails icx_create instead of
-// corrupting this GPU's output.
-icx_status self_check(icx_ctx* c)
+// Device self-check of a new context: a constant table
+// missing or wrong on this device (an upload to the wrong device, a stale
+// symbol) fails icx_create instead of corrupting this GPU's output.
+//  * the first context on a device: one colour and one grey 16x16 encode,
+//    compared with the known answers (the whole encoder, tables included);
+//  * every context: the device's digest of its constant tables
+//    (k_const_digest) against the host's, ~0.1 ms.
+bool self_check_off()
 {
-    if (const char* e = getenv("ICX_SELF_CHECK"))
-        if (atoi(e) == 0) return ICX_OK;
+    const char* e = getenv("ICX_SELF_CHECK");
+    return e && atoi(e) == 0;
+}
+
+icx_status self_check_encode(icx_ctx* c)
+{
     uint8_t px[2][16 * 16 * 3];
     uint8_t out[2][2048];
     icx_fit_job j[2] = {};
@@ -1294,9 +1301,33 @@ icx_status icx_create(int device, icx_ctx** out)
         budget_mb = std::max<size_t>(2048, (free_b / 5 * 2) >> 20);
     if (const char* env = getenv("ICX_WORKSPACE_MB")) budget_mb = (size_t)atoll(env);
     c->budget = budget_mb << 20;
-    if (self_check(c) != ICX_OK) {
-        icx_destroy(c);
-        return ICX_E_DEVICE;
+    if (!self_check_off()) {
+        // (up_mu: one digest buffer per device; the first context's encode check)
+        std::lock_guard<std::mutex> lk(up_mu);
+        static std::vector<std::pair<int, uint64_t*>> digest_buf;
+        static std::vector<int> encode_checked;
+        uint64_t* d_dig = nullptr;
+        for (auto& b : digest_buf)
+            if (b.first == device) d_dig = b.second;
+        hipError_t e = hipSuccess;
+        if (!d_dig && (e = hipMalloc(&d_dig, sizeof(uint64_t))) == hipSuccess) digest_buf.push_back({device, d_dig});
+        uint64_t got = 0;
+        if (e == hipSuccess) {
+            launch_const_digest(d_dig, c->stream);
+            e = hipMemcpyAsync(&got, d_dig, sizeof(got), hipMemcpyDeviceToHost, c->stream);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        const uint64_t want = const_digest_host(K.nat2zz, K.zz2nat, K.dc, K.ac, K.hdr, K.dith);
+        icx_status st = e != hipSuccess ? ICX_E_DEVICE : got != want ? ICX_E_DEVICE : ICX_OK;
+        if (st == ICX_OK && std::find(encode_checked.begin(), encode_checked.end(), device) == encode_checked.end()) {
+            st = self_check_encode(c);
+            if (st == ICX_OK) encode_checked.push_back(device);
+        }
+        if (st != ICX_OK) {
+            (void)hipGetLastError();
+            icx_destroy(c);
+            return ICX_E_DEVICE;
+        }
     }
     *out = c;
     return ICX_OK;
@@ -1317,6 +1348,7 @@ void icx_destroy(icx_ctx* ctx)
         hipStreamSynchronize(ctx->dec_aux[k]);
         hipStreamDestroy(ctx->dec_aux[k]);
         hipEventDestroy(ctx->ev_dec_aux[k]);
+        if (ctx->ev_dec_wr[k]) hipEventDestroy(ctx->ev_dec_wr[k]);
     }
     if (ctx->ev_dec_split) hipEventDestroy(ctx->ev_dec_split);
     for (int k = 0; k < icx_ctx::UP_STREAMS; k++)

@@ -147,12 +147,14 @@ icx_ctx* icx_pool_context(icx_pool* pool, int32_t i);
 /* GPUs visible to this process (0 when there are none): the CLI's default
  * device list when one process drives the node. */
 int32_t icx_device_count(void);
-/* icx_create's device self-check: every new context
- * encodes a fixed 16x16 BGR24 and a fixed 16x16 GRAY8 frame at quality 0.75
- * on its own device and compares the files with known answers (length and
- * 64-bit FNV-1a digest, pinned against the CPU oracle by the tests); a
- * mismatch fails icx_create with ICX_E_DEVICE, so a constant table missing
- * or wrong on one GPU cannot silently corrupt that GPU's output.  Debug
+/* icx_create's device self-check: the first context on
+ * a device encodes a fixed 16x16 BGR24 and a fixed 16x16 GRAY8 frame at
+ * quality 0.75 there and compares the files with known answers (length and
+ * 64-bit FNV-1a digest, pinned against the CPU oracle by the tests); every
+ * context compares the device's digest of the encoder's constant tables with
+ * the host's (~0.1 ms).  A mismatch fails icx_create with ICX_E_DEVICE, so a
+ * constant table missing or wrong on one GPU cannot silently corrupt that
+ * GPU's output (ICX_SELF_CHECK=0 skips both).  Debug
  * helpers: the known-answer image (px: 16*16*3 or 16*16 bytes) and its
  * expected file; and a hook that overwrites (on = 1) or restores (on = 0)
  * the encoder's constant Huffman tables on `device`. */

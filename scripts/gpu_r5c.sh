@@ -13,7 +13,7 @@ grep "icx_create ms" gpurun_out/pytest_gpu_r5c.log
 echo "== decode A/B 200 frames"
 FRAMES=200 AB_ARGS="--distinct 16" ROUNDS=2 bash scripts/ab_decode.sh lib/libicx_r4.so base ICX_DEC_PAIR=0 lib/libicx_nt448.so lib/libicx_nt192.so lib/libicx_nosplit.so || exit 1
 echo "== decode A/B 1000 frames"
-FRAMES=1000 STEPS=3 AB_ARGS="--distinct 16" ROUNDS=1 bash scripts/ab_decode.sh lib/libicx_r4.so base lib/libicx_nt448.so lib/libicx_nt192.so || exit 1
+FRAMES=1000 STEPS=3 AB_ARGS="--distinct 16" ROUNDS=1 bash scripts/ab_decode.sh lib/libicx_r4.so base lib/libicx_nt448.so lib/libicx_nt192.so ICX_DEC_TAIL_SPLIT=2 ICX_DEC_TAIL_SPLIT=3 || exit 1
 for g in 64 128; do
   for dv in 0 0,0; do
     timeout -k 10 300 python scripts/bench_pipeline.py --files 1000 --group $g --devices $dv > gpurun_out/pipeline_r5c_g${g}_d${dv/,/}.json 2>> gpurun_out/pipeline_r5c.err \

@@ -584,10 +584,12 @@ def test_palette_resize_matches_restatement(codec, oracle):
 
 
 def test_create_self_check_catches_a_bad_device_constant(codec, oracle):
-    """icx_create encodes two known-answer frames on its
-    own device; with the encoder's Huffman constants overwritten on that
-    device (debug hook) icx_create fails with ICX_E_DEVICE, and once they
-    are restored it succeeds again.  The check costs < 1 ms per context."""
+    """the first context on a device encodes two
+    known-answer frames there, every context compares the device's digest of
+    the encoder's constant tables with the host's; with the Huffman constants
+    overwritten on the device (debug hook) icx_create fails with
+    ICX_E_DEVICE, and once they are restored it succeeds again.  The check
+    costs < 1 ms per context."""
     import ctypes
     import time
     L = N.load()
