@@ -115,6 +115,12 @@ void dec_geometry(const JpegHeader& J, int s, DecDesc& d)
         d.nbmcu = d.nby + 2;
         d.mcux = (J.w + 8 * d.hs - 1) / (8 * d.hs);
         d.mcuy = (J.h + 8 * d.vs - 1) / (8 * d.vs);
+    } else if (J.ncomp == 4) {  // CMYK / YCCK, every component 1x1: four blocks per MCU
+        d.hs = d.vs = 1;
+        d.nby = 1;
+        d.nbmcu = 4;
+        d.mcux = (J.w + 7) / 8;
+        d.mcuy = (J.h + 7) / 8;
     } else {  // non-interleaved single component: one block per MCU
         d.hs = d.vs = 1;
         d.nby = d.nbmcu = 1;
@@ -122,7 +128,7 @@ void dec_geometry(const JpegHeader& J, int s, DecDesc& d)
         d.mcuy = (J.h + 7) / 8;
     }
     d.nblocks = (int64_t)d.mcux * d.mcuy * d.nbmcu;
-    for (int c = 0; c < 3; c++) d.pw[c] = d.ph[c] = d.cw[c] = d.ch[c] = 0;
+    for (int c = 0; c < 4; c++) d.pw[c] = d.ph[c] = d.cw[c] = d.ch[c] = 0;
     for (int c = 0; c < J.ncomp; c++) {
         const int hc = J.ncomp == 3 ? (c == 0 ? d.hs : 1) : 1, vc = J.ncomp == 3 ? (c == 0 ? d.vs : 1) : 1;
         d.cw[c] = (J.w * hc + d.hs - 1) / d.hs;  // downsampled_width
@@ -132,6 +138,7 @@ void dec_geometry(const JpegHeader& J, int s, DecDesc& d)
     }
     d.fancy = J.ncomp == 3 && d.hs == 2 && d.cw[1] > 2;  // do_fancy_upsampling && downsampled_width > 2
     d.rgb = J.ncomp == 3 && J.rgb;
+    d.cmyk = J.ncomp == 4 ? J.cmyk : 0;
     d.wmcu = dec_walk_mcu(J.ncomp, d.nbmcu, J.td, J.ta);
     d.fuse420 = s == 1 && J.ncomp == 3 && d.hs == 2 && d.vs == 2 && d.fancy && !d.rgb;
     d.s = s;
@@ -236,7 +243,7 @@ icx_status run_progressive(icx_ctx* c, std::vector<DecItem>& items, int16_t* coe
             dec_geometry(it.J, it.s, d);
             const size_t nb = (size_t)d.nblocks;
             size_t per = align_up(nb * 128, 256) + align_up(nb * 4, 256) + 4096;
-            for (int k = 0; k < 3; k++) per += align_up((size_t)d.pw[k] * d.ph[k], 256);
+            for (int k = 0; k < 4; k++) per += align_up((size_t)d.pw[k] * d.ph[k], 256);
             const bool host_out = !coef_out && !is_device_ptr(it.job->out);
             if (host_out) per += align_up(it.job->out_len, 256);
             const size_t hper = align_up(nb * 128, 64) + align_up(nb * 4, 64) + (it.dev_in ? align_up(it.job->len, 64) : 0);
@@ -364,8 +371,10 @@ icx_status run_progressive(icx_ctx* c, std::vector<DecItem>& items, int16_t* coe
     return ICX_OK;
 }
 
-// mode 0: decode to pixels; mode 1: coefficients only (debug: natural order, DC in [0])
-icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out, size_t coef_cap)
+// mode 0: decode to pixels; mode 1: coefficients only (debug: natural order, DC in [0]).
+// raw4: 4-component files out as libjpeg's CMYK samples (4 bytes a pixel, debug)
+icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out, size_t coef_cap,
+                      bool raw4 = false)
 {
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     HostSpan call{c, "host.call_decode"};  // the whole call, wall time (profiling)
@@ -404,8 +413,8 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         if (j.status != ICX_OK) continue;
         const int s = j.subsampling > 0 ? j.subsampling : icx_subsampling_factor(it.J.w, it.J.h);
         it.s = s;
-        it.nch = it.J.ncomp == 3 ? 3 : 1;
-        j.fmt = it.nch == 3 ? ICX_BGR24 : ICX_GRAY8;
+        it.nch = it.J.ncomp == 1 ? 1 : it.J.ncomp == 4 && raw4 ? 4 : 3;  // CMYK / YCCK: BGR24 (k_dec_color)
+        j.fmt = it.nch == 1 ? ICX_GRAY8 : ICX_BGR24;
         j.width = (it.J.w + s - 1) / s;
         j.height = (it.J.h + s - 1) / s;
         j.out_len = (size_t)j.width * j.height * it.nch;
@@ -432,6 +441,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             DecItem& it = items[pos];
             DecDesc d{};
             dec_geometry(it.J, it.s, d);
+            d.raw4 = raw4;
             const int64_t scan_len = (int64_t)(it.job->len - it.J.scan_off);
             const int64_t nmcu = (int64_t)d.mcux * d.mcuy;
             d.nseg_max = it.J.ri ? (int32_t)((nmcu + it.J.ri - 1) / it.J.ri) + 1 : 1;
@@ -440,7 +450,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             it.nblocks = d.nblocks;
             size_t per = (it.dev_in ? 0 : align_up(scan_len, 256)) + align_up(it.ent_cap, 256) + it.ntiles * 8 + 512 +
                          (size_t)d.nseg_max * 4 + (size_t)d.nblocks * (128 + 4) + sizeof(DecTab) + 4096;
-            for (int k = 0; k < 3; k++) per += align_up((size_t)d.pw[k] * d.ph[k], 256);
+            for (int k = 0; k < 4; k++) per += align_up((size_t)d.pw[k] * d.ph[k], 256);
             per += (size_t)(it.ent_cap * 8 / 2048 + 2) * (8 + 2 + 4 + 4);  // subsequence arrays at S >= 2048
             per += (size_t)(it.ent_cap * 8 / 2048 + 2) * DEC_CK_MAX * 8;  // checkpoints
             if (!coef_out && !is_device_ptr(it.job->out)) per += align_up(it.job->out_len, 256);
@@ -965,6 +975,19 @@ icx_status icx_upload(icx_ctx* ctx, void* dst, const void* src, size_t bytes)
     if (e == hipSuccess) return ICX_OK;
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     return hip_fail(ctx, e, "icx_upload");
+}
+
+icx_status icx_debug_decode_cmyk(icx_ctx* ctx, const uint8_t* data, size_t len, uint8_t* out, size_t cap)
+{
+    if (!ctx || !data || !out) return ICX_E_NULL;
+    icx_decode_job j{};
+    j.data = data;
+    j.len = len;
+    j.subsampling = 1;
+    j.out = out;
+    j.cap = cap;
+    const icx_status s = run_decode(ctx, &j, 1, nullptr, 0, true);
+    return s != ICX_OK ? s : j.status;
 }
 
 icx_status icx_debug_decode_coefs(icx_ctx* ctx, const uint8_t* data, size_t len, int16_t* coefs, size_t ncoefs)

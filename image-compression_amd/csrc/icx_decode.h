@@ -43,7 +43,10 @@
 namespace icx {
 
 constexpr int DEC_SUB_BITS = 1024;   // bits per subsequence (one thread)
-constexpr int DEC_LUT_BITS = 10;     // Huffman fast-lookup width
+#ifndef ICX_DEC_LUT_BITS
+#define ICX_DEC_LUT_BITS 10
+#endif
+constexpr int DEC_LUT_BITS = ICX_DEC_LUT_BITS;  // Huffman fast-lookup width
 // k_dec_write workgroup size.  The pass is LDS-limited (a 128-B block slot
 // per lane + the first-level tables): 256 lanes = 40 KiB, four workgroups =
 // 16 waves per CU.  576 lanes (80 KiB, meant as two workgroups = 18 waves)
@@ -127,10 +130,10 @@ struct DecTab {
     DecHuff h[4];
     DecLean lean[4];  // h[] as state-transition entries (DecLean), for the state-only walks
     DecSlow slow[4];
-    uint16_t qt[3][64];    // dequantisation tables, natural order, per component
-    uint8_t sel[6];
+    uint16_t qt[4][64];    // dequantisation tables, natural order, per component
+    uint8_t sel[8];
     uint8_t ntab;
-    uint8_t pad[9];
+    uint8_t pad[7];
 };
 
 // Per-image descriptor (host-built, read-only on the device).
@@ -150,17 +153,19 @@ struct DecDesc {
     uint32_t* boff;        // blocks completed before each subsequence
     int16_t* coefs;        // nblocks x 64, natural order, quantised; [0] = DC difference
     int32_t* dc;           // nblocks: DC differences (write pass), then DC values (k_dec_dc)
-    uint8_t* plane[3];     // IDCT output planes (pitch pw[c])
+    uint8_t* plane[4];     // IDCT output planes (pitch pw[c])
     uint8_t* out;          // BGR24 / GRAY8 rows, stride ostride
     const DecTab* tab;
     int64_t nblocks;
     int32_t ntiles, nsub_max, nseg_max;
     int32_t w, h, ncomp, hs, vs, nby, nbmcu, mcux, mcuy, ri;
-    int32_t pw[3], ph[3], cw[3], ch[3];
+    int32_t pw[4], ph[4], cw[4], ch[4];
     int32_t fancy;         // chroma upsampled with the triangle filter (cw > 2)
     int32_t fuse420;       // s == 1, 4:2:0, fancy: luma IDCT fused into the colour pass (no luma plane)
     int32_t s, ow, oh, ostride;
     int32_t rgb;           // components are R, G, B (jdcolor.c null_convert), not YCbCr
+    int32_t cmyk;          // 4 components: 1 CMYK, 2 YCCK (jdcolor.c ycck_cmyk_convert first)
+    int32_t raw4;          // 4 components out as libjpeg's CMYK samples (debug), else BGR (k_dec_color)
     int32_t wmcu;          // blocks per MCU as the entropy walk sees them (dec_walk_mcu)
 };
 
@@ -174,8 +179,10 @@ struct DecDesc {
 // unaffected.
 ICX_HD int dec_walk_mcu(int ncomp, int nbmcu, const int* td, const int* ta)
 {
-    if (ncomp != 3) return nbmcu;
-    return td[0] == td[1] && td[0] == td[2] && ta[0] == ta[1] && ta[0] == ta[2] ? 1 : nbmcu;
+    if (ncomp != 3 && ncomp != 4) return nbmcu;
+    for (int c = 1; c < ncomp; c++)
+        if (td[c] != td[0] || ta[c] != ta[0]) return nbmcu;
+    return 1;
 }
 
 // the IDCT kernels load a dequantisation row as one 16-byte load

@@ -583,7 +583,7 @@ __device__ __forceinline__ void load_first_levels(const DecTab* T, uint32_t (*L1
 __device__ __forceinline__ uint32_t selector(const DecTab* T)
 {
     uint32_t s = 0;
-    for (int k = 0; k < 6; k++) s |= (uint32_t)(T->sel[k] & 3) << (4 * k);
+    for (int k = 0; k < 8; k++) s |= (uint32_t)(T->sel[k] & 3) << (4 * k);
     return s;
 }
 
@@ -900,7 +900,7 @@ __global__ void __launch_bounds__(DEC_WRITE_NT) k_dec_write(const DecDesc* D, De
 // 4; it was a 32-MCU sequential run per thread in two passes: 8.7 ms per
 // 1000 4K frames)
 struct DcAgg {
-    int32_t v[3];
+    int32_t v[4];  // per component (CMYK / YCCK: four)
     int f;  // a restart interval starts inside the span: what came before does not count
 };
 
@@ -908,7 +908,7 @@ __device__ __forceinline__ DcAgg dc_join(const DcAgg& a, const DcAgg& b)  // a b
 {
     DcAgg r;
 #pragma unroll
-    for (int c = 0; c < 3; c++) r.v[c] = b.f ? b.v[c] : a.v[c] + b.v[c];
+    for (int c = 0; c < 4; c++) r.v[c] = b.f ? b.v[c] : a.v[c] + b.v[c];
     r.f = a.f | b.f;
     return r;
 }
@@ -919,7 +919,7 @@ __device__ __forceinline__ void dc_tile(ICX_GLOBAL int32_t* dc, int nb, int ny, 
 {
     const int n = NB > 0 ? NB : nb;
     int32_t d[NB > 0 ? NB : 10];  // T.81: at most 10 blocks per MCU
-    DcAgg a{{0, 0, 0}, 0};
+    DcAgg a{{0, 0, 0, 0}, 0};
     if (in) {
 #pragma unroll
         for (int k = 0; k < (NB > 0 ? NB : 10); k++)
@@ -936,7 +936,7 @@ __device__ __forceinline__ void dc_tile(ICX_GLOBAL int32_t* dc, int nb, int ny, 
     for (int o = 1; o < 64; o <<= 1) {
         DcAgg y;
 #pragma unroll
-        for (int c = 0; c < 3; c++) y.v[c] = __shfl_up(x.v[c], o, 64);
+        for (int c = 0; c < 4; c++) y.v[c] = __shfl_up(x.v[c], o, 64);
         y.f = __shfl_up(x.f, o, 64);
         if (lane >= o) x = dc_join(y, x);
     }
@@ -951,12 +951,12 @@ __device__ __forceinline__ void dc_tile(ICX_GLOBAL int32_t* dc, int nb, int ny, 
     // interval starts at it
     DcAgg prev;
 #pragma unroll
-    for (int c = 0; c < 3; c++) prev.v[c] = __shfl_up(x.v[c], 1, 64);
+    for (int c = 0; c < 4; c++) prev.v[c] = __shfl_up(x.v[c], 1, 64);
     prev.f = __shfl_up(x.f, 1, 64);
-    if (lane == 0) prev = DcAgg{{0, 0, 0}, 0};
+    if (lane == 0) prev = DcAgg{{0, 0, 0, 0}, 0};
     const DcAgg excl = dc_join(pre, prev);
     if (in) {
-        int32_t acc[3] = {a.f ? 0 : excl.v[0], a.f ? 0 : excl.v[1], a.f ? 0 : excl.v[2]};
+        int32_t acc[4] = {a.f ? 0 : excl.v[0], a.f ? 0 : excl.v[1], a.f ? 0 : excl.v[2], a.f ? 0 : excl.v[3]};
 #pragma unroll
         for (int k = 0; k < (NB > 0 ? NB : 10); k++)
             if (k < n) {
@@ -976,7 +976,7 @@ __device__ __forceinline__ void dc_image(const DecDesc& d, DcAgg (*s_w)[16])
     ICX_GLOBAL int32_t* dc = (ICX_GLOBAL int32_t*)d.dc;
     const int nb = d.nbmcu, ri = d.ri, ny = d.nby;
     const int t = threadIdx.x;
-    DcAgg carry{{0, 0, 0}, 0};
+    DcAgg carry{{0, 0, 0, 0}, 0};
     for (int64_t m0 = 0; m0 < nmcu; m0 += 1024) {
         const int64_t m = m0 + t;
         dc_tile<NB>(dc, nb, ny, m, m < nmcu, ri, carry, s_w, t);
@@ -1145,9 +1145,9 @@ __global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecSta
     const ICX_GLOBAL int16_t* const coefs = (const ICX_GLOBAL int16_t*)d.coefs;
     const ICX_GLOBAL int32_t* const dcs = (const ICX_GLOBAL int32_t*)d.dc;
     const ICX_GLOBAL uint16_t* const qts = (const ICX_GLOBAL uint16_t*)d.tab->qt[0];
-    ICX_GLOBAL uint8_t* const planes[3] = {(ICX_GLOBAL uint8_t*)d.plane[0], (ICX_GLOBAL uint8_t*)d.plane[1],
-                                           (ICX_GLOBAL uint8_t*)d.plane[2]};
-    const int pw[3] = {d.pw[0], d.pw[1], d.pw[2]};
+    ICX_GLOBAL uint8_t* const planes[4] = {(ICX_GLOBAL uint8_t*)d.plane[0], (ICX_GLOBAL uint8_t*)d.plane[1],
+                                           (ICX_GLOBAL uint8_t*)d.plane[2], (ICX_GLOBAL uint8_t*)d.plane[3]};
+    const int pw[4] = {d.pw[0], d.pw[1], d.pw[2], d.pw[3]};
     int tile = (int)wg * DEC_IDCT_TILES;
     if (tile >= ntile) return;
     // i < 2^31: at most 65535^2 * 3 / 64 blocks
@@ -1225,6 +1225,39 @@ __global__ void __launch_bounds__(256) k_dec_color(const DecDesc* D, const DecSt
     const uint8_t* yrow = d.plane[0] + (int64_t)Y * d.pw[0];
     if (d.ncomp == 1) {
         for (int k = 0; k < 4 && x0 + k < d.ow; k++) orow[x0 + k] = yrow[(x0 + k) * d.s];
+        return;
+    }
+    if (d.ncomp == 4) {  // CMYK / YCCK: every component 1x1 (icx_jpeg_parse.cpp)
+        const int64_t off = (int64_t)Y * d.pw[0];
+        for (int k = 0; k < 4 && x0 + k < d.ow; k++) {
+            const int X = (x0 + k) * d.s;
+            int c0 = d.plane[0][off + X], c1 = d.plane[1][off + X], c2 = d.plane[2][off + X];
+            const int kk = d.plane[3][off + X];
+            if (d.cmyk == 2) {  // ycck_cmyk_convert (jdcolor.c): C, M, Y = 255 - R, G, B of ycc_rgb_convert
+                const int cb = c1 - 128, cr = c2 - 128, yy = c0;
+                c0 = 255 - clamp255(yy + ((91881 * cr + 32768) >> 16));
+                c1 = 255 - clamp255(yy + ((-22554 * cb + 32768 - 46802 * cr) >> 16));
+                c2 = 255 - clamp255(yy + ((116130 * cb + 32768) >> 16));
+            }
+            if (d.raw4) {  // libjpeg's CMYK samples (debug / parity)
+                uint8_t* o = orow + (int64_t)(x0 + k) * 4;
+                o[0] = (uint8_t)c0, o[1] = (uint8_t)c1, o[2] = (uint8_t)c2, o[3] = (uint8_t)kk;
+                continue;
+            }
+            // to RGB as the host path did (Pillow: the samples read as Adobe-inverted
+            // CMYK, then cmyk2rgb: nk - nk * c / 255 with nk = 255 - k); TwelveMonkeys'
+            // ICC conversion is not restatable here (parity unpinned)
+            const int nk = kk;  // 255 - (255 - raw k)
+            uint8_t* o = orow + (int64_t)(x0 + k) * 3;
+            const int cv[3] = {255 - c0, 255 - c1, 255 - c2};
+            int rgb[3];
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const int t = cv[q] * nk + 128;
+                rgb[q] = nk - (((t >> 8) + t) >> 8);
+            }
+            o[0] = clamp255(rgb[2]), o[1] = clamp255(rgb[1]), o[2] = clamp255(rgb[0]);  // BGR
+        }
         return;
     }
     uint8_t px[12];

@@ -109,8 +109,9 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
             J.h = (s[1] << 8) | s[2];
             J.w = (s[3] << 8) | s[4];
             J.ncomp = s[5];
-            if (s[0] != 8 || J.w == 0 || J.h == 0 || (J.ncomp != 1 && J.ncomp != 3)) unsupported = true;
-            if (J.ncomp >= 1 && J.ncomp <= 3) {
+            if (s[0] != 8 || J.w == 0 || J.h == 0 || (J.ncomp != 1 && J.ncomp != 3 && J.ncomp != 4)) unsupported = true;
+            if (J.ncomp == 4 && J.progressive) unsupported = true;  // progressive CMYK / YCCK: the host reader
+            if (J.ncomp >= 1 && J.ncomp <= 4) {
                 if (n < 6 + 3 * (size_t)J.ncomp) return ICX_E_CORRUPT;
                 for (int c = 0; c < J.ncomp; c++) {
                     J.id[c] = s[6 + 3 * c];
@@ -152,6 +153,14 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
                 if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0) return ICX_E_UNSUPPORTED;
             }
             J.scan_off = i;
+            if (J.ncomp == 4) {
+                // jdapimin.c default_decompress_parms: an Adobe marker's transform 0 ->
+                // CMYK, anything else -> YCCK; no marker -> CMYK.  One block per
+                // component per MCU only (the CMYK layout libjpeg writes)
+                J.cmyk = adobe && transform != 0 ? 2 : 1;
+                for (int c = 0; c < 4; c++)
+                    if (J.hs[c] != 1 || J.vs[c] != 1) return ICX_E_UNSUPPORTED;
+            }
             if (J.ncomp == 3) {
                 const int cs = colour_space(J, jfif, exif, adobe, transform);
                 if (cs < 0) return ICX_E_UNSUPPORTED;
@@ -281,7 +290,7 @@ bool build_dec_tab(const JpegHeader& J, DecTab& T)
 uint32_t dec_selector(const DecTab& T)
 {
     uint32_t s = 0;
-    for (int k = 0; k < 6; k++) s |= (uint32_t)(T.sel[k] & 3) << (4 * k);
+    for (int k = 0; k < 8; k++) s |= (uint32_t)(T.sel[k] & 3) << (4 * k);
     return s;
 }
 

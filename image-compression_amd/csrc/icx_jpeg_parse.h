@@ -23,7 +23,7 @@ namespace icx {
 
 struct JpegHeader {
     int w = 0, h = 0, ncomp = 0, ri = 0;
-    int id[3] = {}, hs[3] = {}, vs[3] = {}, tq[3] = {}, td[3] = {}, ta[3] = {};
+    int id[4] = {}, hs[4] = {}, vs[4] = {}, tq[4] = {}, td[4] = {}, ta[4] = {};
     uint16_t qt[4][64] = {};  // natural order
     bool qt_ok[4] = {};
     uint8_t hbits[2][4][16] = {};   // [dc|ac][slot] counts per code length
@@ -33,6 +33,7 @@ struct JpegHeader {
     size_t scan_off = 0;  // first byte of the entropy-coded segment (progressive: of the first scan)
     bool progressive = false;  // SOF2: td/ta/scan_off unused, prog_decode walks every scan
     bool rgb = false;          // 3 components stored as R, G, B (colour_space): no YCbCr conversion
+    int cmyk = 0;              // 4 components: 1 CMYK, 2 YCCK (jdapimin.c default_decompress_parms)
 };
 
 // Parse markers up to the SOS.  `avail` bytes of the file are present at p

@@ -563,7 +563,8 @@ class Codec:
             if info[0] == N.OK:
                 _, w, h, nc = info
                 s = subsampling if subsampling > 0 else subsampling_factor(w, h)
-                shape = (-(-h // s), -(-w // s), 3) if nc == 3 else (-(-h // s), -(-w // s))
+                # (CMYK / YCCK files decode to BGR too: k_dec_color)
+                shape = (-(-h // s), -(-w // s), 3) if nc >= 3 else (-(-h // s), -(-w // s))
                 if device_out:
                     out = DeviceImage(self, shape)
                     jobs[i].out, jobs[i].cap = out.data_ptr(), out.numel()
@@ -587,6 +588,17 @@ class Codec:
         st, img = self.decode_jpg_batch([data], subsampling, device_out)[0]
         self._check(st, "icx_decode_jpg")
         return img
+
+    def debug_decode_cmyk(self, data) -> np.ndarray:
+        """A 4-component JPEG's CMYK samples (H, W, 4) as libjpeg outputs them
+        (icx_debug_decode_cmyk: YCCK through ycck_cmyk_convert)."""
+        a = np.frombuffer(bytes(data), np.uint8)
+        st, w, h, nc = jpeg_info(a)
+        self._check(st, "icx_jpeg_info")
+        out = np.empty((h, w, 4), np.uint8)
+        self._check(self._lib.icx_debug_decode_cmyk(self._ctx, a.ctypes.data, a.nbytes, out.ctypes.data, out.nbytes),
+                    "icx_debug_decode_cmyk")
+        return out
 
     def debug_decode_coefs(self, data) -> np.ndarray:
         a = np.frombuffer(bytes(data), np.uint8)
@@ -712,6 +724,8 @@ def _scan_blocks(a):
             nc = int(a[i + 9])
             if nc == 1:
                 return -(-w // 8) * -(-h // 8)
+            if nc == 4:  # CMYK / YCCK, every component 1x1
+                return -(-w // 8) * -(-h // 8) * 4
             hs, vs = int(a[i + 11]) >> 4, int(a[i + 11]) & 15
             return -(-w // (8 * hs)) * -(-h // (8 * vs)) * (hs * vs + 2)
         if m == 0xFF or m == 0xD8:

@@ -351,6 +351,11 @@ icx_status icx_memcpy(icx_ctx* ctx, void* dst, const void* src, size_t bytes);
 icx_status icx_upload(icx_ctx* ctx, void* dst, const void* src, size_t bytes);
 
 /* ------------------------------------------------------- parity / metrics */
+/* A 4-component (CMYK / YCCK) baseline file decoded to libjpeg's CMYK samples
+ * (jdcolor.c: YCCK through ycck_cmyk_convert, CMYK as stored), 4 bytes a
+ * pixel, W x H, host or device `out` - the samples icx_decode_jpg converts
+ * to BGR24 (debug / parity). */
+icx_status icx_debug_decode_cmyk(icx_ctx* ctx, const uint8_t* data, size_t len, uint8_t* out, size_t cap);
 /* Quantised coefficients after DC prediction (natural order, 64 per block,
  * scan/MCU block order incl. dummy blocks) as the device decoder produced them. */
 icx_status icx_debug_decode_coefs(icx_ctx* ctx, const uint8_t* data, size_t len, int16_t* coefs, size_t ncoefs);

@@ -117,6 +117,8 @@ int oracle_jpeg_coefs(const uint8_t* jpg, size_t len, int16_t* coefs, size_t nbl
 /* decode + source subsampling s: ceil(W/s) x ceil(H/s), BGR24 or GRAY8, packed */
 int oracle_jpeg_decode(const uint8_t* jpg, size_t len, int s, uint8_t* out, size_t cap, int* w,
                        int* h, int* fmt);
+/* 4-component (CMYK / YCCK) file: libjpeg's CMYK samples, W x H x 4 */
+int oracle_jpeg_decode_cmyk(const uint8_t* jpg, size_t len, uint8_t* out, size_t cap, int* w, int* h);
 
 #ifdef __cplusplus
 }

@@ -18,9 +18,17 @@
  *   jdsample.c   h2v2/h2v1 "fancy" (triangle) upsampling when
  *                downsampled_width > 2, else box replication; context rows
  *                replicate the first / last real sample row (jdmainct.c)
- *   jdcolor.c    ycc_rgb_convert (SCALEBITS 16 tables)
+ *   jdcolor.c    ycc_rgb_convert (SCALEBITS 16 tables); for 4-component
+ *                files (jdapimin.c: Adobe transform 0 or no marker -> CMYK,
+ *                other transforms -> YCCK) ycck_cmyk_convert or CMYK as stored
  * then keeps pixels (x*s, y*s) as the JDK reader does for source subsampling
- * and returns TYPE_3BYTE_BGR (3 components) or TYPE_BYTE_GRAY.
+ * and returns TYPE_3BYTE_BGR (3 components) or TYPE_BYTE_GRAY.  CMYK / YCCK
+ * (SURVEY §8f rank 4): the reference reads them through TwelveMonkeys, whose
+ * ICC CMYK -> RGB conversion cannot be restated here (no profile, no CMM:
+ * parity unpinned); the RGB step restated is the one the build's host path
+ * used before (Pillow: the samples read as Adobe-inverted CMYK, then
+ * cmyk2rgb), and oracle_jpeg_decode_cmyk gives libjpeg's CMYK samples, which
+ * libjpeg-turbo pins (tests/golden/gen_cmyk_golden.py).
  *
  * Pinned against libjpeg-turbo 3.1.4 (6b API level, via Pillow) decodes of
  * tests/golden/decode/ (gen_decode_golden.py).
@@ -41,7 +49,8 @@ typedef struct {
 typedef struct {
     int w, h, ncomp, ri;
     int rgb; /* 3 components stored as R, G, B (colour_space below): no ycc_rgb_convert */
-    int id[3], hs[3], vs[3], tq[3], td[3], ta[3];
+    int cmyk; /* 4 components: 1 CMYK, 2 YCCK */
+    int id[4], hs[4], vs[4], tq[4], td[4], ta[4];
     int hmax, vmax, mcux, mcuy;
     uint16_t qt[4][64]; /* natural order */
     int qt_present[4];
@@ -165,7 +174,7 @@ static int parse(const uint8_t* p, size_t len, jinfo_t* J)
             J->w = (s[3] << 8) | s[4];
             J->ncomp = s[5];
             if (J->w == 0 || J->h == 0) return 5; /* DNL-defined height */
-            if (J->ncomp != 1 && J->ncomp != 3) return 5;
+            if (J->ncomp != 1 && J->ncomp != 3 && J->ncomp != 4) return 5;
             if (n < 6 + 3 * (size_t)J->ncomp) return 6;
             for (int c = 0; c < J->ncomp; c++) {
                 J->id[c] = s[6 + 3 * c];
@@ -214,7 +223,13 @@ static int parse(const uint8_t* p, size_t len, jinfo_t* J)
     /* sampling: colour = Y (1|2 x 1|2) with Cb, Cr at 1x1 except 1x2 (4:4:0,
      * whose 6b upsampler is not the one libjpeg-turbo uses); grey = any */
     J->hmax = J->vmax = 1;
-    if (J->ncomp == 3) {
+    if (J->ncomp == 4) { /* CMYK / YCCK: one block per component per MCU only */
+        J->cmyk = adobe && transform != 0 ? 2 : 1;
+        for (int c = 0; c < 4; c++)
+            if (J->hs[c] != 1 || J->vs[c] != 1) return 5;
+        J->mcux = (J->w + 7) / 8;
+        J->mcuy = (J->h + 7) / 8;
+    } else if (J->ncomp == 3) {
         int cs = colour_space(J, jfif, exif, adobe, transform);
         if (cs < 0) return 5;
         J->rgb = cs;
@@ -331,16 +346,17 @@ static int restart(breader_t* b)
 static int decode_scan(const jinfo_t* J, int16_t* coefs)
 {
     breader_t b = {J->scan, J->scan_len, 0, 0, 0, 0};
-    int nb_mcu = J->ncomp == 3 ? J->hs[0] * J->vs[0] + 2 : 1;
+    int nb_mcu = J->ncomp == 3 ? J->hs[0] * J->vs[0] + 2 : J->ncomp == 4 ? 4 : 1;
     int comp_of[6];
-    for (int k = 0; k < nb_mcu; k++) comp_of[k] = J->ncomp == 1 ? 0 : (k < nb_mcu - 2 ? 0 : k - (nb_mcu - 3));
+    for (int k = 0; k < nb_mcu; k++)
+        comp_of[k] = J->ncomp == 1 ? 0 : J->ncomp == 4 ? k : (k < nb_mcu - 2 ? 0 : k - (nb_mcu - 3));
     long nmcu = (long)J->mcux * J->mcuy;
-    int pred[3] = {0, 0, 0};
+    int pred[4] = {0, 0, 0, 0};
     int16_t* blk = coefs;
     for (long m = 0; m < nmcu; m++) {
         if (J->ri && m > 0 && m % J->ri == 0) {
             if (restart(&b)) return 6;
-            pred[0] = pred[1] = pred[2] = 0;
+            pred[0] = pred[1] = pred[2] = pred[3] = 0;
         }
         for (int k = 0; k < nb_mcu; k++, blk += 64) {
             int c = comp_of[k];
@@ -449,7 +465,7 @@ long oracle_jpeg_num_blocks(const uint8_t* jpg, size_t len)
 {
     jinfo_t J;
     if (parse(jpg, len, &J)) return -1;
-    int nb = J.ncomp == 3 ? J.hs[0] * J.vs[0] + 2 : 1;
+    int nb = J.ncomp == 3 ? J.hs[0] * J.vs[0] + 2 : J.ncomp == 4 ? 4 : 1;
     return (long)J.mcux * J.mcuy * nb;
 }
 
@@ -458,9 +474,73 @@ int oracle_jpeg_coefs(const uint8_t* jpg, size_t len, int16_t* coefs, size_t nbl
     jinfo_t J;
     int rc = parse(jpg, len, &J);
     if (rc) return rc;
-    int nb = J.ncomp == 3 ? J.hs[0] * J.vs[0] + 2 : 1;
+    int nb = J.ncomp == 3 ? J.hs[0] * J.vs[0] + 2 : J.ncomp == 4 ? 4 : 1;
     if ((size_t)J.mcux * J.mcuy * nb > nblocks) return 4;
     return decode_scan(&J, coefs);
+}
+
+/* Sample planes of a 4-component file (every component 1x1): coefficients,
+ * then the ISLOW IDCT of each block into its plane (pw x ph, pitch pw). */
+static int cmyk_planes(const jinfo_t* J, uint8_t* plane[4], int* pitch)
+{
+    long nblk = (long)J->mcux * J->mcuy * 4;
+    int16_t* coefs = (int16_t*)malloc((size_t)nblk * 64 * sizeof(int16_t));
+    if (!coefs) return 2;
+    int rc = decode_scan(J, coefs);
+    if (rc) {
+        free(coefs);
+        return rc;
+    }
+    int pw = J->mcux * 8, ph = J->mcuy * 8;
+    *pitch = pw;
+    for (int c = 0; c < 4; c++) plane[c] = (uint8_t*)malloc((size_t)pw * ph);
+    const int16_t* blk = coefs;
+    for (int my = 0; my < J->mcuy; my++)
+        for (int mx = 0; mx < J->mcux; mx++)
+            for (int c = 0; c < 4; c++, blk += 64)
+                idct_islow(blk, J->qt[J->tq[c]], plane[c] + (size_t)my * 8 * pw + mx * 8, pw);
+    free(coefs);
+    return 0;
+}
+
+/* libjpeg's CMYK sample of a pixel (jdcolor.c ycck_cmyk_convert for YCCK:
+ * C, M, Y = range_limit[255 - (R, G, B of ycc_rgb_convert)], K as stored) */
+static void cmyk_px(const jinfo_t* J, uint8_t* const plane[4], size_t at, int* v)
+{
+    int y = plane[0][at], c1 = plane[1][at], c2 = plane[2][at];
+    v[3] = plane[3][at];
+    if (J->cmyk == 2) {
+        int cb = c1 - 128, cr = c2 - 128;
+        v[0] = clamp255(255 - (y + ((91881 * cr + 32768) >> 16)));
+        v[1] = clamp255(255 - (y + ((-22554 * cb + 32768 - 46802 * cr) >> 16)));
+        v[2] = clamp255(255 - (y + ((116130 * cb + 32768) >> 16)));
+    } else {
+        v[0] = y;
+        v[1] = c1;
+        v[2] = c2;
+    }
+}
+
+int oracle_jpeg_decode_cmyk(const uint8_t* jpg, size_t len, uint8_t* out, size_t cap, int* ow, int* oh)
+{
+    jinfo_t J;
+    int rc = parse(jpg, len, &J);
+    if (rc) return rc;
+    if (J.ncomp != 4) return 1;
+    *ow = J.w;
+    *oh = J.h;
+    if ((size_t)J.w * J.h * 4 > cap) return 4;
+    uint8_t* plane[4];
+    int pitch;
+    if ((rc = cmyk_planes(&J, plane, &pitch))) return rc;
+    for (int y = 0; y < J.h; y++)
+        for (int x = 0; x < J.w; x++) {
+            int v[4];
+            cmyk_px(&J, plane, (size_t)y * pitch + x, v);
+            for (int k = 0; k < 4; k++) out[((size_t)y * J.w + x) * 4 + k] = (uint8_t)v[k];
+        }
+    for (int c = 0; c < 4; c++) free(plane[c]);
+    return 0;
 }
 
 int oracle_jpeg_decode(const uint8_t* jpg, size_t len, int s, uint8_t* out, size_t cap, int* ow,
@@ -472,11 +552,29 @@ int oracle_jpeg_decode(const uint8_t* jpg, size_t len, int s, uint8_t* out, size
     if (s < 1) return 1;
     int W = J.w, H = J.h;
     int dw = (W + s - 1) / s, dh = (H + s - 1) / s;
-    int nch = J.ncomp == 3 ? 3 : 1;
+    int nch = J.ncomp == 1 ? 1 : 3;
     *ow = dw;
     *oh = dh;
     *ofmt = nch == 3 ? OR_BGR24 : OR_GRAY8;
     if ((size_t)dw * dh * nch > cap) return 4;
+    if (J.ncomp == 4) { /* to BGR: Pillow's read as Adobe-inverted CMYK, then cmyk2rgb */
+        uint8_t* plane[4];
+        int pitch;
+        if ((rc = cmyk_planes(&J, plane, &pitch))) return rc;
+        for (int y = 0; y < dh; y++)
+            for (int x = 0; x < dw; x++) {
+                int v[4];
+                cmyk_px(&J, plane, (size_t)(y * s) * pitch + x * s, v);
+                int nk = v[3]; /* 255 - (255 - K) */
+                uint8_t* o = out + ((size_t)y * dw + x) * 3;
+                for (int q = 0; q < 3; q++) {
+                    int t = (255 - v[q]) * nk + 128;
+                    o[2 - q] = clamp255(nk - (((t >> 8) + t) >> 8));
+                }
+            }
+        for (int c = 0; c < 4; c++) free(plane[c]);
+        return 0;
+    }
 
     int nb_mcu = J.ncomp == 3 ? J.hs[0] * J.vs[0] + 2 : 1;
     long nblk = (long)J.mcux * J.mcuy * nb_mcu;

@@ -48,6 +48,12 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
         d.nbmcu = d.nby + 2;
         d.mcux = (J.w + 8 * d.hs - 1) / (8 * d.hs);
         d.mcuy = (J.h + 8 * d.vs - 1) / (8 * d.vs);
+    } else if (J.ncomp == 4) {  // CMYK / YCCK: four 1x1 components (icx_decode.cpp dec_geometry)
+        d.hs = d.vs = 1;
+        d.nby = 1;
+        d.nbmcu = 4;
+        d.mcux = (J.w + 7) / 8;
+        d.mcuy = (J.h + 7) / 8;
     } else {
         d.hs = d.vs = 1;
         d.nby = d.nbmcu = 1;
@@ -188,11 +194,11 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
     }
     if (bad) return ICX_E_CORRUPT;
     // ---- DC prediction per component, reset every restart interval
-    int pred[3] = {0, 0, 0};
+    int pred[4] = {0, 0, 0, 0};
     for (int64_t b = 0; b < d.nblocks; b++) {
         const int64_t m = b / d.nbmcu;
         const int k = (int)(b % d.nbmcu);
-        if (k == 0 && d.ri && m % d.ri == 0) pred[0] = pred[1] = pred[2] = 0;
+        if (k == 0 && d.ri && m % d.ri == 0) pred[0] = pred[1] = pred[2] = pred[3] = 0;
         const int c = k < d.nby ? 0 : k - d.nby + 1;
         pred[c] += dc[b];
         coefs[(size_t)b * 64] = (int16_t)pred[c];
@@ -219,7 +225,7 @@ extern "C" long dec_emu_lean_check(const uint8_t* jpg, size_t len, int nstarts, 
     DecDesc d{};
     d.ncomp = J.ncomp;
     d.nby = J.ncomp == 3 ? J.hs[0] * J.vs[0] : 1;
-    d.nbmcu = J.ncomp == 3 ? d.nby + 2 : 1;
+    d.nbmcu = J.ncomp == 3 ? d.nby + 2 : J.ncomp == 4 ? 4 : 1;
     d.wmcu = dec_walk_mcu(J.ncomp, d.nbmcu, J.td, J.ta);
     d.ri = J.ri;
     const uint8_t* sc = jpg + J.scan_off;

@@ -32,6 +32,13 @@ def _make_inputs(d):
     Image.fromarray(np.ascontiguousarray(smooth(480, 640, 98)[:, :, ::-1])).save(pj, "JPEG", quality=95,
                                                                                 progressive=True)
     files.append(str(pj))
+    # CMYK and its YCCK twin (Adobe transform 2): decoded on the device now
+    from tests.golden.gen_cmyk_golden import cmyk_source, set_transform
+    cm = d / "cmyk.jpg"
+    Image.fromarray(cmyk_source(300, 410, 9), "CMYK").save(cm, "JPEG", quality=92)
+    files.append(str(cm))
+    (d / "ycck.jpg").write_bytes(set_transform(cm.read_bytes(), 2))
+    files.append(str(d / "ycck.jpg"))
     p = d / "pic.png"
     Image.fromarray(smooth(500, 700, 5)[:, :, ::-1]).save(p)
     files.append(str(p))
