@@ -43,8 +43,14 @@
 namespace icx {
 
 constexpr int DEC_SUB_BITS = 1024;   // bits per subsequence (one thread)
+// First-level look-up width.  9 bits since the symbol pairs (round 5): the
+// write pass's first levels (32-bit entries) then take 8 KiB of LDS, so with
+// its 32 KiB of block slots four workgroups still fit a CU; 0.8 % of q95
+// symbols have longer codes (0.3-0.5 % at 10 bits), and pairs must fit 9
+// bits.  Decode per 1000 / 200 4K q95 frames: 10 bits 80.4 / 18.9 ms, 9 bits
+// 78.0 / 18.5 ms (profiles/r5/ab_r5d_dec_lut.txt).
 #ifndef ICX_DEC_LUT_BITS
-#define ICX_DEC_LUT_BITS 10
+#define ICX_DEC_LUT_BITS 9
 #endif
 constexpr int DEC_LUT_BITS = ICX_DEC_LUT_BITS;  // Huffman fast-lookup width
 // k_dec_write workgroup size.  The pass is LDS-limited (a 128-B block slot

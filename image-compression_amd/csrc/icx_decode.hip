@@ -513,13 +513,12 @@ __device__ __forceinline__ void load_tables(const DecTab* T, DecLean* L);
 __device__ __forceinline__ void load_first_levels(const DecTab* T, uint32_t (*L1)[1 << DEC_LUT_BITS]);
 __device__ __forceinline__ uint32_t selector(const DecTab* T);
 
-// The state-only walks (k_dec_init, k_dec_sync) keep the first levels of the
-// image's tables in LDS (32-bit entries with the symbol pairs: 16 KiB) and
-// read the second levels of the rare long codes through the scalar cache, as
-// the write pass does (SplitLean); ICX_DEC_SYNC_SPLIT=0: both levels in LDS
-// (24 KiB).
+// The state-only walks (k_dec_init, k_dec_sync) keep both levels of the
+// image's tables in LDS (24 KiB at 9 bits); ICX_DEC_SYNC_SPLIT=1: only the
+// first levels there, the second levels of the long codes through the scalar
+// cache as in the write pass (SplitLean) - 1-3 % slower (ab_r5d_dec_lut.txt).
 #ifndef ICX_DEC_SYNC_SPLIT
-#define ICX_DEC_SYNC_SPLIT 1
+#define ICX_DEC_SYNC_SPLIT 0
 #endif
 #if ICX_DEC_SYNC_SPLIT
 #define DEC_WALK_TABLES                                                                   \

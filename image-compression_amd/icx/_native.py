@@ -37,13 +37,13 @@ EXPORTS = [
     "icx_pool_create", "icx_pool_destroy", "icx_pool_size", "icx_pool_context", "icx_pool_compress_jpg_batch",
     "icx_pool_decode_jpg_batch", "icx_pool_png_fit_batch",
     "icx_device_count", "icx_debug_self_check_image", "icx_debug_corrupt_constants", "icx_upload",
-    "icx_debug_decode_cmyk",
+    "icx_debug_decode_cmyk", "icx_stage_files", "icx_write_file",
 ]
 
 
 # entry points added within ABI version 4 (round 5); the rest are required
 LATER = {"icx_device_count", "icx_debug_self_check_image", "icx_debug_corrupt_constants", "icx_upload",
-         "icx_debug_decode_cmyk"}
+         "icx_debug_decode_cmyk", "icx_stage_files", "icx_write_file"}
 
 
 class NativeLibraryError(RuntimeError):
@@ -87,6 +87,15 @@ class PngFitJob(ctypes.Structure):
                 ("status", ctypes.c_int32)]
 
 
+class StageJob(ctypes.Structure):
+    """icx_stage_job (include/icx.h): one file of icx_stage_files."""
+    _fields_ = [("path", ctypes.c_char_p), ("min_size", ctypes.c_int64), ("min_width", ctypes.c_int32),
+                ("min_height", ctypes.c_int32), ("exists", ctypes.c_int32), ("size", ctypes.c_int64),
+                ("read_errno", ctypes.c_int32), ("jpeg_status", ctypes.c_int32), ("width", ctypes.c_int32),
+                ("height", ctypes.c_int32), ("ncomp", ctypes.c_int32), ("dev", ctypes.c_void_p),
+                ("status", ctypes.c_int)]
+
+
 class DecodeJob(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_size_t), ("subsampling", ctypes.c_int32),
                 ("out", ctypes.c_void_p), ("cap", ctypes.c_size_t),
@@ -119,6 +128,8 @@ def load():
         "icx_debug_corrupt_constants": (c.c_int, [c.c_int32, c.c_int32]),
         "icx_upload": (c.c_int, [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]),
         "icx_debug_decode_cmyk": (c.c_int, [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t]),
+        "icx_stage_files": (c.c_int, [c.c_void_p, P(StageJob), c.c_int32]),
+        "icx_write_file": (c.c_int, [c.c_char_p, c.c_void_p, c.c_size_t, P(c.c_int32)]),
         "icx_destroy": (None, [c.c_void_p]),
         "icx_status_string": (c.c_char_p, [c.c_int]),
         "icx_last_error": (c.c_char_p, [c.c_void_p]),

@@ -209,6 +209,17 @@ class DeviceImage:
         return out
 
     @classmethod
+    def adopt(cls, codec, ptr, shape) -> "DeviceImage":
+        """Take ownership of a buffer this codec's context allocated
+        (icx_device_alloc, e.g. a file icx_stage_files staged)."""
+        d = cls.__new__(cls)
+        d.codec = codec
+        d.shape = tuple(int(x) for x in shape)
+        d.nbytes = int(np.prod(d.shape))
+        d.ptr = ptr
+        return d
+
+    @classmethod
     def from_host(cls, codec, arr) -> "DeviceImage":
         a = np.ascontiguousarray(np.frombuffer(arr, np.uint8) if isinstance(arr, (bytes, bytearray)) else arr)
         d = cls(codec, a.shape)

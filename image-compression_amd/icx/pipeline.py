@@ -290,6 +290,44 @@ class DeviceReader:
         from .core import PinnedBuffer
         return PinnedBuffer.read_file(self.by_dev[self.devices[0]], path)
 
+    def pick(self, nbytes):
+        """The device with the fewest bytes assigned so far (nbytes more now)."""
+        with self.lock:
+            d = min(self.devices, key=lambda k: self.assigned[k])
+            self.assigned[d] += nbytes
+        return d
+
+    def stage(self, pairs, params, output_dir):
+        """processImage up to the decode for a chunk of (index, path) pairs,
+        staged natively (icx_stage_files: stat, read, header parse, dims gate
+        and the copy to HBM without the interpreter lock) on one device;
+        returns their _Items.  Files that are not device JPEGs go through
+        _prepare's host readers."""
+        from .core import DeviceImage
+        d = self.pick(0)
+        codec = self.by_dev[d]
+        n = len(pairs)
+        jobs = (N.StageJob * n)()
+        keep = []
+        for k, (_, path) in enumerate(pairs):
+            b = os.fsencode(path)
+            keep.append(b)
+            jobs[k].path = b
+            jobs[k].min_size = int(params.min_size_bytes)
+            jobs[k].min_width, jobs[k].min_height = int(params.min_width), int(params.min_height)
+        with _span("stage"):
+            st = codec._lib.icx_stage_files(codec._ctx, jobs, n)
+        if st != N.OK:
+            log.warning("icx_stage_files: %s", codec.last_error())
+        with self.lock:
+            self.assigned[d] += sum(int(jobs[k].size) for k in range(n) if jobs[k].dev)
+        out = []
+        for k, (i, path) in enumerate(pairs):
+            j = jobs[k]
+            dev = DeviceImage.adopt(codec, j.dev, (j.size,)) if j.dev else None
+            out.append(_staged_item(i, path, j, dev, params, output_dir, self))
+        return out
+
     def upload(self, buf):
         from .core import DeviceImage
         with self.lock:
@@ -302,6 +340,43 @@ class DeviceReader:
         finally:
             buf.free()
         return dev
+
+
+def _staged_item(index, path, job, dev, params: CompressionParams, output_dir, reader) -> "_Item":
+    """_prepare (ImageCompression.java:53-76) from a file icx_stage_files
+    staged: the same gates, results and log lines in the same order; a file
+    that is not a JPEG the device decoder takes goes to _prepare's readers."""
+    it = _Item(index, path)
+    if not job.exists:
+        log.warning("%s - 檔案不存在或不可讀，跳過", path)
+        it.report = CompressionReport(CompressionResult.SKIPPED_NOT_FOUND, 0, 0)
+        return it
+    it.original_size = int(job.size)
+    if it.original_size <= params.min_size_bytes:
+        log.info("%s - 跳過: 檔案大小 %s 未超過最小壓縮門檻 %s", path, format_file_size(it.original_size),
+                 format_file_size(params.min_size_bytes))
+        it.report = CompressionReport(CompressionResult.SKIPPED_CONDITION_NOT_MET, it.original_size,
+                                      it.original_size)
+        return it
+    if job.read_errno:
+        log.warning("%s - 處理圖片時發生 I/O 錯誤 (可能非支援格式或檔案損毀)", path)
+        it.report = CompressionReport(CompressionResult.FAILED_IO_ERROR, it.original_size, 0)
+        return it
+    w, h = int(job.width), int(job.height)
+    if dev is None:
+        if job.jpeg_status == N.OK and (w <= params.min_width or h <= params.min_height):
+            log.debug("%s - 跳過: 圖片尺寸 %dx%d 未超過最小壓縮門檻 %dx%d", path, w, h, params.min_width,
+                      params.min_height)
+            it.report = CompressionReport(CompressionResult.FAILED_UNSUPPORTED_FORMAT, it.original_size,
+                                          it.original_size)
+            return it
+        return _prepare(index, path, output_dir, params, reader)  # PNG, other formats, unsupported JPEG
+    s = subsampling_factor(w, h)
+    if s > 1:
+        log.debug("%s - 對圖片應用二次取樣，比率: %d", os.path.basename(str(path)), s)
+    it.decoded = DecodedImage(None, "jpeg", w, h, s, dev, int(job.ncomp))
+    it.output = os.path.join(str(output_dir), os.path.basename(str(path)))
+    return it
 
 
 def decode_image_with_subsampling(input_path, params: CompressionParams, file_size: int,
@@ -847,20 +922,35 @@ class CompressionBatch:
         # read-ahead bound: file bytes read (and uploaded) but not yet decoded
         inflight = threading.Semaphore(max(4 * self.group_size * max(1, len(self.codecs)), 256)) if per_dev else None
 
-        def prepare(i, p):
-            got = False
-            if inflight is not None:
-                while not got:
-                    got = inflight.acquire(timeout=0.5)
-                    if not got and time.perf_counter() > deadline:
-                        break
-            it = _prepare(i, p, self.save_dir, self.params, self.device_decode)
-            if got:
-                if it.decoded is not None and it.decoded.data is not None:
+        def slots(k):  # k read-ahead slots (fewer once the deadline has passed)
+            got = 0
+            while got < k:
+                if inflight.acquire(timeout=0.5):
+                    got += 1
+                elif time.perf_counter() > deadline:
+                    break
+            return got
+
+        def keep_slots(its, got):  # a slot per item until its decode, the rest back now
+            for it in its:
+                if got and it.decoded is not None and it.decoded.data is not None:
                     it.release = inflight.release  # after its decode (compress_jpeg_group)
-                else:
-                    inflight.release()
-            return it
+                    got -= 1
+            for _ in range(got):
+                inflight.release()
+
+        def prepare(i, p):
+            got = slots(1) if inflight is not None else 0
+            it = _prepare(i, p, self.save_dir, self.params, self.device_decode)
+            if inflight is not None:
+                keep_slots([it], got)
+            return [it]
+
+        def prepare_chunk(pairs):  # DeviceReader: native staging, one device per chunk
+            got = slots(len(pairs))
+            its = self.device_decode.stage(pairs, self.params, self.save_dir)
+            keep_slots(its, got)
+            return its
 
         done_items: List[_Item] = []
         lock = threading.Lock()
@@ -906,34 +996,39 @@ class CompressionBatch:
         pending_jpeg = {k: [] for k in keys}
         pending_png: List[_Item] = []
         with cf.ThreadPoolExecutor(self.decode_threads) as pool:
-            futs = [pool.submit(_in_batch, self.stage_times, prepare, i, p) for i, p in mine]
+            if per_dev and hasattr(self.codecs[0], "_lib") and hasattr(self.codecs[0]._lib, "icx_stage_files"):
+                step = max(1, min(8, self.group_size // 4))  # files per native staging call
+                futs = [pool.submit(_in_batch, self.stage_times, prepare_chunk, mine[k:k + step])
+                        for k in range(0, len(mine), step)]
+            else:
+                futs = [pool.submit(_in_batch, self.stage_times, prepare, i, p) for i, p in mine]
             try:
                 for f in cf.as_completed(futs, timeout=max(0.0, deadline - time.perf_counter())):
-                    it = f.result()
-                    with lock:
-                        done_items.append(it)
-                    if it.report is not None:
-                        continue
-                    it.mp = it.decoded.width * it.decoded.height / 1e6  # source pixels
-                    if not self.codecs:
-                        raise RuntimeError("no GPU codec available to compress decoded images")
-                    fmt = it.decoded.format_name
-                    if fmt in ("jpeg", "jpg"):
-                        d = dev_of(it)
-                        if d not in pending_jpeg:  # a host-decoded JPEG: any device's group
-                            d = min(keys, key=lambda k: len(pending_jpeg[k]))
-                        pj = pending_jpeg[d]
-                        pj.append(it)
-                        if len(pj) >= self.group_size:
-                            put("jpeg", list(pj), d)
-                            pj.clear()
-                    elif fmt == "png":
-                        pending_png.append(it)
-                        if len(pending_png) >= self.group_size:
-                            put("png", pending_png)
-                            pending_png = []
-                    else:
-                        put("other", [it])
+                    for it in f.result():
+                        with lock:
+                            done_items.append(it)
+                        if it.report is not None:
+                            continue
+                        it.mp = it.decoded.width * it.decoded.height / 1e6  # source pixels
+                        if not self.codecs:
+                            raise RuntimeError("no GPU codec available to compress decoded images")
+                        fmt = it.decoded.format_name
+                        if fmt in ("jpeg", "jpg"):
+                            d = dev_of(it)
+                            if d not in pending_jpeg:  # a host-decoded JPEG: any device's group
+                                d = min(keys, key=lambda k: len(pending_jpeg[k]))
+                            pj = pending_jpeg[d]
+                            pj.append(it)
+                            if len(pj) >= self.group_size:
+                                put("jpeg", list(pj), d)
+                                pj.clear()
+                        elif fmt == "png":
+                            pending_png.append(it)
+                            if len(pending_png) >= self.group_size:
+                                put("png", pending_png)
+                                pending_png = []
+                        else:
+                            put("other", [it])
             except cf.TimeoutError:
                 log.warning("執行緒池等待逾時，部分任務可能未完成。")
                 for f in futs:

@@ -350,6 +350,36 @@ icx_status icx_memcpy(icx_ctx* ctx, void* dst, const void* src, size_t bytes);
  * files path; the decode then reads device-resident files). */
 icx_status icx_upload(icx_ctx* ctx, void* dst, const void* src, size_t bytes);
 
+/* ------------------------------------------------------------- file staging */
+/* The reader side of the files -> files path (CompressionBatch.java:64-88,
+ * ImageCompression.java:53-76 / 113-126) without an interpreter lock: per
+ * job, exists && readable (stat + access), the file size, and - for files
+ * larger than min_size (-s) - one read into pinned memory, the JPEG header
+ * parse of icx_jpeg_info and, for a JPEG the device decoder takes whose
+ * dimensions pass the gate (w > min_width && h > min_height), one copy of the
+ * whole file to this context's device (icx_device_alloc'd: the caller frees
+ * `dev`, typically after icx_decode_jpg_batch read it).  Every decision
+ * (skips, format fallbacks) stays with the caller.  jpeg_status: -1 = not
+ * read or no JPEG SOI, else icx_jpeg_info's status.  read_errno: the read's
+ * errno (-> FAILED_IO_ERROR).  Returns ICX_OK unless the device failed. */
+typedef struct icx_stage_job {
+    const char* path;                /* in */
+    int64_t min_size;                /* in: -s */
+    int32_t min_width, min_height;   /* in: -w, -i */
+    int32_t exists;                  /* out */
+    int64_t size;
+    int32_t read_errno;
+    int32_t jpeg_status;
+    int32_t width, height, ncomp;
+    void* dev;
+    icx_status status;
+} icx_stage_job;
+icx_status icx_stage_files(icx_ctx* ctx, icx_stage_job* jobs, int32_t n);
+/* Write len bytes (host memory, e.g. a pinned output buffer) to a new or
+ * truncated file: ICX_OK, or ICX_E_DEVICE with *err = errno (an I/O error,
+ * FAILED_IO_ERROR). */
+icx_status icx_write_file(const char* path, const uint8_t* data, size_t len, int32_t* err);
+
 /* ------------------------------------------------------- parity / metrics */
 /* A 4-component (CMYK / YCCK) baseline file decoded to libjpeg's CMYK samples
  * (jdcolor.c: YCCK through ycck_cmyk_convert, CMYK as stored), 4 bytes a

@@ -617,3 +617,42 @@ def test_stage_times_are_per_batch(tmp_path):
         assert reps[k].success == 3
         assert reps[k].stages["write"]["calls"] == 3, reps[k].stages
         assert reps[k].stages["gpu_fit"]["calls"] == 1
+
+
+def test_staged_items_follow_process_image_gates(tmp_path, caplog):
+    """_staged_item (files staged natively by icx_stage_files) maps the staged
+    facts to the results _prepare gives, in ImageCompression.java:53-76's
+    order: not found, the -s size gate, an I/O error, the dims gate (a JPEG
+    the device decoder took but no larger than -w/-i: FAILED_UNSUPPORTED_
+    FORMAT, ImageCompression.java:69-72), other formats to the host readers,
+    and a staged device JPEG with its header's facts."""
+    from icx import _native as N
+    P = CompressionParams(0.25, 1000, 100, 60, 20000)
+
+    def job(**k):
+        j = N.StageJob()
+        j.exists, j.size, j.jpeg_status = 1, 5000, N.OK
+        j.width, j.height, j.ncomp = 300, 200, 3
+        for a, v in k.items():
+            setattr(j, a, v)
+        return j
+
+    png = tmp_path / "x.png"
+    Image.fromarray(noise(80, 120, 3)).save(png)
+    reader = lambda p: open(p, "rb").read()  # noqa: E731 (host bytes: _prepare's own readers)
+    R = CompressionResult
+    it = pipeline._staged_item(0, "gone.jpg", job(exists=0), None, P, tmp_path, reader)
+    assert it.report.result == R.SKIPPED_NOT_FOUND
+    it = pipeline._staged_item(0, "small.jpg", job(size=1000), None, P, tmp_path, reader)
+    assert it.report.result == R.SKIPPED_CONDITION_NOT_MET and it.report.original_size == 1000
+    it = pipeline._staged_item(0, "bad.jpg", job(read_errno=5), None, P, tmp_path, reader)
+    assert it.report.result == R.FAILED_IO_ERROR
+    it = pipeline._staged_item(0, "tiny.jpg", job(width=100), None, P, tmp_path, reader)
+    assert it.report.result == R.FAILED_UNSUPPORTED_FORMAT and it.report.compressed_size == 5000
+    it = pipeline._staged_item(3, str(png), job(jpeg_status=-1, size=png.stat().st_size), None, P, tmp_path, reader)
+    assert it.report is None and it.decoded.format_name == "png" and it.index == 3
+    dev = object()
+    it = pipeline._staged_item(4, "/in/a.jpg", job(width=9000, height=5000, ncomp=4), dev, P, tmp_path, reader)
+    assert it.report is None and it.decoded.data is dev and it.decoded.subsampling == 2
+    assert (it.decoded.width, it.decoded.height, it.decoded.ncomp) == (9000, 5000, 4)
+    assert it.output == os.path.join(str(tmp_path), "a.jpg") and it.original_size == 5000
