@@ -154,6 +154,12 @@ struct DevPool {
     // with one allocation per file); carved buffers always return to the free
     // lists, the slabs are released with the pool
     static constexpr size_t kSlab = (size_t)64 << 20, kSlabMax = (size_t)16 << 20;
+    // device buffers of 1-32 MiB (staged files, decoded 4K frames) likewise,
+    // 16 per slab: a first files -> files run staged ~500 files and decoded
+    // as many frames with one hipMalloc each (round 5)
+    static constexpr size_t kDevSlabMin = (size_t)1 << 20, kDevSlabMax = (size_t)32 << 20;
+    bool slabbed(size_t c) const { return host ? c <= kSlabMax : c >= kDevSlabMin && c <= kDevSlabMax; }
+    size_t slab_bytes(size_t c) const { return host ? (c > kSlab ? c : kSlab) : 16 * c; }
     std::vector<void*> slabs;
     std::set<void*> carved;
     ~DevPool()
@@ -163,7 +169,7 @@ struct DevPool {
                 if (!carved.count(p)) (void)(host ? hipHostFree(p) : hipFree(p));
         for (auto& kv : live_)
             if (!carved.count(kv.first)) (void)(host ? hipHostFree(kv.first) : hipFree(kv.first));
-        for (void* s : slabs) (void)hipHostFree(s);
+        for (void* s : slabs) (void)(host ? hipHostFree(s) : hipFree(s));
     }
 };
 

@@ -875,8 +875,8 @@ icx_status pool_alloc(icx_ctx* ctx, DevPool& P, size_t bytes, void** ptr)
     }
     // a new buffer (or slab): allocated outside every lock (a pinned
     // allocation takes milliseconds; other threads keep taking cached buffers)
-    const bool slab = P.host && c <= DevPool::kSlabMax;
-    const size_t bytes_new = slab ? std::max(c, DevPool::kSlab) : c;
+    const bool slab = P.slabbed(c);
+    const size_t bytes_new = slab ? P.slab_bytes(c) : c;
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = P.host ? hipHostMalloc(ptr, bytes_new, hipHostMallocPortable) : hipMalloc(ptr, bytes_new);
     if (e != hipSuccess) {

@@ -119,25 +119,4 @@ icx_status icx_stage_files(icx_ctx* ctx, icx_stage_job* jobs, int32_t n)
     return ret;
 }
 
-icx_status icx_write_file(const char* path, const uint8_t* data, size_t len, int32_t* err)
-{
-    if (err) *err = 0;
-    if (!path || (!data && len)) return ICX_E_NULL;
-    const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-    int e = fd < 0 ? errno : 0;
-    size_t put = 0;
-    while (!e && put < len) {
-        const ssize_t r = write(fd, data + put, len - put);
-        if (r < 0) {
-            if (errno == EINTR) continue;
-            e = errno;
-            break;
-        }
-        put += (size_t)r;
-    }
-    if (fd >= 0 && close(fd) != 0 && !e) e = errno;
-    if (err) *err = e;
-    return e ? ICX_E_DEVICE : ICX_OK;
-}
-
 }  // extern "C"

@@ -37,13 +37,13 @@ EXPORTS = [
     "icx_pool_create", "icx_pool_destroy", "icx_pool_size", "icx_pool_context", "icx_pool_compress_jpg_batch",
     "icx_pool_decode_jpg_batch", "icx_pool_png_fit_batch",
     "icx_device_count", "icx_debug_self_check_image", "icx_debug_corrupt_constants", "icx_upload",
-    "icx_debug_decode_cmyk", "icx_stage_files", "icx_write_file",
+    "icx_debug_decode_cmyk", "icx_stage_files",
 ]
 
 
 # entry points added within ABI version 4 (round 5); the rest are required
 LATER = {"icx_device_count", "icx_debug_self_check_image", "icx_debug_corrupt_constants", "icx_upload",
-         "icx_debug_decode_cmyk", "icx_stage_files", "icx_write_file"}
+         "icx_debug_decode_cmyk", "icx_stage_files"}
 
 
 class NativeLibraryError(RuntimeError):
@@ -129,7 +129,6 @@ def load():
         "icx_upload": (c.c_int, [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]),
         "icx_debug_decode_cmyk": (c.c_int, [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t]),
         "icx_stage_files": (c.c_int, [c.c_void_p, P(StageJob), c.c_int32]),
-        "icx_write_file": (c.c_int, [c.c_char_p, c.c_void_p, c.c_size_t, P(c.c_int32)]),
         "icx_destroy": (None, [c.c_void_p]),
         "icx_status_string": (c.c_char_p, [c.c_int]),
         "icx_last_error": (c.c_char_p, [c.c_void_p]),

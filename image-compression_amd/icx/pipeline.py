@@ -20,7 +20,8 @@ threads; each device group decodes them on the GPU (icx_decode_jpg_batch: the
 JDK reader's IJG 6b arithmetic plus source subsampling; a progressive file's
 scans are entropy-decoded by libicx on host threads, its IDCT and colour run
 on the device) straight into HBM tensors that the encoder then reads, so no
-decoded pixel crosses PCIe.  Other files (CMYK/YCCK or arithmetic JPEG, PNG,
+decoded pixel crosses PCIe (CMYK / YCCK JPEGs too, to BGR on the device).
+Other files (arithmetic or progressive-CMYK JPEG, PNG,
 GIF, BMP, ...) and JPEGs the device decoder rejects (corrupt, or a truncated
 progressive script the JDK would block-smooth) are decoded on the host with
 libjpeg-turbo / Pillow (6b-lineage ISLOW IDCT + h2v2 fancy upsampling for

@@ -375,10 +375,6 @@ typedef struct icx_stage_job {
     icx_status status;
 } icx_stage_job;
 icx_status icx_stage_files(icx_ctx* ctx, icx_stage_job* jobs, int32_t n);
-/* Write len bytes (host memory, e.g. a pinned output buffer) to a new or
- * truncated file: ICX_OK, or ICX_E_DEVICE with *err = errno (an I/O error,
- * FAILED_IO_ERROR). */
-icx_status icx_write_file(const char* path, const uint8_t* data, size_t len, int32_t* err);
 
 /* ------------------------------------------------------- parity / metrics */
 /* A 4-component (CMYK / YCCK) baseline file decoded to libjpeg's CMYK samples
