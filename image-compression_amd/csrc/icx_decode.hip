@@ -1300,6 +1300,9 @@ __global__ void __launch_bounds__(256) k_dec_color(const DecDesc* D, const DecSt
 // and converts the current one, so the HBM reads of a CU's workgroups stay in
 // flight through their barrier phases (one tile per workgroup left each
 // workgroup's loads exposed, then a few microseconds of compute with none).
+#ifndef ICX_DEC_LC_DWORD
+#define ICX_DEC_LC_DWORD 0
+#endif
 constexpr int LC_NM = 8;  // dec_lc_items
 constexpr int LC_W = 16 * LC_NM;      // output columns per tile
 constexpr int LC_CD = LC_W / 8 + 2;   // chroma dwords per staged row
@@ -1403,16 +1406,32 @@ __global__ void __launch_bounds__(256) k_dec_luma_color_420(const DecDesc* D, co
             int cv[2][2][4];                     // [comp][top|bottom row][column]
 #pragma unroll
             for (int comp = 0; comp < 2; comp++) {
+                int cs_t[4], cs_b[4];  // column sums for i0-1 .. i0+2
+#if ICX_DEC_LC_DWORD
+                // the 4 bytes li-1 .. li+2 of rows cy0+rp-1 .. +1: two aligned
+                // dword reads per row and a funnel shift, not four byte reads
+                const uint32_t* r0 = lc + comp * 10 * LC_CD + rp * LC_CD + ((li - 1) >> 2);
+                const uint32_t sh = (uint32_t)(li - 1) & 3u;
+                const uint32_t v0 = __builtin_amdgcn_alignbyte(r0[1], r0[0], sh);
+                const uint32_t v1 = __builtin_amdgcn_alignbyte(r0[LC_CD + 1], r0[LC_CD], sh);
+                const uint32_t v2 = __builtin_amdgcn_alignbyte(r0[2 * LC_CD + 1], r0[2 * LC_CD], sh);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int a = (int)((v1 >> (8 * k)) & 255u) * 3;
+                    cs_t[k] = a + (int)((v0 >> (8 * k)) & 255u);
+                    cs_b[k] = a + (int)((v2 >> (8 * k)) & 255u);
+                }
+#else
                 const uint8_t* c0 = (const uint8_t*)(lc + comp * 10 * LC_CD + rp * LC_CD);  // rows cy0+rp-1 .. +1
                 const uint8_t* c1 = c0 + LC_CD * 4;
                 const uint8_t* c2 = c1 + LC_CD * 4;
-                int cs_t[4], cs_b[4];  // column sums for i0-1 .. i0+2
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     const int a = c1[li - 1 + k] * 3;
                     cs_t[k] = a + c0[li - 1 + k];
                     cs_b[k] = a + c2[li - 1 + k];
                 }
+#endif
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     const int* cs = h ? cs_b : cs_t;
