@@ -80,7 +80,10 @@ constexpr uint32_t DEC_END = 0xFFFFFFFFu;
 // DEC_SUB | k and lut2[k][next 6 bits] holds (length << 8) | symbol.  0 = no
 // valid code.  Tables with more than DEC_NSUB long-code prefixes mark the rest
 // DEC_SLOW and decode those codes with the canonical maxcode loop (DecSlow).
-constexpr int DEC_NSUB = 16;
+#ifndef ICX_DEC_NSUB
+#define ICX_DEC_NSUB 16
+#endif
+constexpr int DEC_NSUB = ICX_DEC_NSUB;  // second-level tables per Huffman table (a power of two)
 constexpr uint32_t DEC_SUB = 0x2000u, DEC_SLOW = 0x4000u;
 struct DecHuff {
     uint16_t lut[1 << DEC_LUT_BITS];

@@ -60,7 +60,8 @@ def main(d, bench_json):
     per_unit = {SHORT[k.split("::")[-1].split("<")[0]]: v["hbm_bytes_per_unit"]
                 for k, v in out.items() if "hbm_bytes_per_unit" in v}
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of: bench.py " +
-                     " ".join(sys.argv[3:]), "kernels": out, "bytes_per_unit": per_unit}
+                     " ".join(sys.argv[3:]), "tree_commit": os.environ.get("ICX_COMMIT", "unknown"),
+           "kernels": out, "bytes_per_unit": per_unit}
     # the file bench.py reads (profiles/pmc_summary.json is a copy of it, not
     # of stdout): "bytes_per_unit" maps the bench's kernel names to HBM bytes
     json.dump(res, open(os.path.join(d, "pmc_summary.json"), "w"), indent=1)

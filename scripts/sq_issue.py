@@ -19,7 +19,9 @@ def run(d, frames, huff_blocks):
     with contextlib.redirect_stdout(io.StringIO()):
         acc = summarize(d)["libicx"]
     units = {"icx::k_fdct_color<true>": frames * 3840 * 2160, "icx::k_huff": huff_blocks}
-    out = {"source": "rocprofv3 SQ counters, bench.py headline workload", "units": {}, "per_unit": {}}
+    import os
+    out = {"source": "rocprofv3 SQ counters, bench.py headline workload",
+           "tree_commit": os.environ.get("ICX_COMMIT", "unknown"), "units": {}, "per_unit": {}}
     for k, u in units.items():
         v = acc[k]
         name = "fdct" if "fdct" in k else "huff"

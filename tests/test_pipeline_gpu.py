@@ -148,3 +148,35 @@ def test_config_c1_single_1080p_jpeg(codec, tmp_path):
     assert len(a) <= 524288 and calls and 4 <= calls[0] <= 5
     with Image.open(tmp_path / "gpu" / "c1.jpg") as im:
         assert im.size == (1920, 1080)
+
+
+def test_stage_files_facts_and_device_copies(codec, tmp_path):
+    """icx_stage_files (the native reader side of the batch): per file
+    exists/readable, size, header facts, the dims gate, and for a JPEG the
+    device decoder takes, a device copy equal to the file's bytes; small
+    files (<= -s) and non-JPEGs are not staged; a missing path is reported."""
+    import ctypes
+    from icx import _native as N
+    from icx.core import DeviceImage
+    big = tmp_path / "big.jpg"
+    Image.fromarray(np.ascontiguousarray(noise(300, 420, 1)[:, :, ::-1])).save(big, "JPEG", quality=95)
+    tiny = tmp_path / "tiny.jpg"
+    Image.fromarray(np.ascontiguousarray(noise(50, 400, 2)[:, :, ::-1])).save(tiny, "JPEG", quality=95)
+    png = tmp_path / "p.png"
+    Image.fromarray(noise(300, 420, 3)).save(png)
+    small = tmp_path / "small.jpg"
+    Image.fromarray(smooth(300, 420, 4)).save(small, "JPEG", quality=10)
+    paths = [big, tmp_path / "missing.jpg", tiny, png, small]
+    min_size = small.stat().st_size  # small.jpg sits exactly at -s: not read
+    jobs = (N.StageJob * len(paths))()
+    keep = [str(p).encode() for p in paths]
+    for j, b in zip(jobs, keep):
+        j.path, j.min_size, j.min_width, j.min_height = b, min_size, 100, 100
+    assert codec._lib.icx_stage_files(codec._ctx, jobs, len(paths)) == N.OK
+    j = jobs[0]
+    assert j.exists and j.size == big.stat().st_size and j.jpeg_status == N.OK and (j.width, j.height, j.ncomp) == (420, 300, 3)
+    assert j.dev and np.array_equal(DeviceImage.adopt(codec, j.dev, (j.size,)).numpy(), np.frombuffer(big.read_bytes(), np.uint8))
+    assert not jobs[1].exists and not jobs[1].dev
+    assert jobs[2].exists and jobs[2].jpeg_status == N.OK and jobs[2].height == 50 and not jobs[2].dev  # dims gate
+    assert jobs[3].exists and jobs[3].jpeg_status == -1 and not jobs[3].dev  # not a JPEG
+    assert jobs[4].exists and jobs[4].size == min_size and jobs[4].jpeg_status == -1 and not jobs[4].dev  # at -s
