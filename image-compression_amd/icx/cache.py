@@ -57,7 +57,7 @@ class SharedCache(LockedDict):
 
     Each rank keeps a local map (loaded from the same L2 file); an entry a
     rank learns is also appended to one log key in the process group's
-    key-value store (the torchrun rendezvous TCPStore: 16 bytes per entry,
+    key-value store (the torchrun rendezvous TCPStore: 28 bytes per entry,
     no collective, ranks never wait on each other), and refresh() - called
     by the pipeline before it probes a group's keys - applies the entries
     other ranks appended since the last refresh.  Every rank applies the log

@@ -656,3 +656,38 @@ def test_staged_items_follow_process_image_gates(tmp_path, caplog):
     assert it.report is None and it.decoded.data is dev and it.decoded.subsampling == 2
     assert (it.decoded.width, it.decoded.height, it.decoded.ncomp) == (9000, 5000, 4)
     assert it.output == os.path.join(str(tmp_path), "a.jpg") and it.original_size == 5000
+
+
+def test_shared_cache_log_semantics():
+    """SharedCache over a key-value store (the process group's store; a dict
+    stand-in here): puts append 28-byte records to one log key, refresh()
+    applies records appended since the last refresh in log order (later
+    writers win), quality stays float32-exact, and a refresh with nothing
+    new reads nothing."""
+    from icx.cache import SharedCache
+    from icx.core import LearnedParams, SimilarityKey
+
+    class Store:
+        def __init__(self):
+            self.kv = {}
+
+        def append(self, k, b):
+            self.kv[k] = self.kv.get(k, b"") + b
+
+        def check(self, keys):
+            return all(k in self.kv for k in keys)
+
+        def get(self, k):
+            return self.kv[k]
+
+    st = Store()
+    a, b = SharedCache(st), SharedCache(st)
+    assert a.refresh() == 0
+    k1, k2 = SimilarityKey(38, 21, 7), SimilarityKey(76, 43, 12)
+    a[k1] = LearnedParams(0.2421875, 1.0)
+    b[k2] = LearnedParams(0.1, 0.85)
+    b[k1] = LearnedParams(0.125, 0.7224999999999999)  # later writer
+    assert len(st.kv[SharedCache.LOG]) == 3 * SharedCache._REC.itemsize == 84
+    assert a.refresh() == 3 and b.refresh() == 3 and a.refresh() == 0
+    assert dict(a) == dict(b)
+    assert a[k1] == LearnedParams(0.125, 0.7224999999999999) and a[k2].quality == float(np.float32(0.1))
