@@ -998,26 +998,49 @@ __global__ void __launch_bounds__(1024) k_dec_dc(const DecDesc* D, const DecStat
 }
 
 // ------------------------------------------------------------------- IDCT
+// Two signed values shifted right by sh and saturated to 0..255, as bytes 0
+// and 1 (gfx950 v_ashr_pk_u8_i32: the shift, both clamps and the packing in
+// one instruction).
+__device__ __forceinline__ uint32_t ashr_pk_u8(int a, int b, int sh)
+{
+    uint32_t r;
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(sh));
+    return r;
+}
+// bytes 0, 1 of lo and of hi as one dword
+__device__ __forceinline__ uint32_t pk16(uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x05040100u); }
+
 #define CONST_BITS 13
 #define PASS1_BITS 2
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
 
+// Products of the IDCT: v_mul_i32_i24 (full rate) when the data operand is
+// known to fit 24 signed bits - then its low 32 bits equal the 32-bit
+// product's - else v_mul_lo_u32 (a quarter-rate instruction).
+template <bool M24>
+__device__ __forceinline__ int32_t imul(int32_t a, int32_t c)
+{
+    return M24 ? __mul24(a, c) : a * c;
+}
+
 // One 1-D pass of jpeg_idct_islow (jidctint.c, IJG 6b); d[0..7] in place.
-template <int SH>
+// M24: every data operand of a product is a sum of at most four inputs, so
+// inputs below 2^21 in magnitude keep them inside 24 bits.
+template <int SH, bool M24>
 __device__ __forceinline__ void idct8(int32_t* v)
 {
     int32_t z2 = v[2], z3 = v[6];
-    int32_t z1 = (z2 + z3) * 4433;                   // FIX_0_541196100
-    const int32_t t2 = z1 + z3 * (-15137);           // FIX_1_847759065
-    const int32_t t3 = z1 + z2 * 6270;               // FIX_0_765366865
+    int32_t z1 = imul<M24>(z2 + z3, 4433);                   // FIX_0_541196100
+    const int32_t t2 = z1 + imul<M24>(z3, -15137);           // FIX_1_847759065
+    const int32_t t3 = z1 + imul<M24>(z2, 6270);             // FIX_0_765366865
     const int32_t t0 = (v[0] + v[4]) << CONST_BITS;
     const int32_t t1 = (v[0] - v[4]) << CONST_BITS;
     const int32_t t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
     int32_t o0 = v[7], o1 = v[5], o2 = v[3], o3 = v[1];
     int32_t q1 = o0 + o3, q2 = o1 + o2, q3 = o0 + o2, q4 = o1 + o3;
-    const int32_t z5 = (q3 + q4) * 9633;             // FIX_1_175875602
-    o0 *= 2446; o1 *= 16819; o2 *= 25172; o3 *= 12299;
-    q1 *= -7373; q2 *= -20995; q3 *= -16069; q4 *= -3196;
+    const int32_t z5 = imul<M24>(q3 + q4, 9633);             // FIX_1_175875602
+    o0 = imul<M24>(o0, 2446); o1 = imul<M24>(o1, 16819); o2 = imul<M24>(o2, 25172); o3 = imul<M24>(o3, 12299);
+    q1 = imul<M24>(q1, -7373); q2 = imul<M24>(q2, -20995); q3 = imul<M24>(q3, -16069); q4 = imul<M24>(q4, -3196);
     q3 += z5; q4 += z5;
     o0 += q1 + q3; o1 += q2 + q4; o2 += q2 + q3; o3 += q1 + q4;
     v[0] = DESCALE(t10 + o3, SH);
@@ -1030,11 +1053,13 @@ __device__ __forceinline__ void idct8(int32_t* v)
     v[4] = DESCALE(t13 - o0, SH);
 }
 
-// IDCT_range_limit(cinfo)[x & RANGE_MASK] (jdmaster.c prepare_range_limit_table)
+// IDCT_range_limit(cinfo)[x & RANGE_MASK] (jdmaster.c prepare_range_limit_table):
+// the table maps the low 10 bits, read as a signed value s, to clamp(s + 128)
 __device__ __forceinline__ uint32_t idct_limit(int32_t v)
 {
-    const int x = v & 1023;
-    return x < 128 ? (uint32_t)(x + 128) : x < 512 ? 255u : x < 896 ? 0u : (uint32_t)(x - 896);
+    const int s = (int)((uint32_t)v << 22) >> 22;
+    const int x = s + 128;
+    return (uint32_t)(x < 0 ? 0 : x > 255 ? 255 : x);
 }
 
 // jpeg_idct_islow of one block by 8 threads (thread r owns coefficient row r,
@@ -1057,11 +1082,24 @@ __device__ __forceinline__ uint2 idct_row_of(const uint4& q, int32_t dc, const u
 #pragma unroll
         for (int c = 0; c < 8; c++) ws[r * 9 + c] = v[c];
     }
+    // pass 1 runs on 24-bit products when every dequantised value of the
+    // wave's blocks is below 2^21 in magnitude (a block's 8 threads are lanes
+    // of one wave; any real image's are below 2^14); pass 2 always can: its
+    // inputs are 32-bit values shifted right by 11, below 2^20
+    uint32_t acc = 0;
+    if (real) {
+#pragma unroll
+        for (int c = 0; c < 8; c++) acc |= (uint32_t)(v[c] + (1 << 21));
+    }
+    const bool m24 = __all(acc < (1u << 22));
     __syncthreads();
     if (real) {  // pass 1: column r
 #pragma unroll
         for (int k = 0; k < 8; k++) v[k] = ws[k * 9 + r];
-        idct8<CONST_BITS - PASS1_BITS>(v);
+        if (m24)
+            idct8<CONST_BITS - PASS1_BITS, true>(v);
+        else
+            idct8<CONST_BITS - PASS1_BITS, false>(v);
 #pragma unroll
         for (int k = 0; k < 8; k++) ws[k * 9 + r] = v[k];
     }
@@ -1070,12 +1108,13 @@ __device__ __forceinline__ uint2 idct_row_of(const uint4& q, int32_t dc, const u
     if (real) {  // pass 2: row r
 #pragma unroll
         for (int c = 0; c < 8; c++) v[c] = ws[r * 9 + c];
-        idct8<CONST_BITS + PASS1_BITS + 3>(v);
+        idct8<CONST_BITS + PASS1_BITS + 3, true>(v);
+        // idct_limit: clamp(sext10(v) + 128), two samples per ashr_pk
+        int x[8];
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-            lo |= idct_limit(v[c]) << (8 * c);
-            hi |= idct_limit(v[c + 4]) << (8 * c);
-        }
+        for (int c = 0; c < 8; c++) x[c] = ((int)((uint32_t)v[c] << 22) >> 22) + 128;
+        lo = pk16(ashr_pk_u8(x[0], x[1], 0), ashr_pk_u8(x[2], x[3], 0));
+        hi = pk16(ashr_pk_u8(x[4], x[5], 0), ashr_pk_u8(x[6], x[7], 0));
     }
     return make_uint2(lo, hi);
 }
@@ -1206,6 +1245,32 @@ __device__ __forceinline__ int chroma_at(const DecDesc& d, const uint8_t* P, int
 
 __device__ __forceinline__ uint8_t clamp255(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
 
+// a * k + c on v_mad_i32_i24 (full rate), a and k within 24 signed bits.
+// Inline asm: with the operands' ranges known the compiler turns __mul24 back
+// into v_mul_lo_u32 / v_mad_u64_u32, quarter-rate instructions.
+__device__ __forceinline__ int mad24(int a, int k, int c)
+{
+    int r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(k), "v"(c));
+    return r;
+}
+
+// ycc_rgb_convert (jdcolor.c, SCALEBITS 16) of one pixel, cb / cr already
+// less 128: y + ((k * c + ONE_HALF) >> 16) computed as ((y << 16) + ONE_HALF
+// + k * c) >> 16 (y << 16 is a multiple of 2^16; |c| <= 128, |k| < 2^17)
+struct Bgr {
+    uint32_t b, g, r;
+};
+__device__ __forceinline__ Bgr ycc_bgr(int yy, int cb, int cr)
+{
+    const int y16 = (yy << 16) + 32768;
+    Bgr o;
+    o.b = clamp255(mad24(cb, 116130, y16) >> 16);
+    o.g = clamp255(mad24(cr, -46802, mad24(cb, -22554, y16)) >> 16);
+    o.r = clamp255(mad24(cr, 91881, y16) >> 16);
+    return o;
+}
+
 // Thread per 4 output pixels of one output row; one image per workgroup.
 __global__ void __launch_bounds__(256) k_dec_color(const DecDesc* D, const DecState* S, Plan p)
 {
@@ -1272,10 +1337,10 @@ __global__ void __launch_bounds__(256) k_dec_color(const DecDesc* D, const DecSt
             px[3 * k + 2] = (uint8_t)yy;
             continue;
         }
-        // ycc_rgb_convert (jdcolor.c), SCALEBITS 16
-        px[3 * k + 0] = clamp255(yy + ((116130 * cb + 32768) >> 16));
-        px[3 * k + 1] = clamp255(yy + ((-22554 * cb + 32768 - 46802 * cr) >> 16));
-        px[3 * k + 2] = clamp255(yy + ((91881 * cr + 32768) >> 16));
+        const Bgr c = ycc_bgr(yy, cb, cr);
+        px[3 * k + 0] = (uint8_t)c.b;
+        px[3 * k + 1] = (uint8_t)c.g;
+        px[3 * k + 2] = (uint8_t)c.r;
     }
     uint8_t* o = orow + x0 * 3;
     if (n == 4 && (((uintptr_t)o) & 3) == 0) {
@@ -1346,7 +1411,8 @@ __device__ __forceinline__ void lc_fetch(const LcImg& g, int item, int t, LcLoad
         rr = rr < 0 ? 0 : rr > g.ch - 1 ? g.ch - 1 : rr;
         int dw = (cx0 >> 2) - 1 + q;
         dw = dw < 0 ? 0 : dw > g.pwd - 1 ? g.pwd - 1 : dw;  // clamped dwords hold only unused columns
-        L.c[h] = ((const ICX_GLOBAL uint32_t*)(g.plane[comp] + (int64_t)rr * g.pitch[comp]))[dw];
+        const ICX_GLOBAL uint32_t* row = (const ICX_GLOBAL uint32_t*)(g.plane[comp] + (int64_t)rr * g.pitch[comp]);
+        L.c[h] = row[dw];
     }
 }
 
@@ -1396,14 +1462,30 @@ __global__ void __launch_bounds__(256) k_dec_luma_color_420(const DecDesc* D, co
             *(uint2*)&ly[(k >> 1) * 8 + r][(lb >> 2) * 4 + (k & 1) * 2] = row;
         }
         __syncthreads();
+        {
+            // the edge columns replicated (h2v2_fancy_upsample's first / last
+            // column: c * 4 = c * 3 + the column itself), so the colour pass
+            // below has no edge cases: column -1 := column 0 (local bytes 3 <-
+            // 4), column cw := column cw - 1; tile-uniform, so the extra
+            // barrier runs in edge tiles only
+            const int cx0 = mx0 * 8, lr = cw - cx0 + 4;  // local byte of column cw
+            const bool left = cx0 == 0, right = lr < 4 * LC_CD;
+            if (left || right) {
+                if (t < 20) {  // one staged row (2 planes x 10 rows) per thread
+                    uint8_t* row = (uint8_t*)(lc + t * LC_CD);
+                    if (left) row[3] = row[4];
+                    if (right) row[lr] = row[lr - 1];
+                }
+                __syncthreads();
+            }
+        }
         const int rp = t >> 5, xt = 4 * (t & 31);  // chroma row cy0 + rp -> output rows 2rp, 2rp+1; columns xt..xt+3
         const int x0 = mx0 * 16;
         const int n = ow - x0 - xt;
         const int y0 = my * 16 + 2 * rp;
         if (n > 0 && y0 < oh) {
-            const int i0 = (x0 + xt) >> 1;       // chroma columns i0, i0 + 1
             const int li = (xt >> 1) + 4;        // local byte of i0
-            int cv[2][2][4];                     // [comp][top|bottom row][column]
+            int cv[2][2][4];                     // [comp][top|bottom row][column]: upsampled value - 128
 #pragma unroll
             for (int comp = 0; comp < 2; comp++) {
                 int cs_t[4], cs_b[4];  // column sums for i0-1 .. i0+2
@@ -1432,14 +1514,17 @@ __global__ void __launch_bounds__(256) k_dec_luma_color_420(const DecDesc* D, co
                     cs_b[k] = a + c2[li - 1 + k];
                 }
 #endif
+                // chroma column i0 + u -> output columns 2u (with column i0+u-1)
+                // and 2u + 1 (with i0+u+1); the staged edge columns are
+                // replicas, and (s + 8 - 2048) >> 4 = ((s + 8) >> 4) - 128
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     const int* cs = h ? cs_b : cs_t;
 #pragma unroll
-                    for (int u = 0; u < 2; u++) {  // chroma column i0 + u -> output columns 2u, 2u + 1
-                        const int i = i0 + u, c = cs[1 + u];
-                        cv[comp][h][2 * u] = i == 0 ? (c * 4 + 8) >> 4 : (c * 3 + cs[u] + 8) >> 4;
-                        cv[comp][h][2 * u + 1] = i == cw - 1 ? (c * 4 + 7) >> 4 : (c * 3 + cs[2 + u] + 7) >> 4;
+                    for (int u = 0; u < 2; u++) {
+                        const int a = cs[1 + u] * 3;
+                        cv[comp][h][2 * u] = (a + cs[u] - 2040) >> 4;
+                        cv[comp][h][2 * u + 1] = (a + cs[2 + u] - 2041) >> 4;
                     }
                 }
             }
@@ -1449,19 +1534,20 @@ __global__ void __launch_bounds__(256) k_dec_luma_color_420(const DecDesc* D, co
             for (int h = 0; h < 2; h++) {  // unrolled: cv stays in registers
                 if (h >= rows) break;
                 const uint32_t yq = ly[2 * rp + h][xt >> 2];
-                uint32_t w[3] = {0, 0, 0};
+                int cb_[4], cg_[4], cr_[4];  // (y << 16) + ONE_HALF + products (ycc_bgr before the shift)
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    const int yy = (yq >> (8 * k)) & 255;
-                    const int cb = cv[0][h][k] - 128, cr = cv[1][h][k] - 128;
-                    const uint32_t B = clamp255(yy + ((116130 * cb + 32768) >> 16));
-                    const uint32_t G = clamp255(yy + ((-22554 * cb + 32768 - 46802 * cr) >> 16));
-                    const uint32_t R = clamp255(yy + ((91881 * cr + 32768) >> 16));
-                    const int o = 3 * k;  // byte offset inside the 12-byte group
-                    w[o >> 2] |= B << (8 * (o & 3));
-                    w[(o + 1) >> 2] |= G << (8 * ((o + 1) & 3));
-                    w[(o + 2) >> 2] |= R << (8 * ((o + 2) & 3));
+                    // (y << 16) + 32768 from byte k of yq in one v_perm_b32
+                    const int y16 = (int)__builtin_amdgcn_perm(0x8000u, yq, 0x0C000504u | ((uint32_t)k << 16));
+                    const int cb = cv[0][h][k], cr = cv[1][h][k];
+                    cb_[k] = mad24(cb, 116130, y16);
+                    cg_[k] = mad24(cr, -46802, mad24(cb, -22554, y16));
+                    cr_[k] = mad24(cr, 91881, y16);
                 }
+                // B0 G0 R0 B1 | G1 R1 B2 G2 | R2 B3 G3 R3: >> 16, clamp, pack
+                const uint32_t w[3] = {pk16(ashr_pk_u8(cb_[0], cg_[0], 16), ashr_pk_u8(cr_[0], cb_[1], 16)),
+                                       pk16(ashr_pk_u8(cg_[1], cr_[1], 16), ashr_pk_u8(cb_[2], cg_[2], 16)),
+                                       pk16(ashr_pk_u8(cr_[2], cb_[3], 16), ashr_pk_u8(cg_[3], cr_[3], 16))};
                 ICX_GLOBAL uint8_t* o = out + (int64_t)(y0 + h) * ostride + (int64_t)(x0 + xt) * 3;
                 if (m == 4 && (((uintptr_t)o) & 3) == 0) {
                     *(ICX_GLOBAL uint3*)o = make_uint3(w[0], w[1], w[2]);
