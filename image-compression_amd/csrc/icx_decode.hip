@@ -1368,6 +1368,9 @@ __global__ void __launch_bounds__(256) k_dec_color(const DecDesc* D, const DecSt
 #ifndef ICX_DEC_LC_DWORD
 #define ICX_DEC_LC_DWORD 0
 #endif
+#ifndef ICX_DEC_LC_WAVES
+#define ICX_DEC_LC_WAVES 1
+#endif
 constexpr int LC_NM = 8;  // dec_lc_items
 constexpr int LC_W = 16 * LC_NM;      // output columns per tile
 constexpr int LC_CD = LC_W / 8 + 2;   // chroma dwords per staged row
@@ -1416,7 +1419,7 @@ __device__ __forceinline__ void lc_fetch(const LcImg& g, int item, int t, LcLoad
     }
 }
 
-__global__ void __launch_bounds__(256) k_dec_luma_color_420(const DecDesc* D, const DecState* S, Plan p)
+__global__ void __launch_bounds__(256, ICX_DEC_LC_WAVES) k_dec_luma_color_420(const DecDesc* D, const DecState* S, Plan p)
 {
     __shared__ int32_t ws[32][8 * 9];
     // luma tile rows padded to 36 dwords: the IDCT's 8-byte row stores (lanes
