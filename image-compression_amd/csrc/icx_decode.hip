@@ -514,9 +514,10 @@ __device__ __forceinline__ void load_first_levels(const DecTab* T, uint32_t (*L1
 __device__ __forceinline__ uint32_t selector(const DecTab* T);
 
 // The state-only walks (k_dec_init, k_dec_sync) keep both levels of the
-// image's tables in LDS (24 KiB at 9 bits); ICX_DEC_SYNC_SPLIT=1: only the
-// first levels there, the second levels of the long codes through the scalar
-// cache as in the write pass (SplitLean) - 1-3 % slower (ab_r5d_dec_lut.txt).
+// image's tables in LDS (16 KiB at 9 bits with 8 second-level tables);
+// ICX_DEC_SYNC_SPLIT=1: only the first levels there, the second levels of the
+// long codes through the scalar cache as in the write pass (SplitLean) - 1-3 %
+// slower (ab_r5d_dec_lut.txt).
 #ifndef ICX_DEC_SYNC_SPLIT
 #define ICX_DEC_SYNC_SPLIT 0
 #endif
