@@ -7,6 +7,19 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pipe_q
+# k_huff's per-dispatch fetch: which launches carry the excess (pmc_summary
+# r5p: 10 of 12 fetch 0.965x the algorithmic bytes, two 1.39x)
+R=$(pwd)
+( cd /tmp && timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_q" -o run \
+    -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --e2e 0 --host-io-frames 0 > "$R/gpurun_out/pmc_q.out" 2>&1 ) \
+    || { echo "pmc failed"; tail -20 gpurun_out/pmc_q.out; exit 1; }
+for f in $(find gpurun_out/pmc_q -name '*counter_collection.csv'); do
+  { head -1 "$f"; grep -E 'k_huff|k_fdct|k_scan|k_stuff' "$f" || true; } > gpurun_out/pmc_q_huff_dispatches.csv
+done
+for f in $(find gpurun_out/pmc_q -name '*kernel_trace.csv'); do
+  { head -1 "$f"; grep -E 'k_huff|k_fdct|k_scan|k_stuff|k_list' "$f" || true; } > gpurun_out/pmc_q_trace.csv
+done
+rm -rf gpurun_out/pmc_q
 run() {  # name env... -- args
   local name=$1; shift
   local envs=()
