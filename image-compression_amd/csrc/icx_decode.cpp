@@ -161,10 +161,14 @@ uint32_t pick_sub_bits(uint64_t total_bits)
     // 65536: 22.4 / 22.8 / 23.9 ms.  With the two-step walks (round 4 end,
     // ab_r4zf_dec_win_sub.txt / ab_r4zg_dec_sub.txt) 200 frames: 16384 /
     // 32768 / 65536 = 20.7 / 20.2 / 21.9 ms.  65536 while at least 2^19 of
-    // them remain, 32768 while 2^18 do; below that 16384, and shorter only
-    // when the batch would not give the chip ~64k threads.
+    // them remain, 32768 while 2^16 do (round 5: files -> files, two workers
+    // on one GPU, 64-frame calls: 32768 instead of 16384 gave 4105 / 3571
+    // files/s against 3880 / 3183, 65536 3075 / 2693 - one relaxation launch
+    // fewer per call, profiles/r5/pipeline/ab_r5q_pipeline.txt); below that
+    // 16384, and shorter only when the batch would not give the chip ~64k
+    // threads.
     uint32_t S = 65536;
-    if (total_bits / S < (1u << 19)) S = total_bits / 32768 >= (1u << 18) ? 32768 : 16384;
+    if (total_bits / S < (1u << 19)) S = total_bits / 32768 >= (1u << 16) ? 32768 : 16384;
     while (S > 2048 && total_bits / S < 65536) S /= 2;
     return S;
 }
