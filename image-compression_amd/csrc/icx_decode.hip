@@ -161,6 +161,20 @@ __global__ void __launch_bounds__(256) k_stage(const StageJob* J, Plan p)
 }
 
 // ------------------------------------------------------------------ unstuff
+// True when one of the 16 bytes or the byte before them is 0xFF: only then can
+// a byte of this thread be a stuffed zero, a marker or an RSTn code.
+__device__ __forceinline__ bool any_ff(const uint4& v, int prev)
+{
+    uint32_t m = 0;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t x = ~w[k];  // 0xFF bytes -> zero bytes
+        m |= (x - 0x01010101u) & ~x & 0x80808080u;
+    }
+    return m != 0 || prev == 0xFF;
+}
+
 // Byte classes of 16 stuffed bytes as 16-bit masks (bit k = byte k), SWAR on
 // the four dwords: 0xFF bytes, 0x00 bytes, RSTn codes (0xD0..0xD7).
 __device__ __forceinline__ uint32_t zero_bytes4(uint32_t x)  // bit j: byte j of x is 0
@@ -185,39 +199,6 @@ __device__ __forceinline__ ByteClass classify16(const uint4& v)
         c.r |= zero_bytes4((w[k] ^ 0xD0D0D0D0u) & 0xF8F8F8F8u) << (4 * k);
     }
     return c;
-}
-
-// Byte classes for the rule below without classifying every byte three ways:
-// the 0xFF mask exactly (SWAR), then the zero / RSTn classes only at the
-// bytes that follow a 0xFF (the only places the rule reads them), one loop
-// trip per such byte - usually none or one (ICX_DEC_UNSTUFF_LAZY=0: all 16
-// bytes classified three ways, classify16).
-#ifndef ICX_DEC_UNSTUFF_LAZY
-#define ICX_DEC_UNSTUFF_LAZY 0
-#endif
-__device__ __forceinline__ uint32_t ff_mask16(const uint4& v)
-{
-    return zero_bytes4(~v.x) | (zero_bytes4(~v.y) << 4) | (zero_bytes4(~v.z) << 8) | (zero_bytes4(~v.w) << 12);
-}
-__device__ __forceinline__ ByteClass classify16_after_ff(const uint4& v, uint32_t ff, int prev)
-{
-#if ICX_DEC_UNSTUFF_LAZY
-    ByteClass c{ff, 0, 0};
-    uint32_t m = ((ff << 1) | (prev == 0xFF ? 1u : 0u)) & 0xFFFFu;
-    while (m) {
-        const int k = __builtin_ctz(m);
-        m &= m - 1;
-        const uint32_t dw = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
-        const uint32_t b = (dw >> (8 * (k & 3))) & 255u;
-        c.z |= (b == 0 ? 1u : 0u) << k;
-        c.r |= ((b & 0xF8u) == 0xD0u ? 1u : 0u) << k;
-    }
-    return c;
-#else
-    (void)ff;
-    (void)prev;
-    return classify16(v);
-#endif
 }
 
 // The unstuffing rule (dec_unstuff_rule) over 16 bytes at once, given the byte
@@ -277,11 +258,10 @@ __global__ void __launch_bounds__(256) k_unstuff_count(const DecDesc* D, DecStat
         const int pv = base > 0 ? prev[u] : 0;
         uint32_t c = 0;
         if (base < len) {
-            const uint32_t ff = ff_mask16(q[u].v);
-            if (ff == 0 && pv != 0xFF) {
+            if (!any_ff(q[u].v, pv)) {
                 c = (uint32_t)min((int64_t)16, len - base);
-            } else {  // the rule over the 16 bytes as masks
-                const Unstuff16 x = unstuff16(classify16_after_ff(q[u].v, ff, pv), pv, q[u].next);
+            } else {  // branch-free rule over the 16 bytes (SWAR masks)
+                const Unstuff16 x = unstuff16(classify16(q[u].v), pv, q[u].next);
                 const int64_t rem = len - base;  // bytes of this thread below scan_len
                 const uint32_t valid = rem >= 16 ? 0xFFFFu : (1u << rem) - 1;
                 const uint32_t nr = (uint32_t)__popc(x.rst & valid);
@@ -433,10 +413,9 @@ __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const
         if (base < end) {
             v = q[u].v;
             const int prev_b = base > 0 ? prev[u] : 0;
-            const uint32_t ff = ff_mask16(v);
-            plain = base + 16 <= end && ff == 0 && prev_b != 0xFF;
+            plain = base + 16 <= end && !any_ff(v, prev_b);
             if (!plain) {  // the rule over the 16 bytes as masks (bytes from `end` on drop out)
-                const Unstuff16 x = unstuff16(classify16_after_ff(v, ff, prev_b), prev_b, q[u].next);
+                const Unstuff16 x = unstuff16(classify16(v), prev_b, q[u].next);
                 const int64_t rem = end - base;
                 const uint32_t valid = rem >= 16 ? 0xFFFFu : (1u << rem) - 1;
                 keep = x.keep & valid;
