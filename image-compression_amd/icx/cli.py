@@ -3,12 +3,15 @@ defaults, plus GPU placement flags.
 
   python -m icx -f list.txt -o outdir [-q 0.25] [-s 1048576] [-w 1920] [-i 1920]
                 [-t 1048576] [--timeOut 24] [--cache-db image-compression-cache]
-                [--devices 0,1] [--workers-per-device 2] [--group 64] [--decode-threads N]
+                [--devices 0,1] [--workers-per-device 3] [--group 64] [--decode-threads N]
 
 Each device gets --workers-per-device GPU worker threads, each with its own
 libicx context, so one group's host work (file bytes to the decoder, results
-to the writers) overlaps another group's kernels: files -> files JPEG on one
-MI355X, 1830 files/s with one worker, 2422 with two.
+to the writers) overlaps another group's kernels, and one context's
+latency-bound relaxation launches overlap another's bulk kernels: files ->
+files JPEG on one MI355X (round 5, warm cache, three runs each) 3611-4009
+files/s with two workers, 3952-4178 with three (the default), 4011-4584 with
+four, whose learning runs are 10 % slower.
 Multi-GPU: by default one process drives every visible GPU (worker threads
 per device sharing one L1 cache, the reference's one ConcurrentHashMap); or
 one process per GPU under torchrun (RANK/WORLD_SIZE/LOCAL_RANK): the file
@@ -41,7 +44,7 @@ def build_parser():
     p.add_argument("--cache-db", default="image-compression-cache")
     p.add_argument("--devices", default=None,
                    help="GPU ordinals for this process, e.g. 0,1 (default: every visible GPU; LOCAL_RANK under torchrun)")
-    p.add_argument("--workers-per-device", type=int, default=2,
+    p.add_argument("--workers-per-device", type=int, default=3,
                    help="GPU worker threads (libicx contexts) per device")
     p.add_argument("--group", type=int, default=64, help="JPEGs (or PNGs) per device batch")
     p.add_argument("--decode-threads", type=int, default=None)

@@ -38,7 +38,8 @@ def main():
     ap.add_argument("--group", type=int, default=64)
     ap.add_argument("--dir", default=None)
     ap.add_argument("--png", type=int, default=0, help="4K PNG files added to the list (configs[4] mix)")
-    ap.add_argument("--devices", default="0", help="GPUs driven by this process (one worker each)")
+    ap.add_argument("--devices", default="0,0,0",
+                    help="GPU of each worker (one libicx context each); default: the CLI's, three workers on GPU 0")
     ap.add_argument("--procs", type=int, default=1, help="processes sharing the list (warm-cache run only)")
     ap.add_argument("--decode-threads", type=int, default=0, help="host reader threads (0: every usable core)")
     a = ap.parse_args()

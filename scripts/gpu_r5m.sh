@@ -36,7 +36,7 @@ python3 -c "
 import json; d=json.load(open('gpurun_out/dec_timeline_$T.json'))
 for c in d['calls']:
     print(c['span_ms'], 'busy', c['busy_union_ms'], {k: (v['ms'], v['alone_ms']) for k, v in c['kernels_ms'].items()})"
-for dv in ${PIPE_DEVS:-0,0 0 0,0,0}; do
+for dv in ${PIPE_DEVS:-0,0,0 0,0 0}; do
   timeout -k 10 300 python scripts/bench_pipeline.py --files 1000 --group 64 --devices $dv > gpurun_out/pipeline_${T}_d${dv//,/}.json 2>> gpurun_out/pipeline_$T.err \
       || { echo "pipeline $dv failed"; tail -20 gpurun_out/pipeline_$T.err; exit 1; }
   python3 -c "
