@@ -1073,17 +1073,25 @@ ICX_HD DecLeanWriter<LeanPtr> dec_lean_writer(const DecDesc& d, LeanPtr H, const
 // count plus the difference at the checkpoint.  A re-walk from a corrected
 // entry state typically resynchronises within a few hundred bits, so relaunch
 // walks cost about one checkpoint interval instead of a whole subsequence.
+//
+// Checkpoint intervals (= write-pass pieces) per subsequence: 8 (intervals of
+// at least 2048 bits) below 65536-bit subsequences, DEC_CK_DIV from there.
+// 16 at 65536 bits (4096-bit intervals): 1000 frames 75.1 vs 75.7-76.6 ms per
+// call (write pass -0.7 ms: shorter pieces even out its lanes); at 200 frames
+// (32768 bits) 16 intervals of 2048 bits cost +0.3 ms, so the shorter
+// subsequences keep 8 (profiles/r5/ab_r5w_dec_ck.txt).
 #ifndef ICX_DEC_CK_DIV
-#define ICX_DEC_CK_DIV 8  // checkpoint intervals (= write-pass pieces) per subsequence
+#define ICX_DEC_CK_DIV 16
 #endif
 constexpr int DEC_CK_DIV = ICX_DEC_CK_DIV;
+static_assert(DEC_CK_DIV >= 8, "shorter subsequences use 8 intervals");
 constexpr int DEC_CK_MAX = DEC_CK_DIV - 1;
 constexpr uint64_t DEC_CK_NONE = ~0ull;
 constexpr uint64_t DEC_CK_STATE = (1ull << 48) - 1;
 ICX_HD uint32_t dec_ck_bits(uint32_t sub_bits)
 {
-    constexpr uint32_t floor_bits = 16384 / DEC_CK_DIV;
-    return sub_bits / DEC_CK_DIV > floor_bits ? sub_bits / DEC_CK_DIV : floor_bits;
+    if (sub_bits >= 65536) return sub_bits / DEC_CK_DIV;
+    return sub_bits / 8 > 2048 ? sub_bits / 8 : 2048;
 }
 ICX_HD int dec_ck_slots(uint32_t sub_bits)
 {
