@@ -137,7 +137,7 @@ int main(int argc, char** argv) {
     assert r.returncode == 0 and "bad=0" in r.stdout, (r.stdout[-500:], r.stderr[-3000:])
 
 
-@pytest.mark.parametrize("sub", [4096, 16384, 32768])
+@pytest.mark.parametrize("sub", [4096, 16384, 32768, 65536])  # 65536: 16 checkpoint intervals
 def test_emulated_checkpoint_early_exit(emu, oracle, sub):
     """Subsequences long enough to carry sync checkpoints (dec_sync_walk):
     re-walks stop where they meet their previous walk, and the coefficients
