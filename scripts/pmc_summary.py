@@ -34,6 +34,37 @@ def load(d, ctr):
     return vals
 
 
+def aggregate(out, kern):
+    """Bytes per unit of each bench kernel name over every icx:: kernel that
+    maps to it (k_fdct_color and k_fdct_gray are both "fdct"; icx_create's
+    self-check dispatches each on a 16x16 image, so a name's dispatches are
+    not all one kernel's).  The per-kernel entries keep their own bytes;
+    their unit ratios are dropped where a name has several kernels."""
+    groups = defaultdict(list)
+    for k in out:
+        short = SHORT.get(k.split("::")[-1].split("<")[0])
+        if short:
+            groups[short].append(k)
+    per_unit, info = {}, {}
+    for short, ks in groups.items():
+        if short not in kern or not kern[short].get("units"):
+            continue
+        hb = sum(out[k]["hbm_bytes"] for k in ks)
+        ku = kern[short]
+        per_unit[short] = hb / ku["units"]
+        info[short] = {"kernels": ks, "hbm_bytes": hb, "units": ku["units"], "hbm_bytes_per_unit": per_unit[short]}
+        if ku.get("algo_bytes"):
+            info[short]["algo_bytes_per_unit"] = ku["algo_bytes"] / ku["units"]
+            info[short]["traffic_over_algo"] = hb / ku["algo_bytes"]
+        if len(ks) > 1:
+            for k in ks:
+                for f in ("units", "bench_launches", "hbm_bytes_per_unit", "algo_bytes", "algo_bytes_per_unit",
+                          "traffic_over_algo"):
+                    out[k].pop(f, None)
+                out[k]["bench_kernel"] = short
+    return per_unit, info
+
+
 def main(d, bench_json):
     line = json.loads([l for l in open(bench_json) if l.startswith("{")][-1])
     kern = line["kernels"]
@@ -57,11 +88,10 @@ def main(d, bench_json):
                 e["algo_bytes_per_unit"] = ku["algo_bytes"] / ku["units"]
                 e["traffic_over_algo"] = (fb + wb) / ku["algo_bytes"]
         out[k] = e
-    per_unit = {SHORT[k.split("::")[-1].split("<")[0]]: v["hbm_bytes_per_unit"]
-                for k, v in out.items() if "hbm_bytes_per_unit" in v}
+    per_unit, info = aggregate(out, kern)
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of: bench.py " +
                      " ".join(sys.argv[3:]), "tree_commit": os.environ.get("ICX_COMMIT", "unknown"),
-           "kernels": out, "bytes_per_unit": per_unit}
+           "kernels": out, "bench_kernels": info, "bytes_per_unit": per_unit}
     # the file bench.py reads (profiles/pmc_summary.json is a copy of it, not
     # of stdout): "bytes_per_unit" maps the bench's kernel names to HBM bytes
     json.dump(res, open(os.path.join(d, "pmc_summary.json"), "w"), indent=1)
