@@ -183,7 +183,7 @@ def e2e_leg(codec, dev, frames, n_frames, steps, cpu_sample=0, threads=16, small
     if small and small < n_frames:
         line["at_small_batch"] = {k: v for k, v in _e2e_run(codec, dev, frames, small, steps, dist, world).items()
                                   if k in ("value", "frames", "ms_per_step", "decode_ms_per_step",
-                                           "encode_ms_per_step", "decode_mp_s")}
+                                           "encode_ms_per_step", "decode_mp_s", "decode_roofline")}
     if cpu_sample:
         srcs = _e2e_sources(codec, dev, frames, min(16, n_frames))[0]
         line["cpu_baseline"] = e2e_cpu_baseline([s.cpu().numpy().tobytes() for s in srcs], cpu_sample, threads)
@@ -237,6 +237,13 @@ def _e2e_run(codec, dev, frames, n_frames, steps, dist=None, world=1):
             "encode_ms_per_step": round(tf / steps * 1e3, 3),
             "decode_mp_s": round(mp * steps / td, 1),
             "mean_src_jpeg_bytes": int(np.mean(lens))}
+    # the decode against HBM on SURVEY §8(d)'s decode bytes: the compressed
+    # file read + the 3 B/px BGR frame written (the walks are latency-bound,
+    # DESIGN.md §10, so this fraction stays small)
+    dbytes = float(sum(lens)) + 3.0 * W * H * n_frames
+    gbps = dbytes * steps / td / 1e9
+    line["decode_roofline"] = {"bound": "hbm", "achieved": round(gbps, 1), "peak": 8000.0, "unit": "GB/s",
+                               "frac": round(gbps / 8000.0, 4), "bytes_per_call": int(dbytes)}
     return line
 
 
