@@ -111,9 +111,12 @@ struct DecSlow {
 //
 // Symbol pairs (round 5).  A first-level entry of an AC table also says, in
 // its high half, what the NEXT symbol does when that symbol's whole code lies
-// inside the same 10-bit look-ahead (first symbol's code + extra bits + the
-// second's code <= 10 bits): bits 16..19 its code length (0 = no pair), 20..23
-// its extra bits, 24..30 its zig-zag advance.  A walk applies both symbols in
+// inside the same look-ahead (first symbol's code + extra bits + the second's
+// code <= DEC_LUT_BITS): bits 16..20 the bits it consumes, code + extra (0 =
+// no pair), 21..24 its extra bits, 25..31 its zig-zag advance - the fields a
+// step adds as they are (round 5: code length and extra bits were separate
+// fields until the consumed total saved the state-only walks an add and a
+// bit-field extract per step).  A walk applies both symbols in
 // one step unless the first ends the block (z + advance >= 64: the next
 // symbol is then the next block's DC).  Over 4K q95 content a 10-bit window
 // pairs 40 % (smooth) / 32 % (noise) of the symbol steps away
@@ -815,11 +818,12 @@ struct DecLeanWalker {
         // it is), then the rare invalid-code path overrides it
         const int z1 = z + (act ? (int)((e >> 5) & 127) : 0);
         // the pair's second symbol, unless the first ended the block
-        two = act && ((e >> DEC_PAIR_SHIFT) & 15) != 0 && z1 < 64;
-        const int c = c1 + (two ? (int)(((e >> 16) & 15) + ((e >> 20) & 15)) : 0);
+        const int c2 = (int)((e >> DEC_PAIR_SHIFT) & 31);
+        two = act && c2 != 0 && z1 < 64;
+        const int c = c1 + (two ? c2 : 0);
         R.skip(c);
         pos += (uint32_t)c;
-        z = z1 + (two ? (int)((e >> 24) & 127) : 0);
+        z = z1 + (two ? (int)(e >> 25) : 0);
         const bool end = z >= 64;
         n += end ? 1u : 0u;
         const int bn = b + 1 == nbmcu ? 0 : b + 1;
@@ -984,11 +988,10 @@ struct DecLeanWriter {
         z += zadd;
         // the pair's second symbol (an AC code inside the same look-ahead),
         // unless the first ended the block: its value bits follow its code
-        const int len2 = (int)((e >> DEC_PAIR_SHIFT) & 15);
-        two = len2 != 0 && z < 64;
+        const int c2 = (int)((e >> DEC_PAIR_SHIFT) & 31);
+        two = c2 != 0 && z < 64;
         if (two) {
-            const int sz2 = (int)((e >> 20) & 15), zadd2 = (int)((e >> 24) & 127);
-            const int c2 = len2 + sz2;
+            const int sz2 = (int)((e >> 21) & 15), zadd2 = (int)(e >> 25);
             const uint32_t v2 = (uint32_t)(R.buf >> (64 - c2)) & ((1u << sz2) - 1u);
             R.skip(c2);
             pos += (uint32_t)c2;

@@ -252,7 +252,7 @@ void build_dec_lean(const DecHuff& h, bool ac, DecLean& lean)
                 if (e2 && !(e2 & (DEC_SUB | DEC_SLOW)) && (e2 >> 8) <= room) {
                     const uint32_t l2 = conv(e2);                     // (length + extra) | advance | extra
                     const uint32_t len2 = e2 >> 8, sz2 = (l2 >> 12) & 15, zadd2 = (l2 >> 5) & 127;
-                    x |= (len2 | sz2 << 4 | zadd2 << 8) << DEC_PAIR_SHIFT;
+                    x |= ((len2 + sz2) | sz2 << 5 | zadd2 << 9) << DEC_PAIR_SHIFT;  // bits consumed, extra bits, advance
                 }
             }
         }
