@@ -675,7 +675,9 @@ template <class LeanPtr>
 ICX_HD uint32_t dec_lean_symbol(LeanPtr t, const ICX_GLOBAL DecSlow* slow, uint32_t pk, bool ac)
 {
     const uint32_t e = t->lut[pk >> (16 - DEC_LUT_BITS)];
-    if ((e & 31) || !e) return e;  // codes of at most 10 bits (or none): one branch on the common path
+    // codes of at most DEC_LUT_BITS bits (or none): one bit test on the common
+    // path - DEC_LEAN_LONG is a zig-zag advance of 32, which no symbol has
+    if (!(e & DEC_LEAN_LONG)) return e;
     if (!(e & DEC_LEAN_SLOW)) return t->lut2[(e >> 5) & (DEC_NSUB - 1)][pk & ((1u << (16 - DEC_LUT_BITS)) - 1)];
     for (int l = DEC_LUT_BITS + 1; l <= 16; l++) {
         const int code = (int)(pk >> (16 - l));
@@ -714,7 +716,7 @@ ICX_HD uint32_t dec_lean_lookup(const SplitLean& H, int ti, const ICX_GLOBAL Dec
     // a lane of the wave in ~15 % of steps) through the scalar cache, one lane
     // at a time: a vector load here would be waited for with vmcnt, i.e.
     // behind every coefficient store the wave still has in flight.
-    uint64_t m = __ballot(!(e & 31) && e && !(e & DEC_LEAN_SLOW));
+    uint64_t m = __ballot((e & (DEC_LEAN_LONG | DEC_LEAN_SLOW)) == DEC_LEAN_LONG);
     if (m) {
         const uint32_t off = (uint32_t)(ti * sizeof(DecLean) + offsetof(DecLean, lut2)) +
                              ((((e >> 5) & (DEC_NSUB - 1)) << (16 - DEC_LUT_BITS)) | (pk & ((1u << (16 - DEC_LUT_BITS)) - 1))) * 2;
@@ -734,13 +736,13 @@ ICX_HD uint32_t dec_lean_lookup(const SplitLean& H, int ti, const ICX_GLOBAL Dec
     // branch (the v_mov), it is also waited for there; consumed after the
     // join, the compiler waited vmcnt(0) at the join on every step - behind
     // every coefficient store the wave still had in flight.
-    if (!((e & 31) || !e)) {
+    if (e & DEC_LEAN_LONG) {
         const uint32_t e2 = dec_lean_symbol(&H.full[ti], &slow[ti], pk, ac);
         asm volatile("v_mov_b32 %0, %1" : "=v"(e) : "v"(e2));
     }
     return e;
 #else
-    return (e & 31) || !e ? e : dec_lean_symbol(&H.full[ti], &slow[ti], pk, ac);
+    return !(e & DEC_LEAN_LONG) ? e : dec_lean_symbol(&H.full[ti], &slow[ti], pk, ac);
 #endif
 }
 
