@@ -363,6 +363,9 @@ using DecReader = DecReaderT<DEC_WIN>;
 #ifndef ICX_DEC_WALK_UNROLL2
 #define ICX_DEC_WALK_UNROLL2 1  // state-only walks: two steps per top-up check (-2.6 %, profiles/r4/ab_r4ze_dec_walk_unroll.txt)
 #endif
+#ifndef ICX_DEC_WALK_ALL
+#define ICX_DEC_WALK_ALL 0  // state-only walks: an unpredicated loop while every lane of the wave walks
+#endif
 #ifndef ICX_DEC_PEND32
 #define ICX_DEC_PEND32 1  // write walk: pending block as a 32-bit count from the piece's first block (-0.2 % / -1 % at 200 frames, ab_r4zc_dec_pend32.txt)
 #endif
@@ -894,6 +897,21 @@ ICX_HD uint64_t dec_lean_walk(const DecDesc& d, LeanPtr H, const DecSlow* slow, 
         w.park();
     }
 #if defined(__HIP_DEVICE_COMPILE__) && ICX_DEC_WALK_UNROLL2
+#if ICX_DEC_WALK_ALL
+    // while every lane walks, steps without the per-lane predication
+    while (__all(run)) {  // the second step stays before the top-up check either way
+        w.step(true);
+        run = w.running(stop);
+        if (__all(run)) {
+            w.step(true);
+            run = w.running(stop);
+        } else {
+            w.step(run);
+            run = run && w.running(stop);
+        }
+        if (__any(run && w.R.nq <= 2) && run) w.R.top_up();
+    }
+#endif
     while (__any(run)) {  // two steps per top-up check (a step consumes <= 1 window word)
         w.step(run);
         run = run && w.running(stop);
@@ -985,8 +1003,12 @@ struct DecLeanWriter {
 #else
         const int x = sz ? dec_extend((int)v, sz) : 0;
 #endif
-        const int zc = z + zadd - 1;  // zig-zag index of a coefficient (DC: 0)
-        sink.put(!own ? 0 : sz ? (zc > 63 ? 63 : zc) : z, x);
+        // zig-zag index of a coefficient (DC: 0).  A size-0 symbol (EOB, ZRL,
+        // a zero DC difference) puts its 0 at z + advance - 1 (clamped), a
+        // position its zero run covers and nothing wrote yet in the zeroed
+        // slot - no select for it
+        const int zc = z + zadd - 1;
+        sink.put(!own ? 0 : (zc > 63 ? 63 : zc), x);
         z += zadd;
         // the pair's second symbol (an AC code inside the same look-ahead),
         // unless the first ended the block: its value bits follow its code
@@ -1000,7 +1022,7 @@ struct DecLeanWriter {
             const int half2 = (1 << sz2) >> 1;
             const int x2 = (int)v2 - ((int)v2 < half2 ? (1 << sz2) - 1 : 0);
             const int zc2 = z + zadd2 - 1;
-            sink.put(!own ? 0 : sz2 ? (zc2 > 63 ? 63 : zc2) : z, x2);
+            sink.put(!own ? 0 : (zc2 > 63 ? 63 : zc2), x2);
             z += zadd2;
         }
         const bool end = z >= 64;
@@ -1190,6 +1212,30 @@ ICX_HD uint64_t dec_sync_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, 
         run = run && !early && w.running(stop);
     };
 #if defined(__HIP_DEVICE_COMPILE__) && ICX_DEC_WALK_UNROLL2
+#if ICX_DEC_WALK_ALL
+    // while every lane walks, steps without the per-lane predication (the
+    // first sync walk: nearly all of it)
+    auto all_one = [&]() {
+        w.step(true);
+        while (k < nck && w.pos >= ckpos) {
+            if (ck.visit(k, w.state() | ((uint64_t)w.n << 48), nblk)) {
+                early = true;
+                break;
+            }
+            k++;
+            ckpos += ckb;
+        }
+        run = !early && w.running(stop);
+    };
+    while (__all(run)) {  // the second step stays before the top-up check either way
+        all_one();
+        if (__all(run))
+            all_one();
+        else
+            one();
+        if (__any(run && w.R.nq <= 2) && run) w.R.top_up();
+    }
+#endif
     while (__any(run)) {  // two steps per top-up check (a step consumes <= 1 window word)
         one();
         one();

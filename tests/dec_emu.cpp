@@ -283,7 +283,13 @@ extern "C" long dec_emu_lean_check(const uint8_t* jpg, size_t len, int nstarts, 
     // the write walks: every sink call (index, value; flushed block) in order
     struct Rec {
         std::vector<int64_t> ev;
-        void put(int z, int v) { ev.push_back(((int64_t)z << 32) ^ (uint32_t)v); }
+        // the value puts; a 0 lands in a zeroed slot position that nothing
+        // else writes in the block, so where it lands is free (the lean writer
+        // puts a size-0 symbol's 0 at the end of its zero run, DecWalker at z)
+        void put(int z, int v)
+        {
+            if (v) ev.push_back(((int64_t)z << 32) ^ (uint32_t)v);
+        }
         void flush_if(bool c, int64_t bi)
         {
             if (c) ev.push_back(-1 - bi);
