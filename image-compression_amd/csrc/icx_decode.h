@@ -33,6 +33,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #ifdef __HIPCC__
 #include <hip/hip_runtime.h>
 #define ICX_HD __host__ __device__ __forceinline__
@@ -265,15 +267,27 @@ ICX_HD uint32_t dec_be32(uint32_t v)
 #endif
 
 // MSB-first bit reader over the unstuffed stream (big-endian 32-bit words).
-// The words ahead of the 64-bit bit buffer sit in an 8-word register window
-// (q[0] next).  On the device the window is reloaded only at wave-uniform
-// points (top_up() when low(), driven by the caller's loop) followed at once by
-// an explicit vmcnt(0): vector-memory counters are in-order and count stores
-// too, so a load consumed one symbol later would also wait for every block
-// store issued in between.  A step consumes at most one window word and the
-// device loops top up every lane once any holds <= 1, so a device refill never
-// finds the window empty; host loops (no top-ups) reload inside refill().  The stream buffer extends 64 + 4 DEC_WIN
-// bytes past its padded end, so a window never reads outside it.
+// The next word q0 sits in a register; the words after it in a window of
+// DEC_WIN words ("rows") read from the stream at once.  On the device the
+// window is reloaded only at wave-uniform points (top_up() when low(), driven
+// by the caller's loop) followed at once by an explicit vmcnt(0):
+// vector-memory counters are in-order and count stores too, so a load
+// consumed one symbol later would also wait for every block store issued in
+// between.  A step consumes at most one window word and the device loops top
+// up every lane once any holds <= 1 (<= 2 when they check every second step),
+// so a device refill never finds the window empty; host loops (no top-ups)
+// reload inside refill().  The stream buffer extends 64 + 4 DEC_WIN bytes past
+// its padded end, so a window never reads outside it.
+//
+// Where the window lives (LDS_WIN): in registers a refill shifts the whole
+// window by one word under the lane's "need" (one select per word, every
+// step - the walks are instruction-issue bound); in LDS (rows [row][lane] of
+// the wave, dec_win_lane) a refill advances a row pointer and reads the next
+// q0 unconditionally (the LDS read returns before the next step's table
+// look-up, which waits on LDS anyway).  The state-only walks keep it in LDS
+// (9 KiB more per workgroup: 6 workgroups per CU instead of 8, still a gain;
+// 6 / 12 words there: slower / +-0, ab_r5ai_dec_lds_win_size.txt); the write
+// pass in registers (its workgroups fill LDS already).
 #ifndef ICX_DEC_WIN
 #define ICX_DEC_WIN 8
 #endif
@@ -286,34 +300,115 @@ constexpr int DEC_WIN = ICX_DEC_WIN;
 #endif
 constexpr int DEC_WIN_WRITE = ICX_DEC_WIN_WRITE;
 constexpr int DEC_WIN_MAX = DEC_WIN > DEC_WIN_WRITE ? DEC_WIN : DEC_WIN_WRITE;
+// state-only walks (k_dec_init, k_dec_sync) / the write pass: window in LDS
+#ifndef ICX_DEC_LDS_WIN
+#define ICX_DEC_LDS_WIN 1  // -1.2 ms at 1000 frames (sync0 12.9 -> 12.1), +-0 at 200 (ab_r5ah_dec_lds_win.txt)
+#endif
+#ifndef ICX_DEC_LDS_WIN_WRITE
+#define ICX_DEC_LDS_WIN_WRITE 0  // +4.6 ms: 10 KiB more LDS per workgroup leaves 3 workgroups per CU, not 4 (ab_r5ah)
+#endif
+constexpr int DEC_WIN_NT = 256;  // workgroup size of the kernels that walk
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define ICX_LDS __attribute__((address_space(3)))
+// The lane's row 0 of the LDS window: rows of one wave are 64 words apart
+// (a row read by the wave's lanes is bank-conflict free whatever row each
+// lane is at), one spare row past the window (a refill reads the row after
+// the last word before the caller tops up).
 template <int WIN>
+__device__ __forceinline__ ICX_LDS uint32_t* dec_win_lane()
+{
+    __shared__ uint32_t win[(WIN + 1) * DEC_WIN_NT];
+    const int t = (int)threadIdx.x;
+    return (ICX_LDS uint32_t*)(win + (t >> 6) * (WIN + 1) * 64 + (t & 63));
+}
+#endif
+
+template <int WIN, bool LDS_WIN = false>
 struct DecReaderT {
     static constexpr int DEC_WIN = WIN;  // (shadows the global inside the reader)
+    static constexpr bool LDS = LDS_WIN;
     const ICX_GLOBAL uint32_t* w;
     uint64_t buf;
     int avail;
-    uint32_t wi;    // stream word index of q[0]
-    int nq;         // valid words in q
-    uint32_t q[WIN];
+    uint32_t wi;    // stream word index of row 0 of the window
+    uint32_t q0;    // the next word (row used())
+    struct Regs {
+        int nq;  // words left, q0 included (q[0] = q0)
+        uint32_t q[WIN];
+    };
+#if defined(__HIP_DEVICE_COMPILE__)
+    struct Lds {
+        ICX_LDS uint32_t* lw;  // row 0
+        ICX_LDS uint32_t* rp;  // q0's row
+        ICX_HD int row() const { return (int)(rp - lw) >> 6; }
+        ICX_HD void bind() { rp = lw = dec_win_lane<WIN>(); }
+        ICX_HD void put(int j, uint32_t v) { lw[j * 64] = v; }
+        ICX_HD uint32_t next(bool need)
+        {
+            rp += need ? 64 : 0;
+            return *rp;
+        }
+    };
+#else
+    struct Lds {  // the host's stand-in (tests/dec_emu.cpp runs the same row logic)
+        uint32_t rows[WIN + 1];
+        int r;
+        ICX_HD int row() const { return r; }
+        ICX_HD void bind() { r = 0; }
+        ICX_HD void put(int j, uint32_t v) { rows[j] = v; }
+        ICX_HD uint32_t next(bool need)
+        {
+            r += need ? 1 : 0;
+            return rows[r];
+        }
+    };
+#endif
+    typename std::conditional<LDS_WIN, Lds, Regs>::type m;
 
+    ICX_HD int used() const
+    {
+        if constexpr (LDS) return m.row();
+        else return WIN - m.nq;
+    }
+    ICX_HD int left() const { return WIN - used(); }
     ICX_HD void fetch(uint32_t at)
     {
         wi = at;
-        nq = DEC_WIN;
         const ICX_GLOBAL uint32_t* const wa = w + at;  // one address, the words at immediate offsets
+        uint32_t t[WIN];
 #pragma unroll
-        for (int j = 0; j < DEC_WIN; j++) q[j] = wa[j];
+        for (int j = 0; j < WIN; j++) t[j] = wa[j];
 #if defined(__HIP_DEVICE_COMPILE__)
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing later waits on q
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing later waits on the window
 #endif
+        if constexpr (LDS) {
+            m.bind();
+#pragma unroll
+            for (int j = 0; j < WIN; j++) m.put(j, t[j]);  // row 0 too: a refill without need reads q0's row again
+        } else {
+#pragma unroll
+            for (int j = 0; j < WIN; j++) m.q[j] = t[j];
+            m.nq = WIN;
+        }
+        q0 = t[0];
+    }
+    // past q0 by `need` words (0 or 1): the next q0
+    ICX_HD void advance(bool need)
+    {
+        if constexpr (LDS) {
+            q0 = m.next(need);  // unconditional read: the same word again without need
+        } else {
+#pragma unroll
+            for (int j = 0; j + 1 < WIN; j++) m.q[j] = need ? m.q[j + 1] : m.q[j];
+            m.nq -= need ? 1 : 0;
+            q0 = m.q[0];
+        }
     }
     ICX_HD uint32_t pop()  // next window word, byte-swapped
     {
-        const uint32_t v = q[0];
-#pragma unroll
-        for (int j = 0; j + 1 < DEC_WIN; j++) q[j] = q[j + 1];
-        wi++;
-        nq--;
+        const uint32_t v = q0;
+        advance(true);
         return dec_be32(v);
     }
     ICX_HD void init(const uint32_t* words, uint32_t pos)
@@ -324,25 +419,38 @@ struct DecReaderT {
         buf = ((hi << 32) | pop()) << (pos & 31);
         avail = 64 - (int)(pos & 31);
     }
-    ICX_HD bool low() const { return nq <= 1; }
+    // a lane with no walk: reads no stream memory, never asks for a top-up
+    ICX_HD void park()
+    {
+        buf = 0;
+        avail = 64;
+        wi = 0;
+        q0 = 0;
+        if constexpr (LDS) {
+            m.bind();
+        } else {
+            m.nq = WIN;
+            for (int j = 0; j < WIN; j++) m.q[j] = 0;
+        }
+    }
+    ICX_HD bool low() const { return left() <= 1; }
 #ifndef ICX_DEC_TOPUP_HALF
 #define ICX_DEC_TOPUP_HALF 0
 #endif
-    ICX_HD bool wants() const { return !ICX_DEC_TOPUP_HALF || nq <= DEC_WIN / 2; }  // joins a top-up
-    ICX_HD void top_up() { fetch(wi); }
+    ICX_HD bool wants() const { return !ICX_DEC_TOPUP_HALF || left() <= DEC_WIN / 2; }  // joins a top-up
+    ICX_HD void top_up() { fetch(wi + (uint32_t)used()); }
     ICX_HD void refill()  // select-based: the common case takes no branch
     {
 #if !defined(__HIP_DEVICE_COMPILE__)
-        if (nq == 0 && avail < 32) top_up();  // device loops top up first: nq >= 1 here
+        // host loops have no top-up points: top up where a device lane may be
+        // (any left() <= 2), so refills right after a top-up run here too
+        if (left() <= 2) top_up();
 #endif
         const bool need = avail < 32;
-        const uint32_t v = dec_be32(q[0]);
-#pragma unroll
-        for (int j = 0; j + 1 < DEC_WIN; j++) q[j] = need ? q[j + 1] : q[j];
+        const uint32_t v = dec_be32(q0);
         buf |= need ? (uint64_t)v << (32 - avail) : 0ull;
-        wi += need ? 1u : 0u;
-        nq -= need ? 1 : 0;
         avail += need ? 32 : 0;
+        advance(need);
     }
     ICX_HD uint32_t peek16() const { return (uint32_t)(buf >> 48); }
     ICX_HD void skip(int n)
@@ -358,14 +466,13 @@ struct DecReaderT {
         return v;
     }
 };
-using DecReader = DecReaderT<DEC_WIN>;
+using DecReader = DecReaderT<DEC_WIN, ICX_DEC_LDS_WIN != 0>;
 
 #ifndef ICX_DEC_WALK_UNROLL2
 #define ICX_DEC_WALK_UNROLL2 1  // state-only walks: two steps per top-up check (-2.6 %, profiles/r4/ab_r4ze_dec_walk_unroll.txt)
 #endif
-#ifndef ICX_DEC_WALK_ALL
-#define ICX_DEC_WALK_ALL 0  // state-only walks: an unpredicated loop while every lane of the wave walks
-#endif
+// (an unpredicated loop while every lane of a wave walks, ahead of this one:
+// +30 % sync0, profiles/r5/ab_r5ag_walk_all.txt)
 #ifndef ICX_DEC_PEND32
 #define ICX_DEC_PEND32 1  // write walk: pending block as a 32-bit count from the piece's first block (-0.2 % / -1 % at 200 frames, ab_r4zc_dec_pend32.txt)
 #endif
@@ -805,11 +912,7 @@ struct DecLeanWalker {
         pos = DEC_END;
         b = z = ti = 0;
         n = 0;
-        R.buf = 0;
-        R.avail = 64;
-        R.wi = 0;
-        R.nq = DEC_WIN;
-        for (int j = 0; j < DEC_WIN; j++) R.q[j] = 0;
+        R.park();
     }
     // act == false: a lane whose walk has ended keeps the wave's loop company
     // without changing its state (no exec-masked region around the step: the
@@ -897,27 +1000,12 @@ ICX_HD uint64_t dec_lean_walk(const DecDesc& d, LeanPtr H, const DecSlow* slow, 
         w.park();
     }
 #if defined(__HIP_DEVICE_COMPILE__) && ICX_DEC_WALK_UNROLL2
-#if ICX_DEC_WALK_ALL
-    // while every lane walks, steps without the per-lane predication
-    while (__all(run)) {  // the second step stays before the top-up check either way
-        w.step(true);
-        run = w.running(stop);
-        if (__all(run)) {
-            w.step(true);
-            run = w.running(stop);
-        } else {
-            w.step(run);
-            run = run && w.running(stop);
-        }
-        if (__any(run && w.R.nq <= 2) && run) w.R.top_up();
-    }
-#endif
     while (__any(run)) {  // two steps per top-up check (a step consumes <= 1 window word)
         w.step(run);
         run = run && w.running(stop);
         w.step(run);
         run = run && w.running(stop);
-        if (__any(run && w.R.nq <= 2) && run) w.R.top_up();
+        if (__any(run && w.R.left() <= 2) && run) w.R.top_up();
     }
 #elif defined(__HIP_DEVICE_COMPILE__)
     while (__any(run)) {
@@ -960,7 +1048,7 @@ struct DecLeanWriter {
     bool two;  // the last step was a symbol pair
     int64_t blk_base;
     uint32_t nlim;  // blocks from blk_base to the image's end (clamped to 32 bits)
-    DecReaderT<DEC_WIN_WRITE> R;
+    DecReaderT<DEC_WIN_WRITE, ICX_DEC_LDS_WIN_WRITE != 0> R;
     const uint32_t* words;
 
 #if ICX_DEC_BSEL
@@ -1212,34 +1300,10 @@ ICX_HD uint64_t dec_sync_walk(const DecDesc& d, HuffPtr H, const DecSlow* slow, 
         run = run && !early && w.running(stop);
     };
 #if defined(__HIP_DEVICE_COMPILE__) && ICX_DEC_WALK_UNROLL2
-#if ICX_DEC_WALK_ALL
-    // while every lane walks, steps without the per-lane predication (the
-    // first sync walk: nearly all of it)
-    auto all_one = [&]() {
-        w.step(true);
-        while (k < nck && w.pos >= ckpos) {
-            if (ck.visit(k, w.state() | ((uint64_t)w.n << 48), nblk)) {
-                early = true;
-                break;
-            }
-            k++;
-            ckpos += ckb;
-        }
-        run = !early && w.running(stop);
-    };
-    while (__all(run)) {  // the second step stays before the top-up check either way
-        all_one();
-        if (__all(run))
-            all_one();
-        else
-            one();
-        if (__any(run && w.R.nq <= 2) && run) w.R.top_up();
-    }
-#endif
     while (__any(run)) {  // two steps per top-up check (a step consumes <= 1 window word)
         one();
         one();
-        if (__any(run && w.R.nq <= 2) && run) w.R.top_up();
+        if (__any(run && w.R.left() <= 2) && run) w.R.top_up();
     }
 #elif defined(__HIP_DEVICE_COMPILE__)
     while (__any(run)) {

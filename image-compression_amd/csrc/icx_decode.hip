@@ -871,7 +871,7 @@ __global__ void __launch_bounds__(DEC_WRITE_NT) k_dec_write(const DecDesc* D, De
             w.step(sk);
             run = w.running(stop);
         }
-        if (__any(run && w.R.nq <= 2) && run) w.R.top_up();
+        if (__any(run && w.R.left() <= 2) && run) w.R.top_up();
         flush();
     }
 #else
