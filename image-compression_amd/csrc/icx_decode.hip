@@ -231,6 +231,9 @@ __device__ __forceinline__ Unstuff16 unstuff16(const ByteClass& c, int prev, int
 // workgroup counts DEC_UNSTUFF_TILES consecutive tiles, all their loads
 // issued first (one 4 KiB tile per workgroup left each workgroup a single
 // 16-byte load per thread in flight).
+#ifndef ICX_UNSTUFF_COMPACT
+#define ICX_UNSTUFF_COMPACT 1  // unstuffing 7.93 -> 7.14 ms at 1000 frames (ab_r5aj_dec_unstuff_compact.txt)
+#endif
 __global__ void __launch_bounds__(256) k_unstuff_count(const DecDesc* D, DecState* S, Plan p)
 {
     constexpr int U = DEC_UNSTUFF_TILES;
@@ -252,6 +255,59 @@ __global__ void __launch_bounds__(256) k_unstuff_count(const DecDesc* D, DecStat
         prev[u] = ((const ICX_GLOBAL uint8_t*)d.scan)[bc > 0 ? bc - 1 : 0];
     }
     uint32_t cnt[U];  // output bytes (bits 0..19) + RSTn markers << 20 of this thread's 16 bytes
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#if ICX_UNSTUFF_COMPACT
+    // Chunks with a 0xFF byte (or one before them) are ~6 % of the stream,
+    // but nearly every wave holds one, so a per-lane branch ran the masks of
+    // classify16 / unstuff16 (~140 VALU) for every chunk of every wave.  Here
+    // the wave counts its plain chunks directly and moves the others into
+    // LDS (compacted: wave-uniform rounds of 64), so the masks run once per
+    // 64 such chunks, on full lanes.
+    __shared__ uint4 cv[4][64];
+    __shared__ uint32_t cm[4][64];  // prev | next << 8 | u << 16 | thread << 20
+    bool spc[U];
+    uint32_t nsp = 0;  // special chunks of the wave so far
+    uint32_t ord[U];   // this lane's index among them, per tile
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int64_t base = (tile0 + u) * DEC_TILE + threadIdx.x * 16;
+        const int pv = base > 0 ? prev[u] : 0;
+        spc[u] = base < len && any_ff(q[u].v, pv);
+        cnt[u] = base < len && !spc[u] ? (uint32_t)min((int64_t)16, len - base) : 0u;
+        const uint64_t m = __ballot(spc[u]);
+        ord[u] = nsp + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        nsp += (uint32_t)__popcll(m);
+    }
+    for (uint32_t r0 = 0; r0 < nsp; r0 += 64) {  // wave-uniform
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (spc[u] && ord[u] >= r0 && ord[u] < r0 + 64) {
+                const int64_t base = (tile0 + u) * DEC_TILE + threadIdx.x * 16;
+                const uint32_t pv = base > 0 ? (uint32_t)prev[u] : 0u;
+                cv[w][ord[u] - r0] = q[u].v;
+                cm[w][ord[u] - r0] = pv | (uint32_t)q[u].next << 8 | (uint32_t)u << 16 | threadIdx.x << 20;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // (a wave's LDS accesses complete in order)
+        if (r0 + lane < nsp) {
+            const uint4 v = cv[w][lane];
+            const uint32_t mt = cm[w][lane];
+            const int su = (int)((mt >> 16) & 15);
+            const int64_t base = (tile0 + su) * DEC_TILE + (int64_t)(mt >> 20) * 16;
+            const Unstuff16 x = unstuff16(classify16(v), (int)(mt & 255), (int)((mt >> 8) & 255));
+            const int64_t rem = len - base;  // bytes of that chunk below scan_len
+            const uint32_t valid = rem >= 16 ? 0xFFFFu : (1u << rem) - 1;
+            const uint32_t nr = (uint32_t)__popc(x.rst & valid);
+            const uint32_t c = (uint32_t)__popc(x.keep & valid) + DEC_PAD * nr + (nr << 20);
+#pragma unroll
+            for (int u = 0; u < U; u++) cnt[u] += su == u ? c : 0u;
+            // a marker needs its next byte below scan_len
+            const uint32_t mk = x.mark & (rem - 1 >= 16 ? 0xFFFFu : (1u << (rem - 1)) - 1);
+            if (mk) atomicMin((unsigned long long*)&S[img].end, (unsigned long long)(base + __builtin_ctz(mk)));
+        }
+        __builtin_amdgcn_wave_barrier();  // the reads before the next round's writes
+    }
+#else
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const int64_t base = (tile0 + u) * DEC_TILE + threadIdx.x * 16;
@@ -273,9 +329,9 @@ __global__ void __launch_bounds__(256) k_unstuff_count(const DecDesc* D, DecStat
         }
         cnt[u] = c;
     }
+#endif
     // workgroup sums: wave reductions, then the four wave totals (a tile's
     // bytes < 2^20, its markers < 2^12)
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
     for (int u = 0; u < U; u++) {
         uint32_t c = cnt[u];
