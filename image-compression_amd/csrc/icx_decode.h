@@ -68,7 +68,7 @@ constexpr int DEC_TILE = 4096;       // stuffed bytes per unstuff tile (256 thre
 #define ICX_DEC_UNSTUFF_TILES 4
 #endif
 #ifndef ICX_DEC_SCATTER_TILES
-#define ICX_DEC_SCATTER_TILES 4  // with the compacted masks (ICX_SCATTER_COMPACT): 1 / 2 / 4 tiles 7.4 / 6.7 / 6.35 ms unstuffing per 1000 frames, per-lane masks 7.1 (ab_r5ak_dec_scatter_compact.txt)
+#define ICX_DEC_SCATTER_TILES 4  // with the compacted masks (ICX_SCATTER_COMPACT): 1 / 2 / 4 / 8 tiles 7.4 / 6.7 / 6.35 / 8.3 ms unstuffing per 1000 frames, per-lane masks 7.1 (ab_r5ak_dec_scatter_compact.txt, ab_r5al_dec_unstuff_tiles8.txt)
 #endif
 constexpr int DEC_UNSTUFF_TILES = ICX_DEC_UNSTUFF_TILES;  // consecutive tiles per k_unstuff_count workgroup
 constexpr int DEC_SCATTER_TILES = ICX_DEC_SCATTER_TILES;  // ... per k_unstuff_scatter workgroup (4: +10 %, r4e)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 5 (al): 8 tiles per unstuffing workgroup (count: lib/libicx_cu8.so,
+# scatter: su8, both: u8) against 4 (base).  Decode parity (u8), then A/B.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+T="python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_decode_gpu.py tests/test_cmyk_gpu.py"
+ICX_LIB=$PWD/image-compression_amd/lib/libicx_u8.so timeout -k 10 300 $T > gpurun_out/pytest_gpu_r5al_u8.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_r5al_u8.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu_r5al_u8.log
+echo "== 1000 frames"
+FRAMES=1000 STEPS=3 AB_ARGS="--distinct 16" ROUNDS=3 bash scripts/ab_decode.sh base lib/libicx_cu8.so lib/libicx_su8.so lib/libicx_u8.so || exit 1
+echo "== 200 frames"
+FRAMES=200 AB_ARGS="--distinct 16" ROUNDS=2 bash scripts/ab_decode.sh base lib/libicx_cu8.so lib/libicx_su8.so lib/libicx_u8.so || exit 1
