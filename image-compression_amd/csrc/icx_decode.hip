@@ -1490,6 +1490,12 @@ __global__ void __launch_bounds__(256) k_dec_color(const DecDesc* D, const DecSt
 #ifndef ICX_DEC_LC_WAVES
 #define ICX_DEC_LC_WAVES 1
 #endif
+#ifndef ICX_DEC_LC_PF
+#define ICX_DEC_LC_PF 3  // tiles whose loads are in flight ahead of the one being converted: 1 / 2 / 3 = 11.15 / 11.1 / 10.85 ms colour pass per 1000 frames (ab_r5an_dec_color_pipe.txt)
+#endif
+#ifndef ICX_DEC_LC_FULL
+#define ICX_DEC_LC_FULL 1  // interior tiles: a fixed store sequence (below); without: 11.7 ms
+#endif
 constexpr int LC_NM = 8;  // dec_lc_items
 constexpr int LC_W = 16 * LC_NM;      // output columns per tile
 constexpr int LC_CD = LC_W / 8 + 2;   // chroma dwords per staged row
@@ -1566,12 +1572,20 @@ __global__ void __launch_bounds__(256, ICX_DEC_LC_WAVES) k_dec_luma_color_420(co
     int item = (int)wg * LC_T;
     if (item >= ntile) return;
     const uint4 qt = *(const ICX_GLOBAL uint4*)(qtab + (t & 7) * 8);
-    LcLoad cur;
-    lc_fetch(g, item, t, cur);
+    // The tile loop unrolled, each tile's loads in registers of their own,
+    // issued LC_PF tiles ahead: no register copies between tiles (a copy of
+    // a load's destination waits for the load) and no branch around a load
+    // (the tile index is clamped to the image's last tile instead), so the
+    // compiler's counter waits see every load and store in flight.
+    LcLoad L[LC_T];
+    constexpr int PF = ICX_DEC_LC_PF;
+#pragma unroll
+    for (int k = 0; k < PF && k < LC_T; k++) lc_fetch(g, min(item + k, ntile - 1), t, L[k]);
+#pragma unroll
     for (int it = 0; it < LC_T; it++, item++) {
         if (item >= ntile) break;  // workgroup-uniform
-        LcLoad nxt = cur;
-        if (it + 1 < LC_T && item + 1 < ntile) lc_fetch(g, item + 1, t, nxt);
+        if (it + PF < LC_T) lc_fetch(g, min(item + PF, ntile - 1), t, L[it + PF < LC_T ? it + PF : 0]);
+        const LcLoad& cur = L[it];
         const int my = item / tpr, mx0 = (item - my * tpr) * LC_NM;
         uint32_t* lc = lcb[it & 1];  // the previous tile's colour pass may still read the other one
         lc[t] = cur.c[0];
@@ -1605,7 +1619,23 @@ __global__ void __launch_bounds__(256, ICX_DEC_LC_WAVES) k_dec_luma_color_420(co
         const int x0 = mx0 * 16;
         const int n = ow - x0 - xt;
         const int y0 = my * 16 + 2 * rp;
-        if (n > 0 && y0 < oh) {
+#if ICX_DEC_LC_FULL
+        // A tile whose 128 x 16 output pixels are all inside the image, on a
+        // 4-byte aligned output, stores two 12-byte groups per thread and
+        // nothing else; edge tiles keep the per-pixel tests and byte stores
+        // and then wait for their stores.  The loop's wait for the next
+        // tile's loads (vector-memory counters count stores too, in order)
+        // then leaves a full tile's two stores in flight instead of waiting
+        // for every store the tile issued - the compiler only counts stores
+        // it can see issued on every path.
+        const bool full = x0 + LC_W <= ow && my * 16 + 16 <= oh && (((uintptr_t)out | (uintptr_t)ostride) & 3) == 0;
+        auto convert = [&](auto full_c) {
+        constexpr bool FULL = decltype(full_c)::value;
+#else
+        {
+        constexpr bool FULL = false;
+#endif
+        if (FULL || (n > 0 && y0 < oh)) {
             const int li = (xt >> 1) + 4;        // local byte of i0
             int cv[2][2][4];                     // [comp][top|bottom row][column]: upsampled value - 128
 #pragma unroll
@@ -1650,8 +1680,8 @@ __global__ void __launch_bounds__(256, ICX_DEC_LC_WAVES) k_dec_luma_color_420(co
                     }
                 }
             }
-            const int m = n < 4 ? n : 4;
-            const int rows = oh - y0 < 2 ? 1 : 2;
+            const int m = FULL ? 4 : n < 4 ? n : 4;
+            const int rows = FULL ? 2 : oh - y0 < 2 ? 1 : 2;
 #pragma unroll
             for (int h = 0; h < 2; h++) {  // unrolled: cv stays in registers
                 if (h >= rows) break;
@@ -1671,14 +1701,24 @@ __global__ void __launch_bounds__(256, ICX_DEC_LC_WAVES) k_dec_luma_color_420(co
                                        pk16(ashr_pk_u8(cg_[1], cr_[1], 16), ashr_pk_u8(cb_[2], cg_[2], 16)),
                                        pk16(ashr_pk_u8(cr_[2], cb_[3], 16), ashr_pk_u8(cg_[3], cr_[3], 16))};
                 ICX_GLOBAL uint8_t* o = out + (int64_t)(y0 + h) * ostride + (int64_t)(x0 + xt) * 3;
-                if (m == 4 && (((uintptr_t)o) & 3) == 0) {
+                if (FULL || (m == 4 && (((uintptr_t)o) & 3) == 0)) {
                     *(ICX_GLOBAL uint3*)o = make_uint3(w[0], w[1], w[2]);
                 } else {
                     for (int k = 0; k < 3 * m; k++) o[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
                 }
             }
         }
-        cur = nxt;
+#if ICX_DEC_LC_FULL
+        };
+        if (full) {
+            convert(std::true_type{});
+        } else {
+            convert(std::false_type{});
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this path's stores are all done here
+        }
+#else
+        }
+#endif
     }
 }
 
