@@ -380,12 +380,26 @@ __device__ __forceinline__ void fdct_load(const FdctTile& T, uint32_t (&wv)[2][6
     for (int h = 0; h < 2; h++) {
         const int y = min(y0 + 2 * i + h, H - 1);
         const uint8_t* row = px + (size_t)y * D.stride;
+#if ICX_FDCT_STATIC
+        {
+            // the three loads on every path (an edge tile reads 24 aligned
+            // bytes at the start of the image's allocation instead, then
+            // assembles its pixels below): a value merged from two branches
+            // costs a copy, and the copy waits for the load at once
+            const uint8_t* p = fast ? row + (size_t)(x0 + sg * 8) * 3 : (const uint8_t*)((uintptr_t)px & ~(uintptr_t)7);
+            const int2 a = ld8(p), b = ld8(p + 8), c = ld8(p + 16);
+            wv[h][0] = a.x; wv[h][1] = a.y; wv[h][2] = b.x;
+            wv[h][3] = b.y; wv[h][4] = c.x; wv[h][5] = c.y;
+        }
+        if (!fast) {
+#else
         if (fast) {
             const uint8_t* p = row + (size_t)(x0 + sg * 8) * 3;
             const int2 a = ld8(p), b = ld8(p + 8), c = ld8(p + 16);
             wv[h][0] = a.x; wv[h][1] = a.y; wv[h][2] = b.x;
             wv[h][3] = b.y; wv[h][4] = c.x; wv[h][5] = c.y;
         } else {
+#endif
             const GAS uint8_t* g = gp(row);
             // opaque here, so the compiler does not hoist this path's eight
             // clamped pixel offsets in front of the (wave-uniform) branch
@@ -428,6 +442,9 @@ __device__ __forceinline__ void fdct_load(const FdctTile& T, uint32_t (&wv)[2][6
 // the lanes with nothing to store write to (never read, shared by the waves,
 // so the stores need no exec mask), and per block (offset in its group << 7)
 // | list length.
+#ifndef ICX_FDCT_STATIC
+#define ICX_FDCT_STATIC 1  // k_fdct_color: loads and stores the compiler can count on every path (below); FDCT -2 % (ab_r5ao_fdct_static.txt)
+#endif
 #ifndef ICX_FDCT_EMIT_LA
 #define ICX_FDCT_EMIT_LA 1
 #endif
@@ -454,7 +471,8 @@ __device__ __forceinline__ int writelane(int v, int x, int a)
 
 template <int NB, int STEP, bool FULL, class Fix, class Luma>
 __device__ __forceinline__ uint32_t emit_lists(const ImgDesc& D, int64_t base, int nblk, int16_t (*oz)[WSTR],
-                                               ListStage<NB, STEP>& L, const float (&thr)[2], Fix fix, Luma luma)
+                                               ListStage<NB, STEP>& L, const float (&thr)[2], Fix fix, Luma luma,
+                                               int nat_in = -1)
 {
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -462,15 +480,27 @@ __device__ __forceinline__ uint32_t emit_lists(const ImgDesc& D, int64_t base, i
     uint32_t* const st0 = &L.st[0][0];
     const int dummy_at = 4 * STEP * 64 + lane;  // L.dummy[lane] as an index into st0
     uint32_t total = 0;
-    const int nat = c_zz_to_nat[lane];  // oz holds natural order; lane = zig-zag index
+    // oz holds natural order; lane = zig-zag index (nat_in: the caller's copy,
+    // loaded once per workgroup - a vector load here, behind the next tile's
+    // pixel loads, would wait for them)
+    const int nat = nat_in >= 0 ? nat_in : c_zz_to_nat[lane];
     // wave w takes groups NB/(4 STEP) * w .. (consecutive blocks) and packs their
     // lists back to back in its own region: one partly used cache line per wave
     // region instead of one per group (k_huff's gathers fetch whole lines)
     constexpr int GPW = NB / (4 * STEP);  // groups per wave
     GAS u32x4_t* const region = (GAS u32x4_t*)(D.coefs + base + (int64_t)wave * GPW * STEP * COEF_SLOTS);
+#if ICX_FDCT_STATIC
+    // every group runs (one store each, on every path: see the stores below);
+    // a group past the tile's last block codes nothing (run = 0)
+#pragma unroll
+#endif
     for (int g = 0; g < GPW; g++) {
         const int blk0 = (wave * GPW + g) * STEP;
+#if ICX_FDCT_STATIC
+        const bool live = blk0 < nblk;  // wave-uniform
+#else
         if (blk0 >= nblk) break;
+#endif
         int c[STEP];
 #pragma unroll
         for (int a = 0; a < STEP; a++)
@@ -513,15 +543,45 @@ __device__ __forceinline__ uint32_t emit_lists(const ImgDesc& D, int64_t base, i
             meta = writelane(meta, (((int)total + run) << 5) | cnt, a);  // scalar arithmetic, one VALU op
             run += r4;
         }
+#if ICX_FDCT_STATIC
+        run = live ? run : 0;
+#endif
         if (lane < STEP && blk0 + lane < nblk) L.meta[blk0 + lane] = (uint16_t)meta;
         __builtin_amdgcn_wave_barrier();
         GAS u32x4_t* dst = region + total / 4;
+#if ICX_FDCT_STATIC
+        {
+            // one store per lane whatever the lists' length (lanes past the
+            // group's last 16-B piece store that piece again: same address,
+            // same bytes; an empty group stores stage garbage at the group's
+            // start, inside the region and past every list that k_huff codes),
+            // so the stores are one instruction the compiler counts on every
+            // path (see k_fdct_color); a group of more than 256 entries stores
+            // the rest and then waits for its stores (rare: noise content)
+            const int n4 = run / 4;
+            const int p = lane < n4 ? lane : n4 > 0 ? n4 - 1 : 0;
+            const uint4 v = *(const uint4*)&st[4 * p];
+            u32x4_t w;
+            w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+            dst[p] = w;
+            if (n4 > 64) {
+                for (int q = lane + 64; q < n4; q += 64) {
+                    const uint4 v2 = *(const uint4*)&st[4 * q];
+                    u32x4_t w2;
+                    w2.x = v2.x; w2.y = v2.y; w2.z = v2.z; w2.w = v2.w;
+                    dst[q] = w2;
+                }
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            }
+        }
+#else
         for (int p = lane; p < run / 4; p += 64) {
             const uint4 v = *(const uint4*)&st[4 * p];
             u32x4_t w;
             w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
             dst[p] = w;
         }
+#endif
         total += run;
         __builtin_amdgcn_wave_barrier();
     }
@@ -535,6 +595,22 @@ __device__ __forceinline__ void store_list_meta(const ImgDesc& D, int64_t base, 
 {
     constexpr int GPW = NB / (4 * STEP);
     // WAVE: after a wave barrier, each wave stores the meta of its own blocks
+#if ICX_FDCT_STATIC
+    if (WAVE) {
+        // every lane stores (the compiler counts the stores on every path):
+        // a lane without a block of its own stores its wave's last block -
+        // or the tile's last - again, the same bytes to the same address
+        const int lim = min((int)(threadIdx.x >> 6) * (GPW * STEP) + GPW * STEP, nblk) - 1;
+        int t = (threadIdx.x >> 6) * (GPW * STEP) + (threadIdx.x & 63);
+        t = t < lim ? t : lim >= 0 ? lim : nblk - 1;
+        const uint32_t m = L.meta[t];
+        // global, not flat, stores: a flat store counts on the LDS counter too,
+        // and the next tile's LDS waits would wait for it
+        gp(D.ncoef)[bbase + t] = (uint8_t)(m & 127);
+        gp(D.coff)[bbase + t] = (uint32_t)((base + (t / (GPW * STEP)) * (GPW * STEP * COEF_SLOTS)) >> 2) + (m >> 7);
+        return;
+    }
+#endif
     const int t = WAVE ? (threadIdx.x >> 6) * (GPW * STEP) + (threadIdx.x & 63) : threadIdx.x;
     if ((!WAVE || (threadIdx.x & 63) < GPW * STEP) && t < nblk) {
         const uint32_t m = L.meta[t];
@@ -548,7 +624,7 @@ template <bool BGR>
 __device__ __forceinline__ uint32_t fdct_compute(const FdctTile& T, const uint32_t (&wv)[2][6],
                                              const QNode* __restrict__ nodes, ImgState* states,
                                              uint8_t (*cds)[8][FDC_PX / 2], int16_t (*ws)[WSTR],
-                                             ListStage<FDC_BLK, 6>& L)
+                                             ListStage<FDC_BLK, 6>& L, int nat = -1, const float* thr_in = nullptr)
 {
     const ImgDesc& D = *T.D;
     const int tx = T.tx, my = T.my;
@@ -556,7 +632,8 @@ __device__ __forceinline__ uint32_t fdct_compute(const FdctTile& T, const uint32
     const int t = threadIdx.x;
     int16_t (*oz)[WSTR] = ws;     // natural-order output (phase D)
     const QNode& CN = nodes[D.cand_node];
-    const float thr[2] = {(t & 63) ? CN.qf[0][t & 63].x : -1.0f, (t & 63) ? CN.qf[1][t & 63].x : -1.0f};
+    const float thr[2] = {(t & 63) ? (thr_in ? thr_in[0] : CN.qf[0][t & 63].x) : -1.0f,
+                          (t & 63) ? (thr_in ? thr_in[1] : CN.qf[1][t & 63].x) : -1.0f};
     const int crows = (H + 1) >> 1;             // chroma rows with image data
     const bool tail = crows - my * 8 < 8;       // ... ending inside this tile (workgroup-uniform)
 
@@ -735,9 +812,9 @@ __device__ __forceinline__ uint32_t fdct_compute(const FdctTile& T, const uint32
     auto luma = [](int a) { return a < 4; };  // one MCU per step: Y0 Y1 Y2 Y3 Cb Cr
     uint32_t entries;
     if (plain)  // interior tile: no dummy blocks
-        entries = emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, L, thr, [](int, int, int c) { return c; }, luma);
+        entries = emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, L, thr, [](int, int, int c) { return c; }, luma, nat);
     else
-        entries = emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, L, thr, fix, luma);
+        entries = emit_lists<FDC_BLK, 6, true>(D, base, nblk, oz, L, thr, fix, luma, nat);
     fdct_phase_sync();
     store_list_meta<FDC_BLK, 6, FDCT_WAVE>(D, base, bbase, nblk, L);
     // LDS free for the next tile (wave-local: the wave's next phase B writes
@@ -786,6 +863,37 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
     } u;
     const int64_t total = gridDim.y > 1 ? prefix[1] - prefix[0] : prefix[m];  // items of this launch row
     const int64_t item0 = (int64_t)blockIdx.x * FDCT_TILES;
+#if ICX_FDCT_STATIC
+    // Each tile's pixels in registers of their own, the next tile's loads
+    // issued before this tile is computed - unconditionally (a launch's last
+    // workgroup loads its last tile again instead of branching around the
+    // loads), and no register copies between tiles (a copy of a load's
+    // destination waits for the load).  With the list and meta stores one
+    // instruction each on every path, the compiler's wait for the next tile's
+    // pixels leaves this tile's stores in flight (vector-memory counters count
+    // stores too, in order: a store it cannot count on every path is waited
+    // for).
+    const int nat = c_zz_to_nat[threadIdx.x & 63];  // emit_lists' gather index, ahead of every pixel load
+    uint32_t px[FDCT_TILES][2][6];
+    float thr[FDCT_TILES][2];  // the tile's candidate thresholds (fdct_compute), loaded with its pixels
+    FdctTile tl[FDCT_TILES];
+    auto fetch = [&](int k, int64_t item) {
+        tl[k] = fdct_tile(descs, ids, prefix, m, item);
+        fdct_load(tl[k], px[k]);
+        // raw values, lane 0's replaced where they are used: a select here
+        // would wait for the loads at once
+        const QNode& CN = nodes[tl[k].D->cand_node];
+        thr[k][0] = CN.qf[0][threadIdx.x & 63].x;
+        thr[k][1] = CN.qf[1][threadIdx.x & 63].x;
+    };
+    fetch(0, item0);
+#pragma unroll
+    for (int k = 0; k < FDCT_TILES; k++) {
+        if (k > 0 && item0 + k >= total) break;  // workgroup-uniform
+        if (k + 1 < FDCT_TILES) fetch(k + 1 < FDCT_TILES ? k + 1 : 0, min(item0 + k + 1, total - 1));
+        fdct_compute<BGR>(tl[k], px[k], nodes, states, u.cds, ws, u.ls, nat, thr[k]);
+    }
+#else
     uint32_t cur[2][6], nxt[2][6];
     FdctTile tc = fdct_tile(descs, ids, prefix, m, item0);
     fdct_load(tc, cur);
@@ -805,6 +913,7 @@ __global__ __launch_bounds__(256) void k_fdct_color(const ImgDesc* __restrict__ 
 #pragma unroll
             for (int q = 0; q < 6; q++) cur[h][q] = nxt[h][q];
     }
+#endif
 }
 
 // Grey (1 component, non-interleaved): one workgroup = 8 rows x 128 px = 16 blocks.
