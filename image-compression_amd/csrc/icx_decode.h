@@ -1024,6 +1024,21 @@ ICX_HD uint64_t dec_lean_walk(const DecDesc& d, LeanPtr H, const DecSlow* slow, 
     return w.state();
 }
 
+// The last sz of the first c bits of an MSB-first bit buffer (c <= 32: the
+// field lies in its high word), a symbol's value bits: one bit-field extract
+// on the device instead of a 64-bit shift and a mask.
+#ifndef ICX_DEC_VALUE_BFE
+#define ICX_DEC_VALUE_BFE 1  // +-0 alone (ab_r5aq_dec_write_lim.txt)
+#endif
+ICX_HD uint32_t dec_value_bits(uint64_t buf, int c, int sz)
+{
+#if defined(__HIP_DEVICE_COMPILE__) && ICX_DEC_VALUE_BFE
+    return __builtin_amdgcn_ubfe((uint32_t)(buf >> 32), (uint32_t)(32 - c), (uint32_t)sz);
+#else
+    return (uint32_t)(buf >> (64 - c)) & ((1u << sz) - 1u);
+#endif
+}
+
 // The write pass's walk (k_dec_write): DecWalker<true>'s transitions and
 // sink calls over DecLean entries - the coefficient's value is the last
 // `extra bits` of the bits the entry consumes, its zig-zag index z + zadd - 1.
@@ -1043,7 +1058,11 @@ struct DecLeanWriter {
     uint64_t bsel;  // dec_block_sel
     uint32_t pos, n;
     int b, z, ti;
-    bool own;
+    // 63 once the walk owns its block, 0 before (the partial block it starts
+    // in belongs to the previous piece): a put goes to min(index, own), so a
+    // put before the first owned block lands on index 0, which that block's
+    // DC overwrites - one v_min per put instead of a clamp and a select
+    int own;
     bool bad;
     bool two;  // the last step was a symbol pair
     int64_t blk_base;
@@ -1062,7 +1081,7 @@ struct DecLeanWriter {
         b = (int)((st >> 8) & 7);
         z = (int)(st & 63);
         n = 0;
-        own = z == 0;
+        own = z == 0 ? 63 : 0;
         bad = false;
         ti = table(b, z);
         R.init(words, pos);
@@ -1081,7 +1100,7 @@ struct DecLeanWriter {
             return;
         }
         const int sz = (int)((e >> 12) & 15), zadd = (int)((e >> 5) & 127);
-        const uint32_t v = (uint32_t)(R.buf >> (64 - c)) & ((1u << sz) - 1u);
+        const uint32_t v = dec_value_bits(R.buf, c, sz);
         R.skip(c);
         pos += (uint32_t)c;
 #if ICX_DEC_EXT_BF
@@ -1096,7 +1115,7 @@ struct DecLeanWriter {
         // position its zero run covers and nothing wrote yet in the zeroed
         // slot - no select for it
         const int zc = z + zadd - 1;
-        sink.put(!own ? 0 : (zc > 63 ? 63 : zc), x);
+        sink.put(zc < own ? zc : own, x);
         z += zadd;
         // the pair's second symbol (an AC code inside the same look-ahead),
         // unless the first ended the block: its value bits follow its code
@@ -1104,23 +1123,23 @@ struct DecLeanWriter {
         two = c2 != 0 && z < 64;
         if (two) {
             const int sz2 = (int)((e >> 21) & 15), zadd2 = (int)(e >> 25);
-            const uint32_t v2 = (uint32_t)(R.buf >> (64 - c2)) & ((1u << sz2) - 1u);
+            const uint32_t v2 = dec_value_bits(R.buf, c2, sz2);
             R.skip(c2);
             pos += (uint32_t)c2;
             const int half2 = (1 << sz2) >> 1;
             const int x2 = (int)v2 - ((int)v2 < half2 ? (1 << sz2) - 1 : 0);
             const int zc2 = z + zadd2 - 1;
-            sink.put(!own ? 0 : (zc2 > 63 ? 63 : zc2), x2);
+            sink.put(zc2 < own ? zc2 : own, x2);
             z += zadd2;
         }
         const bool end = z >= 64;
 #if ICX_DEC_PEND32
-        sink.flush_if(end && own && n < nlim, blk_base + n);  // 32-bit bound: nlim = nblocks - blk_base
+        sink.flush_if(end && own != 0 && n < nlim, blk_base + n);  // 32-bit bound: nlim = nblocks - blk_base
 #else
         const int64_t bi = blk_base + n;
-        sink.flush_if(end && own && bi < nblocks, bi);
+        sink.flush_if(end && own != 0 && bi < nblocks, bi);
 #endif
-        own = own || end;
+        own = end ? 63 : own;
         n += end ? 1u : 0u;
         const int bn = b + 1 == nbmcu ? 0 : b + 1;
         b = end ? bn : b;
@@ -1136,7 +1155,7 @@ struct DecLeanWriter {
         b = 0;
         z = 0;
         ti = table(0, 0);
-        own = true;
+        own = 63;
         if (pos + 8 < bound) {
             bad = true;
             pos++;

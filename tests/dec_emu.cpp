@@ -317,7 +317,7 @@ extern "C" long dec_emu_lean_check(const uint8_t* jpg, size_t len, int nstarts, 
                 }
                 a.step(ra);
             }
-            if (a.state() != b.state() || a.n != b.n || a.bad != b.bad || a.own != b.own) {
+            if (a.state() != b.state() || a.n != b.n || a.bad != b.bad || (a.own != 0) != (b.own != 0)) {
                 bad++;
                 break;
             }
