@@ -564,6 +564,8 @@ __device__ __forceinline__ uint32_t emit_lists(const ImgDesc& D, int64_t base, i
             u32x4_t w;
             w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
             dst[p] = w;
+            // (a second store per lane on every path instead of this branch:
+            // FDCT +1 %, ab_r5as_fdct_two_stores.txt)
             if (n4 > 64) {
                 for (int q = lane + 64; q < n4; q += 64) {
                     const uint4 v2 = *(const uint4*)&st[4 * q];
