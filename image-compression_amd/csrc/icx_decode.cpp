@@ -247,7 +247,7 @@ icx_status run_progressive(icx_ctx* c, std::vector<DecItem>& items, int16_t* coe
             dec_geometry(it.J, it.s, d);
             const size_t nb = (size_t)d.nblocks;
             size_t per = align_up(nb * 128, 256) + align_up(nb * 4, 256) + 4096;
-            for (int k = 0; k < 4; k++) per += align_up((size_t)d.pw[k] * d.ph[k], 256);
+            for (int k = 0; k < 4; k++) per += align_up((size_t)d.pw[k] * d.ph[k] + DEC_PLANE_SPARE, 256);
             const bool host_out = !coef_out && !is_device_ptr(it.job->out);
             if (host_out) per += align_up(it.job->out_len, 256);
             const size_t hper = align_up(nb * 128, 64) + align_up(nb * 4, 64) + (it.dev_in ? align_up(it.job->len, 64) : 0);
@@ -335,7 +335,7 @@ icx_status run_progressive(icx_ctx* c, std::vector<DecItem>& items, int16_t* coe
                 e = hipMemcpyAsync(d.dc, hdc[k], (size_t)d.nblocks * 4, hipMemcpyHostToDevice, c->stream);
             if (e != hipSuccess) return hip_fail(c, e, "coefficient upload");
             for (int q = d.fuse420 ? 1 : 0; q < d.ncomp; q++)
-                d.plane[q] = (uint8_t*)c->dev.take((size_t)d.pw[q] * d.ph[q]);
+                d.plane[q] = (uint8_t*)c->dev.take((size_t)d.pw[q] * d.ph[q] + DEC_PLANE_SPARE);
             d.out = sub[k]->host_out ? (uint8_t*)c->dev.take(j.out_len) : j.out;
             d.ostride = d.ow * sub[k]->nch;
             d.tab = d_tab + k;
@@ -454,7 +454,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             it.nblocks = d.nblocks;
             size_t per = (it.dev_in ? 0 : align_up(scan_len, 256)) + align_up(it.ent_cap, 256) + it.ntiles * 8 + 512 +
                          (size_t)d.nseg_max * 4 + (size_t)d.nblocks * (128 + 4) + sizeof(DecTab) + 4096;
-            for (int k = 0; k < 4; k++) per += align_up((size_t)d.pw[k] * d.ph[k], 256);
+            for (int k = 0; k < 4; k++) per += align_up((size_t)d.pw[k] * d.ph[k] + DEC_PLANE_SPARE, 256);
             per += (size_t)(it.ent_cap * 8 / 2048 + 2) * (8 + 2 + 4 + 4);  // subsequence arrays at S >= 2048
             per += (size_t)(it.ent_cap * 8 / 2048 + 2) * DEC_CK_MAX * 8;  // checkpoints
             if (!coef_out && !is_device_ptr(it.job->out)) per += align_up(it.job->out_len, 256);
@@ -564,7 +564,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
             d.dc = (int32_t*)c->dev.take((size_t)d.nblocks * 4);
             if (!coef_out) {
                 for (int q = d.fuse420 ? 1 : 0; q < d.ncomp; q++)  // fuse420: luma stays in LDS
-                    d.plane[q] = (uint8_t*)c->dev.take((size_t)d.pw[q] * d.ph[q]);
+                    d.plane[q] = (uint8_t*)c->dev.take((size_t)d.pw[q] * d.ph[q] + DEC_PLANE_SPARE);
                 it.host_out = !is_device_ptr(it.job->out);
                 d.out = it.host_out ? (uint8_t*)c->dev.take(it.job->out_len) : it.job->out;
                 d.ostride = d.ow * it.nch;

@@ -206,9 +206,13 @@ ICX_HD int dec_walk_mcu(int ncomp, int nbmcu, const int* td, const int* ta)
 static_assert(offsetof(DecTab, qt) % 16 == 0 && sizeof(DecTab) % 16 == 0, "DecTab.qt rows 16-byte aligned");
 
 // k_dec_idct work items per image: tiles of 32 blocks (nblk_tiles),
+// Bytes past each IDCT plane: k_dec_idct stores a dummy block's rows there
+// (jdcoefct.c transforms no dummy block) so that every lane stores on every
+// path.
+constexpr int DEC_PLANE_SPARE = 64;
 // DEC_IDCT_TILES consecutive tiles per workgroup.
 #ifndef ICX_DEC_IDCT_TILES
-#define ICX_DEC_IDCT_TILES 1
+#define ICX_DEC_IDCT_TILES 2  // with ICX_DEC_IDCT_PF: 1 / 2 / 4 tiles 3.86 / 3.40 / 3.62 ms per 1000 frames (ab_r5at_dec_idct_pipe.txt)
 #endif
 constexpr int DEC_IDCT_TILES = ICX_DEC_IDCT_TILES;  // 4: +20 % (r4e) - one tile per workgroup at 8 per CU overlaps
 ICX_HD long long dec_idct_items(long long nblk_tiles)

@@ -1288,6 +1288,9 @@ __device__ __forceinline__ IdctBlk idct_blk(const DecDesc& d, int i)
     return r;
 }
 
+#ifndef ICX_DEC_IDCT_PF
+#define ICX_DEC_IDCT_PF 1  // > 0: the pipelined tile loop below, loads this many tiles ahead (0: the loop before it)
+#endif
 __global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecState* S, Plan p)
 {
     __shared__ int32_t ws[32][8 * 9];
@@ -1307,6 +1310,40 @@ __global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecSta
     const int pw[4] = {d.pw[0], d.pw[1], d.pw[2], d.pw[3]};
     int tile = (int)wg * DEC_IDCT_TILES;
     if (tile >= ntile) return;
+#if ICX_DEC_IDCT_PF
+    // as k_dec_luma_color_420: the tile loop unrolled, each tile's loads in
+    // registers of their own issued IDCT_PF tiles ahead (tile index clamped,
+    // no branch around them), and one store per lane on every path (a dummy
+    // block's rows go to the plane's spare bytes), so the compiler's wait for
+    // a tile's loads does not wait for the previous tiles' stores
+    constexpr int T = DEC_IDCT_TILES, PF = ICX_DEC_IDCT_PF;
+    IdctBlk B[T];
+    uint4 Q[T], QT[T];
+    int32_t DCv[T];
+    auto fetch = [&](int k, int tl) {
+        B[k] = idct_blk(d, tl * 32 + lb);
+        const int64_t bb = B[k].b < d.nblocks ? B[k].b : 0;
+        Q[k] = *(const ICX_GLOBAL uint4*)(coefs + bb * 64 + r * 8);
+        DCv[k] = dcs[bb];
+        QT[k] = *(const ICX_GLOBAL uint4*)(qts + B[k].comp * 64 + r * 8);
+    };
+#pragma unroll
+    for (int k = 0; k < PF && k < T; k++) fetch(k, min(tile + k, ntile - 1));
+#pragma unroll
+    for (int it = 0; it < T; it++, tile++) {
+        if (tile >= ntile) break;  // workgroup-uniform
+        if (it + PF < T) fetch(it + PF < T ? it + PF : 0, min(tile + PF, ntile - 1));
+        const IdctBlk& cb = B[it];
+        const uint2 row = idct_row_of(Q[it], DCv[it], QT[it], r, cb.real, ws[lb]);
+        // a lane past the image's blocks has no component of its own: the
+        // spare bytes of a plane this launch always has (fuse420: no luma plane)
+        const int c = cb.real ? cb.comp : d.fuse420 ? 1 : 0;
+        ICX_GLOBAL uint8_t* const dst = cb.real ? planes[c] + (int64_t)(cb.by * 8 + r) * pw[c] + cb.bx * 8
+                                                : planes[c] + (int64_t)pw[c] * d.ph[c] + r * 8;
+        *(ICX_GLOBAL uint2*)dst = row;
+    }
+    return;
+#endif
     // i < 2^31: at most 65535^2 * 3 / 64 blocks
     IdctBlk cb = idct_blk(d, tile * 32 + lb);
     const int64_t b0 = cb.b < d.nblocks ? cb.b : 0;
