@@ -1224,12 +1224,16 @@ ICX_HD DecLeanWriter<LeanPtr> dec_lean_writer(const DecDesc& d, LeanPtr H, const
 constexpr int DEC_CK_DIV = ICX_DEC_CK_DIV;
 static_assert(DEC_CK_DIV >= 8, "shorter subsequences use 8 intervals");
 constexpr int DEC_CK_MAX = DEC_CK_DIV - 1;
+#ifndef ICX_DEC_CK_SMALL_DIV
+#define ICX_DEC_CK_SMALL_DIV 8  // intervals below 65536-bit subsequences (at least 2048 bits each); 16: +0.3 ms at 200 frames, +-0 at 64 (ab_r5av_dec_ck_small16.txt)
+#endif
+static_assert(ICX_DEC_CK_SMALL_DIV <= DEC_CK_DIV, "checkpoint slots");
 constexpr uint64_t DEC_CK_NONE = ~0ull;
 constexpr uint64_t DEC_CK_STATE = (1ull << 48) - 1;
 ICX_HD uint32_t dec_ck_bits(uint32_t sub_bits)
 {
     if (sub_bits >= 65536) return sub_bits / DEC_CK_DIV;
-    return sub_bits / 8 > 2048 ? sub_bits / 8 : 2048;
+    return sub_bits / ICX_DEC_CK_SMALL_DIV > 2048 ? sub_bits / ICX_DEC_CK_SMALL_DIV : 2048;
 }
 ICX_HD int dec_ck_slots(uint32_t sub_bits)
 {
