@@ -411,8 +411,8 @@ def e2e_cpu_baseline(srcs, n_sample, threads):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--images", type=int, default=1000, help="4K frames per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="4K frames for the CPU baseline (0 = 20 per host core, at least 320: ~10 s of wall time)")
