@@ -30,8 +30,12 @@ def emu():
     srcs = [os.path.join(ROOT, "tests", "dec_emu.cpp"), os.path.join(CSRC, "icx_jpeg_parse.cpp")]
     deps = srcs + [os.path.join(CSRC, "icx_decode.h"), os.path.join(CSRC, "icx_jpeg_parse.h")]
     if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(f) for f in deps):
-        subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", CSRC] + flags + ["-o", lib] + srcs,
+        # built under a name of this process, then renamed into place: test
+        # workers running side by side (pytest -n) never load a half-written file
+        tmp = "%s.%d.tmp" % (lib, os.getpid())
+        subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", CSRC] + flags + ["-o", tmp] + srcs,
                        check=True)
+        os.replace(tmp, lib)
     L = ctypes.CDLL(lib)
     L.dec_emu_coefs.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                 ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
