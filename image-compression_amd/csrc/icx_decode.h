@@ -1219,7 +1219,7 @@ ICX_HD DecLeanWriter<LeanPtr> dec_lean_writer(const DecDesc& d, LeanPtr H, const
 // (32768 bits) 16 intervals of 2048 bits cost +0.3 ms, so the shorter
 // subsequences keep 8 (profiles/r5/ab_r5w_dec_ck.txt).
 #ifndef ICX_DEC_CK_DIV
-#define ICX_DEC_CK_DIV 16
+#define ICX_DEC_CK_DIV 16  // 8 / 32: +0.7 / +1.6 ms per 1000 frames (ab_r5x_dec_ck16.txt, ab_r5ay_dec_ck32.txt)
 #endif
 constexpr int DEC_CK_DIV = ICX_DEC_CK_DIV;
 static_assert(DEC_CK_DIV >= 8, "shorter subsequences use 8 intervals");
