@@ -589,7 +589,7 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         for (int k = 0; k < m; k++) {
             cnt_tiles[k] = (sub[k]->ntiles + DEC_SCATTER_TILES - 1) / DEC_SCATTER_TILES;  // k_unstuff_scatter
             cnt_ctiles[k] = (sub[k]->ntiles + DEC_UNSTUFF_TILES - 1) / DEC_UNSTUFF_TILES;  // k_unstuff_count
-            cnt_subs[k] = (desc[k].nsub_max + 1 + 255) / 256;
+            cnt_subs[k] = (desc[k].nsub_max + 1 + DEC_SYNC_NT - 1) / DEC_SYNC_NT;
             cnt_pieces[k] = ((int64_t)(desc[k].nsub_max + 1) * dec_pieces(S) + DEC_WRITE_NT - 1) / DEC_WRITE_NT;  // k_dec_write
             // colour: luma IDCT fused with upsampling + conversion for s == 1 4:2:0 fancy (chroma
             // blocks alone go through k_dec_idct), the per-pixel gather kernel otherwise

@@ -311,7 +311,14 @@ constexpr int DEC_WIN_MAX = DEC_WIN > DEC_WIN_WRITE ? DEC_WIN : DEC_WIN_WRITE;
 #ifndef ICX_DEC_LDS_WIN_WRITE
 #define ICX_DEC_LDS_WIN_WRITE 0  // +4.6 ms: 10 KiB more LDS per workgroup leaves 3 workgroups per CU, not 4 (ab_r5ah)
 #endif
-constexpr int DEC_WIN_NT = 256;  // workgroup size of the kernels that walk
+// Workgroup size of the state-only walks (k_dec_init, k_dec_sync): their
+// LDS is the image's tables (16 KiB, once per workgroup) plus the lanes'
+// windows, so larger workgroups share the tables among more waves.
+#ifndef ICX_DEC_SYNC_NT
+#define ICX_DEC_SYNC_NT 256  // 512 (8 waves per SIMD): first sync walk 12.1 -> 12.85 ms per 1000 frames, slower at 64 frames (ab_r5ba_dec_sync_nt512.txt)
+#endif
+constexpr int DEC_SYNC_NT = ICX_DEC_SYNC_NT;
+constexpr int DEC_WIN_NT = DEC_SYNC_NT;  // workgroup size of the kernels whose windows are in LDS
 
 #if defined(__HIP_DEVICE_COMPILE__)
 #define ICX_LDS __attribute__((address_space(3)))

@@ -711,7 +711,7 @@ __device__ __forceinline__ uint32_t selector(const DecTab* T);
 #define DEC_WALK_H(T) ((const DecLean*)L)
 #endif
 
-__global__ void __launch_bounds__(256) k_dec_init(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
+__global__ void __launch_bounds__(DEC_SYNC_NT) k_dec_init(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
                                                   uint32_t warm)
 {
     DEC_WALK_TABLES
@@ -721,8 +721,8 @@ __global__ void __launch_bounds__(256) k_dec_init(const DecDesc* D, const DecSta
     const int img = p.ids[slot];
     const DecDesc& d = D[img];
     const DecState& st = S[img];
-    const int64_t j = wg * 256 + threadIdx.x;
-    const bool live = st.status == 0 && wg * 256 < (int64_t)st.nsub;
+    const int64_t j = wg * DEC_SYNC_NT + threadIdx.x;
+    const bool live = st.status == 0 && wg * DEC_SYNC_NT < (int64_t)st.nsub;
     if (live) DEC_WALK_LOAD(d.tab);
     if (j > d.nsub_max) return;
     const uint32_t start = (uint32_t)j * sub_bits;
@@ -767,7 +767,7 @@ __device__ __forceinline__ uint32_t selector(const DecTab* T)
 }
 
 // One relaxation launch.  Launch 0 walks every subsequence; launch r > 0 walks
-// the worklist launch r-1 built (entry k of workgroup w: wl[r & 1][256 w + k]),
+// the worklist launch r-1 built (entry k of workgroup w: wl[r & 1][DEC_SYNC_NT w + k]),
 // so the few subsequences still moving fill whole waves.  A thread whose exit
 // differs from the stored next entry stores it and appends j + 1 to the next
 // worklist (only thread j writes E[j+1], so entries are unique per launch).
@@ -777,7 +777,7 @@ __device__ __forceinline__ uint32_t selector(const DecTab* T)
 #define ICX_DEC_AGG 0  // k_dec_sync: wave-aggregated worklist / change-count atomics (+-0: few lanes change)
 #endif
 template <bool FIRST>
-__global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
+__global__ void __launch_bounds__(DEC_SYNC_NT) k_dec_sync(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
                                                   int iter, int nimg, uint32_t* changed)
 {
     DEC_WALK_TABLES
@@ -788,9 +788,9 @@ __global__ void __launch_bounds__(256) k_dec_sync(const DecDesc* D, const DecSta
     const DecDesc& d = D[img];
     const DecState& st = S[img];
     if (st.status) return;
-    const int64_t k = wg * 256 + threadIdx.x;
+    const int64_t k = wg * DEC_SYNC_NT + threadIdx.x;
     const uint32_t n = FIRST ? st.nsub : d.wl_cnt[(int64_t)(iter - 1) * nimg + img];
-    if (wg * 256 >= (int64_t)n) return;
+    if (wg * DEC_SYNC_NT >= (int64_t)n) return;
     DEC_WALK_LOAD(d.tab);
     if (k >= n) return;
     const uint32_t j = FIRST ? (uint32_t)k : d.wl[iter & 1][k];
@@ -1844,14 +1844,14 @@ void launch_unstuff(const DecDesc* d, DecState* s, const Plan& cnt, int64_t ncnt
 void launch_dec_init(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
                      uint32_t warm, hipStream_t st)
 {
-    if (nwg > 0) hipLaunchKernelGGL(k_dec_init, grid_of(subs, nwg), dim3(256), 0, st, d, s, subs, sub_bits, warm);
+    if (nwg > 0) hipLaunchKernelGGL(k_dec_init, grid_of(subs, nwg), dim3(DEC_SYNC_NT), 0, st, d, s, subs, sub_bits, warm);
 }
 
 void launch_dec_sync(const DecDesc* d, const DecState* s, const Plan& subs, int64_t nwg, uint32_t sub_bits,
                      int iter, int nimg, uint32_t* changed, hipStream_t st)
 {
     if (nwg > 0)
-        hipLaunchKernelGGL(iter == 0 ? k_dec_sync<true> : k_dec_sync<false>, grid_of(subs, nwg), dim3(256), 0, st,
+        hipLaunchKernelGGL(iter == 0 ? k_dec_sync<true> : k_dec_sync<false>, grid_of(subs, nwg), dim3(DEC_SYNC_NT), 0, st,
                            d, s, subs, sub_bits, iter, nimg, changed);
 }
 
