@@ -600,16 +600,23 @@ __device__ __forceinline__ void store_list_meta(const ImgDesc& D, int64_t base, 
 #if ICX_FDCT_STATIC
     if (WAVE) {
         // every lane stores (the compiler counts the stores on every path):
-        // a lane without a block of its own stores its wave's last block -
-        // or the tile's last - again, the same bytes to the same address
-        const int lim = min((int)(threadIdx.x >> 6) * (GPW * STEP) + GPW * STEP, nblk) - 1;
-        int t = (threadIdx.x >> 6) * (GPW * STEP) + (threadIdx.x & 63);
-        t = t < lim ? t : lim >= 0 ? lim : nblk - 1;
-        const uint32_t m = L.meta[t];
+        // a lane without a block of its own stores its wave's last block
+        // again, the same bytes to the same address.  A wave with no block in
+        // this (edge) tile owns nothing it could repeat - the tile's last
+        // block is another wave's, whose meta it may read before the owner
+        // writes it (no barrier between waves) - so its lanes store to the
+        // image's dummy slot past the padded block arrays (never read).
+        const int w0 = (int)(threadIdx.x >> 6) * (GPW * STEP);
+        const bool dead = w0 >= nblk;  // wave-uniform
+        const int lim = min(w0 + GPW * STEP, nblk) - 1;
+        int t = w0 + (int)(threadIdx.x & 63);
+        t = dead ? w0 : t < lim ? t : lim;
+        const uint32_t m = L.meta[t];  // (a dead wave reads its own stale entry: unused)
+        const uint32_t at = dead ? (uint32_t)D.nchunks * CHUNK_BLOCKS : bbase + (uint32_t)t;
         // global, not flat, stores: a flat store counts on the LDS counter too,
         // and the next tile's LDS waits would wait for it
-        gp(D.ncoef)[bbase + t] = (uint8_t)(m & 127);
-        gp(D.coff)[bbase + t] = (uint32_t)((base + (t / (GPW * STEP)) * (GPW * STEP * COEF_SLOTS)) >> 2) + (m >> 7);
+        gp(D.ncoef)[at] = (uint8_t)(m & 127);
+        gp(D.coff)[at] = (uint32_t)((base + (t / (GPW * STEP)) * (GPW * STEP * COEF_SLOTS)) >> 2) + (m >> 7);
         return;
     }
 #endif

@@ -608,7 +608,7 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
         ImgDesc g{};
         geometry(g, j.img.width, j.img.height, j.img.fmt);
         const size_t px = (size_t)j.img.width * j.img.height * channels(j.img.fmt);
-        size_t per = coef_bytes(g) + (size_t)g.nchunks * CHUNK_BLOCKS * 5 + (size_t)g.nblocks * BLOCK_WORDS * 4 + 1024 +
+        size_t per = coef_bytes(g) + ((size_t)g.nchunks * CHUNK_BLOCKS + 1) * 5 + 512 + (size_t)g.nblocks * BLOCK_WORDS * 4 + 1024 +
                      2 * ((size_t)g.nchunks * CHUNK_WORDS + 1) * 4 +
                      (size_t)g.nchunks * (2 * 4 + 2 * 8 + 2 * 4 + 2 * 32 + 8) + 64 + 8 * 256 + 4096;
         if (mode == Mode::Fit) per += px;  // resize buffer
@@ -783,8 +783,8 @@ icx_status run_batch(icx_ctx* c, icx_fit_job* jobs, int n, Mode mode, int16_t* f
             d.stride = j.img.stride;
             d.target = j.target_max_size;
             d.coefs = (int32_t*)c->dev.take(coef_bytes(d));
-            d.coff = (uint32_t*)c->dev.take((size_t)d.nchunks * CHUNK_BLOCKS * 4);
-            d.ncoef = (uint8_t*)c->dev.take((size_t)d.nchunks * CHUNK_BLOCKS);
+            d.coff = (uint32_t*)c->dev.take(((size_t)d.nchunks * CHUNK_BLOCKS + 1) * 4);  // + the dummy slot (store_list_meta)
+            d.ncoef = (uint8_t*)c->dev.take((size_t)d.nchunks * CHUNK_BLOCKS + 1);
             d.ovf = (uint32_t*)c->dev.take((size_t)d.nblocks * BLOCK_WORDS * 4 + 1024);
             for (int b = 0; b < 2; b++) {
                 d.scratch[b] = (uint32_t*)c->dev.take(((size_t)d.nchunks * CHUNK_WORDS + 1) * 4);

@@ -647,3 +647,24 @@ def test_upload_from_a_reader_thread_during_a_call(codec):
     assert not errs
     for s, d in zip(src, dst):
         assert np.array_equal(d.numpy(), s.array)
+
+
+def test_edge_tile_dead_waves_repeated(codec, oracle):
+    """Widths whose right-edge FDCT tile leaves whole waves without a block
+    (1920 px: 8 MCUs in the last tile, waves 2 and 3 empty; 200 px: 7 MCUs)
+    encoded repeatedly in one batch: a dead wave must not store a block's list
+    metadata it does not own.  The last block of every edge tile
+    is checked through the bitstream, byte-exact against the oracle."""
+    imgs, refs = [], []
+    for i in range(8):
+        for h, w in ((1080, 1920), (136, 200), (72, 968)):
+            img = noise(h, w, 900 + i) if i % 2 else smooth(h, w, 900 + i)
+            imgs.append(img)
+    cached = [icx.LearnedParams(0.5, 1.0)] * len(imgs)
+    for rep in range(3):
+        res = codec.fit(imgs, 1 << 30, 0.5, cached=cached)
+        for k, (img, r) in enumerate(zip(imgs, res)):
+            if rep == 0:
+                refs.append(oracle.encode(img, 0.5))
+            assert r["status"] == N.OK and r["success"] and r["cache_hit"], (rep, k)
+            assert r["data"] == refs[k], (rep, k, img.shape)
