@@ -107,8 +107,12 @@ long oracle_fit_batch(int n, const uint8_t* const* px, const int* w, const int* 
                       int nthreads, int64_t* out_sizes, float* out_q, double* out_scale);
 
 /* ---- A11 decode (icx_oracle_decode.c): IJG 6b baseline decompression as the
- * JDK JPEGImageReader runs it (ImageCompression.java:113-155).  Status codes
- * as include/icx.h: 0 ok, 4 cap too small, 5 unsupported, 6 corrupt. */
+ * JDK JPEGImageReader runs it (ImageCompression.java:113-155), including
+ * libjpeg's recovery from damaged entropy data (truncation, bad codes,
+ * restart markers out of sequence).  Status codes as include/icx.h: 0 ok,
+ * 4 cap too small, 5 not read here (the host reader reads it), 6 corrupt
+ * (the JDK reader throws), 8 refused (arithmetic / hierarchical / not 8-bit:
+ * the JDK reader throws at read()). */
 int oracle_jpeg_info(const uint8_t* jpg, size_t len, int* w, int* h, int* ncomp);
 /* blocks in the scan (MCU order, dummy blocks included); -1 if unparsable */
 long oracle_jpeg_num_blocks(const uint8_t* jpg, size_t len);
@@ -117,6 +121,8 @@ int oracle_jpeg_coefs(const uint8_t* jpg, size_t len, int16_t* coefs, size_t nbl
 /* decode + source subsampling s: ceil(W/s) x ceil(H/s), BGR24 or GRAY8, packed */
 int oracle_jpeg_decode(const uint8_t* jpg, size_t len, int s, uint8_t* out, size_t cap, int* w,
                        int* h, int* fmt);
+/* 3-component file: its luma samples alone, W x H (JCS_GRAYSCALE output) */
+int oracle_jpeg_decode_luma(const uint8_t* jpg, size_t len, uint8_t* out, size_t cap, int* w, int* h);
 /* 4-component (CMYK / YCCK) file: libjpeg's CMYK samples, W x H x 4 */
 int oracle_jpeg_decode_cmyk(const uint8_t* jpg, size_t len, uint8_t* out, size_t cap, int* w, int* h);
 

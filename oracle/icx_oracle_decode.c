@@ -39,11 +39,14 @@
 #include "icx_oracle.h"
 
 typedef struct {
-    uint16_t maxcode_ok[18];
-    int32_t maxcode[18]; /* largest code of length l, -1 if none */
+    int32_t maxcode[18]; /* largest code of length l, -1 if none; [17] ends the search */
     int32_t valoff[17];  /* huffval index of the first code of length l minus that code */
     uint8_t vals[256];
+    int nvals;
+    uint8_t look_nbits[256]; /* jdhuff.c HUFF_LOOKAHEAD (8) tables: length of the code */
+    uint8_t look_sym[256];   /* starting with these 8 bits (0: longer / none), its symbol */
     int present;
+    int bad; /* fails jpeg_make_d_derived_tbl: an error only if the scan uses it */
 } dhuff_t;
 
 typedef struct {
@@ -69,24 +72,31 @@ static const int ZZ_NAT[64 + 16] = {
 
 static int build_dhuff(const uint8_t* counts, const uint8_t* vals, int nvals, dhuff_t* t)
 {
+    /* jdhuff.c jpeg_make_d_derived_tbl: canonical codes, length by length; the
+     * codes of a length must leave room below the all-ones code (code < 2^l
+     * after them), else JERR_BAD_HUFF_TABLE */
     int code = 0, k = 0;
     memset(t, 0, sizeof(*t));
     for (int l = 1; l <= 16; l++) {
         int n = counts[l - 1];
         t->valoff[l] = k - code;
-        if (n) {
-            code += n;
-            k += n;
-            t->maxcode[l] = code - 1;
-        } else {
-            t->maxcode[l] = -1;
+        for (int i = 0; i < n; i++, code++, k++) {
+            if (l <= 8) { /* look-ahead entries of every 8-bit string starting with this code */
+                int lb = code << (8 - l);
+                for (int f = 0; f < (1 << (8 - l)); f++) {
+                    t->look_nbits[lb + f] = (uint8_t)l;
+                    t->look_sym[lb + f] = vals[k];
+                }
+            }
         }
-        if (code > (1 << l)) return 6; /* over-subscribed */
+        t->maxcode[l] = n ? code - 1 : -1;
+        if (code >= (1 << l)) return 6;
         code <<= 1;
     }
-    t->maxcode[17] = 0x7FFFFFFF;
+    t->maxcode[17] = 0xFFFFF; /* jdhuff.c: ensures jpeg_huff_decode terminates */
     if (k != nvals) return 6;
     memcpy(t->vals, vals, (size_t)nvals);
+    t->nvals = nvals;
     t->present = 1;
     return 0;
 }
@@ -164,12 +174,21 @@ static int parse(const uint8_t* p, size_t len, jinfo_t* J)
                 int tot = 0;
                 for (int l = 0; l < 16; l++) tot += s[o + 1 + l];
                 if (tot > 256 || o + 17 + (size_t)tot > n) return 6;
-                int rc = build_dhuff(s + o + 1, s + o + 17, tot, tc ? &J->ac[th] : &J->dc[th]);
-                if (rc) return rc;
+                dhuff_t* t = tc ? &J->ac[th] : &J->dc[th];
+                if (build_dhuff(s + o + 1, s + o + 17, tot, t)) {
+                    memset(t, 0, sizeof(*t));
+                    t->present = t->bad = 1;
+                }
                 o += 17 + (size_t)tot;
             }
         } else if (m == 0xC0 || m == 0xC1) { /* SOF0 / SOF1: sequential Huffman */
-            if (n < 6 || s[0] != 8) return 5;
+            if (n < 6) return 6;
+            if (s[0] != 8) { /* jdinput.c initial_setup: JERR_BAD_PRECISION (6b is built 8-bit) */
+                J->h = (s[1] << 8) | s[2];
+                J->w = (s[3] << 8) | s[4];
+                J->ncomp = s[5];
+                return 8;
+            }
             J->h = (s[1] << 8) | s[2];
             J->w = (s[3] << 8) | s[4];
             J->ncomp = s[5];
@@ -185,11 +204,18 @@ static int parse(const uint8_t* p, size_t len, jinfo_t* J)
             }
             have_sof = 1;
         } else if ((m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC)) {
-            if (n >= 6) { /* progressive / lossless / arithmetic: dims only */
+            if (n >= 6) { /* progressive / lossless / hierarchical / arithmetic: dims only */
                 J->h = (s[1] << 8) | s[2];
                 J->w = (s[3] << 8) | s[4];
                 J->ncomp = s[5];
             }
+            /* refused by the JDK's 6b reader: arithmetic coding (SOF9-11:
+             * jdmaster.c JERR_ARITH_NOTIMPL), hierarchical (SOF5-7, 13-15:
+             * jdmarker.c JERR_SOF_UNSUPPORTED), a progressive file of another
+             * precision (JERR_BAD_PRECISION).  SOF2 (8-bit) and SOF3
+             * (lossless: TwelveMonkeys' own decoder) are read, just not here */
+            if (m != 0xC2 && m != 0xC3) return 8;
+            if (m == 0xC2 && n >= 1 && s[0] != 8) return 8;
             return 5;
         } else if (m == 0xDD) { /* DRI */
             if (n < 2) return 6;
@@ -234,8 +260,14 @@ static int parse(const uint8_t* p, size_t len, jinfo_t* J)
         if (cs < 0) return 5;
         J->rgb = cs;
         if (J->hs[1] != 1 || J->vs[1] != 1 || J->hs[2] != 1 || J->vs[2] != 1) return 5;
-        if (J->hs[0] > 2 || J->vs[0] > 2) return 5;
-        if (J->hs[0] == 1 && J->vs[0] == 2) return 5;
+        /* Y 1x1, 2x1, 2x2 (fancy upsampling), 1x2 (4:4:0) and 4x1 (4:1:1):
+         * int_upsample replication (jdsample.c jinit_upsampler) */
+        {
+            const int hy = J->hs[0], vy = J->vs[0];
+            if (!((hy == 1 && vy == 1) || (hy == 2 && vy == 1) || (hy == 2 && vy == 2) || (hy == 1 && vy == 2) ||
+                  (hy == 4 && vy == 1)))
+                return 5;
+        }
         J->hmax = J->hs[0];
         J->vmax = J->vs[0];
         J->mcux = (J->w + 8 * J->hmax - 1) / (8 * J->hmax);
@@ -247,6 +279,11 @@ static int parse(const uint8_t* p, size_t len, jinfo_t* J)
     }
     for (int c = 0; c < J->ncomp; c++) {
         if (!J->qt_present[J->tq[c]] || !J->dc[J->td[c]].present || !J->ac[J->ta[c]].present) return 6;
+        if (J->dc[J->td[c]].bad || J->ac[J->ta[c]].bad) return 6;
+        /* jdhuff.c jpeg_make_d_derived_tbl: a DC table's symbols are 0..15 */
+        const dhuff_t* t = &J->dc[J->td[c]];
+        for (int k = 0; k < t->nvals; k++)
+            if (t->vals[k] > 15) return 6;
     }
     return 0;
 }
@@ -255,7 +292,7 @@ int oracle_jpeg_info(const uint8_t* jpg, size_t len, int* w, int* h, int* ncomp)
 {
     jinfo_t J;
     int rc = parse(jpg, len, &J);
-    if (rc == 0 || rc == 5) {
+    if (rc == 0 || rc == 5 || rc == 8) {
         if (w) *w = J.w;
         if (h) *h = J.h;
         if (ncomp) *ncomp = J.ncomp;
@@ -263,118 +300,197 @@ int oracle_jpeg_info(const uint8_t* jpg, size_t len, int* w, int* h, int* ncomp)
     return rc;
 }
 
-/* ----------------------------------------------------- jdhuff.c bit reader */
+/* ------------------------------------------- jdhuff.c + jdmarker.c (6b) */
+/* The entropy decoder reads the file from the first scan byte on through the
+ * JDK's source manager (imageioJPEG.c imageio_fill_input_buffer), which on
+ * end of stream warns and inserts a fake EOI marker (FF D9): past the end the
+ * bytes read FF D9 FF D9 ...  (Pillow's LOAD_TRUNCATED_IMAGES does the same,
+ * JpegImagePlugin.load_read, which is how libjpeg-turbo pins this below.) */
 typedef struct {
     const uint8_t* p;
     size_t len, pos;
-    uint64_t acc;
-    int nbits;
-    int hit_marker;
-} breader_t;
+    uint64_t buf;     /* get_buffer: the low `bits` bits are unread */
+    int bits;         /* bits_left */
+    int marker;       /* cinfo->unread_marker: 0, or the marker the reader stopped at */
+    int insufficient; /* entropy->insufficient_data */
+    int next_rst;     /* marker->next_restart_num */
+} src6_t;
 
-static void fill(breader_t* b)
+#define MIN_GET_BITS 25 /* jdhuff.h: BIT_BUF_SIZE (32) - 7 */
+
+static int rd_byte(src6_t* s)
 {
-    while (b->nbits <= 56) {
-        int v;
-        if (b->hit_marker || b->pos >= b->len) {
-            v = 0; /* jdhuff.c: past a marker / the end, feed zeros (with a warning) */
-            b->hit_marker = 1;
-        } else {
-            v = b->p[b->pos];
-            if (v == 0xFF) {
-                size_t q = b->pos + 1;
-                while (q < b->len && b->p[q] == 0xFF) q++;
-                if (q < b->len && b->p[q] == 0x00) {
-                    b->pos = q + 1;
+    size_t i = s->pos++;
+    if (i < s->len) return s->p[i];
+    return ((i - s->len) & 1) ? 0xD9 : 0xFF;
+}
+
+/* jpeg_fill_bit_buffer: load bytes up to MIN_GET_BITS bits unless a marker
+ * stops the reader (FF 00 is a data FF; FF FF... are fill bytes); once it has,
+ * a request for more bits than are left warns (JWRN_HIT_MARKER), sets
+ * insufficient_data and pads the buffer with zero bits. */
+static void fill6(src6_t* s, int nbits)
+{
+    if (!s->marker) {
+        while (s->bits < MIN_GET_BITS) {
+            int c = rd_byte(s);
+            if (c == 0xFF) {
+                do c = rd_byte(s);
+                while (c == 0xFF);
+                if (c == 0) {
+                    c = 0xFF;
                 } else {
-                    b->hit_marker = 1;
-                    v = 0;
+                    s->marker = c;
+                    break;
                 }
-            } else {
-                b->pos++;
             }
+            s->buf = (s->buf << 8) | (uint64_t)c;
+            s->bits += 8;
         }
-        b->acc |= (uint64_t)v << (56 - b->nbits);
-        b->nbits += 8;
+        if (!s->marker) return;
+    }
+    if (nbits > s->bits) {
+        s->insufficient = 1;
+        s->buf <<= MIN_GET_BITS - s->bits;
+        s->bits = MIN_GET_BITS;
     }
 }
 
-static inline int get_bits(breader_t* b, int n)
+static inline int get_bits6(src6_t* s, int n)
 {
-    if (n == 0) return 0;
-    if (b->nbits < n) fill(b);
-    int v = (int)(b->acc >> (64 - n));
-    b->acc <<= n;
-    b->nbits -= n;
-    return v;
+    s->bits -= n;
+    return (int)((s->buf >> s->bits) & ((1u << n) - 1));
 }
 
-static int decode_sym(breader_t* b, const dhuff_t* t)
+/* HUFF_DECODE + jpeg_huff_decode: the 8-bit look-ahead, else the canonical
+ * maxcode walk from 9 bits (from 1 bit when fewer than 8 are left).  A bad
+ * code (no match within 16 bits) has consumed 17 bits and decodes as symbol
+ * 0 (JWRN_HUFF_BAD_CODE: "fake a zero as the safest result"). */
+static int huff_decode6(src6_t* s, const dhuff_t* t)
 {
-    if (b->nbits < 16) fill(b);
-    int code = 0;
-    for (int l = 1; l <= 16; l++) {
-        code = (code << 1) | (int)(b->acc >> 63);
-        b->acc <<= 1;
-        b->nbits--;
-        if (code <= t->maxcode[l]) return t->vals[(t->valoff[l] + code) & 0xFF];
+    int l;
+    if (s->bits < 8) {
+        fill6(s, 0);
+        if (s->bits < 8) {
+            l = 1;
+            goto slow;
+        }
     }
-    return -1; /* bad Huffman code */
+    {
+        const int look = (int)((s->buf >> (s->bits - 8)) & 0xFF);
+        const int nb = t->look_nbits[look];
+        if (nb) {
+            s->bits -= nb;
+            return t->look_sym[look];
+        }
+        l = 9;
+    }
+slow:
+    if (s->bits < l) fill6(s, l);
+    int code = get_bits6(s, l);
+    while (code > t->maxcode[l]) {
+        code <<= 1;
+        if (s->bits < 1) fill6(s, 1);
+        code |= get_bits6(s, 1);
+        l++;
+    }
+    if (l > 16) return 0;
+    return t->vals[(t->valoff[l] + code) & 0xFF];
 }
 
 static inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
-/* After an interval: skip to the RSTn marker, reset the reader (jdhuff.c process_restart). */
-static int restart(breader_t* b)
+/* jdmarker.c next_marker: skip to the next FF, swallow fill FFs, skip FF 00
+ * data pairs, stop at a marker */
+static void next_marker6(src6_t* s)
 {
-    /* discard buffered bits; find the marker following the bytes consumed */
-    size_t q = b->pos;
-    while (q + 1 < b->len && !(b->p[q] == 0xFF && b->p[q + 1] >= 0xD0 && b->p[q + 1] <= 0xD7)) {
-        if (b->p[q] == 0xFF && b->p[q + 1] != 0x00 && b->p[q + 1] != 0xFF) return 6;
-        q++;
+    for (;;) {
+        int c = rd_byte(s);
+        while (c != 0xFF) c = rd_byte(s);
+        do c = rd_byte(s);
+        while (c == 0xFF);
+        if (c != 0) {
+            s->marker = c;
+            return;
+        }
     }
-    if (q + 1 >= b->len) return 6;
-    b->pos = q + 2;
-    b->acc = 0;
-    b->nbits = 0;
-    b->hit_marker = 0;
-    return 0;
+}
+
+/* jdmarker.c jpeg_resync_to_restart: the reader met marker `marker` where
+ * RST`desired` was due.  1: discard it and resume; 2: scan to the next marker
+ * and decide again; 3: leave it (the entropy decoder then sees an empty
+ * segment) */
+static void resync6(src6_t* s, int desired)
+{
+    for (;;) {
+        const int m = s->marker;
+        int action;
+        if (m < 0xC0) action = 2; /* invalid marker */
+        else if (m < 0xD0 || m > 0xD7) action = 3; /* a valid non-restart marker */
+        else if (m == 0xD0 + ((desired + 1) & 7) || m == 0xD0 + ((desired + 2) & 7)) action = 3;
+        else if (m == 0xD0 + ((desired - 1) & 7) || m == 0xD0 + ((desired - 2) & 7)) action = 2;
+        else action = 1; /* the desired restart, or too far away */
+        if (action == 1) {
+            s->marker = 0;
+            return;
+        }
+        if (action == 3) return;
+        next_marker6(s);
+    }
+}
+
+/* jdhuff.c process_restart: drop the bit buffer, read_restart_marker (the
+ * expected RSTn is swallowed, anything else resynchronises), reset the DC
+ * predictors; insufficient_data is cleared only when no marker is left
+ * pending (else the next segment is treated as empty) */
+static void process_restart6(src6_t* s, int* last_dc)
+{
+    s->bits = 0;
+    if (!s->marker) next_marker6(s);
+    if (s->marker == 0xD0 + s->next_rst) s->marker = 0;
+    else resync6(s, s->next_rst);
+    s->next_rst = (s->next_rst + 1) & 7;
+    last_dc[0] = last_dc[1] = last_dc[2] = last_dc[3] = 0;
+    if (!s->marker) s->insufficient = 0;
 }
 
 /* Decode the scan into quantised coefficients, natural order, scan (MCU) block
- * order including dummy blocks.  Returns 0 / 6. */
+ * order including dummy blocks, as jdhuff.c decode_mcu fills the zeroed
+ * MCU_buffer (jdcoefct.c decompress_onepass): once insufficient_data is set
+ * (bits wanted past a marker or the end of the file: the MCU being decoded
+ * finishes on zero bits) every later MCU of the segment stays zero, i.e.
+ * uniform grey; a bad Huffman code decodes as 0.  Never fails. */
 static int decode_scan(const jinfo_t* J, int16_t* coefs)
 {
-    breader_t b = {J->scan, J->scan_len, 0, 0, 0, 0};
+    src6_t s = {J->scan, J->scan_len, 0, 0, 0, 0, 0, 0};
     int nb_mcu = J->ncomp == 3 ? J->hs[0] * J->vs[0] + 2 : J->ncomp == 4 ? 4 : 1;
-    int comp_of[6];
+    int comp_of[10];
     for (int k = 0; k < nb_mcu; k++)
         comp_of[k] = J->ncomp == 1 ? 0 : J->ncomp == 4 ? k : (k < nb_mcu - 2 ? 0 : k - (nb_mcu - 3));
     long nmcu = (long)J->mcux * J->mcuy;
-    int pred[4] = {0, 0, 0, 0};
+    int last_dc[4] = {0, 0, 0, 0};
     int16_t* blk = coefs;
-    for (long m = 0; m < nmcu; m++) {
-        if (J->ri && m > 0 && m % J->ri == 0) {
-            if (restart(&b)) return 6;
-            pred[0] = pred[1] = pred[2] = pred[3] = 0;
-        }
-        for (int k = 0; k < nb_mcu; k++, blk += 64) {
-            int c = comp_of[k];
-            memset(blk, 0, 64 * sizeof(int16_t));
-            int s = decode_sym(&b, &J->dc[J->td[c]]);
-            if (s < 0 || s > 15) return 6;
-            if (s) s = extend(get_bits(&b, s), s);
-            pred[c] += s;
-            blk[0] = (int16_t)pred[c];
+    memset(coefs, 0, (size_t)nmcu * nb_mcu * 64 * sizeof(int16_t));
+    for (long m = 0; m < nmcu; m++, blk += 64 * nb_mcu) {
+        if (J->ri && m > 0 && m % J->ri == 0) process_restart6(&s, last_dc); /* restarts_to_go == 0 */
+        if (s.insufficient) continue;
+        for (int k = 0; k < nb_mcu; k++) {
+            const int c = comp_of[k];
+            int16_t* b = blk + 64 * k;
+            int v = huff_decode6(&s, &J->dc[J->td[c]]);
+            if (v) {
+                if (s.bits < v) fill6(&s, v);
+                v = extend(get_bits6(&s, v), v);
+            }
+            last_dc[c] += v;
+            b[0] = (int16_t)last_dc[c];
             for (int z = 1; z < 64; z++) {
-                int rs = decode_sym(&b, &J->ac[J->ta[c]]);
-                if (rs < 0) return 6;
-                int r = rs >> 4;
-                s = rs & 15;
-                if (s) {
+                const int rs = huff_decode6(&s, &J->ac[J->ta[c]]);
+                const int r = rs >> 4, sz = rs & 15;
+                if (sz) {
                     z += r;
-                    int v = extend(get_bits(&b, s), s);
-                    blk[ZZ_NAT[z]] = (int16_t)v;
+                    if (s.bits < sz) fill6(&s, sz);
+                    b[ZZ_NAT[z]] = (int16_t)extend(get_bits6(&s, sz), sz);
                 } else {
                     if (r != 15) break;
                     z += 15;
@@ -543,16 +659,20 @@ int oracle_jpeg_decode_cmyk(const uint8_t* jpg, size_t len, uint8_t* out, size_t
     return 0;
 }
 
-int oracle_jpeg_decode(const uint8_t* jpg, size_t len, int s, uint8_t* out, size_t cap, int* ow,
-                       int* oh, int* ofmt)
+/* luma_only: the first component's samples alone (GRAY8), as a reader asked
+ * for JCS_GRAYSCALE output of a YCbCr file gives them (jdcolor.c
+ * grayscale_convert) - what the 4:4:0 fixtures can pin */
+static int decode_impl(const uint8_t* jpg, size_t len, int s, uint8_t* out, size_t cap, int* ow, int* oh,
+                       int* ofmt, int luma_only)
 {
     jinfo_t J;
     int rc = parse(jpg, len, &J);
     if (rc) return rc;
     if (s < 1) return 1;
+    if (luma_only && J.ncomp != 3) return 1;
     int W = J.w, H = J.h;
     int dw = (W + s - 1) / s, dh = (H + s - 1) / s;
-    int nch = J.ncomp == 1 ? 1 : 3;
+    int nch = J.ncomp == 1 || luma_only ? 1 : 3;
     *ow = dw;
     *oh = dh;
     *ofmt = nch == 3 ? OR_BGR24 : OR_GRAY8;
@@ -612,12 +732,15 @@ int oracle_jpeg_decode(const uint8_t* jpg, size_t len, int s, uint8_t* out, size
     if (nch == 1) {
         for (int y = 0; y < dh; y++)
             for (int x = 0; x < dw; x++) out[(size_t)y * dw + x] = plane[0][(size_t)(y * s) * pw[0] + x * s];
-        free(plane[0]);
+        for (int c = 0; c < J.ncomp; c++) free(plane[c]);
         return 0;
     }
     /* upsample Cb/Cr to full width/height rows (jdsample.c), then convert */
     int hx = J.hmax, vy = J.vmax;
-    int fancy = cw[1] > 2; /* do_fancy && downsampled_width > 2 */
+    /* jdsample.c jinit_upsampler: h2v1 / h2v2 fancy when do_fancy &&
+     * downsampled_width > 2, their box versions otherwise; any other integral
+     * ratio (1x2 = 4:4:0, 4x1 = 4:1:1) int_upsample replication */
+    int fancy = hx == 2 && cw[1] > 2;
     int fullw = cw[1] * hx;
     int* up[2];
     up[0] = (int*)malloc(sizeof(int) * (size_t)fullw * 2);
@@ -628,11 +751,11 @@ int oracle_jpeg_decode(const uint8_t* jpg, size_t len, int s, uint8_t* out, size
             const uint8_t* P = plane[1 + k];
             int stride = pw[1 + k];
             int* o = up[k];
-            int r0 = vy == 2 ? Y >> 1 : Y;
+            int r0 = Y / vy;
             if (hx == 1 && vy == 1) {
                 for (int x = 0; x < cw[1]; x++) o[x] = P[(size_t)r0 * stride + x];
-            } else if (!fancy) { /* h2v1_upsample / h2v2_upsample: replication */
-                for (int x = 0; x < fullw; x++) o[x] = P[(size_t)r0 * stride + x / 2];
+            } else if (!fancy) { /* h2v1_upsample / h2v2_upsample / int_upsample: replication */
+                for (int x = 0; x < fullw; x++) o[x] = P[(size_t)r0 * stride + x / hx];
             } else if (vy == 1) { /* h2v1_fancy_upsample */
                 const uint8_t* in = P + (size_t)r0 * stride;
                 int n = cw[1];
@@ -689,4 +812,16 @@ int oracle_jpeg_decode(const uint8_t* jpg, size_t len, int s, uint8_t* out, size
     free(up[0]);
     for (int c = 0; c < 3; c++) free(plane[c]);
     return 0;
+}
+
+int oracle_jpeg_decode(const uint8_t* jpg, size_t len, int s, uint8_t* out, size_t cap, int* ow, int* oh,
+                       int* ofmt)
+{
+    return decode_impl(jpg, len, s, out, cap, ow, oh, ofmt, 0);
+}
+
+int oracle_jpeg_decode_luma(const uint8_t* jpg, size_t len, uint8_t* out, size_t cap, int* ow, int* oh)
+{
+    int fmt;
+    return decode_impl(jpg, len, 1, out, cap, ow, oh, &fmt, 1);
 }

@@ -59,6 +59,7 @@ class Oracle:
         L.oracle_jpeg_decode.argtypes = [c.c_void_p, c.c_size_t, c.c_int, c.c_void_p, c.c_size_t, P(c.c_int),
                                          P(c.c_int), P(c.c_int)]
         L.oracle_jpeg_decode_cmyk.argtypes = [c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t, P(c.c_int), P(c.c_int)]
+        L.oracle_jpeg_decode_luma.argtypes = [c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t, P(c.c_int), P(c.c_int)]
         L.oracle_set_table_layout.argtypes = [c.c_int]
         L.oracle_resize_indexed.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_void_p,
                                             c.c_int, c.c_int, c.c_int]
@@ -195,6 +196,18 @@ class Oracle:
         if rc:
             return rc, None
         return 0, out[:dw * dh * min(n, 3)].reshape((oh.value, ow.value, 3) if n >= 3 else (oh.value, ow.value))
+
+    def jpeg_decode_luma(self, data):
+        """(status, samples): a 3-component file's luma samples alone (H, W)."""
+        data = np.frombuffer(bytes(data), np.uint8)
+        rc, w, h, n = self.jpeg_info(data)
+        if rc:
+            return rc, None
+        out = np.empty(w * h, np.uint8)
+        ow, oh = ctypes.c_int(), ctypes.c_int()
+        rc = self.L.oracle_jpeg_decode_luma(data.ctypes.data, data.size, out.ctypes.data, out.size, ctypes.byref(ow),
+                                            ctypes.byref(oh))
+        return (rc, None) if rc else (0, out.reshape(h, w))
 
     def jpeg_decode_cmyk(self, data):
         """(status, samples): a 4-component file's CMYK samples (H, W, 4) as libjpeg outputs them."""
