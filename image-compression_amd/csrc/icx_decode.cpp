@@ -228,13 +228,16 @@ int host_threads()
     return std::max(1, std::min(n, 16));
 }
 
-// Progressive files (SOF2).  Each file's scans are entropy-decoded on a host
-// thread (icx_progressive.cpp: one sequential walk per scan) straight into
-// pinned staging, in the coefficient layout k_dec_write leaves for baseline
-// files; one copy per file takes the coefficients and DC values to HBM, and
-// the device's IDCT and colour passes (the same launches as the baseline
-// tail) produce the pixels.  Device-resident files are downloaded first.
-icx_status run_progressive(icx_ctx* c, std::vector<DecItem>& items, int16_t* coef_out, size_t coef_cap)
+// Files whose entropy decode runs on host threads: progressive files (SOF2,
+// icx_progressive.cpp: one sequential walk per scan), and sequential files
+// the device's decode flagged (icx_seqdecode.cpp: IJG 6b's recovery from
+// truncated scans, bad codes and restart markers out of sequence).  Each
+// file's coefficients go straight into pinned staging, in the layout
+// k_dec_write leaves for baseline files; one copy per file takes the
+// coefficients and DC values to HBM, and the device's IDCT and colour passes
+// (the same launches as the baseline tail) produce the pixels.
+// Device-resident files are downloaded first.
+icx_status run_host_entropy(icx_ctx* c, std::vector<DecItem>& items, int16_t* coef_out, size_t coef_cap)
 {
     size_t pos = 0;
     while (pos < items.size()) {
@@ -295,13 +298,19 @@ icx_status run_progressive(icx_ctx* c, std::vector<DecItem>& items, int16_t* coe
         if (U.overflow) return fail(c, ICX_E_NOMEM, "upload staging exhausted");
         std::vector<icx_status> st(m, ICX_OK);
         {
-            HostSpan hs{c, "host.dec_progressive"};
+            HostSpan hs{c, sub[0]->J.progressive ? "host.dec_progressive" : "host.dec_recovery"};
             std::atomic<int> next{0};
             auto work = [&]() {
                 for (int k; (k = next++) < m;) {
-                    memset(hco[k], 0, (size_t)desc[k].nblocks * 128);
+                    const JpegHeader& J = sub[k]->J;
                     h_tab[k] = DecTab{};
-                    st[k] = prog_decode(file[k], sub[k]->job->len, sub[k]->J, hco[k], hdc[k], h_tab[k].qt);
+                    if (J.progressive) {
+                        memset(hco[k], 0, (size_t)desc[k].nblocks * 128);
+                        st[k] = prog_decode(file[k], sub[k]->job->len, J, hco[k], hdc[k], h_tab[k].qt);
+                    } else {
+                        for (int q = 0; q < J.ncomp; q++) memcpy(h_tab[k].qt[q], J.qt[J.tq[q]], sizeof(h_tab[k].qt[q]));
+                        st[k] = seq_decode(file[k], sub[k]->job->len, J, hco[k], hdc[k]);
+                    }
                 }
             };
             const int nt = std::min(m, host_threads());
@@ -433,7 +442,8 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         (it.J.progressive ? prog : items).push_back(it);
     }
     if (!prog.empty())
-        if (icx_status s = run_progressive(c, prog, coef_out, coef_cap)) return s;
+        if (icx_status s = run_host_entropy(c, prog, coef_out, coef_cap)) return s;
+    std::vector<DecItem> recover;  // flagged by the device decode: icx_seqdecode.cpp
     size_t pos = 0;
     while (pos < items.size()) {
         // ---- size a sub-batch against the workspace budget
@@ -802,8 +812,8 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         for (int k = 0; k < m; k++) {
             icx_decode_job& j = *sub[k]->job;
             if (j.status != ICX_OK) continue;
-            if (h_state[k].status) {
-                j.status = ICX_E_CORRUPT;
+            if (h_state[k].status) {  // not the clean case: IJG 6b's recovery on a host thread
+                recover.push_back(*sub[k]);
                 continue;
             }
             if (coef_out) {
@@ -827,6 +837,10 @@ icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out
         e = hipStreamSynchronize(c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "output download");
         resolve_profile(c);
+    }
+    if (!recover.empty()) {
+        c->stats["dec_recovered"].units += (int64_t)recover.size();
+        if (icx_status s = run_host_entropy(c, recover, coef_out, coef_cap)) return s;
     }
     return ICX_OK;
 }

@@ -713,14 +713,18 @@ struct DecWalker {
             R.init(words, pos);
             return;
         }
-        // the interval's 1-bit padding (< 8 bits) or its pad bytes: next interval
+        // the interval's 1-bit padding (< 8 bits) or its pad bytes: next interval.
+        // A symbol that reached past the interval's data read pad bits (ones)
+        // where libjpeg reads zeros after setting insufficient_data: not the
+        // clean case either (seq_decode's)
+        if (OWNED && pos > bound) bad = true;
         if (nx == DEC_END) {
             pos = DEC_END;
             return;
         }
         // the true walk leaves interval k-1 after exactly its ri MCUs; an RSTn
-        // anywhere else (a stray or missing marker) is corrupt data, on which
-        // libjpeg's resynchronisation and zero fill would give other pixels
+        // anywhere else (a stray or missing marker) is damaged data, on which
+        // libjpeg's resynchronisation and zero fill give other pixels
         if (OWNED && ri > 0 && blk_base + (int64_t)n != (int64_t)k * ri * nbm) bad = true;
         pos = nx * 8;
         R.init(words, pos);
@@ -1173,6 +1177,7 @@ struct DecLeanWriter {
             R.init(words, pos);
             return;
         }
+        if (pos > bound) bad = true;  // read pad bits (DecWalker<true>::invalid)
         if (nx == DEC_END) {
             pos = DEC_END;
             return;
@@ -1180,6 +1185,19 @@ struct DecLeanWriter {
         if (ri > 0 && blk_base + (int64_t)n != (int64_t)k * ri * nbm) bad = true;
         pos = nx * 8;
         R.init(words, pos);
+    }
+    // After the walk: it stopped (at its exit mark) past the data of the
+    // interval its last symbol came from, i.e. that symbol read pad bits, and
+    // no invalid code followed to flag it.  A position exactly at an interval
+    // start is a jump (invalid() above), not a symbol's end: a symbol can
+    // reach at most 31 bits into the DEC_PAD bytes of all-ones.
+    ICX_HD bool overran() const
+    {
+        if (pos == DEC_END || pos == 0) return false;
+        uint32_t k;
+        const uint32_t nx = dec_next_seg(seg, nseg, (pos - 1) >> 3, &k);
+        const uint32_t bound = nx == DEC_END ? ent_bits : (nx - DEC_PAD) * 8;
+        return pos > bound && (nx == DEC_END || pos != nx * 8);
     }
 };
 

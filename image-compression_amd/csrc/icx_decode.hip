@@ -412,6 +412,10 @@ __global__ void __launch_bounds__(1024) k_unstuff_scan(const DecDesc* D, DecStat
         for (int k = threadIdx.x; k < DEC_TAIL + 8; k += blockDim.x) d.ent[len + k] = 0xFF;
     if (threadIdx.x == 0) {
         if (!fits) st.status = 6;
+        // the scan ends at a marker other than EOI: jpeg_finish_decompress
+        // reads the markers after it (the JDK reader throws on a bad one), a
+        // walk icx_seqdecode.cpp's route does - never the clean case's
+        if (end < d.scan_len && d.scan[end + 1] != 0xD9) st.status = 6;
         st.ent_len = len;
         st.nseg = carry_r + 1 <= (uint32_t)d.nseg_max ? carry_r + 1 : (uint32_t)d.nseg_max;
         if (carry_r + 1 > (uint32_t)d.nseg_max) st.status = 6;
@@ -959,11 +963,12 @@ __global__ void __launch_bounds__(DEC_WRITE_NT) k_dec_write(const DecDesc* D, De
     const SplitLean H{(const uint32_t (*)[1 << DEC_LUT_BITS])L1, (const ICX_GLOBAL DecLean*)d.tab->lean};
     DecLeanWriter<SplitLean> w = dec_lean_writer(d, H, d.tab->slow, selector(d.tab), (const uint32_t*)d.ent, d.seg,
                                                  st.nseg, st.ent_len * 8, pc.blk);
-    bool run = false;
+    bool run = false, started = false;
     if (pc.have) {
         run = !(dec_pos(pc.e) >= stop && (pc.e & 63) == 0);
         if (run) {
             w.start(pc.e);
+            started = true;
             run = w.running(stop);
         }
     }
@@ -1064,9 +1069,11 @@ __global__ void __launch_bounds__(DEC_WRITE_NT) k_dec_write(const DecDesc* D, De
     }
 #endif
     // The settled states are the true decode: an invalid code met on it
-    // (outside an interval's padding) means corrupt data (jdhuff.c warns and
-    // zero-fills there; the caller decides what to do with the file).
-    if (w.bad) atomicOr(&S[img].status, 6);
+    // (outside an interval's padding), a symbol reaching into the padding or
+    // an interval of the wrong length is damaged data (jdhuff.c warns,
+    // zero-fills and resynchronises there): the caller re-decodes the file
+    // with libjpeg's recovery (icx_seqdecode.cpp).
+    if (started && (w.bad || w.overran())) atomicOr(&S[img].status, 6);
 }
 
 // One workgroup per image: DC values from the differences the write pass left
@@ -1437,12 +1444,13 @@ __global__ void __launch_bounds__(256) k_dec_idct(const DecDesc* D, const DecSta
 
 // ----------------------------------------------------------- colour output
 // Upsampled chroma sample of component plane P at full-resolution (X, Y)
-// (jdsample.c: h2v2/h2v1 fancy when cw > 2, else replication; 1x1 direct).
+// (jdsample.c: h2v2/h2v1 fancy when cw > 2, else replication - also
+// int_upsample's for 1x2 (4:4:0) and 4x1 (4:1:1) luma; 1x1 direct).
 __device__ __forceinline__ int chroma_at(const DecDesc& d, const uint8_t* P, int pitch, int cw, int ch, int X, int Y)
 {
     if (d.hs == 1 && d.vs == 1) return P[(int64_t)Y * pitch + X];
+    if (!d.fancy) return P[(int64_t)(Y / d.vs) * pitch + X / d.hs];
     const int i = X >> 1;
-    if (!d.fancy) return P[(int64_t)(d.vs == 2 ? Y >> 1 : Y) * pitch + i];
     if (d.vs == 1) {  // h2v1_fancy_upsample
         const uint8_t* in = P + (int64_t)Y * pitch;
         const int c = in[i];

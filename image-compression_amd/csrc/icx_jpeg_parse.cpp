@@ -45,7 +45,8 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
     if (avail < 4) return ICX_E_BUFFER;
     if (p[0] != 0xFF || p[1] != 0xD8) return ICX_E_CORRUPT;
     size_t i = 2;
-    bool sof = false, unsupported = false, adobe = false, jfif = false, exif = false, saved_any = false;
+    bool sof = false, unsupported = false, refused = false, adobe = false, jfif = false, exif = false,
+         saved_any = false;
     int transform = 0;
     for (;;) {
         // next marker: skip non-0xFF garbage, then fill bytes (jdmarker.c next_marker)
@@ -109,7 +110,9 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
             J.h = (s[1] << 8) | s[2];
             J.w = (s[3] << 8) | s[4];
             J.ncomp = s[5];
-            if (s[0] != 8 || J.w == 0 || J.h == 0 || (J.ncomp != 1 && J.ncomp != 3 && J.ncomp != 4)) unsupported = true;
+            // jdinput.c initial_setup: JERR_BAD_PRECISION (the JDK's 6b is built for 8-bit samples)
+            if (s[0] != 8) refused = true;
+            if (J.w == 0 || J.h == 0 || (J.ncomp != 1 && J.ncomp != 3 && J.ncomp != 4)) unsupported = true;
             if (J.ncomp == 4 && J.progressive) unsupported = true;  // progressive CMYK / YCCK: the host reader
             if (J.ncomp >= 1 && J.ncomp <= 4) {
                 if (n < 6 + 3 * (size_t)J.ncomp) return ICX_E_CORRUPT;
@@ -140,6 +143,7 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
             break;
         case 0xDA: {  // SOS
             if (!sof) return ICX_E_CORRUPT;
+            if (refused) return ICX_E_REFUSED;
             if (unsupported) return ICX_E_UNSUPPORTED;
             const int ns = n >= 1 ? s[0] : 0;
             if (!J.progressive) {
@@ -166,7 +170,12 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
                 if (cs < 0) return ICX_E_UNSUPPORTED;
                 J.rgb = cs == 1;
                 if (J.hs[1] != 1 || J.vs[1] != 1 || J.hs[2] != 1 || J.vs[2] != 1) return ICX_E_UNSUPPORTED;
-                if (J.hs[0] > 2 || J.vs[0] > 2 || (J.hs[0] == 1 && J.vs[0] == 2)) return ICX_E_UNSUPPORTED;
+                // Y 1x1, 2x1, 2x2 (fancy upsampling when wide enough), 1x2 (4:4:0) and
+                // 4x1 (4:1:1): int_upsample replication (jdsample.c jinit_upsampler)
+                const int hy = J.hs[0], vy = J.vs[0];
+                if (!((hy == 1 && vy == 1) || (hy == 2 && vy == 1) || (hy == 2 && vy == 2) || (hy == 1 && vy == 2) ||
+                      (hy == 4 && vy == 1)))
+                    return ICX_E_UNSUPPORTED;
             }
             // progressive: tables may be (re)defined between scans; prog_decode checks each scan's
             if (!J.progressive)
@@ -176,13 +185,18 @@ icx_status parse_jpeg(const uint8_t* p, size_t avail, size_t total, JpegHeader& 
         }
         default:
             if (m >= 0xC3 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
-                // lossless / hierarchical / arithmetic: dimensions only
+                // lossless / hierarchical / arithmetic: dimensions only.  The
+                // reference's reader (TwelveMonkeys over the JDK's 6b) reads
+                // lossless files (SOF3) with its own decoder: the host reader's
+                // business; it refuses arithmetic coding (SOF9-11, jdmaster.c
+                // JERR_ARITH_NOTIMPL) and hierarchical files (SOF5-7, 13-15,
+                // jdmarker.c JERR_SOF_UNSUPPORTED): read() throws
                 if (n >= 6) {
                     J.h = (s[1] << 8) | s[2];
                     J.w = (s[3] << 8) | s[4];
                     J.ncomp = s[5];
                 }
-                return ICX_E_UNSUPPORTED;
+                return m == 0xC3 ? ICX_E_UNSUPPORTED : ICX_E_REFUSED;
             }
             break;  // APPn, COM, DNL: skipped (ignoreMetadata, ImageCompression.java:126)
         }
@@ -277,6 +291,9 @@ bool build_dec_tab(const JpegHeader& J, DecTab& T)
                 if (ntab == 4) return false;
                 sl = ntab++;
                 if (!build_dec_huff(J.hbits[ac][id], J.hvals[ac][id], J.hn[ac][id], T.h[sl], T.slow[sl])) return false;
+                if (!ac)  // jpeg_make_d_derived_tbl: DC symbols are 0..15 (12..15 the walks leave to seq_decode)
+                    for (int q = 0; q < J.hn[ac][id]; q++)
+                        if (J.hvals[ac][id][q] > 15) return false;
                 build_dec_lean(T.h[sl], ac != 0, T.lean[sl]);
             }
             T.sel[2 * c + ac] = (uint8_t)sl;

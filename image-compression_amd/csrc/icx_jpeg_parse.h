@@ -65,4 +65,14 @@ uint32_t dec_selector(const DecTab& T);
 icx_status prog_decode(const uint8_t* p, size_t len, const JpegHeader& J, int16_t* coefs, int32_t* dc,
                        uint16_t (*qt)[64]);
 
+// Entropy decode of a sequential Huffman file (icx_seqdecode.cpp) whose header
+// parse_jpeg accepted, with IJG 6b's recovery semantics (fake EOI at the end
+// of the file, zero MCUs after insufficient data, symbol 0 for a bad code,
+// jdmarker.c's restart resynchronisation): coefs (nblocks x 64, natural
+// order, MCU order as dec_geometry lays blocks out; DC value in [0]) and dc
+// (nblocks DC values).  ICX_E_CORRUPT only where the JDK reader throws (a
+// Huffman table the scan uses is invalid; a bad marker between the scan and
+// EOI, which jpeg_finish_decompress reads).
+icx_status seq_decode(const uint8_t* p, size_t len, const JpegHeader& J, int16_t* coefs, int32_t* dc);
+
 }  // namespace icx

@@ -1219,6 +1219,7 @@ const char* icx_status_string(icx_status s)
     case ICX_E_UNSUPPORTED: return "unsupported input";
     case ICX_E_CORRUPT: return "corrupt input";
     case ICX_E_NULL: return "null argument";
+    case ICX_E_REFUSED: return "a JPEG flavour the reference's reader refuses";
     }
     return "unknown";
 }

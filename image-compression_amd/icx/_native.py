@@ -11,7 +11,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ICX_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libicx.so")
 
 # icx_status
-OK, E_INVALID, E_NOMEM, E_DEVICE, E_BUFFER, E_UNSUPPORTED, E_CORRUPT, E_NULL = range(8)
+OK, E_INVALID, E_NOMEM, E_DEVICE, E_BUFFER, E_UNSUPPORTED, E_CORRUPT, E_NULL, E_REFUSED = range(9)
 # icx_fmt (XRGB32/ARGB32: TYPE_INT_RGB/ARGB int rasters, ABGR32: TYPE_4BYTE_ABGR, RGBA32: PNG order,
 # GRAY16: TYPE_USHORT_GRAY, uint16 samples)
 # INDEXED8 / BINARY1: TYPE_BYTE_INDEXED / TYPE_BYTE_BINARY, one colour-map index per byte + Image.palette
@@ -31,7 +31,7 @@ EXPORTS = [
     "icx_resize_bilinear", "icx_png_fit", "icx_num_blocks", "icx_debug_fdct",
     "icx_profile_enable", "icx_profile_reset", "icx_profile_query",
     "icx_jpeg_info", "icx_decode_jpg", "icx_decode_jpg_batch", "icx_debug_decode_coefs",
-    "icx_debug_progressive_coefs",
+    "icx_debug_progressive_coefs", "icx_debug_recovery_coefs",
     "icx_device_alloc", "icx_device_free", "icx_memcpy", "icx_host_alloc", "icx_host_free",
     "icx_png_bound", "icx_png_encode", "icx_png_fit_batch",
     "icx_pool_create", "icx_pool_destroy", "icx_pool_size", "icx_pool_context", "icx_pool_compress_jpg_batch",
@@ -163,6 +163,7 @@ def load():
         "icx_decode_jpg_batch": (c.c_int, [c.c_void_p, P(DecodeJob), c.c_int32]),
         "icx_debug_decode_coefs": (c.c_int, [c.c_void_p, c.c_void_p, c.c_size_t, P(c.c_int16), c.c_size_t]),
         "icx_debug_progressive_coefs": (c.c_int, [c.c_void_p, c.c_size_t, P(c.c_int16), c.c_size_t]),
+        "icx_debug_recovery_coefs": (c.c_int, [c.c_void_p, c.c_size_t, P(c.c_int16), c.c_size_t]),
         "icx_device_alloc": (c.c_int, [c.c_void_p, c.c_size_t, P(c.c_void_p)]),
         "icx_device_free": (c.c_int, [c.c_void_p, c.c_void_p]),
         "icx_memcpy": (c.c_int, [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]),
@@ -185,7 +186,7 @@ def load():
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
-    if lib.icx_abi_version() != 4:
+    if lib.icx_abi_version() != 5:
         raise NativeLibraryError("libicx ABI version mismatch")
     _lib = lib
     return lib

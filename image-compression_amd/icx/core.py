@@ -759,6 +759,20 @@ def progressive_coefs(data) -> np.ndarray:
     return out
 
 
+def recovery_coefs(data) -> np.ndarray:
+    """Coefficients of a sequential JPEG from the host entropy decode with
+    IJG 6b's recovery that the device decoder runs for the files its own
+    decode flags (icx_debug_recovery_coefs)."""
+    lib = N.load()
+    a = np.frombuffer(bytes(data), np.uint8)
+    out = np.zeros((_scan_blocks(a), 64), np.int16)
+    st = lib.icx_debug_recovery_coefs(a.ctypes.data, a.nbytes, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)),
+                                      out.size)
+    if st != N.OK:
+        raise N.IcxError(st, "icx_debug_recovery_coefs")
+    return out
+
+
 def quality_tables(quality: float):
     lib = N.load()
     lum = (ctypes.c_uint16 * 64)()

@@ -21,11 +21,16 @@ JDK reader's IJG 6b arithmetic plus source subsampling; a progressive file's
 scans are entropy-decoded by libicx on host threads, its IDCT and colour run
 on the device) straight into HBM tensors that the encoder then reads, so no
 decoded pixel crosses PCIe (CMYK / YCCK JPEGs too, to BGR on the device).
-Other files (arithmetic or progressive-CMYK JPEG, PNG,
-GIF, BMP, ...) and JPEGs the device decoder rejects (corrupt, or a truncated
-progressive script the JDK would block-smooth) are decoded on the host with
+Damaged sequential JPEGs (truncated scans, bad Huffman codes, restart markers
+out of sequence) are decoded by libicx as the JDK's 6b reader decodes them
+(its recovery, icx_seqdecode.cpp), so they compress as in the reference.
+JPEGs that reader refuses (arithmetic coding, hierarchical, not 8-bit:
+ICX_E_REFUSED) fail with FAILED_IO_ERROR after the dims gate, as its read()
+throws.  Other files (lossless or progressive-CMYK JPEG, PNG, GIF, BMP, ...)
+and JPEGs the device decoder rejects (an invalid table, a damaged progressive
+file, a scan script the JDK would block-smooth) are decoded on the host with
 libjpeg-turbo / Pillow (6b-lineage ISLOW IDCT + h2v2 fancy upsampling for
-JPEG).
+JPEG), a JPEG with the JDK source manager's fake EOI appended.
 """
 import concurrent.futures as cf
 import logging
@@ -237,6 +242,42 @@ def _to_array(im, path=None):
     return np.ascontiguousarray(rgb[:, :, ::-1])  # TYPE_3BYTE_BGR
 
 
+def _refused(path, w, h, params: CompressionParams):
+    """A JPEG the reference's reader refuses (arithmetic coding, hierarchical,
+    not 8-bit: icx_jpeg_info's ICX_E_REFUSED).  TwelveMonkeys reports its
+    dimensions from the SOF, so the dims gate (ImageCompression.java:131)
+    still applies; past it reader.read throws an IIOException (the JDK's 6b:
+    JERR_ARITH_NOTIMPL / JERR_SOF_UNSUPPORTED / JERR_BAD_PRECISION), which
+    processImage reports as FAILED_IO_ERROR (:94-96).  Returns False when
+    the dims gate skips the file."""
+    if w <= params.min_width or h <= params.min_height:
+        log.debug("%s - 跳過: 圖片尺寸 %dx%d 未超過最小壓縮門檻 %dx%d", path, w, h, params.min_width,
+                  params.min_height)
+        return False
+    raise OSError(f"{path}: JPEG flavour the reader refuses (arithmetic / hierarchical / not 8-bit)")
+
+
+def _open_image(path):
+    """Image.open for the host readers.  A JPEG (FF D8 FF: the JDK's JPEG
+    reader SPI takes it, JPEGImageReaderSpi.canDecodeInput) is read with a
+    fake EOI appended, as the JDK's source manager inserts one at end of
+    stream (imageioJPEG.c imageio_fill_input_buffer): a truncated scan then
+    decodes with libjpeg's zero fill instead of raising.  A JPEG the host
+    reader cannot open raises OSError: its reader was found, reading failed."""
+    import io
+    from PIL import Image
+    with open(path, "rb") as f:
+        head = f.read(3)
+    if head != b"\xff\xd8\xff":
+        return Image.open(path)
+    with open(path, "rb") as f:
+        data = f.read()
+    try:
+        return Image.open(io.BytesIO(data + b"\xff\xd9"))
+    except (Image.UnidentifiedImageError, ValueError, SyntaxError) as e:
+        raise OSError(f"{path}: unreadable JPEG ({e})") from e
+
+
 def _device_jpeg(input_path, params: CompressionParams, reader=None):
     """The file bytes (read by `reader`: into pinned host memory when the codec
     provides it, and then pushed to the GPU by the reader's upload()) and
@@ -253,6 +294,9 @@ def _device_jpeg(input_path, params: CompressionParams, reader=None):
         return None
     with _span("parse"):
         st, w, h, nc = jpeg_info(data if isinstance(data, bytes) else data.array)
+    if st == N.E_REFUSED:
+        _refused(input_path, w, h, params)  # raises, or returns False (the dims gate)
+        return False
     if st != N.OK:
         return None
     if w > params.min_width and h > params.min_height and hasattr(reader, "upload"):
@@ -365,6 +409,17 @@ def _staged_item(index, path, job, dev, params: CompressionParams, output_dir, r
         return it
     w, h = int(job.width), int(job.height)
     if dev is None:
+        if job.jpeg_status == N.E_REFUSED:
+            try:
+                _refused(path, w, h, params)
+            except OSError as e:
+                log.warning("%s - 處理圖片時發生 I/O 錯誤 (可能非支援格式或檔案損毀)", path)
+                log.debug("%s", e)
+                it.report = CompressionReport(CompressionResult.FAILED_IO_ERROR, it.original_size, 0)
+                return it
+            it.report = CompressionReport(CompressionResult.FAILED_UNSUPPORTED_FORMAT, it.original_size,
+                                          it.original_size)
+            return it
         if job.jpeg_status == N.OK and (w <= params.min_width or h <= params.min_height):
             log.debug("%s - 跳過: 圖片尺寸 %dx%d 未超過最小壓縮門檻 %dx%d", path, w, h, params.min_width,
                       params.min_height)
@@ -398,7 +453,7 @@ def decode_image_with_subsampling(input_path, params: CompressionParams, file_si
             return d
     try:
         with _span("host_decode"):
-            im = Image.open(input_path)
+            im = _open_image(input_path)
     except (Image.UnidentifiedImageError, ValueError):
         log.warning("%s - 找不到對應的圖片讀取器，跳過", input_path)
         return None
@@ -504,9 +559,9 @@ def _fail(it: _Item, exc: BaseException):
 
 
 def _host_decode(path, s):
-    """libjpeg-turbo decode + source subsampling (files the device decoder refused)."""
-    from PIL import Image
-    with Image.open(path) as im:
+    """libjpeg-turbo decode + source subsampling (files the device decoder
+    refused), with the JDK source manager's fake EOI (_open_image)."""
+    with _open_image(path) as im:
         arr = _to_array(im)
     return np.ascontiguousarray(arr[::s, ::s]) if s > 1 else arr
 

@@ -33,8 +33,9 @@
 extern "C" {
 #endif
 
-#define ICX_ABI_VERSION 4  /* 2: four-byte pixel formats, icx_png_encode; 3: ICX_GRAY16, icx_png_fit_batch;
-                              4: icx_set_table_layout, ICX_INDEXED8 / ICX_BINARY1 (icx_image.palette) */
+#define ICX_ABI_VERSION 5  /* 2: four-byte pixel formats, icx_png_encode; 3: ICX_GRAY16, icx_png_fit_batch;
+                              4: icx_set_table_layout, ICX_INDEXED8 / ICX_BINARY1 (icx_image.palette);
+                              5: ICX_E_REFUSED; damaged JPEGs decoded with IJG 6b's recovery */
 
 typedef struct icx_ctx icx_ctx;
 
@@ -46,7 +47,12 @@ typedef enum icx_status {
     ICX_E_BUFFER = 4,      /* output capacity too small; *out_len = needed bytes  */
     ICX_E_UNSUPPORTED = 5, /* valid but unsupported input (e.g. progressive JPEG) */
     ICX_E_CORRUPT = 6,     /* malformed compressed input                          */
-    ICX_E_NULL = 7         /* required pointer argument is NULL                   */
+    ICX_E_NULL = 7,        /* required pointer argument is NULL                   */
+    ICX_E_REFUSED = 8      /* a JPEG the reference's reader refuses at read():
+                              arithmetic coding (SOF9-11), hierarchical (SOF5-7,
+                              13-15), sample precision other than 8 bits; its
+                              dimensions are still reported (TwelveMonkeys reads
+                              the SOF itself), -> FAILED_IO_ERROR               */
 } icx_status;
 
 /* Pixel layouts.  ICX_BGR24 is java.awt.image.BufferedImage.TYPE_3BYTE_BGR,
@@ -302,8 +308,14 @@ icx_status icx_png_encode(const icx_image* img, int32_t level, uint8_t* out, siz
  * ycc_rgb_convert) with ImageReadParam.setSourceSubsampling(s, s, 0, 0) —
  * pixels (x*s, y*s) of the full decode — and ignoreMetadata = true.
  * Baseline/extended-sequential Huffman JPEGs with one interleaved scan
- * (4:2:0, 4:2:2, 4:4:4) or one grey component, with or without restart
- * intervals; anything else returns ICX_E_UNSUPPORTED. */
+ * (4:2:0, 4:2:2, 4:4:4, 4:4:0, 4:1:1; CMYK / YCCK with 1x1 components) or
+ * one grey component, with or without restart intervals, and progressive
+ * files of the same layouts.  Damaged sequential files decode as the JDK's
+ * reader decodes them (IJG 6b's recovery: a truncated scan ends in grey MCUs,
+ * a bad Huffman code reads as 0, restart markers out of sequence are
+ * resynchronised), so a file is ICX_E_CORRUPT only where that reader throws.
+ * ICX_E_REFUSED: arithmetic / hierarchical / not 8-bit (the reader throws at
+ * read()); anything else returns ICX_E_UNSUPPORTED (another reader's file). */
 typedef struct icx_decode_job {
     /* inputs */
     const uint8_t* data;   /* the whole JPEG file; host or device memory */
@@ -320,8 +332,9 @@ typedef struct icx_decode_job {
 } icx_decode_job;
 
 /* Header-only parse (host memory): SOF dimensions and components.  Returns
- * ICX_OK when the device decoder supports the file, ICX_E_UNSUPPORTED (with
- * the dimensions filled in) when it does not, ICX_E_CORRUPT otherwise. */
+ * ICX_OK when the device decoder supports the file, ICX_E_UNSUPPORTED or
+ * ICX_E_REFUSED (with the dimensions filled in) when it does not,
+ * ICX_E_CORRUPT otherwise. */
 icx_status icx_jpeg_info(const uint8_t* data, size_t len, int32_t* width, int32_t* height, int32_t* ncomp);
 
 icx_status icx_decode_jpg(icx_ctx* ctx, icx_decode_job* job);
@@ -390,6 +403,11 @@ icx_status icx_debug_decode_coefs(icx_ctx* ctx, const uint8_t* data, size_t len,
  * same layout as icx_debug_decode_coefs (DC value in [0]).  ICX_E_INVALID for
  * a sequential file; no context and no GPU needed. */
 icx_status icx_debug_progressive_coefs(const uint8_t* data, size_t len, int16_t* coefs, size_t ncoefs);
+/* Host-only: the sequential entropy decode with IJG 6b's recovery (truncated
+ * scans, bad codes, restart resynchronisation) that the device decoder runs
+ * on host threads for the files its own decode flags; same layout as
+ * icx_debug_decode_coefs.  ICX_E_INVALID for a progressive file. */
+icx_status icx_debug_recovery_coefs(const uint8_t* data, size_t len, int16_t* coefs, size_t ncoefs);
 
 /* Raw jpeg_fdct_islow coefficients (x8 scale, before quantisation) in scan
  * block order (MCU: Y0 Y1 Y2 Y3 Cb Cr), zig-zag within each block: the

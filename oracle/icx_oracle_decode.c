@@ -454,12 +454,71 @@ static void process_restart6(src6_t* s, int* last_dc)
     if (!s->marker) s->insufficient = 0;
 }
 
+/* jdapimin.c jpeg_finish_decompress -> jdinput.c consume_markers ->
+ * jdmarker.c read_markers after the file's only scan, up to EOI: the JDK
+ * reader runs it once every scanline is read (imageioJPEG.c readImage), and
+ * an error there throws (status 6).  Past the end of the file the fake EOI
+ * ends it. */
+static int rd2(src6_t* s)
+{
+    const int a = rd_byte(s);
+    return (a << 8) | rd_byte(s);
+}
+
+static int trailer6(src6_t* s)
+{
+    for (;;) {
+        if (!s->marker) next_marker6(s);
+        const int m = s->marker;
+        s->marker = 0;
+        if (m == 0xD9) return 0;                               /* EOI */
+        if ((m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;    /* RSTn, TEM: nothing */
+        if (m == 0xD8) return 6;                               /* JERR_SOI_DUPLICATE */
+        if (m >= 0xC0 && m <= 0xCF && m != 0xC4 && m != 0xCC) return 6; /* SOF / JPG: duplicate, unsupported */
+        if (m == 0xDA) return 6;                               /* JERR_EOI_EXPECTED: a one-scan file */
+        if (m == 0xC4) {                                       /* get_dht */
+            long len = rd2(s) - 2;
+            while (len > 16) {
+                int index = rd_byte(s), count = 0;
+                for (int i = 0; i < 16; i++) count += rd_byte(s);
+                len -= 17;
+                if (count > 256 || count > len) return 6;      /* JERR_BAD_HUFF_TABLE */
+                for (int i = 0; i < count; i++) rd_byte(s);
+                len -= count;
+                if (index & 0x10) index -= 0x10;
+                if (index >= 4) return 6;                      /* JERR_DHT_INDEX */
+            }
+            if (len != 0) return 6;                            /* JERR_BAD_LENGTH */
+        } else if (m == 0xDB) {                                /* get_dqt */
+            long len = rd2(s) - 2;
+            while (len > 0) {
+                const int n = rd_byte(s);
+                if ((n & 15) >= 4) return 6;                   /* JERR_DQT_INDEX */
+                for (int i = 0; i < 64; i++)
+                    if (n >> 4) rd2(s);
+                    else rd_byte(s);
+                len -= (n >> 4) ? 129 : 65;
+            }
+            if (len != 0) return 6;
+        } else if (m == 0xDD) {                                /* get_dri */
+            if (rd2(s) != 4) return 6;
+            rd2(s);
+        } else if ((m >= 0xE0 && m <= 0xEF) || m == 0xFE || m == 0xCC || m == 0xDC) {
+            long len = rd2(s) - 2;                             /* APPn, COM, DAC, DNL: skipped */
+            for (long i = 0; i < len; i++) rd_byte(s);
+        } else {
+            return 6;                                          /* JERR_UNKNOWN_MARKER */
+        }
+    }
+}
+
 /* Decode the scan into quantised coefficients, natural order, scan (MCU) block
  * order including dummy blocks, as jdhuff.c decode_mcu fills the zeroed
  * MCU_buffer (jdcoefct.c decompress_onepass): once insufficient_data is set
  * (bits wanted past a marker or the end of the file: the MCU being decoded
  * finishes on zero bits) every later MCU of the segment stays zero, i.e.
- * uniform grey; a bad Huffman code decodes as 0.  Never fails. */
+ * uniform grey; a bad Huffman code decodes as 0.  Then the markers up to EOI
+ * (trailer6): 6 where the JDK reader would throw there, else 0. */
 static int decode_scan(const jinfo_t* J, int16_t* coefs)
 {
     src6_t s = {J->scan, J->scan_len, 0, 0, 0, 0, 0, 0};
@@ -498,7 +557,7 @@ static int decode_scan(const jinfo_t* J, int16_t* coefs)
             }
         }
     }
-    return 0;
+    return trailer6(&s);
 }
 
 /* ------------------------------------------------------------ jidctint.c */

@@ -190,7 +190,7 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
                                                           seg.data(), (uint32_t)seg.size(), ent_len * 8, pc.blk);
         w.start(pc.e);
         while (w.running(pc.stop)) w.step(sk);
-        bad |= w.bad;  // as k_dec_write: an invalid code on the true path = corrupt data
+        bad |= w.bad || (pc.have && w.overran());  // as k_dec_write: not the clean case
     }
     if (bad) return ICX_E_CORRUPT;
     // ---- DC prediction per component, reset every restart interval

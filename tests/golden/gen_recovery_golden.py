@@ -45,7 +45,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 from gen_decode_golden import encode, noise, smooth  # noqa: E402
 
-ImageFile.LOAD_TRUNCATED_IMAGES = True
+ImageFile.LOAD_TRUNCATED_IMAGES = False
 
 
 def scan_start(data):
@@ -71,10 +71,18 @@ def rst_positions(data, s0):
 
 
 def decode(data, luma_only=False):
-    im = Image.open(io.BytesIO(data))
+    """BGR / grey pixels of the file read with a fake EOI appended (the JDK's
+    source manager inserts one at end of stream; this is what Pillow's
+    LOAD_TRUNCATED_IMAGES does too, but with the flag off an error after the
+    scan - jpeg_finish_decompress walks the markers up to EOI - still raises);
+    None when libjpeg-turbo raises (the JDK reader throws: FAILED_IO_ERROR)."""
+    im = Image.open(io.BytesIO(data + b"\xff\xd9"))
     if luma_only:
         im.draft("L", im.size)
-    im.load()
+    try:
+        im.load()
+    except OSError:
+        return None
     a = np.asarray(im)
     if a.ndim == 3:
         a = a[:, :, ::-1]  # TYPE_3BYTE_BGR
@@ -123,6 +131,26 @@ def damaged(name, data):
     return out
 
 
+def trailers(name, data):
+    """Markers after the scan, before EOI: jpeg_finish_decompress reads them
+    (jdmarker.c read_markers) and throws on a duplicate SOI / SOF, a second
+    SOS in a one-scan file, an unknown marker or a malformed table segment;
+    COM / APPn / DHT / DQT / DRI / RSTn and garbage bytes are fine."""
+    body, eoi = data[:-2], data[-2:]
+    sos = data.index(b"\xff\xda")
+    sof = data.index(b"\xff\xc0")
+    dht = data.index(b"\xff\xc4")
+    dht_seg = data[dht:dht + 2 + int.from_bytes(data[dht + 2:dht + 4], "big")]
+    t = {"com": b"\xff\xfe\x00\x06note", "app1": b"\xff\xe1\x00\x04ab", "dht_ok": dht_seg,
+         "dqt_ok": b"\xff\xdb\x00\x43\x01" + bytes(range(1, 65)), "dri_ok": b"\xff\xdd\x00\x04\x00\x05",
+         "rst_extra": b"\xff\xd3", "garbage": b"\x12\x34\xff\x00\x56", "tem": b"\xff\x01",
+         "dup_sos": data[sos:sos + 2 + int.from_bytes(data[sos + 2:sos + 4], "big")], "unknown": b"\xff\x02",
+         "jpgn": b"\xff\xf3\x00\x02", "bad_dht": b"\xff\xc4\x00\x05\x00\x01\x02",
+         "bad_dqt": b"\xff\xdb\x00\x43\x05" + bytes(64), "bad_dri": b"\xff\xdd\x00\x05\x00\x05\x00",
+         "dup_soi": b"\xff\xd8", "dup_sof": data[sof:sof + 19], "sof9": b"\xff\xc9" + data[sof + 2:sof + 19]}
+    return [(f"{name}_trailer_{k}", body + v + eoi) for k, v in t.items()]
+
+
 def main():
     files = [
         ("c420_200x136", encode(smooth(136, 200, 7001), quality=95, subsampling=2)),
@@ -138,10 +166,14 @@ def main():
     ]
     jpegs, expect, meta = {}, {}, {"libjpeg_turbo": features.version("libjpeg_turbo"),
                                     "pillow": Image.__version__, "jsimd": "forcenone", "cases": {}}
-    for name, data in files:
-        for cname, d in [(name + "_intact", data)] + damaged(name, data):
+    for k, (name, data) in enumerate(files):
+        extra = trailers(name, data) if k in (0, 4, 5) else []
+        for cname, d in [(name + "_intact", data)] + damaged(name, data) + extra:
             out = decode(d)
             jpegs[cname] = np.frombuffer(d, np.uint8)
+            if out is None:  # the reader throws
+                meta["cases"][cname] = {"bytes": len(d), "pinned": "error"}
+                continue
             expect[cname] = out
             meta["cases"][cname] = {"w": int(out.shape[1]), "h": int(out.shape[0]),
                                     "ncomp": 1 if out.ndim == 2 else 3, "bytes": len(d), "pinned": "pixels"}
@@ -156,6 +188,7 @@ def main():
                                                    if v[0].endswith(("cut300", "cut600", "badcode", "rst_missing"))]
             for cname, d in variants:
                 y = decode(d, luma_only=True)
+                assert y is not None, cname
                 jpegs[cname] = np.frombuffer(d, np.uint8)
                 expect[cname] = y
                 meta["cases"][cname] = {"w": int(y.shape[1]), "h": int(y.shape[0]), "ncomp": 3,

@@ -30,8 +30,9 @@ def test_library_exports_all_header_symbols():
 
 def test_abi_version_and_status_strings():
     lib = N.load()
-    assert lib.icx_abi_version() == 4
+    assert lib.icx_abi_version() == 5
     assert lib.icx_status_string(N.E_BUFFER) == b"output buffer too small"
+    assert b"refuses" in lib.icx_status_string(N.E_REFUSED)
     assert lib.icx_jpeg_header_size(N.BGR24) == 623 and lib.icx_jpeg_header_size(N.GRAY8) == 328
     assert lib.icx_jpeg_header_size_layout(N.BGR24, N.TABLES_GROUPED) == 607
     assert lib.icx_jpeg_header_size_layout(N.GRAY8, N.TABLES_GROUPED) == 324

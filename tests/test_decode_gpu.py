@@ -144,12 +144,19 @@ def test_decode_of_own_encodes_round_trip(codec, oracle):
         assert rc == 0 and np.array_equal(codec.decode_jpg(data), ref)
 
 
-def test_decode_refusals_and_corrupt_input(codec, dgolden):
+def test_decode_refusals_and_corrupt_input(codec, oracle, dgolden):
+    """Headers the JDK reader cannot read are corrupt; a scan cut short
+    decodes as that reader decodes it (IJG 6b's recovery: the oracle's
+    pixels); neither spoils the batch."""
     meta, jpgs, _ = dgolden
     good = jpgs["c130x250_s2_q95"]
-    bad = [good[: len(good) // 2], good[:700], b"\xff\xd8\xff\xd9", good[:2] + b"\x00" * 100]
-    res = codec.decode_jpg_batch(bad + [good], subsampling=1)
-    for st, img in res[:-1]:
+    cut = [good[: len(good) // 2], good[: len(good) - 3]]
+    bad = [b"\xff\xd8\xff\xd9", good[:2] + b"\x00" * 100, good[:300]]
+    res = codec.decode_jpg_batch(cut + bad + [good], subsampling=1)
+    for d, (st, img) in zip(cut, res):
+        rc, ref = oracle.jpeg_decode(d)
+        assert st == N.OK and rc == 0 and np.array_equal(img, ref)
+    for st, img in res[len(cut):-1]:
         assert st in (N.E_CORRUPT, N.E_UNSUPPORTED), st
     assert res[-1][0] == N.OK  # a bad file does not spoil the batch
 
@@ -185,14 +192,14 @@ def test_decode_fuzzed_batch(codec, oracle, dgolden):
     res = codec.decode_jpg_batch(datas, subsampling=1)
     ok = 0
     for i, (d, (st, img)) in enumerate(zip(datas, res)):
-        assert st in (N.OK, N.E_UNSUPPORTED, N.E_CORRUPT), (i, st)
+        assert st in (N.OK, N.E_UNSUPPORTED, N.E_CORRUPT, N.E_REFUSED), (i, st)
         if i % 5 == 4:
             assert st == N.OK and np.array_equal(img, pxs[names[i % len(names)]]), i
         if st == N.OK:
             rc, ref = oracle.jpeg_decode(d)
             assert rc == 0 and np.array_equal(img, ref), i
             ok += 1
-    assert ok >= 80
+    assert ok >= 240  # damaged entropy data decodes (6b recovery); header damage may not
 
 
 def _with_comments(data, sizes):
@@ -288,8 +295,9 @@ def test_progressive_refusals_in_a_batch(codec, dgolden):
 
 def test_decode_stray_restart_markers(codec, oracle, dgolden):
     """RSTn markers where the DRI interval does not end (inserted, or one
-    removed): the device decoder refuses the file or decodes it exactly as the
-    oracle does - every interval must end after ri MCUs (DecWalker::invalid)."""
+    removed): the device walk flags the file (every interval must end after
+    ri MCUs, DecWalker::invalid) and libjpeg's resynchronisation decodes it
+    (icx_seqdecode.cpp) exactly as the oracle does."""
     meta, jpgs, pxs = dgolden
     good = jpgs["rst7_130x250"]
     sos = good.index(b"\xff\xda")
@@ -303,8 +311,6 @@ def test_decode_stray_restart_markers(codec, oracle, dgolden):
         datas.append(good[:r] + good[r + 2:])  # one marker removed
     res = codec.decode_jpg_batch(datas + [good], subsampling=1)
     for i, (d, (st, img)) in enumerate(zip(datas, res)):
-        assert st in (N.OK, N.E_CORRUPT), (i, st)
-        if st == N.OK:
-            rc, ref = oracle.jpeg_decode(d)
-            assert rc == 0 and np.array_equal(img, ref), i
+        rc, ref = oracle.jpeg_decode(d)
+        assert st == N.OK and rc == 0 and np.array_equal(img, ref), (i, st)
     assert res[-1][0] == N.OK and np.array_equal(res[-1][1], pxs["rst7_130x250"])

@@ -460,36 +460,123 @@ def test_alpha_resize_restatement_rules():
     assert ((r[:, :, 0] == 0) <= (r[:, :, 1:] == 0).all(-1)).all()  # alpha 0 -> zero pixel
 
 
+def _dc_symbol_16(data):
+    """data with one DC Huffman table symbol set to 16: jdhuff.c
+    jpeg_make_d_derived_tbl refuses the table (JERR_BAD_HUFF_TABLE), so the
+    JDK reader's read() throws."""
+    d = bytearray(data)
+    i = d.index(b"\xff\xc4")
+    assert d[i + 4] >> 4 == 0  # a DC table
+    d[i + 4 + 1 + 16] = 16
+    return bytes(d)
+
+
+def test_truncated_jpeg_is_compressed(tmp_path):
+    """A scan cut short decodes as the JDK's 6b reader decodes it (fake EOI,
+    then the rest of the scan grey: jdhuff.c insufficient_data) and is
+    compressed (the reference compresses such files; it was
+    FAILED_IO_ERROR here)."""
+    from tests.oracle_ffi import Oracle
+    o = Oracle()
+    good = []
+    for i in range(3):
+        f = tmp_path / f"g{i}.jpg"
+        write_jpeg(f, noise(70 + i, 110, 20 + i))
+        good.append(str(f))
+    cut = tmp_path / "cut.jpg"
+    data = (tmp_path / "g0.jpg").read_bytes()
+    cut.write_bytes(data[: len(data) * 3 // 5])  # header intact, scan truncated
+    lst = tmp_path / "list.txt"
+    lst.write_text("\n".join([good[0], str(cut), good[1], good[2]]) + "\n")
+    params = CompressionParams(0.25, 1000, 60, 60, 20000)
+    b = pipeline.CompressionBatch(lst, tmp_path / "out", params, 1, tmp_path / "cache", codecs=[OracleCodec()],
+                                  group_size=4)
+    rep = b.execute(cache=LockedDict())
+    assert rep.total == 4 and rep.success == 4, rep.counts
+    rc, px = o.jpeg_decode(cut.read_bytes())
+    assert rc == 0 and (px[-8:] == 128).all()  # the grey tail
+    ref = o.fit(px, params.target_max_size_bytes, params.quality)
+    assert (tmp_path / "out" / "cut.jpg").read_bytes() == ref["data"]
+
+
 def test_corrupt_jpeg_fails_alone_in_its_group(tmp_path):
-    """A file the device decoder rejects and the host decoder cannot read either
+    """A JPEG the JDK reader cannot read (a DC table with a symbol over 15)
     fails by itself (FAILED_IO_ERROR, as reader.read's IOException does in
-    ImageCompression.java:101-103); the valid files of its device group still
-    compress (one bad file used to fail the whole group)."""
+    ImageCompression.java:94-96); the valid files of its device group still
+    compress (one bad file used to fail the whole group).  The
+    device decoder's refusal goes to the host reader, which refuses it too."""
     good = []
     for i in range(3):
         f = tmp_path / f"g{i}.jpg"
         write_jpeg(f, noise(70 + i, 110, 20 + i))
         good.append(str(f))
     bad = tmp_path / "bad.jpg"
-    data = (tmp_path / "g0.jpg").read_bytes()
-    bad.write_bytes(data[: len(data) * 3 // 5])  # header intact, scan truncated
-    bad_bytes = bad.read_bytes()
-
-    class RejectingCodec(OracleCodec):
-        def decode_jpg_batch(self, datas, subsampling=0, device_out=False):
-            out = super().decode_jpg_batch(datas, subsampling, device_out)
-            return [(icx.core.N.E_CORRUPT, None) if bytes(d) == bad_bytes else r for d, r in zip(datas, out)]
-
+    bad.write_bytes(_dc_symbol_16((tmp_path / "g0.jpg").read_bytes()))
     lst = tmp_path / "list.txt"
     lst.write_text("\n".join([good[0], str(bad), good[1], good[2]]) + "\n")
     b = pipeline.CompressionBatch(lst, tmp_path / "out", CompressionParams(0.25, 1000, 60, 60, 20000), 1,
-                                  tmp_path / "cache", codecs=[RejectingCodec()], group_size=4)
+                                  tmp_path / "cache", codecs=[OracleCodec()], group_size=4)
     rep = b.execute(cache=LockedDict())
     assert rep.total == 4 and rep.success == 3, rep.counts
     assert rep.counts[CompressionResult.FAILED_IO_ERROR] == 1
     for g in good:
         assert (tmp_path / "out" / os.path.basename(g)).exists()
     assert not (tmp_path / "out" / "bad.jpg").exists()
+
+
+@pytest.mark.parametrize("sof", [0xC9, 0xCA, 0xCB, 0xC5, 0xCD, "p12"])
+def test_refused_jpeg_flavours(tmp_path, sof):
+    """Arithmetic coding (SOF9-11), hierarchical (SOF5-7, 13-15) and 12-bit
+    files: the reference's reader reports their size (TwelveMonkeys parses
+    the SOF) and its read() throws (the JDK's 6b: JERR_ARITH_NOTIMPL /
+    JERR_SOF_UNSUPPORTED / JERR_BAD_PRECISION): FAILED_IO_ERROR past the dims
+    gate, FAILED_UNSUPPORTED_FORMAT under it; never a host decode (Pillow's
+    libjpeg-turbo would read an arithmetic file)."""
+    f = tmp_path / "a.jpg"
+    write_jpeg(f, noise(80, 120, 9))
+    d = bytearray(f.read_bytes())
+    i = d.index(b"\xff\xc0")
+    if sof == "p12":
+        d[i + 4] = 12
+    else:
+        d[i + 1] = sof
+    f.write_bytes(bytes(d))
+    size = len(d)
+    out = tmp_path / "out"
+    out.mkdir()
+    r = pipeline.process_image(f, out, CompressionParams(0.25, 10, 100, 60, 10 ** 6), {}, OracleCodec())
+    assert r == icx.CompressionReport(CompressionResult.FAILED_IO_ERROR, size, 0)
+    r = pipeline.process_image(f, out, CompressionParams(0.25, 10, 100, 90, 10 ** 6), {}, OracleCodec())
+    assert r == icx.CompressionReport(CompressionResult.FAILED_UNSUPPORTED_FORMAT, size, size)
+    lst = tmp_path / "list.txt"
+    lst.write_text(str(f) + "\n")
+    rep = pipeline.CompressionBatch(lst, out, CompressionParams(0.25, 10, 100, 60, 10 ** 6), 1, tmp_path / "cache",
+                                    codecs=[OracleCodec()]).execute(cache=LockedDict())
+    assert rep.counts[CompressionResult.FAILED_IO_ERROR] == 1
+
+
+def test_truncated_progressive_jpeg_uses_the_fake_eoi(tmp_path):
+    """A file the device path leaves to the host reader (here a progressive
+    file cut short) is read with the JDK source manager's fake EOI appended,
+    so its damaged scan decodes instead of raising."""
+    f = tmp_path / "p.jpg"
+    buf = io.BytesIO()
+    Image.fromarray(smooth(90, 120, 3)).save(buf, "JPEG", quality=90, progressive=True)
+    data = buf.getvalue()
+    f.write_bytes(data[: len(data) * 2 // 3])
+    out = tmp_path / "out"
+    out.mkdir()
+    r = pipeline.process_image(f, out, CompressionParams(0.25, 10, 100, 60, 10 ** 6), {}, OracleCodec())
+    assert r.result == CompressionResult.COMPRESSED_SUCCESS
+
+
+def test_unopenable_jpeg_is_an_io_error(tmp_path):
+    """FF D8 FF then garbage: the JDK's JPEG reader SPI takes the file
+    (canDecodeInput) and reading fails: FAILED_IO_ERROR, not 'no reader'."""
+    f = tmp_path / "g.jpg"
+    f.write_bytes(b"\xff\xd8\xff\xe0" + b"\x00" * 3000)
+    r = pipeline.process_image(f, tmp_path, CompressionParams(0.25, 10, 100, 60, 10 ** 6), {}, OracleCodec())
+    assert r.result == CompressionResult.FAILED_IO_ERROR
 
 
 def test_host_output_codec_in_the_batch(tmp_path):

@@ -39,6 +39,25 @@ def _make_inputs(d):
     files.append(str(cm))
     (d / "ycck.jpg").write_bytes(set_transform(cm.read_bytes(), 2))
     files.append(str(d / "ycck.jpg"))
+    # damaged JPEGs: the JDK's 6b reader recovers (grey tail, bad code as 0,
+    # restart resync) and the reference compresses them; an arithmetic-coded
+    # one it refuses (FAILED_IO_ERROR)
+    src = open(files[0], "rb").read()
+    (d / "cut.jpg").write_bytes(src[: len(src) * 2 // 3])
+    bad = bytearray(src)
+    bad[len(src) // 2:len(src) // 2 + 8] = b"\xff\x00" * 4
+    (d / "badcode.jpg").write_bytes(bytes(bad))
+    import io
+    buf = io.BytesIO()
+    Image.fromarray(np.ascontiguousarray(smooth(360, 520, 97)[:, :, ::-1])).save(buf, "JPEG", quality=95,
+                                                                                 restart_marker_blocks=3)
+    r = buf.getvalue()
+    k = [i for i in range(len(r) // 2, len(r) - 1) if r[i] == 0xFF and 0xD0 <= r[i + 1] <= 0xD7][0]
+    (d / "rst_missing.jpg").write_bytes(r[:k] + r[k + 2:])
+    arith = bytearray(src)
+    arith[arith.index(b"\xff\xc0") + 1] = 0xC9
+    (d / "arith.jpg").write_bytes(bytes(arith))
+    files += [str(d / n) for n in ("cut.jpg", "badcode.jpg", "rst_missing.jpg", "arith.jpg")]
     p = d / "pic.png"
     Image.fromarray(smooth(500, 700, 5)[:, :, ::-1]).save(p)
     files.append(str(p))
@@ -62,7 +81,10 @@ def test_batch_end_to_end_matches_oracle(codec, tmp_path):
     cpu = pipeline.CompressionBatch(lst, tmp_path / "cpu", params, 1, tmp_path / "ccache", codecs=[OracleCodec()],
                                     group_size=4).execute()
     assert gpu.counts == cpu.counts and gpu.total == cpu.total == len(files)
-    assert gpu.counts[CompressionResult.COMPRESSED_SUCCESS] >= 10
+    assert gpu.counts[CompressionResult.COMPRESSED_SUCCESS] >= 13
+    assert gpu.counts[CompressionResult.FAILED_IO_ERROR] == 1  # arith.jpg
+    for name in ("cut.jpg", "badcode.jpg", "rst_missing.jpg"):
+        assert (tmp_path / "gpu" / name).exists(), name
     for name in sorted(os.listdir(tmp_path / "cpu")):
         a = (tmp_path / "gpu" / name).read_bytes()
         b = (tmp_path / "cpu" / name).read_bytes()
