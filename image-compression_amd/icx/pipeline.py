@@ -694,6 +694,9 @@ def compress_jpeg_group(codec, items: List[_Item], params: CompressionParams, ca
             _finish(it, r["success"])
         except Exception as e:
             _fail(it, e)
+    if hasattr(cache, "flush"):  # SharedCache: the group's new entries go out as one chunk
+        with cache.lock:
+            cache.flush()
 
 
 def _png_write(it: _Item, resized):

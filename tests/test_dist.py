@@ -204,3 +204,70 @@ def test_ranks_share_one_learned_cache(tmp_path):
     assert seen0 == [(False, False)]  # rank 0: cold, full search, learns the key
     assert seen1 == [(True, True)]    # rank 1: probed with rank 0's entry, and it fits
     assert n1 == 1
+
+
+def _cache_stress_worker(rank, world, port, puts, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "image-compression_amd"))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    from torch.distributed.distributed_c10d import _get_default_store
+    from icx.cache import SharedCache
+    from icx.core import LearnedParams, SimilarityKey
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    store = _get_default_store()
+    cache = SharedCache(store)
+    rng = np.random.default_rng(rank)
+    per_refresh = []
+    for g in range(puts // 50):  # groups of 50 puts: refresh (probe), puts, flush - as the pipeline does
+        with cache.lock:
+            before = cache.records_read
+            cache.refresh()
+            per_refresh.append(cache.records_read - before)
+            for _ in range(50):
+                k = SimilarityKey(int(rng.integers(0, 40)), int(rng.integers(0, 30)), int(rng.integers(0, 20)))
+                cache[k] = LearnedParams(float(np.float32(rng.uniform(0.01, 1))), float(rng.choice([1.0, 0.85])))
+            cache.flush()
+    dist.barrier()
+    cache.refresh()
+    serial = None
+    if rank == 0:  # the serial last-writer-wins map: every chunk in counter order
+        n = int(store.add(SharedCache.COUNT, 0))
+        serial = {}
+        for c in range(1, n + 1):
+            for r in np.frombuffer(bytes(store.get(f"{SharedCache.CHUNK}{c}")), SharedCache._REC):
+                serial[SimilarityKey(int(r["w"]), int(r["h"]), int(r["s"]))] = LearnedParams(float(r["q"]),
+                                                                                                 float(r["scale"]))
+        written = sum(len(np.frombuffer(bytes(store.get(f"{SharedCache.CHUNK}{c}")), SharedCache._REC))
+                      for c in range(1, n + 1))
+        serial = (serial, written)
+    q.put((rank, dict(cache), cache.records_read, per_refresh, serial))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shared_cache_eight_ranks_bounded_refresh():
+    """8 gloo ranks, 20k puts in all (2500 each, in groups
+    of 50 between refreshes).  Every rank reads each published record exactly
+    once (total refresh cost = the records written: O(new entries), not the
+    whole log per refresh), and every rank's final map equals the serial
+    last-writer-wins map of all chunks in counter order."""
+    world, puts = 8, 2500
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_cache_stress_worker, args=(r, world, port, puts, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in ps), key=lambda t: t[0])
+    for p in ps:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in ps)
+    serial, written = res[0][4]
+    assert written <= world * puts
+    for rank, final, read, per_refresh, _ in res:
+        assert final == serial, rank
+        assert read == written, (rank, read, written)  # each record read once, whatever the interleaving
+        assert sum(per_refresh) <= written, rank

@@ -750,10 +750,11 @@ def test_staged_items_follow_process_image_gates(tmp_path, caplog):
 
 def test_shared_cache_log_semantics():
     """SharedCache over a key-value store (the process group's store; a dict
-    stand-in here): puts append 28-byte records to one log key, refresh()
-    applies records appended since the last refresh in log order (later
-    writers win), quality stays float32-exact, and a refresh with nothing
-    new reads nothing."""
+    stand-in here): a flush publishes the pending 28-byte records as one
+    chunk under the next counter value, refresh() applies only the chunks it
+    has not applied, in chunk order (later writers win), quality stays
+    float32-exact, a put that changes nothing publishes nothing, and a
+    refresh with nothing new reads nothing."""
     from icx.cache import SharedCache
     from icx.core import LearnedParams, SimilarityKey
 
@@ -761,23 +762,28 @@ def test_shared_cache_log_semantics():
         def __init__(self):
             self.kv = {}
 
-        def append(self, k, b):
-            self.kv[k] = self.kv.get(k, b"") + b
-
-        def check(self, keys):
-            return all(k in self.kv for k in keys)
-
-        def get(self, k):
+        def add(self, k, n):
+            self.kv[k] = int(self.kv.get(k, 0)) + n
             return self.kv[k]
+
+        def set(self, k, b):
+            self.kv[k] = b
+
+        def multi_get(self, keys):
+            return [self.kv[k] for k in keys]
 
     st = Store()
     a, b = SharedCache(st), SharedCache(st)
     assert a.refresh() == 0
     k1, k2 = SimilarityKey(38, 21, 7), SimilarityKey(76, 43, 12)
     a[k1] = LearnedParams(0.2421875, 1.0)
+    assert a.flush() == 1
     b[k2] = LearnedParams(0.1, 0.85)
     b[k1] = LearnedParams(0.125, 0.7224999999999999)  # later writer
-    assert len(st.kv[SharedCache.LOG]) == 3 * SharedCache._REC.itemsize == 84
+    assert b.flush() == 2
+    assert st.kv[SharedCache.COUNT] == 2 and len(st.kv[SharedCache.CHUNK + "2"]) == 2 * 28
     assert a.refresh() == 3 and b.refresh() == 3 and a.refresh() == 0
     assert dict(a) == dict(b)
     assert a[k1] == LearnedParams(0.125, 0.7224999999999999) and a[k2].quality == float(np.float32(0.1))
+    a[k2] = LearnedParams(float(np.float32(0.1)), 0.85)  # no change: nothing to publish
+    assert a.flush() == 0 and b.refresh() == 0
