@@ -703,6 +703,7 @@ struct DecWalker {
         uint32_t k;
         const uint32_t nx = dec_next_seg(seg, nseg, pos >> 3, &k);
         const uint32_t bound = nx == DEC_END ? ent_bits : (nx - DEC_PAD) * 8;  // end of interval data
+        const bool partial = z != 0;  // a block in progress: extra data in the interval (below)
         b = 0;
         z = 0;
         comp = 0;
@@ -718,6 +719,10 @@ struct DecWalker {
         // where libjpeg reads zeros after setting insufficient_data: not the
         // clean case either (seq_decode's)
         if (OWNED && pos > bound) bad = true;
+        // a block left half-decoded: the interval held more data than its MCUs
+        // (libjpeg skips it at the restart); its symbols sit in the assembly
+        // slot the next block would inherit
+        if (OWNED && partial) bad = true;
         if (nx == DEC_END) {
             pos = DEC_END;
             return;
@@ -1167,6 +1172,7 @@ struct DecLeanWriter {
         uint32_t k;
         const uint32_t nx = dec_next_seg(seg, nseg, pos >> 3, &k);
         const uint32_t bound = nx == DEC_END ? ent_bits : (nx - DEC_PAD) * 8;
+        const bool partial = z != 0;  // DecWalker<true>::invalid
         b = 0;
         z = 0;
         ti = table(0, 0);
@@ -1177,7 +1183,7 @@ struct DecLeanWriter {
             R.init(words, pos);
             return;
         }
-        if (pos > bound) bad = true;  // read pad bits (DecWalker<true>::invalid)
+        if (pos > bound || partial) bad = true;  // read pad bits, extra data (DecWalker<true>::invalid)
         if (nx == DEC_END) {
             pos = DEC_END;
             return;

@@ -357,13 +357,33 @@ __global__ void __launch_bounds__(1024) k_unstuff_scan(const DecDesc* D, DecStat
 {
     __shared__ uint32_t sh[24];
     __shared__ uint32_t te_cnt[2];
+    __shared__ int64_t s_end;
+    __shared__ int s_fake;
     const int img = ids[blockIdx.x];
     const DecDesc& d = D[img];
     DecState& st = S[img];
+    // A file that ends in 0xFF bytes inside the scan (cut after an FF of an
+    // FF 00 pair, or in fill bytes): the JDK's source manager appends a fake
+    // EOI, so those FFs start a marker and are no data - k_unstuff_count,
+    // which needs a marker's next byte, kept the last one.  The terminating
+    // marker moves to the start of that FF run.
+    if (threadIdx.x == 0) {
+        int64_t e = st.end;
+        int fake = 0;
+        if (e >= d.scan_len && d.scan_len > 0 && d.scan[d.scan_len - 1] == 0xFF) {
+            e = d.scan_len - 1;
+            while (e > 0 && d.scan[e - 1] == 0xFF) e--;
+            st.end = e;
+            fake = 1;
+        }
+        s_end = e;
+        s_fake = fake;
+    }
+    __syncthreads();
     // k_unstuff_count counted every tile up to scan_len: the tile holding the
     // terminating marker is recounted below it (4 bytes per thread), the
     // tiles after it count nothing
-    const int64_t end = st.end;
+    const int64_t end = s_end;
     const int64_t te = end / DEC_TILE;
     if (te < d.ntiles) {
         uint32_t nb = 0, nr = 0;
@@ -415,7 +435,7 @@ __global__ void __launch_bounds__(1024) k_unstuff_scan(const DecDesc* D, DecStat
         // the scan ends at a marker other than EOI: jpeg_finish_decompress
         // reads the markers after it (the JDK reader throws on a bad one), a
         // walk icx_seqdecode.cpp's route does - never the clean case's
-        if (end < d.scan_len && d.scan[end + 1] != 0xD9) st.status = 6;
+        if (!s_fake && end + 1 < d.scan_len && d.scan[end + 1] != 0xD9) st.status = 6;
         st.ent_len = len;
         st.nseg = carry_r + 1 <= (uint32_t)d.nseg_max ? carry_r + 1 : (uint32_t)d.nseg_max;
         if (carry_r + 1 > (uint32_t)d.nseg_max) st.status = 6;
@@ -655,6 +675,11 @@ __global__ void __launch_bounds__(256) k_unstuff_scatter(const DecDesc* D, const
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 if ((rstm >> k) & 1) {
+                    // marker orr must be RST(orr mod 8): another number makes
+                    // jdmarker.c resynchronise (jpeg_resync_to_restart), which
+                    // the walks do not restate - the host route does
+                    if (((vw[k >> 2] >> (8 * (k & 3))) & 7) != (orr & 7))
+                        atomicOr(&((DecState*)S)[img].status, 6);
                     for (int q = 0; q < DEC_PAD; q++) buf[ob + q] = 0xFF;
                     ob += DEC_PAD;
                     if (orr + 1 < (uint32_t)d.nseg_max) ((ICX_GLOBAL uint32_t*)d.seg)[orr + 1] = tile_off + ob;

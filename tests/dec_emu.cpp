@@ -74,12 +74,23 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
             end = i;
             break;
         }
+    // as k_unstuff_scan: trailing FFs at the end of the file start the fake
+    // EOI; a scan that ends at a marker other than EOI, or an RSTn out of
+    // sequence (below), is not the clean case
+    bool fake = false;
+    if (end == sl && sl > 0 && sc[sl - 1] == 0xFF) {
+        end = sl - 1;
+        while (end > 0 && sc[end - 1] == 0xFF) end--;
+        fake = true;
+    }
+    if (!fake && end + 1 < sl && sc[end + 1] != 0xD9) return ICX_E_CORRUPT;
     std::vector<uint8_t> ent;
     std::vector<uint32_t> seg{0};
     for (int64_t i = 0; i < end; i++) {
         int rst;
         const int k = dec_unstuff_rule(i ? sc[i - 1] : 0, sc[i], i + 1 < sl ? sc[i + 1] : 0, &rst);
         if (rst) {
+            if ((sc[i] & 7) != ((seg.size() - 1) & 7)) return ICX_E_CORRUPT;
             for (int p = 0; p < DEC_PAD; p++) ent.push_back(0xFF);
             seg.push_back((uint32_t)ent.size());
         } else if (k) {

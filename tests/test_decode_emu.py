@@ -181,3 +181,81 @@ def test_lean_walk_equals_full_walk(emu, oracle):
     # the lean walkers step symbol pairs (icx_decode.h): each pair step was
     # checked against two of the spec's single steps
     assert ctypes.c_long.in_dll(emu, "dec_emu_pairs").value > 1000
+
+
+@pytest.mark.parametrize("sub", [64, 1024, 16384])
+def test_emulated_decode_flags_every_damaged_file_it_would_get_wrong(emu, oracle, sub):
+    """The device's entropy decode on the recovery fixtures (truncation, bad
+    codes, RSTn missing / duplicated / renumbered, bad trailers): every file
+    either comes back flagged (ICX_E_CORRUPT: the host route with IJG 6b's
+    recovery, icx_seqdecode.cpp) or with exactly the oracle's coefficients -
+    never accepted with others.  Intact files are never flagged."""
+    import json
+    z = np.load(os.path.join(ROOT, "tests", "golden", "recovery_golden.npz"))
+    with open(os.path.join(ROOT, "tests", "golden", "recovery_golden.json")) as f:
+        meta = json.load(f)
+    flagged = accepted = 0
+    for k, name in enumerate(sorted(meta["cases"])):
+        data = z[f"jpg:{name}"].tobytes()
+        ref = oracle.jpeg_coefs(data)
+        nb = len(ref) if ref is not None else 1 << 16
+        rc, got, _ = run(emu, data, nb, k, sub)
+        if name.endswith("_intact"):
+            assert rc == 0, name
+        if rc == 0:
+            assert ref is not None and np.array_equal(got, ref), name
+            accepted += 1
+        else:
+            assert rc == 6, (name, rc)
+            flagged += 1
+    assert flagged >= 150 and accepted >= 20
+
+
+def test_emulated_decode_fuzz_never_accepts_a_wrong_decode(emu, oracle):
+    """Random damage (cuts, byte flips, planted 0xFF runs, RSTn removed /
+    renumbered, bytes inserted, markers planted) on small files of every
+    layout: the emulated device decode is flagged or equals the oracle."""
+    import io
+    from PIL import Image
+    rng = np.random.default_rng(606)
+    flagged = accepted = 0
+    for i in range(400):
+        h, w = int(rng.integers(8, 70)), int(rng.integers(8, 70))
+        img = smooth(h, w, i) if i % 2 else noise(h, w, i)
+        kw = dict(quality=int(rng.integers(30, 100)), subsampling=int(rng.integers(0, 3)))
+        if i % 3 == 0:
+            kw["restart_marker_blocks"] = int(rng.integers(1, 6))
+        buf = io.BytesIO()
+        Image.fromarray(img if i % 5 else img[:, :, 0]).save(buf, "JPEG", **kw)
+        d = bytearray(buf.getvalue())
+        sos = d.index(b"\xff\xda")
+        s0 = sos + 2 + int.from_bytes(d[sos + 2:sos + 4], "big")
+        op = int(rng.integers(0, 6))
+        if op == 0:
+            d = d[:int(rng.integers(s0, len(d)))]
+        elif op == 1:
+            d[int(rng.integers(s0, len(d) - 2))] = int(rng.integers(0, 256))
+        elif op == 2 and len(d) > s0 + 10:
+            a = int(rng.integers(s0, len(d) - 8))
+            d[a:a + 6] = b"\xff\x00" * 3
+        elif op == 3:
+            r = [k for k in range(s0, len(d) - 1) if d[k] == 0xFF and 0xD0 <= d[k + 1] <= 0xD7]
+            if r:
+                k = r[int(rng.integers(0, len(r)))]
+                d = d[:k] + d[k + 2:] if rng.random() < 0.5 else d[:k + 1] + bytes([0xD0 + int(rng.integers(0, 8))]) + d[k + 2:]
+        elif op == 4:
+            a = int(rng.integers(s0, len(d) - 1))
+            d = d[:a] + bytes(rng.integers(0, 256, int(rng.integers(1, 5)), dtype=np.uint8)) + d[a:]
+        else:
+            a = int(rng.integers(s0, len(d) - 1))
+            d = d[:a] + bytes([0xFF, int(rng.choice([0xD9, 0xC4, 0xFE, 0x01, 0xD3]))]) + d[a:]
+        data = bytes(d)
+        ref = oracle.jpeg_coefs(data)
+        nb = len(ref) if ref is not None else 1 << 16
+        rc, got, _ = run(emu, data, nb, i, int(rng.choice([64, 512, 4096])))
+        if rc == 0:
+            assert ref is not None and np.array_equal(got, ref), (i, op, kw)
+            accepted += 1
+        else:
+            flagged += 1
+    assert accepted >= 40 and flagged >= 200
