@@ -508,7 +508,15 @@ def main():
                 "traffic": pmc_traffic(dom, ks["units"] / ks["launches"]),
                 "issue": issue_rates(dom, ks["units"] / ks["launches"], ks["ms"] / ks["launches"] / 1e3),
                 "avg_launch_ms": round(ks["ms"] / ks["launches"], 4),
-                "algo_bytes_per_launch": int(bytes_of[dom] / ks["launches"])}
+                "algo_bytes_per_launch": int(bytes_of[dom] / ks["launches"]),
+                "frac_basis": f"{UNIT_NAME[dom]}: the bytes the kernel must move (DESIGN.md §4)"}
+        # SURVEY.md §8(d)'s per-unit bytes, beside the kernel's own: 128 B per
+        # block-trial (64 int16 coefficients read) for k_huff, 6 B/px for k_fdct
+        s8d = {"huff": 128.0, "fdct": 6.0}.get(dom)
+        if s8d is not None:
+            roof["frac_s8d"] = round(s8d * ks["units"] / (ks["ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+            roof["frac_s8d_basis"] = ("SURVEY.md 8(d): 128 B per scan block per trial (its coefficients read)"
+                                      if dom == "huff" else "SURVEY.md 8(d): 6 B/px (BGR read + int16 coefficients)")
     # every kernel with an algorithmic-bytes model, against the HBM roofline
     # (the north star's >= 60 % target is for the DCT stage, k_fdct)
     stages = {k: {"achieved_GBps": round(b / (kstats[k]["ms"] / 1e3) / 1e9, 1),
@@ -522,7 +530,14 @@ def main():
         stages["fdct"]["frac_at_6B_per_px"] = round(6 * px / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
     res = batch.results()
     line = {
-        "metric": "megapixels/sec JPEG encode (4K, -t 1MiB, q=0.25 cached)",
+        "metric": ("megapixels/sec JPEG encode (4K, -t 1MiB, q=0.25 cached), frames in HBM -> JPEG bytes in HBM"
+                   if not args.host_io else
+                   "megapixels/sec JPEG encode (4K, -t 1MiB, q=0.25 cached), pinned host BGR -> host JPEG bytes"),
+        "definition": ("value: decoded 4K BGR frames already resident in HBM when the timed region starts, every "
+                       "trial and the final bytes on the device (the task's bench contract); BASELINE.md's "
+                       "'encode path' (host BGR in -> host JPEG bytes out, PCIe included) is the host_io leg"
+                       if not args.host_io else
+                       "value: BASELINE.md's 'encode path', pinned host BGR in -> host JPEG bytes out, PCIe included"),
         "value": round(value, 2), "unit": "MP/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8/int16",

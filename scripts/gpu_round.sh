@@ -3,6 +3,11 @@
 # line, and a rocprofv3 kernel-trace summary of the headline alone (no e2e
 # leg, no CPU baseline: the summary's per-kernel means are the timed region's).
 # Every GPU step has its own time limit; the first failure ends the script.
+# Knobs (environment): TAG, SKIP_TESTS, PYTEST_ARGS, BENCH_ARGS, SKIP_PROF,
+# PROF_ARGS, T_TESTS / T_BENCH / T_PROF, and EXTRA: one more command (an A/B,
+# a decode or pipeline bench) run last under its own limit T_EXTRA, its
+# output in gpurun_out/extra_${TAG}.log - what the round-by-round one-off
+# launchers (git history: scripts/gpu_r*.sh) did.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
@@ -27,4 +32,9 @@ if [ -z "$SKIP_PROF" ]; then
   cd "$R"
   find gpurun_out/prof_${TAG} -name '*kernel_stats.csv' -exec cat {} \;
   grep -h '^{' gpurun_out/prof_${TAG}.out | tail -1 > gpurun_out/prof_${TAG}_bench.json || true
+fi
+if [ -n "$EXTRA" ]; then
+  timeout -k 10 ${T_EXTRA:-600} bash -o pipefail -c "$EXTRA" > gpurun_out/extra_${TAG}.log 2>&1 \
+      || { echo "extra failed rc=$?"; tail -20 gpurun_out/extra_${TAG}.log; exit 1; }
+  tail -20 gpurun_out/extra_${TAG}.log
 fi
