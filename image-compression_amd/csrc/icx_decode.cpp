@@ -386,8 +386,29 @@ icx_status run_host_entropy(icx_ctx* c, std::vector<DecItem>& items, int16_t* co
 
 // mode 0: decode to pixels; mode 1: coefficients only (debug: natural order, DC in [0]).
 // raw4: 4-component files out as libjpeg's CMYK samples (4 bytes a pixel, debug)
+icx_status run_decode_impl(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out, size_t coef_cap,
+                           bool raw4);
+
+// Every decode call returns with its device work finished, on the error paths
+// too ("entropy decode did not settle", a failed launch or copy mid-tail):
+// the aux streams' tails may still read scan and plane buffers that the caller
+// frees after an error, and a recycled buffer can be rewritten at once by an
+// upload on another copy stream (pool_free's invariant).
 icx_status run_decode(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out, size_t coef_cap,
                       bool raw4 = false)
+{
+    const icx_status s = run_decode_impl(c, jobs, n, coef_out, coef_cap, raw4);
+    if (s != ICX_OK) {
+        std::lock_guard<std::recursive_mutex> lk(c->mu);
+        (void)hipStreamSynchronize(c->stream);
+        for (int k = 0; k < c->n_dec_aux; k++) (void)hipStreamSynchronize(c->dec_aux[k]);
+        (void)hipGetLastError();
+    }
+    return s;
+}
+
+icx_status run_decode_impl(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coef_out, size_t coef_cap,
+                           bool raw4)
 {
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     HostSpan call{c, "host.call_decode"};  // the whole call, wall time (profiling)
@@ -893,10 +914,19 @@ icx_status pool_alloc(icx_ctx* ctx, DevPool& P, size_t bytes, void** ptr)
     }
     // a new buffer (or slab): allocated outside every lock (a pinned
     // allocation takes milliseconds; other threads keep taking cached buffers)
-    const bool slab = P.slabbed(c);
-    const size_t bytes_new = slab ? P.slab_bytes(c) : c;
+    bool slab = P.slabbed(c);
+    size_t bytes_new = slab ? P.slab_bytes(c) : c;
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = P.host ? hipHostMalloc(ptr, bytes_new, hipHostMallocPortable) : hipMalloc(ptr, bytes_new);
+    if (e != hipSuccess && slab) {
+        // no room for a whole slab (16x the class on the device): the class
+        // size alone may still fit - a tight device must not fail an
+        // allocation a plain hipMalloc would serve
+        (void)hipGetLastError();
+        slab = false;
+        bytes_new = c;
+        e = P.host ? hipHostMalloc(ptr, bytes_new, hipHostMallocPortable) : hipMalloc(ptr, bytes_new);
+    }
     if (e != hipSuccess) {
         std::lock_guard<std::recursive_mutex> lk(ctx->mu);  // (no pool lock held: no lock-order inversion)
         return hip_fail(ctx, e, P.host ? "hipHostMalloc" : "hipMalloc");
@@ -928,10 +958,12 @@ icx_status pool_free(icx_ctx* ctx, DevPool& P, void* ptr)
         if (l != P.live_.end()) {
             c = l->second;
             P.live_.erase(l);
-            // A recycled buffer's next use is a copy or launch on this context's
-            // stream, ordered after every launch that used it before, so recycling
-            // needs no synchronisation.  (Host buffers: every call that reads one
-            // synchronises before returning.)
+            // Recycling needs no synchronisation because every call that uses a
+            // pool buffer has finished its device work when it returns, on every
+            // path (run_decode synchronises its streams after an error too): the
+            // buffer's next use - a launch on this context's stream, or an
+            // icx_upload / icx_stage_files copy on one of its copy streams - can
+            // only come after that.  (Host buffers: likewise.)
             if (P.cached + c <= P.limit || P.carved.count(ptr)) {
                 P.free_[c].push_back(ptr);
                 P.cached += c;

@@ -330,6 +330,8 @@ class DeviceReader:
         self.devices = sorted(self.by_dev)
         self.assigned = {d: 0 for d in self.devices}
         self.lock = threading.Lock()
+        self.mean_size = 4 << 20  # running mean of staged file sizes (the estimate a chunk reserves)
+        self.staged = 0
 
     def __call__(self, path):
         from .core import PinnedBuffer
@@ -349,9 +351,14 @@ class DeviceReader:
         returns their _Items.  Files that are not device JPEGs go through
         _prepare's host readers."""
         from .core import DeviceImage
-        d = self.pick(0)
-        codec = self.by_dev[d]
         n = len(pairs)
+        # reserve the chunk's estimated bytes up front: reader threads that
+        # pick at the same time then spread over the devices instead of all
+        # taking the one with the fewest bytes so far (ADVICE r5); corrected
+        # to the actual bytes below
+        est = int(self.mean_size) * n
+        d = self.pick(est)
+        codec = self.by_dev[d]
         jobs = (N.StageJob * n)()
         keep = []
         for k, (_, path) in enumerate(pairs):
@@ -364,8 +371,12 @@ class DeviceReader:
             st = codec._lib.icx_stage_files(codec._ctx, jobs, n)
         if st != N.OK:
             log.warning("icx_stage_files: %s", codec.last_error())
+        got = sum(int(jobs[k].size) for k in range(n) if jobs[k].dev)
         with self.lock:
-            self.assigned[d] += sum(int(jobs[k].size) for k in range(n) if jobs[k].dev)
+            self.assigned[d] += got - est
+            if got:
+                self.staged += n
+                self.mean_size += (got / n - self.mean_size) * min(1.0, n / self.staged)
         out = []
         for k, (i, path) in enumerate(pairs):
             j = jobs[k]
@@ -374,16 +385,27 @@ class DeviceReader:
         return out
 
     def upload(self, buf):
+        """The file's bytes in HBM of the device with the fewest bytes so far;
+        if the device has no room for them (or the copy fails), the pinned
+        host bytes themselves: the decode call then reads them from there
+        (the file used to fail with FAILED_UNKNOWN)."""
         from .core import DeviceImage
         with self.lock:
             d = min(self.devices, key=lambda k: self.assigned[k])
             self.assigned[d] += buf.size
         codec = self.by_dev[d]
+        dev = None
         try:
             dev = DeviceImage(codec, (buf.size,))
             codec._check(codec._lib.icx_upload(codec._ctx, dev.ptr, buf.ptr, buf.size), "icx_upload")
-        finally:
-            buf.free()
+        except (N.IcxError, MemoryError) as e:
+            log.warning("file upload to GPU %d failed (%s): decoding from host memory", d, e)
+            if dev is not None:
+                dev.free()
+            with self.lock:
+                self.assigned[d] -= buf.size
+            return buf
+        buf.free()
         return dev
 
 
