@@ -47,6 +47,8 @@ def build_parser():
     p.add_argument("--workers-per-device", type=int, default=3,
                    help="GPU worker threads (libicx contexts) per device")
     p.add_argument("--group", type=int, default=64, help="JPEGs (or PNGs) per device batch")
+    p.add_argument("--group-max", type=int, default=256,
+                   help="files a GPU worker takes at once when more are waiting (larger device calls)")
     p.add_argument("--decode-threads", type=int, default=None)
     p.add_argument("-V", "--version", action="version", version="1.0")
     return p
@@ -90,7 +92,8 @@ def main(argv=None) -> int:
         dist.init_process_group("gloo")
     codecs = [Codec(d) for d in devices for _ in range(max(1, a.workers_per_device))]
     batch = CompressionBatch(a.file_list, a.output_dir, params, a.timeOut, a.cache_db, codecs=codecs,
-                             group_size=a.group, decode_threads=a.decode_threads, rank=rank, world=world)
+                             group_size=a.group, decode_threads=a.decode_threads, rank=rank, world=world,
+                             group_max=a.group_max)
     if dist is None:
         rep = batch.execute()
     else:

@@ -906,6 +906,60 @@ def shard(lines, rank: int, world: int, cost=_file_cost):
     return [(i, lines[i]) for i in mine]
 
 
+class _Feed:
+    """Work for the GPU workers, per device: JPEG items (their files already
+    on that device), PNG items and single other items, put one by one by the
+    reader side.  A worker takes a group once group_size items of a kind are
+    waiting - or whatever is waiting once the readers are done - and then up
+    to group_max of them: when the readers outpace the GPU, files pile up
+    while a worker is busy and its next call is larger (fewer, bigger device
+    calls: a 64-file call costs its device ~2x per frame what a 1000-frame
+    call does); when the GPU outpaces the readers, groups stay
+    at group_size and the device waits for files either way."""
+
+    def __init__(self, keys, group_size, group_max):
+        self.cv = threading.Condition()
+        self.jpeg = {k: [] for k in keys}
+        self.png = []   # any device
+        self.other = {k: [] for k in keys}
+        self.group_size, self.group_max = group_size, group_max
+        self.closed = False
+
+    def put(self, dev, kind, its):
+        with self.cv:
+            if kind == "jpeg":
+                self.jpeg[dev].extend(its)
+            elif kind == "png":
+                self.png.extend(its)
+            else:
+                self.other[dev].extend(its)
+            self.cv.notify_all()
+
+    def waiting(self, dev):
+        with self.cv:
+            return len(self.jpeg[dev])
+
+    def close(self):
+        with self.cv:
+            self.closed = True
+            self.cv.notify_all()
+
+    def take(self, dev):
+        """(kind, items) for a worker of `dev`, or None once closed and empty."""
+        with self.cv:
+            while True:
+                if self.other[dev]:
+                    return "other", [self.other[dev].pop(0)]
+                for kind, lst in (("jpeg", self.jpeg[dev]), ("png", self.png)):
+                    if len(lst) >= self.group_size or (self.closed and lst):
+                        grp = lst[:self.group_max]
+                        del lst[:self.group_max]
+                        return kind, grp
+                if self.closed:
+                    return None
+                self.cv.wait()
+
+
 class CompressionBatch:
     """CompressionBatch.execute: decode on host threads, compress on the GPU(s).
 
@@ -915,7 +969,7 @@ class CompressionBatch:
     def __init__(self, file_list_path, save_dir, params: CompressionParams, time_out_hr: float = 24,
                  h2_cache_path="image-compression-cache", codecs=None, group_size: int = 64,
                  decode_threads: Optional[int] = None, rank: int = 0, world: int = 1,
-                 device_decode: Optional[bool] = None, stage_times: bool = False):
+                 device_decode: Optional[bool] = None, stage_times: bool = False, group_max: int = 0):
         self.file_list_path = file_list_path
         self.save_dir = save_dir
         self.params = params
@@ -923,6 +977,9 @@ class CompressionBatch:
         self.h2_cache_path = h2_cache_path
         self.codecs = codecs or []
         self.group_size = max(1, group_size)
+        # a GPU worker that finds more than group_size files waiting takes up
+        # to group_max of them in one device call (0: group_size, fixed groups)
+        self.group_max = max(self.group_size, group_max)
         self.decode_threads = decode_threads or host_cores()[0]
         self.rank, self.world = rank, world
         self.stage_times = StageTimes() if stage_times else None
@@ -987,14 +1044,14 @@ class CompressionBatch:
         # that GPU's workers take it.  Otherwise one queue for every worker.
         per_dev = isinstance(self.device_decode, DeviceReader)
         keys = sorted({getattr(c, "device", None) for c in self.codecs}) if per_dev else [None]
-        queues = {k: queue.Queue() for k in keys}
+        feed = _Feed(keys, self.group_size, self.group_max)
         rr = [0]
 
         def put(kind, its, dev=None):
             if dev is None:  # host-resident work: any device, round robin
                 dev = keys[rr[0] % len(keys)]
                 rr[0] += 1
-            queues[dev].put((kind, its))
+            feed.put(dev, kind, its)
 
         def dev_of(it):
             d = it.decoded.data if it.decoded is not None else None
@@ -1049,10 +1106,10 @@ class CompressionBatch:
 
         def gpu_worker(codec):
             _tls.stages = self.stage_times
-            work = queues[getattr(codec, "device", None) if per_dev else None]
+            dev = getattr(codec, "device", None) if per_dev else None
             while True:
                 with _span("queue_wait"):
-                    grp = work.get()
+                    grp = feed.take(dev)
                 if grp is None:
                     return
                 kind, its = grp
@@ -1074,8 +1131,6 @@ class CompressionBatch:
         workers = [threading.Thread(target=gpu_worker, args=(c,), daemon=True) for c in self.codecs]
         for w in workers:
             w.start()
-        pending_jpeg = {k: [] for k in keys}
-        pending_png: List[_Item] = []
         with cf.ThreadPoolExecutor(self.decode_threads) as pool:
             if per_dev and hasattr(self.codecs[0], "_lib") and hasattr(self.codecs[0]._lib, "icx_stage_files"):
                 step = max(1, min(8, self.group_size // 4))  # files per native staging call
@@ -1096,31 +1151,18 @@ class CompressionBatch:
                         fmt = it.decoded.format_name
                         if fmt in ("jpeg", "jpg"):
                             d = dev_of(it)
-                            if d not in pending_jpeg:  # a host-decoded JPEG: any device's group
-                                d = min(keys, key=lambda k: len(pending_jpeg[k]))
-                            pj = pending_jpeg[d]
-                            pj.append(it)
-                            if len(pj) >= self.group_size:
-                                put("jpeg", list(pj), d)
-                                pj.clear()
+                            if d not in keys:  # a host-decoded JPEG: any device's group
+                                d = min(keys, key=lambda k: feed.waiting(k))
+                            put("jpeg", [it], d)
                         elif fmt == "png":
-                            pending_png.append(it)
-                            if len(pending_png) >= self.group_size:
-                                put("png", pending_png)
-                                pending_png = []
+                            put("png", [it])
                         else:
                             put("other", [it])
             except cf.TimeoutError:
                 log.warning("執行緒池等待逾時，部分任務可能未完成。")
                 for f in futs:
                     f.cancel()
-        for d, pj in pending_jpeg.items():
-            if pj:
-                put("jpeg", pj, d)
-        if pending_png:
-            put("png", pending_png)
-        for c in self.codecs:
-            queues[getattr(c, "device", None) if per_dev else None].put(None)
+        feed.close()  # workers drain what is left, then stop
         for w in workers:
             w.join(timeout=max(1.0, deadline - time.perf_counter()))
         writer.shutdown(wait=True)
