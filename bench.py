@@ -35,7 +35,7 @@ W, H = 3840, 2160
 TARGET = 1 << 20
 Q0 = 0.25
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s
-# Algorithmic bytes of each kernel (DESIGN.md §Kernels).  fdct and huff move
+# Algorithmic bytes of each kernel (DESIGN.md §4).  fdct and huff move
 # content-dependent amounts (candidate lists), so the library counts them per
 # launch ("<kernel>.bytes" profile entries): fdct = pixels read + lists, list
 # offsets and lengths written; huff = per trial, every block's padded list +
@@ -239,7 +239,7 @@ def _e2e_run(codec, dev, frames, n_frames, steps, dist=None, world=1):
             "mean_src_jpeg_bytes": int(np.mean(lens))}
     # the decode against HBM on SURVEY §8(d)'s decode bytes: the compressed
     # file read + the 3 B/px BGR frame written (the walks are latency-bound,
-    # DESIGN.md §10, so this fraction stays small)
+    # DESIGN.md §5.5, so this fraction stays small)
     dbytes = float(sum(lens)) + 3.0 * W * H * n_frames
     gbps = dbytes * steps / td / 1e9
     line["decode_roofline"] = {"bound": "hbm", "achieved": round(gbps, 1), "peak": 8000.0, "unit": "GB/s",

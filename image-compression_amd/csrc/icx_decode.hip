@@ -849,7 +849,7 @@ __global__ void __launch_bounds__(DEC_SYNC_NT) k_dec_sync(const DecDesc* D, cons
         // workgroup share the image): a worklist slot per changed lane from
         // the wave's base by its rank among the changed lanes - device
         // atomics are slow memory operations the wave's next loads queue
-        // behind (the FDCT's per-wave atomics cost 5.7 %)
+        // behind (the FDCT's per-wave atomics cost 5.7 %, profiles/NOTES.md §9)
         const uint64_t act = __ballot(1);
         const uint64_t mw = __ballot(j + 1 < st.nsub);
         const int lane = threadIdx.x & 63, leader = __ffsll((unsigned long long)act) - 1;
@@ -1109,7 +1109,7 @@ __global__ void __launch_bounds__(DEC_WRITE_NT) k_dec_write(const DecDesc* D, De
 // per component, a segmented scan over the tile (flag = a restart interval
 // starts at the MCU) carried from the previous tile, then the values.  (Round
 // 4; it was a 32-MCU sequential run per thread in two passes: 8.7 ms per
-// 1000 4K frames)
+// 1000 4K frames, profiles/NOTES.md §10.)
 struct DcAgg {
     int32_t v[4];  // per component (CMYK / YCCK: four)
     int f;  // a restart interval starts inside the span: what came before does not count
@@ -1560,7 +1560,7 @@ __global__ void __launch_bounds__(256) k_dec_color(const DecDesc* D, const DecSt
             }
             // to RGB as the host path did (Pillow: the samples read as Adobe-inverted
             // CMYK, then cmyk2rgb: nk - nk * c / 255 with nk = 255 - k); TwelveMonkeys'
-            // ICC conversion is not restatable here (parity unpinned, DESIGN.md §10)
+            // ICC conversion is not restatable here (parity unpinned, DESIGN.md §2)
             const int nk = kk;  // 255 - (255 - raw k)
             uint8_t* o = orow + (int64_t)(x0 + k) * 3;
             const int cv[3] = {255 - c0, 255 - c1, 255 - c2};

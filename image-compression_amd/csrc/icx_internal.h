@@ -1,6 +1,6 @@
 // icx_internal.h — device-visible data structures of the MI355X JPEG path.
 //
-// HBM layout per image (DESIGN.md §Data layout):
+// HBM layout per image:
 //   px          u8 BGR/RGB/grey rows (caller's buffer, or the resize buffer)
 //   coefs       sparse jpeg_fdct_islow output (raw, x8): per scan block
 //               (MCU order Y0 Y1 Y2 Y3 Cb Cr) a list of 32-bit entries
@@ -38,7 +38,7 @@ namespace icx {
 // blocks.  (Round 4 measured one wave per 64-block chunk, four chunks per
 // workgroup sharing the coding tables, no workgroup barrier after the table
 // load: k_huff +2...5 %, step +7 % with the 4x chunk count in k_scan/k_stuff;
-// DESIGN.md §9.)
+// profiles/NOTES.md §9.)
 constexpr int CHUNK_BLOCKS = 256;  // scan blocks per Huffman chunk
 constexpr int HUFF_THREADS = CHUNK_BLOCKS;
 constexpr int MAX_BLOCK_BITS = 1664;     // >= 22 (DC) + 63 * 26 (AC) bits, multiple of 32

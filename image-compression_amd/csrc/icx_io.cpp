@@ -9,7 +9,7 @@
 // dimensions gate, and for a JPEG the device decoder will take, one copy to
 // HBM on a copy stream of the context's own (icx_upload) - all without the
 // Python interpreter lock, so a Python caller's reader threads overlap fully
-// (DESIGN.md §6).  The caller decides every result (skip, format fallback,
+// (DESIGN.md §9).  The caller decides every result (skip, format fallback,
 // decode) from the staged facts, in the reference's order.
 #include <hip/hip_runtime.h>
 

@@ -13,7 +13,7 @@
 //                               the A3 binary-search step (decide_trial)
 //   k_ffscan + k_stuff          final file: header, stuffed bytes, EOI
 //   k_resize                    A12 Java2D bilinear (TransformHelper)
-// No MFMA: integer, byte-oriented work bound by HBM (DESIGN.md §Kernels).
+// No MFMA: integer, byte-oriented work bound by HBM (DESIGN.md §4).
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 

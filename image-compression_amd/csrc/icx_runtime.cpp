@@ -154,7 +154,7 @@ bool is_palette(int fmt) { return fmt == ICX_INDEXED8 || fmt == ICX_BINARY1; }
 // --- default colour maps of the palette types (BufferedImage.java's
 // TYPE_BYTE_INDEXED / TYPE_BYTE_BINARY constructors) and what Java2D derives
 // from a map for storing into it (OpenJDK java.desktop; no JDK here to pin
-// them, parity unpinned: DESIGN.md §11)
+// them, parity unpinned: DESIGN.md §6)
 int default_palette(bool binary, uint32_t* pal)
 {
     if (binary) {  // IndexColorModel(1, 2, {0, 0xff} x 3)

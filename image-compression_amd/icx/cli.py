@@ -11,7 +11,7 @@ to the writers) overlaps another group's kernels, and one context's
 latency-bound relaxation launches overlap another's bulk kernels: files ->
 files JPEG on one MI355X (round 5, warm cache, three runs each) 3611-4009
 files/s with two workers, 3952-4178 with three (the default), 4011-4584 with
-four, whose learning runs are 10 % slower.
+four, whose learning runs are 10 % slower (profiles/NOTES.md §6).
 Multi-GPU: by default one process drives every visible GPU (worker threads
 per device sharing one L1 cache, the reference's one ConcurrentHashMap); or
 one process per GPU under torchrun (RANK/WORLD_SIZE/LOCAL_RANK): the file

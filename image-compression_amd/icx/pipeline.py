@@ -54,7 +54,7 @@ log = logging.getLogger("icx.pipeline")
 class StageTimes:
     """Seconds spent per stage of a CompressionBatch run, summed over the
     threads doing it (thread-seconds): where the host time of the files ->
-    files path goes (DESIGN.md §6).  Stages: stat, read (file bytes into
+    files path goes (DESIGN.md §9).  Stages: stat, read (file bytes into
     pinned memory), parse (JPEG header), host_decode (Pillow: PNG and files
     the device decoder refuses), queue_wait (a GPU worker idle for work),
     gpu_decode / gpu_fit / gpu_png (the batched device calls, wall time of
@@ -220,7 +220,7 @@ def _to_array(im, path=None):
     type and the PNG is written back with it (ImageTools.java:12-15)."""
     if path is not None and im.format == "PNG":
         r = _indexed_raster(im, path)
-        if r is not None:  # TYPE_BYTE_INDEXED / TYPE_BYTE_BINARY (kept by ImageTools, DESIGN.md §11)
+        if r is not None:  # TYPE_BYTE_INDEXED / TYPE_BYTE_BINARY (kept by ImageTools, DESIGN.md §6)
             return r
     mode = im.mode
     if mode == "L":

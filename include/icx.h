@@ -360,7 +360,7 @@ icx_status icx_memcpy(icx_ctx* ctx, void* dst, const void* src, size_t bytes);
  * when it returns), on a copy stream of its own and without waiting for a
  * batch call running on the context: reader threads push file bytes to the
  * GPU while the decode / encode kernels of other files run (the files ->
- * files path, DESIGN.md §6; the decode then reads device-resident files). */
+ * files path, DESIGN.md §9; the decode then reads device-resident files). */
 icx_status icx_upload(icx_ctx* ctx, void* dst, const void* src, size_t bytes);
 
 /* ------------------------------------------------------------- file staging */

@@ -20,7 +20,7 @@
  * Pinning: A5-A10 are checked byte for byte against libjpeg-turbo 3.1.4
  * golden files (tests/golden/, made by gen_golden.py); A3 against search
  * traces computed with that encoder.  A12 is "parity unpinned": no Java2D
- * exists in this container (DESIGN.md §Oracle).
+ * exists in this container (DESIGN.md §2).
  */
 #ifndef ICX_ORACLE_H
 #define ICX_ORACLE_H

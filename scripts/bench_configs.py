@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-config throughput on one MI355X for BASELINE.json's configs (SURVEY.md
 §8d), at bounded frame counts (the multi-GPU variants shard the same work per
-rank with no exchange, DESIGN.md §7).  Inputs and outputs resident in HBM.
+rank with no exchange, DESIGN.md §8).  Inputs and outputs resident in HBM.
 One JSON line per config:
 
   C2  4K frames, -t 1 MiB, cached q = 0.25 (bench.py's headline workload)

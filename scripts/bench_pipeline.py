@@ -47,6 +47,7 @@ def main():
                     help="GPU of each worker (one libicx context each); default: the CLI's, two workers on GPU 0")
     ap.add_argument("--group-max", type=int, default=256, help="files a worker takes at once when more wait")
     ap.add_argument("--no-warmup", action="store_true")
+    ap.add_argument("--reps", type=int, default=3, help="timed repetitions of each run (median reported)")
     ap.add_argument("--procs", type=int, default=1, help="processes sharing the list (warm-cache run only)")
     ap.add_argument("--decode-threads", type=int, default=0, help="host reader threads (0: every usable core)")
     a = ap.parse_args()
@@ -112,7 +113,15 @@ def main():
         shutil.rmtree(os.path.join(work, "out_w"), ignore_errors=True)
         os.sync()
     runs = []
-    for r, name in enumerate(("search", "learn", "warm cache")):
+    order = [("search", k) for k in range(a.reps)]
+    for k in range(a.reps):  # each learn run starts from an empty cache DB; the warm runs reuse the last one's
+        order.append(("learn", k))
+    order += [("warm cache", k) for k in range(a.reps)]
+    for r, (name, rep_k) in enumerate(order):
+        if name == "learn":
+            for f in os.listdir(work):
+                if f.startswith("cache"):
+                    os.remove(os.path.join(work, f))
         out = os.path.join(work, f"out{r}")
         for c in codecs:
             c.profile(True)
@@ -135,7 +144,8 @@ def main():
                 if q["launches"]:
                     host[k] = {"ms": round(host.get(k, {}).get("ms", 0.0) + q["ms"], 2),
                                "calls": host.get(k, {}).get("calls", 0) + q["launches"]}
-        runs.append({"run": name, "seconds": round(dt, 3),
+        shutil.rmtree(out, ignore_errors=True)
+        runs.append({"run": name, "rep": rep_k, "seconds": round(dt, 3),
                      "images_per_s": round(rep.total / dt, 1), "mp_per_s": round(rep.megapixels / dt, 1),
                      "success": rep.success, "failed": rep.failed, "skipped": rep.skipped,
                      "in_bytes": rep.original_size, "out_bytes": rep.compressed_size,
@@ -147,12 +157,19 @@ def main():
                      "file_read_GBps": round(rep.original_size / dt / 1e9, 2)})
     for c in codecs:
         c.close()
+    summary = {}
+    for name in ("search", "learn", "warm cache"):
+        rs = sorted((r for r in runs if r["run"] == name), key=lambda r: r["images_per_s"])
+        med = rs[len(rs) // 2]
+        summary[name] = {"images_per_s_median": med["images_per_s"], "mp_per_s_median": med["mp_per_s"],
+                         "device_busy_frac_median": med["device_busy_frac"],
+                         "images_per_s_all": [r["images_per_s"] for r in rs]}
     print(json.dumps({"metric": "CompressionBatch end-to-end (files -> files), 4K q95 JPEG" +
                                 (" + 4K PNG (configs[4] mix)" if a.png else "") + ", -t 1MiB, devices " + a.devices,
                       "files": a.files, "png_files": a.png, "group_size": a.group, "group_max": a.group_max,
                       "mean_src_bytes": int(np.mean([len(b) for b in blobs])),
                       "mean_png_src_bytes": int(np.mean([len(b) for b in png_blobs])) if png_blobs else 0,
-                      "runs": runs}))
+                      "summary": summary, "runs": runs}))
     if not a.dir:
         shutil.rmtree(work, ignore_errors=True)
 

@@ -13,7 +13,7 @@ inputs: header gather) or k_unstuff_count dispatch.  Per call:
     time it shared the chip (`shared_ms`) - a dispatch that overlaps another
     queue's long kernel (e.g. an 18-image k_dec_dc launched beside a
     1000-image k_dec_write) shows a long duration that is mostly waiting for
-    CUs, not work (DESIGN.md §10);
+    CUs, not work (profiles/NOTES.md §10);
   * the critical path as the busy union of all queues against the span
     (idle = host round trips).
 Usage: dec_timeline.py kernel_trace.csv > summary.json"""
