@@ -3,15 +3,19 @@ defaults, plus GPU placement flags.
 
   python -m icx -f list.txt -o outdir [-q 0.25] [-s 1048576] [-w 1920] [-i 1920]
                 [-t 1048576] [--timeOut 24] [--cache-db image-compression-cache]
-                [--devices 0,1] [--workers-per-device 3] [--group 64] [--decode-threads N]
+                [--devices 0,1] [--workers-per-device 2] [--group 64] [--group-max 0]
+                [--decode-threads N]
 
 Each device gets --workers-per-device GPU worker threads, each with its own
 libicx context, so one group's host work (file bytes to the decoder, results
 to the writers) overlaps another group's kernels, and one context's
-latency-bound relaxation launches overlap another's bulk kernels: files ->
-files JPEG on one MI355X (round 5, warm cache, three runs each) 3611-4009
-files/s with two workers, 3952-4178 with three (the default), 4011-4584 with
-four, whose learning runs are 10 % slower (profiles/NOTES.md §6).
+latency-bound relaxation launches overlap another's bulk kernels.  Files ->
+files JPEG on one MI355X, round 6 (1000 4K q95 files, medians of three runs,
+interleaved configurations; profiles/r6/pipeline/): two workers with groups of
+64 ran 3810-4320 files/s warm and 3825-4198 with every file searched, three
+workers 3078-3148 and larger groups (--group-max 128 / 256) 3160-3670 in the
+same calls; the box drifts 15-25 % over a call, so only the interleaved order
+separates them.
 Multi-GPU: by default one process drives every visible GPU (worker threads
 per device sharing one L1 cache, the reference's one ConcurrentHashMap); or
 one process per GPU under torchrun (RANK/WORLD_SIZE/LOCAL_RANK): the file
@@ -44,11 +48,12 @@ def build_parser():
     p.add_argument("--cache-db", default="image-compression-cache")
     p.add_argument("--devices", default=None,
                    help="GPU ordinals for this process, e.g. 0,1 (default: every visible GPU; LOCAL_RANK under torchrun)")
-    p.add_argument("--workers-per-device", type=int, default=3,
+    p.add_argument("--workers-per-device", type=int, default=2,
                    help="GPU worker threads (libicx contexts) per device")
     p.add_argument("--group", type=int, default=64, help="JPEGs (or PNGs) per device batch")
-    p.add_argument("--group-max", type=int, default=256,
-                   help="files a GPU worker takes at once when more are waiting (larger device calls)")
+    p.add_argument("--group-max", type=int, default=0,
+                   help="files a GPU worker takes at once when more are waiting (0: --group, fixed groups; "
+                        "larger calls measured no faster, DESIGN.md §9)")
     p.add_argument("--decode-threads", type=int, default=None)
     p.add_argument("-V", "--version", action="version", version="1.0")
     return p

@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--png", type=int, default=0, help="4K PNG files added to the list (configs[4] mix)")
     ap.add_argument("--devices", default="0,0",
                     help="GPU of each worker (one libicx context each); default: the CLI's, two workers on GPU 0")
-    ap.add_argument("--group-max", type=int, default=256, help="files a worker takes at once when more wait")
+    ap.add_argument("--group-max", type=int, default=0, help="files a worker takes at once when more wait (0: --group)")
     ap.add_argument("--no-warmup", action="store_true")
     ap.add_argument("--reps", type=int, default=3, help="timed repetitions of each run (median reported)")
     ap.add_argument("--procs", type=int, default=1, help="processes sharing the list (warm-cache run only)")

@@ -170,9 +170,10 @@ def test_cli_default_devices():
     assert default_devices(None, 8, 5, 8) == [5]
     assert default_devices("0,0,3", 1, 0, 8) == [0, 0, 3]
     assert default_devices("2", 4, 1, 8) == [2]
-    # three worker contexts per device (profiles/NOTES.md §6, round 5 r5t)
+    # two worker contexts per device, fixed groups of 64 (DESIGN.md §9, round 6 measurements)
     from icx.cli import build_parser
-    assert build_parser().parse_args(["-f", "l.txt", "-o", "out"]).workers_per_device == 3
+    a = build_parser().parse_args(["-f", "l.txt", "-o", "out"])
+    assert a.workers_per_device == 2 and a.group == 64 and a.group_max == 0
 
 
 def test_shard_partition():
