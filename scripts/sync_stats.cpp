@@ -1,0 +1,177 @@
+// sync_stats.cpp — research tool (not built into the library): how the
+// decoder's entry-state estimates (k_dec_init: a walk of `warm` bits from a
+// guessed state before each subsequence start) miss on a baseline JPEG, and
+// what other estimators would do, on the CPU with the product's own walker
+// (icx_decode.h).  The true path is the walk from the stream start; an
+// estimate is right when its state equals the true path's state at that bit.
+//
+//   g++ -O2 -std=c++17 -I image-compression_amd/csrc scripts/sync_stats.cpp \
+//       image-compression_amd/csrc/icx_jpeg_parse.cpp -o /tmp/sync_stats
+//   /tmp/sync_stats file.jpg [samples]
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <random>
+#include <vector>
+
+#include "icx_decode.h"
+#include "icx_jpeg_parse.h"
+
+using namespace icx;
+
+int main(int argc, char** argv)
+{
+    if (argc < 2) return 2;
+    FILE* f = fopen(argv[1], "rb");
+    if (!f) return 2;
+    std::vector<uint8_t> jpg;
+    {
+        uint8_t buf[1 << 16];
+        size_t n;
+        while ((n = fread(buf, 1, sizeof(buf), f)) > 0) jpg.insert(jpg.end(), buf, buf + n);
+        fclose(f);
+    }
+    const int samples = argc > 2 ? atoi(argv[2]) : 2000;
+    JpegHeader J;
+    if (parse_jpeg(jpg.data(), jpg.size(), jpg.size(), J)) return 3;
+    static DecTab T;
+    if (!build_dec_tab(J, T)) return 3;
+    const uint32_t sel = dec_selector(T);
+    DecDesc d{};
+    d.ncomp = J.ncomp;
+    d.nby = J.ncomp == 3 ? J.hs[0] * J.vs[0] : 1;
+    d.nbmcu = J.ncomp == 3 ? d.nby + 2 : 1;
+    d.wmcu = dec_walk_mcu(J.ncomp, d.nbmcu, J.td, J.ta);
+    const uint8_t* sc = jpg.data() + J.scan_off;
+    const int64_t sl = (int64_t)(jpg.size() - J.scan_off);
+    std::vector<uint8_t> ent;
+    std::vector<uint32_t> seg{0};
+    for (int64_t i = 0; i < sl; i++) {
+        if (i + 1 < sl && sc[i] == 0xFF && sc[i + 1] != 0x00 && sc[i + 1] != 0xFF && !(sc[i + 1] >= 0xD0 && sc[i + 1] <= 0xD7))
+            break;
+        int rst;
+        const int k = dec_unstuff_rule(i ? sc[i - 1] : 0, sc[i], i + 1 < sl ? sc[i + 1] : 0, &rst);
+        if (k && !rst) ent.push_back(sc[i]);
+    }
+    const uint32_t ent_bits = (uint32_t)ent.size() * 8;
+    for (int p = 0; p < DEC_TAIL + 64 + 4 * DEC_WIN_MAX; p++) ent.push_back(0xFF);
+    while (ent.size() % 4) ent.push_back(0xFF);
+    std::vector<uint32_t> words(ent.size() / 4 + 2, 0xFFFFFFFFu);
+    memcpy(words.data(), ent.data(), ent.size());
+    const DecLean* H = (const DecLean*)T.lean;
+    auto walker = [&]() { return dec_lean_walker(d, H, T.slow, sel, words.data(), seg.data(), 1u, ent_bits); };
+
+    // the true path: state (b, z) + 1 at every step boundary, 0 = no boundary
+    std::vector<uint16_t> truth(ent_bits + 64, 0);
+    {
+        auto w = walker();
+        w.start(dec_pack(0, 0, 0));
+        while (w.running(ent_bits)) {
+            truth[w.pos] = (uint16_t)(1 + (w.b << 6 | w.z));
+            w.step();
+        }
+    }
+    auto right = [&](uint64_t st) {
+        const uint32_t p = dec_pos(st);
+        return p < ent_bits && truth[p] == (uint16_t)(1 + (((st >> 8) & 7) << 6 | (st & 63)));
+    };
+    auto walk_to = [&](uint64_t from, uint32_t stop) {
+        uint32_t n;
+        return dec_lean_walk(d, H, T.slow, sel, words.data(), seg.data(), 1u, ent_bits, from, stop, n);
+    };
+    std::mt19937 rng(7);
+    const uint32_t lo = 70000, hi = ent_bits - 70000;
+    std::vector<uint32_t> starts(samples);
+    for (auto& s : starts) s = lo + rng() % (hi - lo);
+
+    // 1. sync distance of a walk from (b = 0, z = 0): bits until its state is the truth's
+    std::vector<uint32_t> dist;
+    int wrong_phase_meets = 0;
+    for (uint32_t s : starts) {
+        auto w = walker();
+        w.start(dec_pack(s, 0, 0));
+        uint32_t got = ~0u;
+        bool wp = false;
+        while (w.running(s + 65536)) {
+            if (right(w.state())) {
+                got = w.pos - s;
+                break;
+            }
+            if (w.z == 0 && truth[w.pos] && ((truth[w.pos] - 1) & 63) == 0) wp = true;  // a block start of the truth, other phase
+            w.step();
+        }
+        wrong_phase_meets += wp && got != ~0u ? 1 : 0;
+        dist.push_back(got);
+    }
+    std::vector<uint32_t> sd = dist;
+    std::sort(sd.begin(), sd.end());
+    auto pct = [&](double q) { return sd[(size_t)(q * (sd.size() - 1))]; };
+    printf("%s: %u bits, %d samples; sync distance p50 %u p90 %u p99 %u; beyond 65536: %ld; met a true block start in another phase first: %d\n",
+           argv[1], ent_bits, samples, pct(0.5), pct(0.9), pct(0.99), (long)std::count(sd.begin(), sd.end(), ~0u),
+           wrong_phase_meets);
+    for (uint32_t W : {1024u, 2048u, 4096u, 8192u, 16384u, 32768u}) {
+        int miss = 0;
+        for (uint32_t s : starts) miss += right(walk_to(dec_pack(s - W, 0, 0), s)) ? 0 : 1;
+        printf("  warm %5u from (0,0): miss %.3f\n", W, miss / (double)samples);
+    }
+    // 2. several phase hypotheses from the same start, majority of their exit states
+    for (uint32_t W : {1024u, 2048u, 4096u}) {
+        int miss = 0, any = 0, agree = 0;
+        for (uint32_t s : starts) {
+            std::map<uint64_t, int> votes;
+            bool one = false;
+            for (int b = 0; b < d.wmcu; b++) {
+                const uint64_t x = walk_to(dec_pack(s - W, b, 0), s);
+                votes[x]++;
+                one |= right(x);
+            }
+            uint64_t best = 0;
+            int bv = -1;
+            for (auto& kv : votes)
+                if (kv.second > bv) best = kv.first, bv = kv.second;
+            miss += right(best) ? 0 : 1;
+            any += one ? 1 : 0;
+            agree += bv == d.wmcu ? 1 : 0;
+        }
+        printf("  %d phases x warm %5u: majority miss %.3f, some phase right %.3f, all agree %.3f\n", d.wmcu, W,
+               miss / (double)samples, any / (double)samples, agree / (double)samples);
+    }
+    // 3. a warm-up walk that treats an overshooting run (a non-EOB AC symbol
+    // past zig-zag 63: never in a valid scan) like an invalid code - a bit
+    // later, block 0 - so a wrong path is dropped as soon as it shows
+    auto walk_v1 = [&](uint64_t from, uint32_t stop, int& drops) {
+        auto w = walker();
+        w.start(from);
+        while (w.running(stop)) {
+            w.R.refill();
+            const uint32_t e = dec_lean_lookup(H, w.ti, (const DecSlow*)T.slow, w.R.peek16(), w.z != 0);
+            const int za = (int)((e >> 5) & 127), z1 = w.z + za;
+            const int c2 = (int)((e >> DEC_PAIR_SHIFT) & 31), za2 = (int)(e >> 25);
+            const bool over = (e & 31) != 0 && w.z != 0 && ((za < 64 && z1 > 64) || (c2 && z1 < 64 && za2 < 64 && z1 + za2 > 64));
+            if (over) {
+                drops++;
+                w.invalid();
+                continue;
+            }
+            w.step();
+        }
+        return w.state();
+    };
+    for (uint32_t W : {2048u, 4096u, 8192u, 16384u}) {
+        int miss = 0, drops = 0;
+        for (uint32_t s : starts) miss += right(walk_v1(dec_pack(s - W, 0, 0), s, drops)) ? 0 : 1;
+        printf("  warm %5u, overshoot = invalid: miss %.3f (%.1f drops per walk)\n", W, miss / (double)samples,
+               drops / (double)samples);
+    }
+    // overshoots on the true path (must be 0)
+    {
+        int drops = 0;
+        walk_v1(dec_pack(0, 0, 0), std::min<uint32_t>(ent_bits, 4000000u), drops);
+        printf("  overshoots on the true path's first 4 Mbit: %d\n", drops);
+    }
+    return 0;
+}
