@@ -805,11 +805,21 @@ __device__ __forceinline__ uint32_t selector(const DecTab* T)
 #ifndef ICX_DEC_AGG
 #define ICX_DEC_AGG 0  // k_dec_sync: wave-aggregated worklist / change-count atomics (+-0: few lanes change)
 #endif
+// Issue priority of the relaxation's later launches: their few long re-walks
+// share SIMDs with the settled images' write and colour passes (aux streams),
+// and a re-walk is a serial chain of table look-ups, so its wave goes first
+// when both are ready (s_setprio; 2: the first launch too).  Decode per call,
+// two interleaved rounds (profiles/r6/ab/ab_r6_sync_prio.txt): 200 frames
+// 17.10 -> 16.80 ms (2: 16.84), 64 and 1000 frames +-0.
+#ifndef ICX_DEC_SYNC_PRIO
+#define ICX_DEC_SYNC_PRIO 1
+#endif
 template <bool FIRST>
 __global__ void __launch_bounds__(DEC_SYNC_NT) k_dec_sync(const DecDesc* D, const DecState* S, Plan p, uint32_t sub_bits,
                                                   int iter, int nimg, uint32_t* changed)
 {
     DEC_WALK_TABLES
+    if (ICX_DEC_SYNC_PRIO > (FIRST ? 1 : 0)) __builtin_amdgcn_s_setprio(3);
     int slot;
     int64_t wg;
     if (!plan_slot(p, slot, wg)) return;

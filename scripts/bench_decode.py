@@ -18,6 +18,20 @@ import numpy as np  # noqa: E402
 
 
 def sources(h, w, distinct, progressive=False):
+    # cached per process tree in /tmp (an A/B runs this script many times)
+    cache = f"/tmp/icx_bench_decode_{h}x{w}_{distinct}_{int(progressive)}.npz"
+    if os.path.exists(cache):
+        z = np.load(cache)
+        return [z[f"s{i}"].tobytes() for i in range(distinct)]
+    out = _make_sources(h, w, distinct, progressive)
+    try:
+        np.savez(cache, **{f"s{i}": np.frombuffer(b, np.uint8) for i, b in enumerate(out)})
+    except OSError:
+        pass
+    return out
+
+
+def _make_sources(h, w, distinct, progressive):
     from PIL import Image
     from tests.oracle_ffi import noise, smooth
     out = []
