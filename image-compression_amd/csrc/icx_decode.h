@@ -479,6 +479,103 @@ struct DecReaderT {
 };
 using DecReader = DecReaderT<DEC_WIN, ICX_DEC_LDS_WIN != 0>;
 
+// The state-only walks' bit reader (ICX_DEC_FUNNEL): the next 32 stream bits
+// are one funnel shift of two byte-swapped words, alignbit(w0, w1, s), with s
+// in [0, 31] (s = 0: w1 itself), so a step costs a subtract, a mask, a compare
+// and two word selects where DecReaderT's 64-bit buffer took a 64-bit shift,
+// an OR-in under selects and its fill count.  Steps consume at most 31 bits
+// (a code and its extra bits, or a symbol pair), so one word moves in per
+// step at most; the next word (q0) comes from the window rows as in
+// DecReaderT (LDS on the device, rows byte-swapped when the window is
+// fetched), read unconditionally ahead of its use.  First sync walk per 1000
+// frames 12.15 -> 11.48 ms, e2e decode 68.3 -> 67.45 ms
+// (profiles/r6/ab/ab_r6_funnel_reader.txt).
+#ifndef ICX_DEC_FUNNEL
+#define ICX_DEC_FUNNEL 1
+#endif
+template <int WIN>
+struct DecFunnelReader {
+    using Base = DecReaderT<WIN, true>;
+    static constexpr int DEC_WIN = WIN;
+    const ICX_GLOBAL uint32_t* w;
+    uint32_t w0, w1, q0;
+    int s;
+    uint32_t wi;  // stream word index of row 0 of the window
+    typename Base::Lds m;
+
+    ICX_HD int used() const { return m.row(); }
+    ICX_HD int left() const { return WIN - used(); }
+    ICX_HD bool low() const { return left() <= 1; }
+    ICX_HD bool wants() const { return true; }
+    ICX_HD void fetch(uint32_t at)
+    {
+        wi = at;
+        const ICX_GLOBAL uint32_t* const wa = w + at;
+        uint32_t t[WIN];
+#pragma unroll
+        for (int j = 0; j < WIN; j++) t[j] = wa[j];
+#if defined(__HIP_DEVICE_COMPILE__)
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
+        m.bind();
+#pragma unroll
+        for (int j = 0; j < WIN; j++) m.put(j, dec_be32(t[j]));
+        q0 = dec_be32(t[0]);
+    }
+    ICX_HD void advance(bool need) { q0 = m.next(need); }
+    ICX_HD void top_up() { fetch(wi + (uint32_t)used()); }
+    ICX_HD void init(const uint32_t* words, uint32_t pos)
+    {
+        w = (const ICX_GLOBAL uint32_t*)words;
+        fetch(pos >> 5);
+        const uint32_t off = pos & 31;
+        const uint32_t a = q0;
+        advance(true);
+        if (off) {
+            w0 = a;
+            w1 = q0;
+            advance(true);
+            s = 32 - (int)off;
+        } else {
+            w0 = 0;
+            w1 = a;
+            s = 0;
+        }
+    }
+    ICX_HD void park()
+    {
+        w0 = w1 = q0 = 0;
+        s = 0;
+        wi = 0;
+        m.bind();
+    }
+    ICX_HD uint32_t peek32() const
+    {
+#if defined(__HIP_DEVICE_COMPILE__)
+        return __builtin_amdgcn_alignbit(w0, w1, (uint32_t)s);
+#else
+        return s ? (w0 << (32 - s)) | (w1 >> s) : w1;
+#endif
+    }
+    ICX_HD uint32_t peek16() const { return peek32() >> 16; }
+    ICX_HD void refill()
+    {
+#if !defined(__HIP_DEVICE_COMPILE__)
+        if (left() <= 2) top_up();  // host loops have no top-up points (as DecReaderT)
+#endif
+    }
+    ICX_HD void skip(int c)  // 0 <= c <= 31
+    {
+        const int s2 = s - c;
+        const bool need = s2 < 0;
+        s = s2 & 31;
+        w0 = need ? w1 : w0;
+        w1 = need ? q0 : w1;
+        advance(need);
+    }
+};
+using DecLeanReader = typename std::conditional<ICX_DEC_FUNNEL && ICX_DEC_LDS_WIN, DecFunnelReader<DEC_WIN>, DecReader>::type;
+
 #ifndef ICX_DEC_WALK_UNROLL2
 #define ICX_DEC_WALK_UNROLL2 1  // state-only walks: two steps per top-up check (-2.6 %, profiles/r4/ab_r4ze_dec_walk_unroll.txt)
 #endif
@@ -906,7 +1003,7 @@ struct DecLeanWalker {
     uint32_t pos, n;
     int b, z, ti;  // ti: table of the next symbol (component of block b, DC at z == 0)
     bool two;      // the last step was a symbol pair (tests compare against DecWalker's single steps)
-    DecReader R;
+    DecLeanReader R;
     const uint32_t* words;
 
 #if ICX_DEC_BSEL
