@@ -493,7 +493,27 @@ using DecReader = DecReaderT<DEC_WIN, ICX_DEC_LDS_WIN != 0>;
 #ifndef ICX_DEC_FUNNEL
 #define ICX_DEC_FUNNEL 1
 #endif
+#ifndef ICX_DEC_FUNNEL_WRITE
+#define ICX_DEC_FUNNEL_WRITE 1  // the write pass's walk too (register window): write pass 28.12 -> 27.66 ms per 1000 frames (ab_r6_funnel_write.txt)
+#endif
+// A window in registers (the write pass: its workgroups fill LDS already)
+// shifts by one word under the lane's need, one select per word.
 template <int WIN>
+struct DecRegRows {
+    uint32_t q[WIN + 1];  // [WIN]: the spare row (a refill may read past the last word before a top-up)
+    int r;
+    ICX_HD int row() const { return r; }
+    ICX_HD void bind() { r = 0; }
+    ICX_HD void put(int j, uint32_t v) { q[j] = v; }
+    ICX_HD uint32_t next(bool need)
+    {
+#pragma unroll
+        for (int j = 0; j < WIN; j++) q[j] = need ? q[j + 1] : q[j];
+        r += need ? 1 : 0;
+        return q[0];
+    }
+};
+template <int WIN, bool LDS_WIN = true>
 struct DecFunnelReader {
     using Base = DecReaderT<WIN, true>;
     static constexpr int DEC_WIN = WIN;
@@ -501,7 +521,7 @@ struct DecFunnelReader {
     uint32_t w0, w1, q0;
     int s;
     uint32_t wi;  // stream word index of row 0 of the window
-    typename Base::Lds m;
+    typename std::conditional<LDS_WIN, typename Base::Lds, DecRegRows<WIN>>::type m;
 
     ICX_HD int used() const { return m.row(); }
     ICX_HD int left() const { return WIN - used(); }
@@ -520,6 +540,7 @@ struct DecFunnelReader {
         m.bind();
 #pragma unroll
         for (int j = 0; j < WIN; j++) m.put(j, dec_be32(t[j]));
+        if constexpr (!LDS_WIN) m.put(WIN, 0u);
         q0 = dec_be32(t[0]);
     }
     ICX_HD void advance(bool need) { q0 = m.next(need); }
@@ -548,6 +569,8 @@ struct DecFunnelReader {
         s = 0;
         wi = 0;
         m.bind();
+        if constexpr (!LDS_WIN)
+            for (int j = 0; j <= WIN; j++) m.put(j, 0u);
     }
     ICX_HD uint32_t peek32() const
     {
@@ -1037,14 +1060,15 @@ struct DecLeanWalker {
     ICX_HD void step(bool act = true)
     {
         R.refill();
-        const uint32_t e = dec_lean_lookup(H, ti, slow, R.peek16(), z != 0);
-        const int c1 = act ? (int)(e & 31) : 0;
+        // a lane without a walk steps on entry 0, which changes nothing
+        const uint32_t e = act ? dec_lean_lookup(H, ti, slow, R.peek16(), z != 0) : 0u;
+        const int c1 = (int)(e & 31);
         // straight-line transition (an invalid entry, 0, leaves the state as
         // it is), then the rare invalid-code path overrides it
-        const int z1 = z + (act ? (int)((e >> 5) & 127) : 0);
+        const int z1 = z + (int)((e >> 5) & 127);
         // the pair's second symbol, unless the first ended the block
         const int c2 = (int)((e >> DEC_PAIR_SHIFT) & 31);
-        two = act && c2 != 0 && z1 < 64;
+        two = c2 != 0 && z1 < 64;
         const int c = c1 + (two ? c2 : 0);
         R.skip(c);
         pos += (uint32_t)c;
@@ -1184,7 +1208,11 @@ struct DecLeanWriter {
     bool two;  // the last step was a symbol pair
     int64_t blk_base;
     uint32_t nlim;  // blocks from blk_base to the image's end (clamped to 32 bits)
+#if ICX_DEC_FUNNEL_WRITE
+    DecFunnelReader<DEC_WIN_WRITE, ICX_DEC_LDS_WIN_WRITE != 0> R;
+#else
     DecReaderT<DEC_WIN_WRITE, ICX_DEC_LDS_WIN_WRITE != 0> R;
+#endif
     const uint32_t* words;
 
 #if ICX_DEC_BSEL
@@ -1205,11 +1233,28 @@ struct DecLeanWriter {
     }
     ICX_HD bool running(uint32_t stop) const { return pos < stop || z != 0; }
     ICX_HD uint64_t state() const { return dec_pack(pos, b, z); }
+#if ICX_DEC_FUNNEL_WRITE
+    // value bits of a symbol whose code and value end `end` bits into the
+    // step's 32-bit look-ahead (end <= 31: a code and its extra bits, or a pair)
+    ICX_HD static uint32_t value_at(uint32_t x, int end, int sz)
+    {
+#if defined(__HIP_DEVICE_COMPILE__)
+        return __builtin_amdgcn_ubfe(x, (uint32_t)(32 - end), (uint32_t)sz);
+#else
+        return (x >> (32 - end)) & ((1u << sz) - 1u);
+#endif
+    }
+#endif
     template <class Sink>
     ICX_HD void step(Sink& sink)
     {
         R.refill();
+#if ICX_DEC_FUNNEL_WRITE
+        const uint32_t X = R.peek32();
+        const uint32_t e = dec_lean_lookup(H, ti, slow, X >> 16, z != 0);
+#else
         const uint32_t e = dec_lean_lookup(H, ti, slow, R.peek16(), z != 0);
+#endif
         const int c = (int)(e & 31);
         two = false;
         if (c == 0) {  // no valid code here
@@ -1217,9 +1262,13 @@ struct DecLeanWriter {
             return;
         }
         const int sz = (int)((e >> 12) & 15), zadd = (int)((e >> 5) & 127);
+#if ICX_DEC_FUNNEL_WRITE
+        const uint32_t v = value_at(X, c, sz);
+#else
         const uint32_t v = dec_value_bits(R.buf, c, sz);
         R.skip(c);
         pos += (uint32_t)c;
+#endif
 #if ICX_DEC_EXT_BF
         // HUFF_EXTEND without the sz == 0 branch: v = 0 and half = 0 then
         const int half = (1 << sz) >> 1;
@@ -1238,11 +1287,22 @@ struct DecLeanWriter {
         // unless the first ended the block: its value bits follow its code
         const int c2 = (int)((e >> DEC_PAIR_SHIFT) & 31);
         two = c2 != 0 && z < 64;
+#if ICX_DEC_FUNNEL_WRITE
+        {  // one skip for the step (a pair's bits are inside the look-ahead)
+            const int ct = c + (two ? c2 : 0);
+            R.skip(ct);
+            pos += (uint32_t)ct;
+        }
+#endif
         if (two) {
             const int sz2 = (int)((e >> 21) & 15), zadd2 = (int)(e >> 25);
+#if ICX_DEC_FUNNEL_WRITE
+            const uint32_t v2 = value_at(X, c + c2, sz2);
+#else
             const uint32_t v2 = dec_value_bits(R.buf, c2, sz2);
             R.skip(c2);
             pos += (uint32_t)c2;
+#endif
             const int half2 = (1 << sz2) >> 1;
             const int x2 = (int)v2 - ((int)v2 < half2 ? (1 << sz2) - 1 : 0);
             const int zc2 = z + zadd2 - 1;
