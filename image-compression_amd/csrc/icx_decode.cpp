@@ -176,11 +176,17 @@ uint32_t pick_sub_bits(uint64_t total_bits)
 // Warm-up walk before each subsequence (k_dec_init): long enough for typical
 // content to resynchronise, short against the subsequence.  Measured on 200
 // 4K q95 frames (half noise): 2048 bits 33.7-34.2 ms per call, 4096 33.2,
-// 8192 32.7-32.9 (init +1.1 ms, sync -1.4 ms), 16384 34.0.
-uint32_t warm_bits(uint32_t sub_bits)
+// 8192 32.7-32.9 (init +1.1 ms, sync -1.4 ms), 16384 34.0.  A small call
+// (fewer than 2^17 subsequences: the files -> files path's 64-frame groups)
+// leaves the chip part-idle in the warm-up launch, and 16384 bits there
+// halves the noise subsequences' misses (scripts/sync_stats.cpp: 33 -> 11 %):
+// 64 frames 7.95 -> 7.78 ms per call, 200 frames +1.5 % (round 6,
+// profiles/r6/ab/ab_r6_warm_small.txt).
+uint32_t warm_bits(uint32_t sub_bits, uint64_t total_bits)
 {
     if (const char* e = getenv("ICX_DEC_WARM")) return (uint32_t)atol(e);
-    return std::min<uint32_t>(8192, sub_bits / 2);
+    const uint32_t w = total_bits / sub_bits < (1u << 17) ? 16384 : 8192;
+    return std::min<uint32_t>(w, sub_bits / 2);
 }
 
 // The header tables build_dec_tab reads are equal (so are the DecTabs).
@@ -679,7 +685,7 @@ icx_status run_decode_impl(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coe
         }
         {
             Timed tm(c, "dec_init", stuffed);
-            launch_dec_init(d_desc, d_state, Ps.p, Ps.total, S, warm_bits(S), c->stream);
+            launch_dec_init(d_desc, d_state, Ps.p, Ps.total, S, warm_bits(S, bits), c->stream);
         }
         // ---- settle the subsequence entry states.  An image whose last sync
         // launch appended nothing to its worklist has settled (its worklists
