@@ -167,8 +167,12 @@ uint32_t pick_sub_bits(uint64_t total_bits)
     // fewer per call, profiles/r5/pipeline/ab_r5q_pipeline.txt); below that
     // 16384, and shorter only when the batch would not give the chip ~64k
     // threads.
+    // Round 6 (profiles/r6/ab/ab_r6_sub_small.txt): a call under 2^32 bits
+    // (~69 4K q95 frames: the files -> files path's 64-frame groups) takes
+    // 16384 with a 24576-bit warm-up (warm_bits): 64 frames 7.80 -> 7.40 ms per
+    // call; 200 frames keep 32768 (16384 there: +4 %).
     uint32_t S = 65536;
-    if (total_bits / S < (1u << 19)) S = total_bits / 32768 >= (1u << 16) ? 32768 : 16384;
+    if (total_bits / S < (1u << 19)) S = total_bits >= (1ull << 32) ? 32768 : 16384;
     while (S > 2048 && total_bits / S < 65536) S /= 2;
     return S;
 }
@@ -177,16 +181,17 @@ uint32_t pick_sub_bits(uint64_t total_bits)
 // content to resynchronise, short against the subsequence.  Measured on 200
 // 4K q95 frames (half noise): 2048 bits 33.7-34.2 ms per call, 4096 33.2,
 // 8192 32.7-32.9 (init +1.1 ms, sync -1.4 ms), 16384 34.0.  A small call
-// (fewer than 2^17 subsequences: the files -> files path's 64-frame groups)
-// leaves the chip part-idle in the warm-up launch, and 16384 bits there
-// halves the noise subsequences' misses (scripts/sync_stats.cpp: 33 -> 11 %):
-// 64 frames 7.95 -> 7.78 ms per call, 200 frames +1.5 % (round 6,
-// profiles/r6/ab/ab_r6_warm_small.txt).
+// (under 2^32 bits, 16384-bit subsequences: pick_sub_bits) leaves the chip
+// part-idle in the warm-up launch, and a long warm-up there cuts the noise
+// subsequences' misses (scripts/sync_stats.cpp: 8192 bits 33 %, 16384 11 %,
+// 32768 1.5 %) and with them the relaxation's launches: 64 frames at 16384
+// bits per subsequence, warm-up 16384 / 24576 bits: 7.52-7.60 / 7.39-7.41 ms
+// per call (profiles/r6/ab/ab_r6_sub_small.txt, ab_r6_warm_small.txt).
 uint32_t warm_bits(uint32_t sub_bits, uint64_t total_bits)
 {
     if (const char* e = getenv("ICX_DEC_WARM")) return (uint32_t)atol(e);
-    const uint32_t w = total_bits / sub_bits < (1u << 17) ? 16384 : 8192;
-    return std::min<uint32_t>(w, sub_bits / 2);
+    if (sub_bits == 16384 && total_bits < (1ull << 32)) return 24576;
+    return std::min<uint32_t>(8192, sub_bits / 2);
 }
 
 // The header tables build_dec_tab reads are equal (so are the DecTabs).
