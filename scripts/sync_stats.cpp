@@ -173,5 +173,56 @@ int main(int argc, char** argv)
         walk_v1(dec_pack(0, 0, 0), std::min<uint32_t>(ent_bits, 4000000u), drops);
         printf("  overshoots on the true path's first 4 Mbit: %d\n", drops);
     }
+    // 4. the relaxation itself, launch by launch (Jacobi order: a launch reads
+    // the entries the previous one left), on this one image: per launch the
+    // re-walks and the bits the longest walked - a launch lasts about as long
+    // as its longest walk.  argv[3] = subsequence bits, argv[4] = warm-up bits.
+    if (argc > 4) {
+        const uint32_t S = (uint32_t)atol(argv[3]), W = (uint32_t)atol(argv[4]);
+        const uint32_t nsub = (ent_bits + S - 1) / S;
+        const int nck = dec_ck_slots(S);
+        const uint32_t ckb = dec_ck_bits(S);
+        std::vector<uint64_t> est(nsub + 1), ck((size_t)(nsub + 1) * DEC_CK_MAX, DEC_CK_NONE);
+        std::vector<uint32_t> ncnt(nsub, 0);
+        for (uint32_t j = 0; j <= nsub; j++)
+            est[j] = j == 0 || j >= nsub ? dec_pack(j * S, 0, 0) : walk_to(dec_pack(j * S > W ? j * S - W : 0, 0, 0), j * S);
+        struct Rec {  // CkInPlace / CkRecord with the last checkpoint visited
+            CkInPlace<uint64_t*> in;
+            CkRecord<uint64_t*> rec;
+            bool first;
+            int last = -1;
+            bool visit(int k, uint64_t st, uint32_t& nb)
+            {
+                last = k;
+                return first ? rec.visit(k, st, nb) : in.visit(k, st, nb);
+            }
+            void finish(int k, bool early) { first ? rec.finish(k, early) : in.finish(k, early); }
+        };
+        std::vector<uint32_t> work(nsub);
+        for (uint32_t j = 0; j < nsub; j++) work[j] = j;
+        printf("  relaxation, %u-bit subsequences (%u), warm-up %u bits, checkpoints every %u bits:\n", S, nsub, W, ckb);
+        for (int it = 0; !work.empty() && it < 64; it++) {
+            std::vector<uint64_t> e0 = est;
+            std::vector<uint32_t> next, lens;
+            for (uint32_t j : work) {
+                uint64_t* mine = ck.data() + (size_t)j * DEC_CK_MAX;
+                Rec r{{mine, nck, ncnt[j], nck > 0 ? mine[0] : DEC_CK_NONE}, {mine, nck}, it == 0};
+                uint32_t n;
+                bool early;
+                const uint64_t x = dec_sync_walk(d, H, T.slow, sel, words.data(), seg.data(), 1u, ent_bits, e0[j], j * S, S,
+                                                 n, early, r);
+                lens.push_back(early ? (uint32_t)(r.last + 1) * ckb : S);
+                ncnt[j] = n;
+                if (!early && x != est[j + 1]) {
+                    est[j + 1] = x;
+                    if (j + 1 < nsub) next.push_back(j + 1);
+                }
+            }
+            std::sort(lens.begin(), lens.end());
+            printf("    launch %d: %zu walks, bits walked p50 %u p90 %u max %u\n", it, lens.size(), lens[lens.size() / 2],
+                   lens[(size_t)(0.9 * (lens.size() - 1))], lens.back());
+            work.swap(next);
+        }
+    }
     return 0;
 }
