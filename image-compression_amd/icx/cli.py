@@ -4,7 +4,7 @@ defaults, plus GPU placement flags.
   python -m icx -f list.txt -o outdir [-q 0.25] [-s 1048576] [-w 1920] [-i 1920]
                 [-t 1048576] [--timeOut 24] [--cache-db image-compression-cache]
                 [--devices 0,1] [--workers-per-device 2] [--group 64] [--group-max 0]
-                [--decode-threads N]
+                [--decode-threads N] [--write-threads 4]
 
 Each device gets --workers-per-device GPU worker threads, each with its own
 libicx context, so one group's host work (file bytes to the decoder, results
@@ -15,7 +15,9 @@ interleaved configurations; profiles/r6/pipeline/): two workers with groups of
 64 ran 3810-4320 files/s warm and 3825-4198 with every file searched, three
 workers 3078-3148 and larger groups (--group-max 128 / 256) 3160-3670 in the
 same calls; the box drifts 15-25 % over a call, so only the interleaved order
-separates them.
+separates them.  The output files go through four writer
+threads of their own (--write-threads): sixteen contended on the output
+directory (warm 3597-4068 files/s against 4869-5548 with four).
 Multi-GPU: by default one process drives every visible GPU (worker threads
 per device sharing one L1 cache, the reference's one ConcurrentHashMap); or
 one process per GPU under torchrun (RANK/WORLD_SIZE/LOCAL_RANK): the file
@@ -55,6 +57,7 @@ def build_parser():
                    help="files a GPU worker takes at once when more are waiting (0: --group, fixed groups; "
                         "larger calls measured no faster, DESIGN.md §9)")
     p.add_argument("--decode-threads", type=int, default=None)
+    p.add_argument("--write-threads", type=int, default=4, help="threads writing the JPEG output files")
     p.add_argument("-V", "--version", action="version", version="1.0")
     return p
 
@@ -98,7 +101,7 @@ def main(argv=None) -> int:
     codecs = [Codec(d) for d in devices for _ in range(max(1, a.workers_per_device))]
     batch = CompressionBatch(a.file_list, a.output_dir, params, a.timeOut, a.cache_db, codecs=codecs,
                              group_size=a.group, decode_threads=a.decode_threads, rank=rank, world=world,
-                             group_max=a.group_max)
+                             group_max=a.group_max, write_threads=a.write_threads)
     if dist is None:
         rep = batch.execute()
     else:

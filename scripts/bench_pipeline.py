@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3, help="timed repetitions of each run (median reported)")
     ap.add_argument("--procs", type=int, default=1, help="processes sharing the list (warm-cache run only)")
     ap.add_argument("--decode-threads", type=int, default=0, help="host reader threads (0: every usable core)")
+    ap.add_argument("--write-threads", type=int, default=4, help="JPEG output writer threads (the CLI default)")
     a = ap.parse_args()
     from PIL import Image
 
@@ -107,7 +108,7 @@ def main():
     def batch(out, cache_db):
         return pipeline.CompressionBatch(lst, out, params, 1, cache_db, codecs=codecs, group_size=a.group,
                                          decode_threads=a.decode_threads or None, stage_times=True,
-                                         group_max=a.group_max)
+                                         group_max=a.group_max, write_threads=a.write_threads)
     if not a.no_warmup:  # untimed: the process's first-use costs (its own cache DB)
         batch(os.path.join(work, "out_w"), os.path.join(work, "cache_w")).execute()
         shutil.rmtree(os.path.join(work, "out_w"), ignore_errors=True)
@@ -167,6 +168,7 @@ def main():
     print(json.dumps({"metric": "CompressionBatch end-to-end (files -> files), 4K q95 JPEG" +
                                 (" + 4K PNG (configs[4] mix)" if a.png else "") + ", -t 1MiB, devices " + a.devices,
                       "files": a.files, "png_files": a.png, "group_size": a.group, "group_max": a.group_max,
+                      "write_threads": a.write_threads,
                       "mean_src_bytes": int(np.mean([len(b) for b in blobs])),
                       "mean_png_src_bytes": int(np.mean([len(b) for b in png_blobs])) if png_blobs else 0,
                       "summary": summary, "runs": runs}))

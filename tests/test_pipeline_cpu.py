@@ -174,6 +174,7 @@ def test_cli_default_devices():
     from icx.cli import build_parser
     a = build_parser().parse_args(["-f", "l.txt", "-o", "out"])
     assert a.workers_per_device == 2 and a.group == 64 and a.group_max == 0
+    assert a.write_threads == 4  # JPEG outputs from a few writer threads (pipeline.CompressionBatch)
 
 
 def test_shard_partition():
