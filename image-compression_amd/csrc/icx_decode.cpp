@@ -602,8 +602,10 @@ icx_status run_decode_impl(icx_ctx* c, icx_decode_job* jobs, int n, int16_t* coe
             d.wl[1] = (uint32_t*)c->dev.take((size_t)(d.nsub_max + 1) * 4);
             d.ncnt = (uint32_t*)c->dev.take((size_t)(d.nsub_max + 1) * 4);
             d.boff = (uint32_t*)c->dev.take((size_t)(d.nsub_max + 1) * 4);
-            d.coefs = (int16_t*)c->dev.take((size_t)d.nblocks * 128);
-            d.dc = (int32_t*)c->dev.take((size_t)d.nblocks * 4);
+            // d.dc right behind the coefficients: k_dec_write stores a block's
+            // coefficients and its DC difference with one instruction
+            d.coefs = (int16_t*)c->dev.take((size_t)d.nblocks * 132);
+            d.dc = (int32_t*)((uint8_t*)d.coefs + (size_t)d.nblocks * 128);
             if (!coef_out) {
                 for (int q = d.fuse420 ? 1 : 0; q < d.ncomp; q++)  // fuse420: luma stays in LDS
                     d.plane[q] = (uint8_t*)c->dev.take((size_t)d.pw[q] * d.ph[q] + DEC_PLANE_SPARE);

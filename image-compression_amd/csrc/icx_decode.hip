@@ -918,6 +918,16 @@ constexpr int SLOT_DW = 32;
 #ifndef ICX_DEC_DC_LANE
 #define ICX_DEC_DC_LANE 1  // 87.8 vs 88.3 ms per 1000-frame decode (profiles/r4/ab_r4o_dec_win.txt)
 #endif
+// Flush addressing in scalar registers (round 6): the finished block's index
+// is one readlane (a 32-bit block index), its store a global_store with the
+// block's 64-bit address in SGPRs and a 32-bit lane offset (lane 32's: d.dc's
+// entry, which follows the coefficients in the same allocation), the slot
+// reads one v_xad each.  The write pass is VALU-issue-bound at four waves per
+// SIMD (five: no faster, three: +18 %, profiles/r6/ab/ab_r6_write_occupancy.txt),
+// and the flush cost ~18 VALU per finished block.
+#ifndef ICX_DEC_FLUSH_SADDR
+#define ICX_DEC_FLUSH_SADDR 1
+#endif
 
 // A lane that finishes an owned block only records its index, and the wave
 // then copies every finished slot together (below), permuting to natural
@@ -953,17 +963,18 @@ struct PendSink {
 // low (DecReader), then ballots the lanes that finished a block and copies
 // each of those 128-byte slots with 32 lanes (one coalesced dword store each,
 // natural order: coefficient pair 2l, 2l+1 read from its zig-zag positions),
-// zeroing it behind (lane 0 also stores the DC difference into d.dc).  The
+// zeroing it behind (lane 32 also stores the DC difference into d.dc; with
+// ICX_DEC_FLUSH_SADDR the addresses are scalar and a block costs 5 VALU).  The
 // block stores are the only vector-memory traffic between top-ups, so no
-// symbol waits for them.  A per-lane flush would cost
-// every lane of the wave ~70 instructions whenever any lane finishes a block,
-// which on q95 content is most iterations.  Only the first levels of the
+// symbol waits for them.  A per-lane flush costs every lane of the wave its
+// copy whenever any lane finishes a block, which on q95 content is most
+// iterations (measured: write pass +28 %, profiles/r6/ab/ab_r6_flush_lane.txt).  Only the first levels of the
 // Huffman tables are in LDS (SplitHuff): the second levels of the few codes
 // longer than 10 bits are read from the image's tables in global memory.
 __global__ void __launch_bounds__(DEC_WRITE_NT) k_dec_write(const DecDesc* D, DecState* S, Plan p, uint32_t sub_bits)
 {
     __shared__ __attribute__((aligned(16))) uint32_t L1[4][1 << DEC_LUT_BITS];
-    __shared__ __attribute__((aligned(16))) uint32_t slots[DEC_WRITE_NT * SLOT_DW];
+    __shared__ __attribute__((aligned(128))) uint32_t slots[DEC_WRITE_NT * SLOT_DW];  // 128-B slots on 128-B boundaries (the flush ORs offsets in)
     int slot;
     int64_t wg;
     if (!plan_slot(p, slot, wg)) return;
@@ -1015,10 +1026,73 @@ __global__ void __launch_bounds__(DEC_WRITE_NT) k_dec_write(const DecDesc* D, De
     ICX_GLOBAL uint32_t* coefs32 = (ICX_GLOBAL uint32_t*)d.coefs;  // global_store: vmcnt only, not lgkmcnt
     ICX_GLOBAL int32_t* dcs = (ICX_GLOBAL int32_t*)d.dc;
     const int zl = dec_zz((2 * lane) & 63), zh = dec_zz((2 * lane + 1) & 63);  // this lane's flush pair (lane % 32)
+#if ICX_DEC_FLUSH_SADDR
+    // d.dc relative to d.coefs: lane 32's store offset is rel - 124 bi (>= 0
+    // while rel >= 128 nblocks; < 2^32 while rel is); otherwise the general path
+    const uint64_t coefs_s = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)(uintptr_t)coefs32 >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)coefs32);  // (int: no sign extension)
+    const uint64_t rel = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)(uintptr_t)dcs >> 32)) << 32 |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dcs)) -
+                         coefs_s;
+    const bool saddr = __builtin_amdgcn_readfirstlane(rel >= (uint64_t)d.nblocks * 128u && rel < (1ull << 32));  // wave-uniform
+    const uint32_t zl2 = (uint32_t)zl << 1, zh2 = (uint32_t)zh << 1, lane4 = (uint32_t)(lane & 31) << 2;
+    // wave-uniform, in SGPRs: the wave's first slot (LDS byte address) and the
+    // coefficient array
+    typedef __attribute__((address_space(3))) uint16_t lds16_t;
+    typedef uint16_t us2_t __attribute__((ext_vector_type(2)));
+    uint32_t offv = lane4;  // store offset: lanes 0..31 their pair, lane 32 (set per block) the DC entry
+    typedef __attribute__((address_space(3))) uint32_t lds32_t;
+    const uint32_t ws_lds = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds32_t*)wave_slots);
+
+#if ICX_DEC_PEND32
+    const uint32_t blk32 = (uint32_t)pc.blk;  // block indices fit 32 bits (nblocks < 2^31)
+#endif
+#endif
     // copy the wave's finished blocks out of their slots (after every step: a
     // lane's next block reuses its slot)
     auto flush = [&]() {
     uint64_t m = __ballot(sk.pend >= 0);
+#if ICX_DEC_FLUSH_SADDR
+    if (saddr) {
+        // every lane's block index, computed before the lane mask below (the
+        // readlane takes it from lanes past 32 too)
+#if ICX_DEC_PEND32
+        uint32_t mine = blk32 + (uint32_t)sk.pend;
+#else
+        uint32_t mine = (uint32_t)sk.pend;
+#endif
+        asm volatile("" : "+v"(mine));  // pinned here, with every lane active (not sunk under the mask)
+        if (m && lane <= 32) {
+            do {
+                const int l = __builtin_ctzll(m);
+                m &= ~(1ull << l);  // s_bitset0
+                const uint32_t bi = (uint32_t)__builtin_amdgcn_readlane(mine, l);
+                // lane l's slot (LDS byte address) and its swizzle, both wave-uniform
+                // slot base + swizzle (a 128-B aligned base: + and ^ commute
+                // with the 7-bit offsets), then one v_xor per read address
+                const uint32_t sw = ws_lds + (uint32_t)l * (SLOT_DW * 4) + ((uint32_t)(l & 62) << 1);
+                lds16_t* const pl = (lds16_t*)(size_t)(sw ^ zl2);
+                lds16_t* const ph = (lds16_t*)(size_t)(sw ^ zh2);
+                us2_t pr;
+                pr.x = *pl;
+                pr.y = *ph;
+                const uint32_t v = __builtin_bit_cast(uint32_t, pr);
+                // zeroed behind, at the addresses read (the wave's LDS
+                // instructions complete in order: lane 0's zeroes follow lane
+                // 32's reads of the same two positions)
+                *pl = 0;
+                *ph = 0;
+                // lanes 0..31: the block's 32 coefficient pairs; lane 32: the pair
+                // (DC difference, zig-zag 1) into d.dc - k_dec_dc takes the low half
+                ICX_GLOBAL uint8_t* const base = (ICX_GLOBAL uint8_t*)(uintptr_t)(coefs_s + ((uint64_t)bi << 7));
+                asm("v_writelane_b32 %0, %1, 32" : "+v"(offv) : "s"((uint32_t)rel - bi * 124u));  // lane 32's offset
+                *(ICX_GLOBAL uint32_t*)(base + offv) = v;
+            } while (m);
+        }
+        sk.pend = -1;
+        return;
+    }
+#endif
 #if ICX_DEC_FLUSH2
     // two finished blocks per round: lanes 0..31 copy the first, 32..63 the second
     while (m) {
@@ -1144,7 +1218,7 @@ __device__ __forceinline__ void dc_tile(ICX_GLOBAL int32_t* dc, int nb, int ny, 
     if (in) {
 #pragma unroll
         for (int k = 0; k < (NB > 0 ? NB : 10); k++)
-            if (k < n) d[k] = dc[m * n + k];
+            if (k < n) d[k] = (int16_t)dc[m * n + k];  // the write pass may leave zig-zag 1 in the high half
 #pragma unroll
         for (int k = 0; k < (NB > 0 ? NB : 10); k++)
             if (k < n) a.v[k < ny ? 0 : k - ny + 1] += d[k];
