@@ -1233,6 +1233,15 @@ struct DecLeanWriter {
     }
     ICX_HD bool running(uint32_t stop) const { return pos < stop || z != 0; }
     ICX_HD uint64_t state() const { return dec_pack(pos, b, z); }
+    ICX_HD static int dec_extend_bf(uint32_t v, int sz)
+    {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const uint32_t m = __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0u, (uint32_t)sz);  // one v_bfe_u32 (sz = 0: 0)
+#else
+        const uint32_t m = (1u << sz) - 1u;
+#endif
+        return (int)(v <= (m >> 1) ? v - m : v);
+    }
 #if ICX_DEC_FUNNEL_WRITE
     // value bits of a symbol whose code and value end `end` bits into the
     // step's 32-bit look-ahead (end <= 31: a code and its extra bits, or a pair)
@@ -1270,9 +1279,10 @@ struct DecLeanWriter {
         pos += (uint32_t)c;
 #endif
 #if ICX_DEC_EXT_BF
-        // HUFF_EXTEND without the sz == 0 branch: v = 0 and half = 0 then
-        const int half = (1 << sz) >> 1;
-        const int x = (int)v - ((int)v < half ? (1 << sz) - 1 : 0);
+        // HUFF_EXTEND without the sz == 0 branch (v = 0 and m = 0 then): v
+        // below half = (m + 1) / 2 is v <= m / 2 - mask, shift, compare,
+        // select, subtract
+        const int x = dec_extend_bf(v, sz);
 #else
         const int x = sz ? dec_extend((int)v, sz) : 0;
 #endif
@@ -1303,8 +1313,7 @@ struct DecLeanWriter {
             R.skip(c2);
             pos += (uint32_t)c2;
 #endif
-            const int half2 = (1 << sz2) >> 1;
-            const int x2 = (int)v2 - ((int)v2 < half2 ? (1 << sz2) - 1 : 0);
+            const int x2 = dec_extend_bf(v2, sz2);
             const int zc2 = z + zadd2 - 1;
             sink.put(zc2 < own ? zc2 : own, x2);
             z += zadd2;
