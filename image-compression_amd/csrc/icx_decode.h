@@ -719,6 +719,22 @@ ICX_HD uint64_t dec_block_sel(uint32_t selp, int nby, int nbmcu)
     return r;
 }
 ICX_HD int dec_block_table(uint64_t bsel, int bb, int zz) { return (int)((bsel >> (4 * bb + (zz != 0 ? 2 : 0))) & 3); }
+// The map in 32 bits (ICX_DEC_BSEL32): a walk's MCU has at most 8 blocks (the
+// walk state packs the block-in-MCU index in 3 bits; the layouts parse_jpeg
+// accepts have <= 6), so a table index is one bit-field extract, and after a
+// step the next symbol's table is the next block's DC table at a block end,
+// else block b's AC table - no compare of z (2 VALU less per step).
+#ifndef ICX_DEC_BSEL32
+#define ICX_DEC_BSEL32 1
+#endif
+ICX_HD uint32_t dec_bsel_bits(uint32_t bsel, uint32_t off)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ubfe(bsel, off, 2u);
+#else
+    return (bsel >> off) & 3u;
+#endif
+}
 // The map is the same for every lane of a workgroup (one image): kept in
 // scalar registers on the device.
 ICX_HD uint64_t dec_uniform(uint64_t v)
@@ -1022,17 +1038,27 @@ struct DecLeanWalker {
     const ICX_GLOBAL uint32_t* seg;
     uint32_t nseg, ent_bits;
     int nby, nbmcu;
+#if ICX_DEC_BSEL32
+    uint32_t bsel;  // dec_block_sel (<= 8 blocks)
+#else
     uint64_t bsel;  // dec_block_sel
+#endif
     uint32_t pos, n;
     int b, z, ti;  // ti: table of the next symbol (component of block b, DC at z == 0)
     bool two;      // the last step was a symbol pair (tests compare against DecWalker's single steps)
     DecLeanReader R;
     const uint32_t* words;
 
-#if ICX_DEC_BSEL
+#if ICX_DEC_BSEL && ICX_DEC_BSEL32
+    ICX_HD int table(int bb, int zz) const { return (int)dec_bsel_bits(bsel, 4u * (uint32_t)bb + (zz != 0 ? 2u : 0u)); }
+    // after a step (z >= 1 unless the block ended): the next symbol's table
+    ICX_HD int table_after(bool end) const { return (int)dec_bsel_bits(bsel, ((uint32_t)b << 2) | (end ? 0u : 2u)); }
+#elif ICX_DEC_BSEL
     ICX_HD int table(int bb, int zz) const { return dec_block_table(bsel, bb, zz); }
+    ICX_HD int table_after(bool) const { return table(b, z); }
 #else
     ICX_HD int table(int bb, int zz) const { return dec_sel(selp, bb < nby ? 0 : bb - nby + 1, zz != 0 ? 1 : 0); }
+    ICX_HD int table_after(bool) const { return table(b, z); }
 #endif
     ICX_HD void start(uint64_t st)
     {
@@ -1078,7 +1104,7 @@ struct DecLeanWalker {
         const int bn = b + 1 == nbmcu ? 0 : b + 1;
         b = end ? bn : b;
         z = end ? 0 : z;
-        ti = table(b, z);
+        ti = table_after(end);  // (a lane without a walk never looks up again)
         if (act && c == 0) invalid();  // no valid code here
     }
     // DecWalker<false>::invalid: resume a bit later mid-interval, else the
@@ -1120,7 +1146,7 @@ ICX_HD DecLeanWalker<LeanPtr> dec_lean_walker(const DecDesc& d, LeanPtr H, const
     w.ent_bits = ent_bits;
     w.nby = d.nby;
     w.nbmcu = d.wmcu;
-    w.bsel = dec_uniform(dec_block_sel(selp, d.nby, d.wmcu));
+    w.bsel = (decltype(w.bsel))dec_uniform(dec_block_sel(selp, d.nby, d.wmcu));
     return w;
 }
 
@@ -1196,7 +1222,11 @@ struct DecLeanWriter {
     int nby, nbmcu;
     int ri, nbm;
     int64_t nblocks;
+#if ICX_DEC_BSEL32
+    uint32_t bsel;  // dec_block_sel (<= 8 blocks)
+#else
     uint64_t bsel;  // dec_block_sel
+#endif
     uint32_t pos, n;
     int b, z, ti;
     // 63 once the walk owns its block, 0 before (the partial block it starts
@@ -1215,10 +1245,16 @@ struct DecLeanWriter {
 #endif
     const uint32_t* words;
 
-#if ICX_DEC_BSEL
+#if ICX_DEC_BSEL && ICX_DEC_BSEL32
+    ICX_HD int table(int bb, int zz) const { return (int)dec_bsel_bits(bsel, 4u * (uint32_t)bb + (zz != 0 ? 2u : 0u)); }
+    // after a step (z >= 1 unless the block ended): the next symbol's table
+    ICX_HD int table_after(bool end) const { return (int)dec_bsel_bits(bsel, ((uint32_t)b << 2) | (end ? 0u : 2u)); }
+#elif ICX_DEC_BSEL
     ICX_HD int table(int bb, int zz) const { return dec_block_table(bsel, bb, zz); }
+    ICX_HD int table_after(bool) const { return table(b, z); }
 #else
     ICX_HD int table(int bb, int zz) const { return dec_sel(selp, bb < nby ? 0 : bb - nby + 1, zz != 0 ? 1 : 0); }
+    ICX_HD int table_after(bool) const { return table(b, z); }
 #endif
     ICX_HD void start(uint64_t st)
     {
@@ -1330,7 +1366,7 @@ struct DecLeanWriter {
         const int bn = b + 1 == nbmcu ? 0 : b + 1;
         b = end ? bn : b;
         z = end ? 0 : z;
-        ti = table(b, z);
+        ti = table_after(end);
     }
     // DecWalker<true>::invalid
     ICX_HD void invalid()
@@ -1394,7 +1430,7 @@ ICX_HD DecLeanWriter<LeanPtr> dec_lean_writer(const DecDesc& d, LeanPtr H, const
     w.blk_base = blk_base;
     const int64_t lim = d.nblocks - blk_base;
     w.nlim = lim <= 0 ? 0u : lim >= (int64_t)0xFFFFFFFF ? 0xFFFFFFFFu : (uint32_t)lim;
-    w.bsel = dec_uniform(dec_block_sel(selp, d.nby, d.wmcu));
+    w.bsel = (decltype(w.bsel))dec_uniform(dec_block_sel(selp, d.nby, d.wmcu));
     return w;
 }
 

@@ -274,7 +274,16 @@ extern "C" long dec_emu_lean_check(const uint8_t* jpg, size_t len, int nstarts, 
         NoSink ns;
         for (int k = 0; k < steps && a.running(DEC_END) && b.running(DEC_END); k++) {
             a.step(ns);
-            if (rng() % 4 == 0) b.step(false);  // an idle lane's step (device loops) changes nothing
+            if (rng() % 4 == 0) {  // an idle lane's step (device loops) changes no state or count
+                // (on a copy: a lane never walks again after an idle step, and its next-table
+                // index may move - ICX_DEC_BSEL32's table_after)
+                DecLeanWalker<const DecLean*> c = b;
+                c.step(false);
+                if (c.state() != b.state() || c.n != b.n) {
+                    bad++;
+                    break;
+                }
+            }
             b.step();
             if (b.two) {  // a symbol pair: the spec's next symbol too (the same block's next AC code)
                 pairs++;
