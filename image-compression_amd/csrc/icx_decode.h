@@ -755,8 +755,15 @@ ICX_HD uint64_t dec_uniform(uint64_t v)
 // at index 0, which the walk's first owned block overwrites with its DC.
 struct NoSink {
     ICX_HD void put(int, int) {}
+    ICX_HD void put2(int, int) {}
     ICX_HD void flush_if(bool, int64_t) {}
 };
+// DecLeanWriter's puts (ICX_DEC_PUT2): put2(2 * index, value) - the byte
+// offset of an int16 slot entry, so the device sink's address is one XOR with
+// its (128-B aligned) slot base and swizzle; `own` is kept doubled too.
+#ifndef ICX_DEC_PUT2
+#define ICX_DEC_PUT2 1
+#endif
 
 // The walk as a state object, one symbol per step() (the device write pass
 // drives it from a wave-uniform loop so finished blocks can be flushed by the
@@ -1234,6 +1241,7 @@ struct DecLeanWriter {
     // put before the first owned block lands on index 0, which that block's
     // DC overwrites - one v_min per put instead of a clamp and a select
     int own;
+    static constexpr int OWN_SCALE = ICX_DEC_PUT2 ? 2 : 1;  // own in put2's units
     bool bad;
     bool two;  // the last step was a symbol pair
     int64_t blk_base;
@@ -1262,7 +1270,7 @@ struct DecLeanWriter {
         b = (int)((st >> 8) & 7);
         z = (int)(st & 63);
         n = 0;
-        own = z == 0 ? 63 : 0;
+        own = z == 0 ? 63 * OWN_SCALE : 0;
         bad = false;
         ti = table(b, z);
         R.init(words, pos);
@@ -1326,9 +1334,17 @@ struct DecLeanWriter {
         // a zero DC difference) puts its 0 at z + advance - 1 (clamped), a
         // position its zero run covers and nothing wrote yet in the zeroed
         // slot - no select for it
+#if ICX_DEC_PUT2
+        z += zadd;
+        {
+            const int zc2 = (z << 1) - 2;
+            sink.put2(zc2 < own ? zc2 : own, x);
+        }
+#else
         const int zc = z + zadd - 1;
         sink.put(zc < own ? zc : own, x);
         z += zadd;
+#endif
         // the pair's second symbol (an AC code inside the same look-ahead),
         // unless the first ended the block: its value bits follow its code
         const int c2 = (int)((e >> DEC_PAIR_SHIFT) & 31);
@@ -1350,9 +1366,15 @@ struct DecLeanWriter {
             pos += (uint32_t)c2;
 #endif
             const int x2 = dec_extend_bf(v2, sz2);
+#if ICX_DEC_PUT2
+            z += zadd2;
+            const int zc2 = (z << 1) - 2;
+            sink.put2(zc2 < own ? zc2 : own, x2);
+#else
             const int zc2 = z + zadd2 - 1;
             sink.put(zc2 < own ? zc2 : own, x2);
             z += zadd2;
+#endif
         }
         const bool end = z >= 64;
 #if ICX_DEC_PEND32
@@ -1361,7 +1383,7 @@ struct DecLeanWriter {
         const int64_t bi = blk_base + n;
         sink.flush_if(end && own != 0 && bi < nblocks, bi);
 #endif
-        own = end ? 63 : own;
+        own = end ? 63 * OWN_SCALE : own;
         n += end ? 1u : 0u;
         const int bn = b + 1 == nbmcu ? 0 : b + 1;
         b = end ? bn : b;
@@ -1378,7 +1400,7 @@ struct DecLeanWriter {
         b = 0;
         z = 0;
         ti = table(0, 0);
-        own = 63;
+        own = 63 * OWN_SCALE;
         if (pos + 8 < bound) {
             bad = true;
             pos++;

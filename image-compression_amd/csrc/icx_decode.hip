@@ -956,6 +956,13 @@ struct PendSink {
     }
 #endif
     __device__ __forceinline__ void put(int z, int v) { *(int16_t*)(slot + ((z ^ sw) << 1)) = (int16_t)v; }
+    // z2 = 2 z (ICX_DEC_PUT2): the entry's LDS byte address is sa ^ z2, sa =
+    // the slot's LDS address | 2 sw (the slot is 128-B aligned)
+    uint32_t sa;
+    __device__ __forceinline__ void put2(int z2, int v)
+    {
+        *(__attribute__((address_space(3))) int16_t*)(size_t)(sa ^ (uint32_t)z2) = (int16_t)v;
+    }
 };
 
 // Write pass.  The walk runs in a wave-uniform loop, one symbol per lane per
@@ -1023,6 +1030,7 @@ __global__ void __launch_bounds__(DEC_WRITE_NT) k_dec_write(const DecDesc* D, De
 #else
     PendSink sk{(uint8_t*)mys, (uint32_t)(lane & 62), -1};
 #endif
+    sk.sa = (uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t*)mys | ((uint32_t)(lane & 62) << 1);
     ICX_GLOBAL uint32_t* coefs32 = (ICX_GLOBAL uint32_t*)d.coefs;  // global_store: vmcnt only, not lgkmcnt
     ICX_GLOBAL int32_t* dcs = (ICX_GLOBAL int32_t*)d.dc;
     const int zl = dec_zz((2 * lane) & 63), zh = dec_zz((2 * lane + 1) & 63);  // this lane's flush pair (lane % 32)

@@ -176,6 +176,7 @@ extern "C" int dec_emu_coefs(const uint8_t* jpg, size_t len, int16_t* out, size_
         int16_t* out;
         int32_t* dcs;
         void put(int z, int v) { buf[z < 64 ? dec_nat(z) : 64] = (int16_t)v; }
+        void put2(int z2, int v) { put(z2 >> 1, v); }
         void flush_if(bool c, int64_t bi)
         {
             if (!c) return;
@@ -310,6 +311,7 @@ extern "C" long dec_emu_lean_check(const uint8_t* jpg, size_t len, int nstarts, 
         {
             if (v) ev.push_back(((int64_t)z << 32) ^ (uint32_t)v);
         }
+        void put2(int z2, int v) { put(z2 >> 1, v); }
         void flush_if(bool c, int64_t bi)
         {
             if (c) ev.push_back(-1 - bi);
